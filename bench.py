@@ -1,0 +1,225 @@
+#!/usr/bin/env python
+"""Benchmark: Langevin z-steps/sec, CIFAR-10 (B=128, z_dim=128, ngf=128) on 1..8 MI355X.
+
+One bench "step" = the Langevin block of one reference training iteration
+(workspace/train_gen_recon.py:203-209): 30 posterior steps on B=128 chains
+(sample_langevin_post_z_with_prior, sigma=.1, s=.1, noise on) + 60 prior steps on 2B=256
+chains (sample_langevin_prior_z, s=.4, noise on).  `value` counts POSTERIOR z-steps only
+(B x 30 per step and rank) against the wall time of the whole block, i.e. the prior's time is
+charged but its (cheap) z-steps are not — conservative against the CPU-reference's 130
+posterior z-steps/s.
+
+Multi-GPU: one process per GPU (torchrun), B=128 chains per rank with globally-indexed
+Philox noise (chain_base = rank * B): per-GPU work is fixed -> "scaling": "weak"; the chains
+never communicate, so there is no collective in the timed path (timing uses a barrier and a
+MAX all-reduce of the elapsed time only).
+
+Data: synthetic (counter-hash weights / x ~ U[-1,1] / z0 ~ N(0,1); no datasets offline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "diffusion-amortized-mcmc_amd"))
+
+import torch  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 (= f32 MFMA rate), MI355X_MICROARCH.md
+B, NZ, NGF = 128, 128, 128
+POST_STEPS, PRIOR_STEPS = 30, 60
+SIGMA, S_POST, S_PRIOR = 0.1, 0.1, 0.4
+
+
+def build(device):
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=NZ, ngf=NGF, nc=3), 0).to(device).eval()
+    E = synth.load_into(dn._netE(nz=NZ), 10).to(device).eval()
+    for p in list(G.parameters()) + list(E.parameters()):
+        p.requires_grad_(False)
+    return G, E
+
+
+def inputs(device, rank):
+    from damc import synth
+
+    x = torch.from_numpy(synth.uniform_f32(1 + 1000 * rank, 0, (B, 3, 32, 32))).to(device)
+    z0 = torch.from_numpy(synth.normal_f32(2 + 1000 * rank, 0, (B, NZ))).to(device)
+    return x, z0
+
+
+def one_block(lv, G, E, x, z0, zbuf, pbuf, seed, rank):
+    """30 posterior steps on B chains + 60 prior steps on 2B chains (train_gen_recon.py:203-209)."""
+    zbuf.copy_(z0)
+    lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=seed, chain_base=rank * B)
+    pbuf[:B].copy_(z0)
+    lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=seed + 1, chain_base=rank * 2 * B)
+
+
+def cpu_baseline(budget_s=12.0):
+    """Oracle (CPU restatement, fp32, op for op the reference algorithm) on a bounded sample."""
+    from damc import synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    threads = torch.get_num_threads()
+    G = synth.load_into(dn._netG_cifar10(nz=NZ, ngf=NGF, nc=3), 0).eval()
+    E = synth.load_into(dn._netE(nz=NZ), 10).eval()
+    L, P = orc.generator_layers(G), orc.ebm_params(E)
+    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32)))
+    z = torch.from_numpy(synth.normal_f32(2, 0, (B, NZ)))
+    zp = torch.cat([z, torch.randn_like(z)])
+    # warm-up (allocator / oneDNN primitive creation)
+    orc.posterior_langevin(L, P, z, x, 1, SIGMA, S_POST)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        # per posterior step, 2 prior steps on 2B chains (the 30:60 ratio of the block)
+        z = orc.posterior_langevin(L, P, z, x, 1, SIGMA, S_POST, noise=torch.randn(1, B, NZ))
+        zp = orc.prior_langevin(P, zp, 2, S_PRIOR, noise=torch.randn(2, 2 * B, NZ))
+        n += 1
+        el = time.perf_counter() - t0
+        if (el > budget_s and n >= 2) or n >= 200:
+            break
+    return dict(value=B * n / el, unit="z-steps/s", cores=threads, kind="port",
+                sample="%d posterior steps (B=128, CIFAR-10 G ngf=128) + %d prior steps (2B=256) of the "
+                       "fp32 oracle restatement, %.1f s" % (n, 2 * n, el))
+
+
+def traffic_from_profiles(kernel_class):
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_class, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from damc import _lib
+    from damc import langevin as lv
+
+    G, E = build(device)
+    x, z0 = inputs(device, rank)
+    zbuf = torch.empty_like(z0)
+    pbuf = torch.randn(2 * B, NZ, device=device)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(device)
+
+    for i in range(args.warmup):
+        one_block(lv, G, E, x, z0, zbuf, pbuf, 1000 + i, rank)
+    L = _lib.lib()
+    L.damc_prof_reset()
+    L.damc_prof_enable(1)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_block(lv, G, E, x, z0, zbuf, pbuf, 2000 + i, rank)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    L.damc_prof_enable(0)
+    if not torch.isfinite(zbuf).all() or not torch.isfinite(pbuf).all():
+        raise RuntimeError("non-finite chains after the timed region")
+
+    # per-class kernel time from the live HIP events
+    import ctypes
+
+    classes = {}
+    for name in ("upconv_fwd", "upconv_dgrad", "proj_fwd", "proj_dgrad", "smallc_fwd", "smallc_dgrad",
+                 "posterior_update", "prior_chain"):
+        ms, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
+        _lib.check(L.damc_prof_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
+        if n.value:
+            classes[name] = dict(total_ms=ms.value, launches=n.value, flops=fl.value)
+
+    t_max = elapsed
+    if dist:
+        t = torch.tensor([elapsed], device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        t_max = float(t.item())
+
+    if rank == 0:
+        zsteps = world * B * POST_STEPS * args.steps
+        value = zsteps / t_max
+        dom = max(("upconv_fwd", "upconv_dgrad"), key=lambda k: classes.get(k, {}).get("total_ms", 0.0))
+        c = classes[dom]
+        avg_s = c["total_ms"] / c["launches"] / 1e3
+        flops_per_launch = c["flops"] / c["launches"]
+        achieved = flops_per_launch / avg_s / 1e12
+        traffic = traffic_from_profiles(dom)
+        gemm_ms = sum(classes[k]["total_ms"] for k in classes if k.startswith(("upconv", "proj")))
+        gemm_fl = sum(classes[k]["flops"] for k in classes if k.startswith(("upconv", "proj")))
+        post_flops_step = 4.0 * B * 1089.2e6  # 4 * B * MAC_G per posterior step
+        out = {
+            "metric": "Langevin z-steps/sec (B=128, z_dim=128, CIFAR-10)",
+            "value": round(value, 2),
+            "unit": "z-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * t_max / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-hash weights, x~U[-1,1], z0~N(0,1); CIFAR-10 _netG_cifar10 ngf=128 + _netE)",
+            "config": {
+                "workload": "cifar10 train-iteration Langevin block: 30 posterior steps on B=128 + 60 prior "
+                            "steps on 2B=256 per rank (value counts posterior z-steps only)",
+                "global_batch": world * B, "z_dim": NZ, "ngf": NGF, "posterior_steps": POST_STEPS,
+                "prior_steps": PRIOR_STEPS, "sigma": SIGMA, "step_size": S_POST, "prior_step_size": S_PRIOR,
+                "parallelism": "dp%d (chains sharded, no collective)" % world,
+            },
+            "roofline": {
+                "bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
+                "traffic": traffic,
+            },
+            "posterior_tflops_effective": round(post_flops_step * POST_STEPS * args.steps / t_max / 1e12, 2),
+            "gemm_classes_tflops": round(gemm_fl / (gemm_ms / 1e3) / 1e12, 2) if gemm_ms else None,
+            "kernel_classes": {k: dict(avg_ms=round(v["total_ms"] / v["launches"], 4), launches=v["launches"])
+                               for k, v in classes.items()},
+            "prior_us_per_step": round(1e3 * classes["prior_chain"]["total_ms"] / classes["prior_chain"]["launches"]
+                                       / PRIOR_STEPS, 2) if "prior_chain" in classes else None,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(args.cpu_budget)
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        print(json.dumps(out))
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

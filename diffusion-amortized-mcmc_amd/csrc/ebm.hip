@@ -1,0 +1,382 @@
+// ebm.hip — latent EBM energy/gradient, the fused Langevin z-update with in-kernel Philox noise,
+// and the persistent prior chain (all n steps of sample_langevin_prior_z in one launch).
+//
+// _netE (workspace/src/diffusion_net.py:207-223): E(z) = w3 . lrelu(W2 lrelu(W1 z + b1) + b2) + b3
+//   grad_z E = W1^T [ lrelu'(a1) * W2^T ( lrelu'(a2) * w3 ) ]
+// A workgroup owns R chains (rows).  Rows are independent, so the chains never communicate:
+// the prior kernel runs every step with z resident in LDS.  At R <= 8 rows per workgroup the
+// three FC layers are tiny-M GEMMs; on the VALU each weight element is loaded once per step
+// (coalesced across the 256 lanes) and reused R times from registers.
+#include "common.h"
+
+namespace {
+
+struct EbmSmem {
+  float* zs;  // [R][nz]
+  float* h1;  // [R][nh]  lrelu(a1)
+  float* h2;  // [R][nh]  lrelu(a2)
+  float* g2;  // [R][nh]
+  float* g1;  // [R][nh]
+  float* gz;  // [R][nz]
+  float* red; // [8]
+};
+
+__host__ __device__ inline size_t ebm_smem_floats(int R, int nz, int nh) {
+  return (size_t)R * nz * 2 + (size_t)R * nh * 4 + 8;
+}
+
+__device__ inline EbmSmem ebm_carve(float* base, int R, int nz, int nh) {
+  EbmSmem s;
+  s.zs = base;
+  s.h1 = s.zs + R * nz;
+  s.h2 = s.h1 + R * nh;
+  s.g2 = s.h2 + R * nh;
+  s.g1 = s.g2 + R * nh;
+  s.gz = s.g1 + R * nh;
+  s.red = s.gz + R * nz;
+  return s;
+}
+
+// Computes gz = grad_z sum_r E(z_r) for the R rows in s.zs; if energy != nullptr also writes
+// per-row energies (valid rows only).  All 256 threads participate; ends with a barrier.
+template <int R>
+__device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* energy_rows) {
+  const int tid = threadIdx.x;
+  const int nz = e.nz, nh = e.nh;
+  const float sl = e.slope;
+  // layer 1: a1 = W1 z + b1   (w1t is (nz, nh): lane j streams column j)
+  for (int j = tid; j < nh; j += blockDim.x) {
+    float acc[R];
+    const float bj = e.b1[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = bj;
+    for (int k = 0; k < nz; ++k) {
+      const float w = e.w1t[(long)k * nh + j];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.zs[r * nz + k], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) s.h1[r * nh + j] = acc[r] > 0.f ? acc[r] : acc[r] * sl;
+  }
+  __syncthreads();
+  // layer 2: a2 = W2 h1 + b2 ; g2 = w3 * lrelu'(a2)
+  for (int j = tid; j < nh; j += blockDim.x) {
+    float acc[R];
+    const float bj = e.b2[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = bj;
+    for (int k = 0; k < nh; ++k) {
+      const float w = e.w2t[(long)k * nh + j];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.h1[r * nh + k], acc[r]);
+    }
+    const float w3 = e.w3[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool pos = acc[r] > 0.f;
+      s.h2[r * nh + j] = pos ? acc[r] : acc[r] * sl;
+      s.g2[r * nh + j] = pos ? w3 : w3 * sl;
+    }
+  }
+  __syncthreads();
+  // energies (optional): e_r = w3 . h2_r + b3, one wave per row
+  if (energy_rows) {
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int r = wave; r < R; r += blockDim.x / 64) {
+      float v = 0.f;
+      for (int j = lane; j < nh; j += 64) v = fmaf(e.w3[j], s.h2[r * nh + j], v);
+      v = wave_sum(v);
+      if (lane == 0 && r < nvalid) energy_rows[r] = v + e.b3[0];
+    }
+  }
+  // layer 2 backward: g1 = (W2^T g2) * lrelu'(a1)   (w2 is (nh, nh) row-major: lane k streams column k)
+  for (int k = tid; k < nh; k += blockDim.x) {
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    for (int j = 0; j < nh; ++j) {
+      const float w = e.w2[(long)j * nh + k];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.g2[r * nh + j], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) s.g1[r * nh + k] = s.h1[r * nh + k] > 0.f ? acc[r] : acc[r] * sl;
+  }
+  __syncthreads();
+  // layer 1 backward: gz = W1^T g1   (w1 is (nh, nz))
+  for (int c = tid; c < nz; c += blockDim.x) {
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    for (int j = 0; j < nh; ++j) {
+      const float w = e.w1[(long)j * nz + c];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.g1[r * nh + j], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) s.gz[r * nz + c] = acc[r];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float noise_at(const float* noise, long noise_idx, int with_noise, uint64_t seed,
+                                          uint64_t chain, uint64_t step, int c, uint32_t stream_id) {
+  if (!with_noise) return 0.f;
+  if (noise) return noise[noise_idx];
+  float n4[4];
+  philox_normal4(seed, chain, step, (uint32_t)(c >> 2), stream_id, n4);
+  return n4[c & 3];
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  __syncthreads();
+  return t;  // valid in thread 0
+}
+
+// ---- posterior update: g = sum_s lik_slab[s] + grad E + z ; z <- (z - c1 g) + step xi
+template <int R>
+__global__ __launch_bounds__(256) void posterior_update_kernel(damc_ebm_t e, int use_ebm, float* z, const float* slabs,
+                                                                int nslab, long slab_stride, int B, int nz, float c1,
+                                                                float step, int with_noise, const float* noise,
+                                                                uint64_t seed, uint64_t step_idx, uint64_t chain_base,
+                                                                float* diag) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nh = use_ebm ? e.nh : 0;
+  EbmSmem s = ebm_carve(smem, R, nz, nh);
+  const int row0 = blockIdx.x * R;
+  const int nvalid = min(R, B - row0);
+  for (int i = threadIdx.x; i < R * nz; i += blockDim.x) {
+    const int r = i / nz;
+    s.zs[i] = r < nvalid ? z[(long)(row0 + r) * nz + (i - r * nz)] : 0.f;
+  }
+  __syncthreads();
+  float erow[R];
+  float* eptr = nullptr;
+  __shared__ float en_rows[R];
+  if (use_ebm) {
+    eptr = diag ? en_rows : nullptr;
+    ebm_rows<R>(e, s, nvalid, eptr);
+  }
+  (void)erow;
+  float zsq = 0.f, gsum = 0.f;
+  for (int i = threadIdx.x; i < nvalid * nz; i += blockDim.x) {
+    const int r = i / nz, c = i - r * nz;
+    const long gi = (long)(row0 + r) * nz + c;
+    float g = 0.f;
+    for (int k = 0; k < nslab; ++k) g += slabs[(long)k * slab_stride + gi];
+    if (use_ebm) g += s.gz[i];
+    const float zv = s.zs[i];
+    g += zv;
+    zsq += zv * zv;
+    gsum += g;
+    float zn = sub_rn(zv, mul_rn(c1, g));
+    if (with_noise) {
+      const float xi = noise_at(noise, gi, 1, seed, chain_base + row0 + r, step_idx, c, DAMC_STREAM_POSTERIOR);
+      zn = add_rn(zn, mul_rn(step, xi));
+    }
+    z[gi] = zn;
+  }
+  if (diag) {
+    float et = 0.f;
+    if (use_ebm && threadIdx.x == 0)
+      for (int r = 0; r < nvalid; ++r) et += en_rows[r];
+    const float zs_t = block_sum(zsq, s.red);
+    const float gs_t = block_sum(gsum, s.red);
+    if (threadIdx.x == 0) {
+      atomicAdd(&diag[0], et);
+      atomicAdd(&diag[2], 0.5f * zs_t);
+      atomicAdd(&diag[3], gs_t / (float)((long)B * nz));
+    }
+  }
+}
+
+// ---- prior chain: every step in one launch, z resident in LDS
+template <int R>
+__global__ __launch_bounds__(256) void prior_chain_kernel(damc_ebm_t e, float* z, int B, int n_steps, float c1, float step,
+                                                           int with_noise, const float* noise, uint64_t seed,
+                                                           uint64_t step_offset, uint64_t chain_base, float* diag) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nz = e.nz;
+  EbmSmem s = ebm_carve(smem, R, nz, e.nh);
+  __shared__ float en_rows[R];
+  const int row0 = blockIdx.x * R;
+  const int nvalid = min(R, B - row0);
+  for (int i = threadIdx.x; i < R * nz; i += blockDim.x) {
+    const int r = i / nz;
+    s.zs[i] = r < nvalid ? z[(long)(row0 + r) * nz + (i - r * nz)] : 0.f;
+  }
+  __syncthreads();
+  for (int it = 0; it < n_steps; ++it) {
+    ebm_rows<R>(e, s, nvalid, diag ? en_rows : nullptr);
+    float zsq = 0.f;
+    for (int i = threadIdx.x; i < nvalid * nz; i += blockDim.x) {
+      const int r = i / nz, c = i - r * nz;
+      const float zv = s.zs[i];
+      zsq += zv * zv;
+      const float g = s.gz[i] + zv;
+      float zn = sub_rn(zv, mul_rn(c1, g));
+      if (with_noise) {
+        const long ni = ((long)it * B + row0 + r) * nz + c;
+        const float xi =
+            noise_at(noise, ni, 1, seed, chain_base + row0 + r, step_offset + it, c, DAMC_STREAM_PRIOR);
+        zn = add_rn(zn, mul_rn(step, xi));
+      }
+      s.zs[i] = zn;
+    }
+    if (diag) {
+      const float zs_t = block_sum(zsq, s.red);
+      if (threadIdx.x == 0) {
+        float et = 0.f;
+        for (int r = 0; r < nvalid; ++r) et += en_rows[r];
+        atomicAdd(&diag[2 * it + 0], et);
+        atomicAdd(&diag[2 * it + 1], 0.5f * zs_t);
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < nvalid * nz; i += blockDim.x) {
+    const int r = i / nz;
+    z[(long)(row0 + r) * nz + (i - r * nz)] = s.zs[i];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void ebm_energy_grad_kernel(damc_ebm_t e, const float* z, int B, float* energy,
+                                                               float* grad) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nz = e.nz;
+  EbmSmem s = ebm_carve(smem, R, nz, e.nh);
+  const int row0 = blockIdx.x * R;
+  const int nvalid = min(R, B - row0);
+  for (int i = threadIdx.x; i < R * nz; i += blockDim.x) {
+    const int r = i / nz;
+    s.zs[i] = r < nvalid ? z[(long)(row0 + r) * nz + (i - r * nz)] : 0.f;
+  }
+  __syncthreads();
+  ebm_rows<R>(e, s, nvalid, energy ? energy + row0 : nullptr);
+  for (int i = threadIdx.x; i < nvalid * nz; i += blockDim.x) grad[(long)row0 * nz + i] = s.gz[i];
+}
+
+__global__ void z_update_kernel(float* z, const float* g, long n, int nz, float c1, float step, int with_noise,
+                                const float* noise, uint64_t seed, uint64_t step_idx, uint64_t chain_base) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long r = i / nz;
+  const int c = (int)(i - r * nz);
+  const float zv = z[i];
+  float zn = sub_rn(zv, mul_rn(c1, g[i] + zv));
+  if (with_noise) {
+    const float xi = noise_at(noise, i, 1, seed, chain_base + r, step_idx, c, DAMC_STREAM_POSTERIOR);
+    zn = add_rn(zn, mul_rn(step, xi));
+  }
+  z[i] = zn;
+}
+
+__global__ void philox_normal_kernel(float* out, int n_steps, int B, int nz, uint64_t seed, uint64_t step_offset,
+                                     uint64_t chain_base, uint32_t stream_id) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)n_steps * B * nz;
+  if (i >= n) return;
+  const long st = i / ((long)B * nz);
+  const long rem = i - st * B * nz;
+  const long r = rem / nz;
+  const int c = (int)(rem - r * nz);
+  float n4[4];
+  philox_normal4(seed, chain_base + r, step_offset + st, (uint32_t)(c >> 2), stream_id, n4);
+  out[i] = n4[c & 3];
+}
+
+constexpr int RP = 4;  // rows per workgroup, prior chain
+constexpr int RU = 8;  // rows per workgroup, posterior update
+
+}  // namespace
+
+// host helpers used by generator.hip
+int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
+                                 int nz, float step, int with_noise, const float* noise, uint64_t seed,
+                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s) {
+  damc_ebm_t ev{};
+  int use_ebm = 0;
+  if (e) {
+    ev = *e;
+    use_ebm = 1;
+    if (ev.nz != nz) return DAMC_ERR_ARG;
+  }
+  const float c1 = (float)(0.5 * (double)step * (double)step);
+  const size_t sm = ebm_smem_floats(RU, nz, use_ebm ? ev.nh : 0) * sizeof(float);
+  ProfScope ps("posterior_update", 0.0, s);
+  hipLaunchKernelGGL((posterior_update_kernel<RU>), dim3((B + RU - 1) / RU), dim3(256), sm, s, ev, use_ebm, z, slabs,
+                     nslab, slab_stride, B, nz, c1, step, with_noise, noise, seed, step_idx, chain_base, diag);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* stream);
+
+extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_steps, float step, int with_noise,
+                                   const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                                   float* diag, void* stream) {
+  if (!e || !z || B <= 0 || n_steps < 0) return DAMC_ERR_ARG;
+  if (!e->w1t || !e->w2t) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
+  if (n_steps == 0) return 0;
+  const float c1 = (float)(0.5 * (double)step * (double)step);
+  const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
+  ProfScope ps("prior_chain", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
+  hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(256), sm, s, *e, z, B, n_steps, c1, step,
+                     with_noise, noise, seed, step_offset, chain_base, diag);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_ebm_energy_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad,
+                                    void* stream) {
+  if (!e || !z || !grad || B <= 0) return DAMC_ERR_ARG;
+  const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
+  hipLaunchKernelGGL((ebm_energy_grad_kernel<RP>), dim3((B + RP - 1) / RP), dim3(256), sm, as_stream(stream), *e, z, B,
+                     energy, grad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_z_update(float* z, const float* g, int B, int nz, float step, int with_noise, const float* noise,
+                             uint64_t seed, uint64_t step_index, uint64_t chain_base, void* stream) {
+  if (!z || !g || B <= 0 || nz <= 0) return DAMC_ERR_ARG;
+  const long n = (long)B * nz;
+  const float c1 = (float)(0.5 * (double)step * (double)step);
+  hipLaunchKernelGGL(z_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), z, g, n, nz, c1,
+                     step, with_noise, noise, seed, step_index, chain_base);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_philox_normal(float* out, int n_steps, int B, int nz, uint64_t seed, uint64_t step_offset,
+                                  uint64_t chain_base, uint32_t stream_id, void* stream) {
+  const long n = (long)n_steps * B * nz;
+  if (!out || n <= 0) return DAMC_ERR_ARG;
+  hipLaunchKernelGGL(philox_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), out,
+                     n_steps, B, nz, seed, step_offset, chain_base, stream_id);
+  return (int)hipGetLastError();
+}
+
+// ---- packing: w1t = w1^T (nz, nh), w2t = w2^T (nh, nh)
+__global__ void transpose_kernel(const float* in, int rows, int cols, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const long r = i / cols, c = i - r * cols;
+  out[c * rows + r] = in[i];
+}
+
+extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* stream) {
+  if (!e || !w1t || !w2t) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  long n1 = (long)e->nh * e->nz, n2 = (long)e->nh * e->nh;
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, s, e->w1, e->nh, e->nz, w1t);
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, e->w2, e->nh, e->nh, w2t);
+  return (int)hipGetLastError();
+}

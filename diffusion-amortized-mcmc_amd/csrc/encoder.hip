@@ -1,0 +1,184 @@
+// encoder.hip — the amortizer's image encoder Encoder_* (workspace/src/diffusion_net.py:227-413):
+// [Conv2d -> InstanceNorm2d(affine, eps=1e-5) -> LeakyReLU(0.2)]* -> Conv2d, on NHWC activations.
+// Convolutions run on the fp32 MFMA implicit-GEMM engine (gemm.hip); InstanceNorm statistics are
+// per (sample, channel) Welford partials merged with Chan's formula (wave shuffles + LDS), then
+// one fused normalise + affine + LeakyReLU pass in place.
+#include "gemm.h"
+
+namespace {
+
+// (Cout,Cin,k,k) -> [(ky,kx,ci)][co]
+__global__ void pack_conv_kernel(const float* w, int cout, int cin, int k, float* wp) {
+  const long n = (long)cout * cin * k * k;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  long t = i;
+  const int kx = (int)(t % k);
+  t /= k;
+  const int ky = (int)(t % k);
+  t /= k;
+  const int ci = (int)(t % cin);
+  const int co = (int)(t / cin);
+  wp[(((long)ky * k + kx) * cin + ci) * cout + co] = w[i];
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* x, int B, int C, int HW, float* y) {
+  const long n = (long)B * C * HW;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // i enumerates the NHWC output
+  const int c = (int)(i % C);
+  const long t = i / C;
+  const int p = (int)(t % HW);
+  const int b = (int)(t / HW);
+  y[i] = x[((long)b * C + c) * HW + p];
+}
+
+struct Wf {
+  float n, mean, m2;
+};
+__device__ __forceinline__ Wf wmerge(Wf a, Wf b) {
+  const float n = a.n + b.n;
+  if (n == 0.f) return a;
+  const float d = b.mean - a.mean;
+  const float fb = b.n / n;
+  Wf r;
+  r.n = n;
+  r.mean = a.mean + d * fb;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * fb;
+  return r;
+}
+
+// grid: (B * ceil(C/64), S); block 256 = 64 channels x 4 pixel lanes
+__global__ __launch_bounds__(256) void in_stats_kernel(const float* y, int B, int HW, int C, int S, float* part) {
+  const int cg = (C + 63) / 64;
+  const int b = blockIdx.x / cg, c = (blockIdx.x % cg) * 64 + (threadIdx.x & 63);
+  const int prow = threadIdx.x >> 6;
+  const int s = blockIdx.y;
+  const int p0 = (int)((long)HW * s / S), p1 = (int)((long)HW * (s + 1) / S);
+  Wf w{0.f, 0.f, 0.f};
+  if (c < C) {
+    for (int p = p0 + prow; p < p1; p += 4) {
+      const float v = y[((long)b * HW + p) * C + c];
+      w.n += 1.f;
+      const float d = v - w.mean;
+      w.mean += d / w.n;
+      w.m2 += d * (v - w.mean);
+    }
+  }
+  __shared__ Wf red[4][64];
+  red[prow][threadIdx.x & 63] = w;
+  __syncthreads();
+  if (prow == 0 && c < C) {
+    Wf a = red[0][threadIdx.x];
+    for (int r = 1; r < 4; ++r) a = wmerge(a, red[r][threadIdx.x]);
+    float* o = part + (((long)b * C + c) * S + s) * 3;
+    o[0] = a.n;
+    o[1] = a.mean;
+    o[2] = a.m2;
+  }
+}
+
+// grid: (B * ceil(C/64), P); merges the S partials of its 64 channels, then normalises its pixels
+__global__ __launch_bounds__(256) void in_apply_kernel(float* y, int B, int HW, int C, int S, const float* part,
+                                                       const float* gamma, const float* beta, float eps, float slope) {
+  const int cg = (C + 63) / 64;
+  const int b = blockIdx.x / cg, c = (blockIdx.x % cg) * 64 + (threadIdx.x & 63);
+  const int prow = threadIdx.x >> 6;
+  __shared__ float sc[64], sh[64];
+  if (prow == 0) {
+    float scale = 0.f, shift = 0.f;
+    if (c < C) {
+      const float* pp = part + ((long)b * C + c) * S * 3;
+      Wf a{pp[0], pp[1], pp[2]};
+      for (int s = 1; s < S; ++s) a = wmerge(a, Wf{pp[3 * s], pp[3 * s + 1], pp[3 * s + 2]});
+      const float var = a.m2 / a.n;  // biased, as InstanceNorm2d
+      const float rstd = 1.f / sqrtf(var + eps);
+      scale = rstd * gamma[c];
+      shift = beta[c] - a.mean * scale;
+    }
+    sc[threadIdx.x] = scale;
+    sh[threadIdx.x] = shift;
+  }
+  __syncthreads();
+  if (c >= C) return;
+  const float scl = sc[threadIdx.x & 63], shf = sh[threadIdx.x & 63];
+  const int P = gridDim.y;
+  const int p0 = (int)((long)HW * blockIdx.y / P), p1 = (int)((long)HW * (blockIdx.y + 1) / P);
+  for (int p = p0 + prow; p < p1; p += 4) {
+    float* q = y + ((long)b * HW + p) * C + c;
+    const float v = fmaf(*q, scl, shf);
+    *q = v > 0.f ? v : v * slope;
+  }
+}
+
+int in_splits(int hw) {
+  int s = hw / 1024;
+  return s < 1 ? 1 : (s > 64 ? 64 : s);
+}
+
+}  // namespace
+
+extern "C" int damc_pack_conv2d(const float* w, int cout, int cin, int k, float* wp, void* stream) {
+  if (!w || !wp || cout <= 0 || cin <= 0 || k <= 0) return DAMC_ERR_ARG;
+  const long n = (long)cout * cin * k * k;
+  hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), w, cout, cin,
+                     k, wp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, void* stream) {
+  if (!x || !y || B <= 0 || C <= 0 || HW <= 0) return DAMC_ERR_ARG;
+  const long n = (long)B * C * HW;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), x, B, C,
+                     HW, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_conv2d_nhwc(const float* x, int B, int hin, int win, int cin, const float* wp, const float* bias,
+                                int cout, int k, int stride, int pad, float* y, void* stream) {
+  if (!x || !wp || !y || B <= 0) return DAMC_ERR_ARG;
+  const int hout = (hin + 2 * pad - k) / stride + 1, wout = (win + 2 * pad - k) / stride + 1;
+  if (hout <= 0 || wout <= 0) return DAMC_ERR_ARG;
+  damc::GemmArgs a;
+  a.A = x;
+  a.Hin = hin;
+  a.Win = win;
+  a.Cg = cin;
+  a.Hq = hout;
+  a.Wq = wout;
+  a.kw = k;
+  a.stride = stride;
+  a.pad_y = pad;
+  a.pad_x = pad;
+  a.B = wp;
+  a.ldb = cout;
+  a.C = y;
+  a.ldc = cout;
+  a.M = B * hout * wout;
+  a.N = cout;
+  a.K = k * k * cin;
+  a.k_per_z = a.K;
+  a.bias = bias;
+  a.bias_mod = cout;
+  a.act = DAMC_ACT_NONE;
+  return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
+                           2.0 * a.M * (double)cout * a.K, as_stream(stream));
+}
+
+extern "C" size_t damc_instnorm_workspace_floats(int B, int hw, int c) {
+  return (size_t)B * c * in_splits(hw) * 3;
+}
+
+extern "C" int damc_instnorm_lrelu_nhwc(float* y, int B, int hw, int c, const float* gamma, const float* beta,
+                                        float eps, float slope, float* ws, void* stream) {
+  if (!y || !gamma || !beta || !ws || B <= 0 || hw <= 0 || c <= 0) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  const int S = in_splits(hw);
+  const int cg = (c + 63) / 64;
+  ProfScope ps("instnorm", 0.0, s);
+  hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, y, B, hw, c, S, ws);
+  const int P = std::max(1, std::min(64, hw / 256));
+  hipLaunchKernelGGL(in_apply_kernel, dim3(B * cg, P), dim3(256), 0, s, y, B, hw, c, S, ws, gamma, beta, eps, slope);
+  return (int)hipGetLastError();
+}

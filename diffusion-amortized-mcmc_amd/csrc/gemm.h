@@ -1,0 +1,47 @@
+// gemm.h — host interface of the fp32 MFMA implicit-GEMM engine (gemm.hip).
+#pragma once
+#include "common.h"
+
+namespace damc {
+
+enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_SCALAR = 2 };
+enum Epi { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_MASK = 2, EPI_RESID = 3 };
+enum OMode { O_DENSE = 0, O_PHASE = 1 };
+
+// C[M,N] (+)= A[M,K] · B[K,N], K reduced in fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fmaf chains).
+//   A_DENSE       : A[m*lda + k]
+//   A_CONV(_SCALAR): A = NHWC tensor X[B][Hin][Win][Cg]; m -> (b, qy, qx) on an Hq x Wq grid,
+//                   k -> (ky, kx, ci) with ci fastest; value X[b][qy*stride-pad_y+ky][qx*stride-pad_x+kx][ci]
+//   O_PHASE       : blockIdx.z = output phase (py,px) of a k4 s2 p1 transposed conv; the GEMM is the
+//                   2x2 conv with pad (1-py, 1-px) and row m = (b,qy,qx) is stored at output pixel
+//                   (b, 2qy+py, 2qx+px) of a Hout x Wout NHWC map; B advanced by z*b_zstride
+//   O_DENSE       : blockIdx.z = split-K slice: k in [z*k_per_z, (z+1)*k_per_z), C advanced by z*c_zstride
+struct GemmArgs {
+  const float* A = nullptr;
+  long lda = 0;
+  int Hin = 1, Win = 1, Cg = 1, Hq = 1, Wq = 1, kw = 1, stride = 1, pad_y = 0, pad_x = 0;
+  const float* B = nullptr;
+  long ldb = 0;
+  long b_zstride = 0;
+  float* C = nullptr;
+  long ldc = 0;
+  long c_zstride = 0;
+  int M = 0, N = 0, K = 0, k_per_z = 0;
+  const float* bias = nullptr;
+  int bias_mod = 1;
+  int act = DAMC_ACT_NONE;
+  float slope = 0.f;
+  const float* mask = nullptr;  // EPI_MASK: post-activation at the same output index
+  int mask_act = DAMC_ACT_LRELU;
+  float mask_slope = 0.2f;
+  const float* xres = nullptr;  // EPI_RESID: target (row-major like C)
+  float inv_s2 = 1.f;
+  float* xhat = nullptr;
+  float* sqerr = nullptr;       // EPI_RESID: accumulates |t - x|^2 * inv_s2 / 2 (diagnostics)
+  int Hout = 1, Wout = 1;
+};
+
+int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
+                hipStream_t s);
+
+}  // namespace damc

@@ -1,0 +1,613 @@
+// generator.hip — ConvTranspose generator forward + input-gradient (J_G^T) and the posterior
+// Langevin loop (sample_langevin_post_z_with_prior, workspace/src/MCMC.py:48-74).
+//
+// Layout in HBM: every hidden activation is NHWC fp32 (channels contiguous = the GEMM K axis);
+// the caller's x / x_hat stay NCHW.  Per step:
+//   fwd : PROJ (GEMM z.W, bias+lrelu)  ->  UP2 x n (4-phase implicit GEMM, bias+lrelu)
+//         -> SMALLC (to-RGB conv, tanh, residual delta = (x_hat - x)/s^2 * (1 - x_hat^2))
+//   bwd : SMALLC dgrad * lrelu'  ->  UP2 dgrad (stride-2 conv implicit GEMM) * lrelu'
+//         -> PROJ dgrad (split-K GEMM into slabs)  ->  fused EBM grad + slab sum + z update
+// dgrad outputs overwrite the activation they are masked with (same thread reads h, writes dh).
+#include <vector>
+
+#include "gemm.h"
+
+using damc::GemmArgs;
+
+int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
+                                 int nz, float step, int with_noise, const float* noise, uint64_t seed,
+                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s);
+
+namespace {
+
+// ------------------------------------------------------------------------------ packing
+// PROJ: w (Cin,Cout,k,k) -> fwd [ci][(oy,ox,co)], bwd [(oy,ox,co)][ci]
+__global__ void pack_proj_kernel(const float* w, int cin, int cout, int k, float* wf, float* wb) {
+  const long n = (long)cin * cout * k * k;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // i enumerates torch layout
+  long t = i;
+  const int kx = (int)(t % k);
+  t /= k;
+  const int ky = (int)(t % k);
+  t /= k;
+  const int co = (int)(t % cout);
+  const int ci = (int)(t / cout);
+  const long col = ((long)ky * k + kx) * cout + co;
+  const float v = w[i];
+  wf[(long)ci * ((long)k * k * cout) + col] = v;
+  wb[col * cin + ci] = v;
+}
+// UP2 (k4 s2 p1): fwd [phase(py,px)][ty][tx][ci][co] = W[ci][co][3-py-2ty][3-px-2tx];
+//                 bwd [ky][kx][co][ci] = W[ci][co][ky][kx]
+__global__ void pack_up2_kernel(const float* w, int cin, int cout, float* wf, float* wb) {
+  const long n = (long)cin * cout * 16;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  long t = i;
+  const int kx = (int)(t % 4);
+  t /= 4;
+  const int ky = (int)(t % 4);
+  t /= 4;
+  const int co = (int)(t % cout);
+  const int ci = (int)(t / cout);
+  const float v = w[i];
+  // ky = 3 - py - 2 ty  ->  py = (3 - ky) & 1, ty = (3 - ky - py) / 2
+  const int py = (3 - ky) & 1, ty = (3 - ky - py) >> 1;
+  const int px = (3 - kx) & 1, tx = (3 - kx - px) >> 1;
+  const int phase = py * 2 + px;
+  wf[((((long)phase * 2 + ty) * 2 + tx) * cin + ci) * cout + co] = v;
+  wb[(((long)ky * 4 + kx) * cout + co) * cin + ci] = v;
+}
+// SMALLC: [ky][kx][ci][co]
+__global__ void pack_smallc_kernel(const float* w, int cin, int cout, int k, float* wf) {
+  const long n = (long)cin * cout * k * k;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  long t = i;
+  const int kx = (int)(t % k);
+  t /= k;
+  const int ky = (int)(t % k);
+  t /= k;
+  const int co = (int)(t % cout);
+  const int ci = (int)(t / cout);
+  wf[(((long)ky * k + kx) * cin + ci) * cout + co] = w[i];
+}
+// LINEAR: w (out,in): fwd = W^T (in,out), bwd = W (out,in)
+__global__ void pack_linear_kernel(const float* w, int in, int out, float* wf, float* wb) {
+  const long n = (long)in * out;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long o = i / in, c = i - o * in;
+  wf[c * out + o] = w[i];
+  wb[i] = w[i];
+}
+
+// ---------------------------------------------------------------- small-Cout output layer
+// One wave per output pixel, lanes across input channels; weights staged once per
+// workgroup in LDS as [tap][ci][co] and the grid strides over pixels.
+template <int NC>
+__global__ __launch_bounds__(256) void smallc_fwd_kernel(const float* h, int B, int Hin, int Win, int Cin, int k,
+                                                         int stride, int pad, int Hout, int Wout, const float* wpk,
+                                                         const float* bias, const float* x, float inv_s2,
+                                                         float* delta, float* xhat, float* sqerr_sum) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+  const int nw = k * k * Cin * NC;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) wl[i] = wpk[i];
+  __shared__ float red[4];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long npix = (long)B * Hout * Wout;
+  float sq_local = 0.f;
+  for (long pix = (long)blockIdx.x * 4 + wave; pix < npix; pix += (long)gridDim.x * 4) {
+    const int b = (int)(pix / ((long)Hout * Wout));
+    const int rem = (int)(pix - (long)b * Hout * Wout);
+    const int oy = rem / Wout, ox = rem - oy * Wout;
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+    for (int ky = 0; ky < k; ++ky) {
+      const int ty = oy + pad - ky;
+      if (ty < 0 || ty % stride) continue;
+      const int iy = ty / stride;
+      if (iy >= Hin) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int tx = ox + pad - kx;
+        if (tx < 0 || tx % stride) continue;
+        const int ix = tx / stride;
+        if (ix >= Win) continue;
+        const float* hp = h + (((long)b * Hin + iy) * Win + ix) * Cin;
+        const float* wp = wl + (ky * k + kx) * Cin * NC;
+        for (int ci = lane; ci < Cin; ci += 64) {
+          const float hv = hp[ci];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) acc[c] = fmaf(hv, wp[ci * NC + c], acc[c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = wave_sum(acc[c]);
+    if (lane < NC) {
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c == lane) a = acc[c];
+      a += bias ? bias[lane] : 0.f;
+      const float t = tanhf(a);
+      const long nchw = (((long)b * NC + lane) * Hout + oy) * Wout + ox;
+      if (xhat) xhat[nchw] = t;
+      if (delta) {
+        const float r = t - x[nchw];
+        delta[pix * NC + lane] = r * inv_s2 * (1.f - t * t);
+        sq_local += r * r;
+      }
+    }
+  }
+  if (sqerr_sum) {
+    sq_local = wave_sum(sq_local);
+    if (lane == 0) red[wave] = sq_local;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
+// dh[b,iy,ix,ci] = lrelu'(h) * sum_{ky,kx,co} delta[b, iy*s-p+ky, ix*s-p+kx, co] W[ci][co][ky][kx]
+// written in place over h.
+template <int NC>
+__global__ __launch_bounds__(256) void smallc_dgrad_kernel(float* h, int B, int Hin, int Win, int Cin, int k,
+                                                           int stride, int pad, int Hout, int Wout, const float* wpk,
+                                                           const float* delta, int mask_act, float mask_slope) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+  const int nw = k * k * Cin * NC;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) wl[i] = wpk[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long npix = (long)B * Hin * Win;
+  for (long pix = (long)blockIdx.x * 4 + wave; pix < npix; pix += (long)gridDim.x * 4) {
+    const int b = (int)(pix / ((long)Hin * Win));
+    const int rem = (int)(pix - (long)b * Hin * Win);
+    const int iy = rem / Win, ix = rem - iy * Win;
+    float* hp = h + pix * Cin;
+    for (int ci0 = 0; ci0 < Cin; ci0 += 64) {
+      const int ci = ci0 + lane;
+      float acc = 0.f;
+      for (int ky = 0; ky < k; ++ky) {
+        const int oy = iy * stride - pad + ky;
+        if (oy < 0 || oy >= Hout) continue;
+        for (int kx = 0; kx < k; ++kx) {
+          const int ox = ix * stride - pad + kx;
+          if (ox < 0 || ox >= Wout) continue;
+          const float* dp = delta + (((long)b * Hout + oy) * Wout + ox) * NC;
+          if (ci < Cin) {
+            const float* wp = wl + ((ky * k + kx) * Cin + ci) * NC;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc = fmaf(dp[c], wp[c], acc);
+          }
+        }
+      }
+      if (ci < Cin) hp[ci] = acc * act_grad_from_out(hp[ci], mask_act, mask_slope);
+    }
+  }
+}
+
+int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta, float* xhat,
+               float* sqerr, hipStream_t s) {
+  const size_t sm = (size_t)L.k * L.k * L.cin * L.cout * sizeof(float);
+  const long npix = (long)B * L.hout * L.wout;
+  const int grid = (int)std::min<long>((npix + 3) / 4, 2048);
+  ProfScope ps("smallc_fwd", 2.0 * npix * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
+#define SC(NC_)                                                                                              \
+  hipLaunchKernelGGL((smallc_fwd_kernel<NC_>), dim3(grid), dim3(256), sm, s, h, B, L.hin, L.win, L.cin, L.k, \
+                     L.stride, L.pad, L.hout, L.wout, L.w_fwd, L.bias, x, inv_s2, delta, xhat, sqerr)
+  switch (L.cout) {
+    case 1: SC(1); break;
+    case 2: SC(2); break;
+    case 3: SC(3); break;
+    case 4: SC(4); break;
+    default: return DAMC_ERR_UNSUPPORTED;
+  }
+#undef SC
+  return (int)hipGetLastError();
+}
+
+int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
+                 hipStream_t s) {
+  const size_t sm = (size_t)L.k * L.k * L.cin * L.cout * sizeof(float);
+  const long npix = (long)B * L.hin * L.win;
+  const int grid = (int)std::min<long>((npix + 3) / 4, 2048);
+  ProfScope ps("smallc_dgrad", 2.0 * npix * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
+#define SD(NC_)                                                                                                \
+  hipLaunchKernelGGL((smallc_dgrad_kernel<NC_>), dim3(grid), dim3(256), sm, s, h, B, L.hin, L.win, L.cin, L.k, \
+                     L.stride, L.pad, L.hout, L.wout, L.w_fwd, delta, mask_act, mask_slope)
+  switch (L.cout) {
+    case 1: SD(1); break;
+    case 2: SD(2); break;
+    case 3: SD(3); break;
+    case 4: SD(4); break;
+    default: return DAMC_ERR_UNSUPPORTED;
+  }
+#undef SD
+  return (int)hipGetLastError();
+}
+
+__global__ void slab_sum_kernel(const float* slabs, int nslab, long n, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int k = 0; k < nslab; ++k) acc += slabs[(long)k * n + i];
+  out[i] = acc;
+}
+
+// ------------------------------------------------------------------------- plan helpers
+long act_floats(const damc_layer_t& L, int B) { return (long)B * L.hout * L.wout * L.cout; }
+
+int validate(const damc_generator_t* g) {
+  if (!g || g->n_layers < 1 || g->n_layers > DAMC_MAX_LAYERS) return DAMC_ERR_ARG;
+  for (int i = 0; i < g->n_layers; ++i) {
+    const damc_layer_t& L = g->layers[i];
+    const bool last = i == g->n_layers - 1;
+    switch (L.kind) {
+      case DAMC_LAYER_PROJ:
+        if (i != 0 || L.hin != 1 || L.win != 1 || L.stride != 1 || L.pad != 0 || L.hout != L.k) return DAMC_ERR_ARG;
+        break;
+      case DAMC_LAYER_UP2:
+        if (i == 0 || last || L.k != 4 || L.stride != 2 || L.pad != 1 || L.hout != 2 * L.hin) return DAMC_ERR_ARG;
+        break;
+      case DAMC_LAYER_SMALLC:
+        if (!last || i == 0 || L.cout > 4 || L.act != DAMC_ACT_TANH) return DAMC_ERR_ARG;
+        break;
+      case DAMC_LAYER_LINEAR:
+        if (L.hin != 1 || L.hout != 1) return DAMC_ERR_ARG;
+        break;
+      default:
+        return DAMC_ERR_ARG;
+    }
+    if (i > 0) {
+      const damc_layer_t& P = g->layers[i - 1];
+      if (P.cout != L.cin || P.hout != L.hin || P.wout != L.win) return DAMC_ERR_ARG;
+    }
+    if (!last && L.act == DAMC_ACT_TANH) return DAMC_ERR_UNSUPPORTED;
+  }
+  const damc_layer_t& F = g->layers[g->n_layers - 1];
+  if (F.kind == DAMC_LAYER_PROJ || F.kind == DAMC_LAYER_UP2) return DAMC_ERR_UNSUPPORTED;
+  if (g->layers[0].cin != g->nz) return DAMC_ERR_ARG;
+  return 0;
+}
+
+// split-K slices for the PROJ/LINEAR-first-layer dgrad: depends on K only (never on the batch),
+// so per-chain results are bitwise identical for any sharding of the batch.
+int proj_slices(long K) {
+  long s = K / 256;
+  if (s < 1) s = 1;
+  if (s > 512) s = 512;
+  return (int)s;
+}
+int proj_k_per(long K, int S) { return (int)(((K + S - 1) / S + 15) / 16 * 16); }
+
+struct Workspace {
+  std::vector<float*> h;  // activations (NHWC), one per layer except the final one
+  float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
+  float* slabs;           // split-K partial gradients
+  int nslab;
+  size_t bytes;
+};
+
+size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
+  size_t off = 0;
+  auto take = [&](long floats) -> float* {
+    float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((size_t)floats * sizeof(float) + 255) / 256 * 256;
+    return p;
+  };
+  if (w) w->h.clear();
+  for (int i = 0; i + 1 < g->n_layers; ++i) {
+    float* p = take(act_floats(g->layers[i], B));
+    if (w) w->h.push_back(p);
+  }
+  const damc_layer_t& F = g->layers[g->n_layers - 1];
+  float* d = take(act_floats(F, B));
+  const damc_layer_t& L0 = g->layers[0];
+  const long K0 = (long)L0.hout * L0.wout * L0.cout;
+  const int S = (g->n_layers == 1) ? 1 : proj_slices(K0);
+  float* sl = take((long)S * B * g->nz);
+  if (w) {
+    w->delta = d;
+    w->slabs = sl;
+    w->nslab = S;
+    w->bytes = off;
+  }
+  return off;
+}
+
+double conv_flops(const damc_layer_t& L, int B) {
+  // MACs of the transposed conv = outputs x Cin x (taps hitting each output)
+  const double taps = (double)L.k * L.k / ((double)L.stride * L.stride);
+  return 2.0 * B * (double)L.hout * L.wout * L.cout * L.cin * taps;
+}
+
+// forward of layers [0, n-1) into ws.h; returns 0 on success
+int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& ws, hipStream_t s) {
+  for (int i = 0; i + 1 < g->n_layers; ++i) {
+    const damc_layer_t& L = g->layers[i];
+    GemmArgs a;
+    a.bias = L.bias;
+    a.bias_mod = L.cout;
+    a.act = L.act;
+    a.slope = L.slope;
+    a.C = ws.h[i];
+    int rc;
+    if (L.kind == DAMC_LAYER_PROJ || L.kind == DAMC_LAYER_LINEAR) {
+      const int N = L.hout * L.wout * L.cout;
+      a.A = (i == 0) ? z : ws.h[i - 1];
+      a.lda = L.cin;
+      a.B = L.w_fwd;
+      a.ldb = N;
+      a.ldc = N;
+      a.M = B;
+      a.N = N;
+      a.K = L.cin;
+      a.k_per_z = a.K;
+      rc = damc::launch_gemm(a, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
+                             2.0 * B * (double)N * L.cin, s);
+    } else {  // UP2
+      a.A = ws.h[i - 1];
+      a.Hin = L.hin;
+      a.Win = L.win;
+      a.Cg = L.cin;
+      a.Hq = L.hin;
+      a.Wq = L.win;
+      a.kw = 2;
+      a.stride = 1;
+      a.B = L.w_fwd;
+      a.ldb = L.cout;
+      a.b_zstride = 4L * L.cin * L.cout;
+      a.ldc = L.cout;
+      a.M = B * L.hin * L.win;
+      a.N = L.cout;
+      a.K = 4 * L.cin;
+      a.Hout = L.hout;
+      a.Wout = L.wout;
+      rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
+    }
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// final layer forward: delta (+ optional x_hat NCHW / row-major) and |x_hat-x|^2/(2s^2) into sqerr
+int forward_final(const damc_generator_t* g, int B, const float* z, const float* x, float inv_s2, Workspace& ws,
+                  float* xhat, float* sqerr, bool want_delta, hipStream_t s) {
+  const int n = g->n_layers;
+  const damc_layer_t& F = g->layers[n - 1];
+  const float* hin = n >= 2 ? ws.h[n - 2] : z;
+  if (F.kind == DAMC_LAYER_SMALLC)
+    return smallc_fwd(F, hin, B, want_delta ? x : nullptr, inv_s2, want_delta ? ws.delta : nullptr, xhat, sqerr, s);
+  // LINEAR final layer
+  GemmArgs a;
+  a.A = hin;
+  a.lda = F.cin;
+  a.B = F.w_fwd;
+  a.ldb = F.cout;
+  a.ldc = F.cout;
+  a.M = B;
+  a.N = F.cout;
+  a.K = F.cin;
+  a.k_per_z = a.K;
+  a.bias = F.bias;
+  a.bias_mod = F.cout;
+  a.act = F.act;
+  a.slope = F.slope;
+  if (want_delta) {
+    a.C = ws.delta;
+    a.xres = x;
+    a.inv_s2 = inv_s2;
+    a.xhat = xhat;
+    a.sqerr = sqerr;
+    int rc = damc::launch_gemm(a, damc::A_DENSE, damc::EPI_RESID, damc::O_DENSE, 1, "linear_out",
+                               2.0 * B * (double)F.cout * F.cin, s);
+    return rc;
+  }
+  a.C = xhat;
+  return damc::launch_gemm(a, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "linear_out",
+                           2.0 * B * (double)F.cout * F.cin, s);
+}
+
+// backward from ws.delta to the PROJ/first-layer split-K slabs
+int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
+  const int n = g->n_layers;
+  const float* d = ws.delta;  // gradient w.r.t. the pre-activation of layer i (current)
+  for (int i = n - 1; i >= 1; --i) {
+    const damc_layer_t& L = g->layers[i];
+    const damc_layer_t& P = g->layers[i - 1];
+    float* out = ws.h[i - 1];  // dgrad overwrites the activation it is masked with
+    int rc;
+    if (L.kind == DAMC_LAYER_SMALLC) {
+      rc = smallc_dgrad(L, out, B, d, P.act, P.slope, s);
+    } else if (L.kind == DAMC_LAYER_UP2) {
+      GemmArgs a;
+      a.A = d;
+      a.Hin = L.hout;
+      a.Win = L.wout;
+      a.Cg = L.cout;
+      a.Hq = L.hin;
+      a.Wq = L.win;
+      a.kw = 4;
+      a.stride = 2;
+      a.pad_y = 1;
+      a.pad_x = 1;
+      a.B = L.w_bwd;
+      a.ldb = L.cin;
+      a.C = out;
+      a.ldc = L.cin;
+      a.M = B * L.hin * L.win;
+      a.N = L.cin;
+      a.K = 16 * L.cout;
+      a.k_per_z = a.K;
+      a.mask = out;
+      a.mask_act = P.act;
+      a.mask_slope = P.slope;
+      rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_MASK, damc::O_DENSE, 1, "upconv_dgrad", conv_flops(L, B), s);
+    } else {  // LINEAR hidden/final
+      GemmArgs a;
+      a.A = d;
+      a.lda = L.cout;
+      a.B = L.w_bwd;
+      a.ldb = L.cin;
+      a.C = out;
+      a.ldc = L.cin;
+      a.M = B;
+      a.N = L.cin;
+      a.K = L.cout;
+      a.k_per_z = a.K;
+      a.mask = out;
+      a.mask_act = P.act;
+      a.mask_slope = P.slope;
+      rc = damc::launch_gemm(a, damc::A_DENSE, damc::EPI_MASK, damc::O_DENSE, 1, "linear_dgrad",
+                             2.0 * B * (double)L.cin * L.cout, s);
+    }
+    if (rc) return rc;
+    d = out;
+  }
+  // first layer: dz = dA0 . W0^T  (split-K into slabs)
+  const damc_layer_t& L0 = g->layers[0];
+  const long K = (long)L0.hout * L0.wout * L0.cout;
+  GemmArgs a;
+  a.A = d;
+  a.lda = K;
+  a.B = L0.w_bwd;
+  a.ldb = L0.cin;
+  a.C = ws.slabs;
+  a.ldc = L0.cin;
+  a.c_zstride = (long)B * L0.cin;
+  a.M = B;
+  a.N = L0.cin;
+  a.K = (int)K;
+  a.k_per_z = proj_k_per(K, ws.nslab);
+  const int S = (int)((K + a.k_per_z - 1) / a.k_per_z);
+  // slices beyond S (when rounding shrank the count) must contribute zeros
+  if (S < ws.nslab) DAMC_CHECK(hipMemsetAsync(ws.slabs, 0, sizeof(float) * ws.nslab * (size_t)B * L0.cin, s));
+  return damc::launch_gemm(a, damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, S, "proj_dgrad",
+                           2.0 * B * (double)K * L0.cin, s);
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" int damc_generator_layer_packed_sizes(const damc_layer_t* L, size_t* fwd, size_t* bwd) {
+  if (!L || !fwd || !bwd) return DAMC_ERR_ARG;
+  const size_t n = (size_t)L->cin * L->cout * (L->kind == DAMC_LAYER_LINEAR ? 1 : (size_t)L->k * L->k);
+  switch (L->kind) {
+    case DAMC_LAYER_PROJ:
+    case DAMC_LAYER_UP2:
+    case DAMC_LAYER_LINEAR:
+      *fwd = n;
+      *bwd = n;
+      return 0;
+    case DAMC_LAYER_SMALLC:
+      *fwd = n;
+      *bwd = 0;
+      return 0;
+  }
+  return DAMC_ERR_ARG;
+}
+
+extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, float* wf, float* wb, void* stream) {
+  if (!L || !w || !wf) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  const long n = (long)L->cin * L->cout * (L->kind == DAMC_LAYER_LINEAR ? 1 : (long)L->k * L->k);
+  const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+  switch (L->kind) {
+    case DAMC_LAYER_PROJ:
+      if (!wb) return DAMC_ERR_ARG;
+      hipLaunchKernelGGL(pack_proj_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf, wb);
+      break;
+    case DAMC_LAYER_UP2:
+      if (!wb || L->k != 4) return DAMC_ERR_ARG;
+      hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, wf, wb);
+      break;
+    case DAMC_LAYER_SMALLC:
+      hipLaunchKernelGGL(pack_smallc_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf);
+      break;
+    case DAMC_LAYER_LINEAR:
+      if (!wb) return DAMC_ERR_ARG;
+      hipLaunchKernelGGL(pack_linear_kernel, grid, blk, 0, s, w, L->cin, L->cout, wf, wb);
+      break;
+    default:
+      return DAMC_ERR_ARG;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" size_t damc_posterior_workspace_bytes(const damc_generator_t* g, int B) {
+  if (validate(g) || B <= 0) return 0;
+  return carve(g, B, nullptr, nullptr);
+}
+
+static int setup_ws(const damc_generator_t* g, int B, void* wsp, size_t wsb, Workspace* ws) {
+  int rc = validate(g);
+  if (rc) return rc;
+  if (B <= 0) return DAMC_ERR_ARG;
+  const size_t need = carve(g, B, nullptr, nullptr);
+  if (!wsp || wsb < need) return DAMC_ERR_WORKSPACE;
+  carve(g, B, reinterpret_cast<char*>(wsp), ws);
+  return 0;
+}
+
+extern "C" int damc_generator_forward(const damc_generator_t* g, const float* z, int B, float* xhat, void* wsp,
+                                      size_t wsb, void* stream) {
+  Workspace ws;
+  int rc = setup_ws(g, B, wsp, wsb, &ws);
+  if (rc) return rc;
+  if (!z || !xhat) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  rc = forward_hidden(g, z, B, ws, s);
+  if (rc) return rc;
+  return forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s);
+}
+
+extern "C" int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int B, float sigma,
+                                    float* grad, void* wsp, size_t wsb, void* stream) {
+  Workspace ws;
+  int rc = setup_ws(g, B, wsp, wsb, &ws);
+  if (rc) return rc;
+  if (!z || !x || !grad) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  const float inv_s2 = (float)(1.0 / ((double)sigma * sigma));
+  if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
+  if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, nullptr, true, s))) return rc;
+  if (g->n_layers == 1) {
+    // single layer: the delta is the gradient w.r.t. layer-0 pre-activation; dz = delta . W
+    return DAMC_ERR_UNSUPPORTED;
+  }
+  if ((rc = backward(g, B, ws, s))) return rc;
+  const long n = (long)B * g->nz;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws.slabs, ws.nslab, n, grad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
+                                       int B, int n_steps, float sigma, float step, int with_noise, const float* noise,
+                                       uint64_t seed, uint64_t step_offset, uint64_t chain_base, float* diag,
+                                       void* wsp, size_t wsb, void* stream) {
+  Workspace ws;
+  int rc = setup_ws(g, B, wsp, wsb, &ws);
+  if (rc) return rc;
+  if (!z || !x || n_steps < 0) return DAMC_ERR_ARG;
+  if (g->n_layers < 2) return DAMC_ERR_UNSUPPORTED;
+  if (ebm && (ebm->nz != g->nz || !ebm->w1t || !ebm->w2t)) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 4 * (size_t)n_steps, s));
+  const float inv_s2 = (float)(1.0 / ((double)sigma * sigma));
+  for (int i = 0; i < n_steps; ++i) {
+    float* dg = diag ? diag + 4 * i : nullptr;
+    if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
+    if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s))) return rc;
+    if ((rc = backward(g, B, ws, s))) return rc;
+    const float* nz_i = noise ? noise + (size_t)i * B * g->nz : nullptr;
+    rc = damc_launch_posterior_update(ebm, z, ws.slabs, ws.nslab, (long)B * g->nz, B, g->nz, step, with_noise, nz_i,
+                                      seed, step_offset + i, chain_base, dg, s);
+    if (rc) return rc;
+  }
+  return 0;
+}

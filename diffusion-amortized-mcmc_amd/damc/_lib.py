@@ -1,0 +1,145 @@
+"""ctypes binding of libdamc.so (include/damc.h).
+
+The library is built in-tree (``make -C diffusion-amortized-mcmc_amd/csrc``) and loaded from
+this directory.  There is deliberately NO fallback: if the .so is missing or a call fails,
+``lib()`` / ``check()`` raise, so a GPU box never silently runs anything but the HIP path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdamc.so")
+
+MAX_LAYERS = 10
+LAYER_PROJ, LAYER_UP2, LAYER_SMALLC, LAYER_LINEAR = 1, 2, 3, 4
+ACT_NONE, ACT_LRELU, ACT_TANH = 0, 1, 2
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+
+
+class Layer(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("k", ctypes.c_int),
+        ("stride", ctypes.c_int), ("pad", ctypes.c_int),
+        ("hin", ctypes.c_int), ("win", ctypes.c_int), ("hout", ctypes.c_int), ("wout", ctypes.c_int),
+        ("act", ctypes.c_int), ("slope", ctypes.c_float),
+        ("w_fwd", ctypes.c_void_p), ("w_bwd", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+    ]
+
+
+class Generator(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", ctypes.c_int), ("nz", ctypes.c_int),
+        ("nc", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+        ("layers", Layer * MAX_LAYERS),
+    ]
+
+
+class Ebm(ctypes.Structure):
+    _fields_ = [
+        ("nz", ctypes.c_int), ("nh", ctypes.c_int), ("slope", ctypes.c_float),
+        ("w1", ctypes.c_void_p), ("b1", ctypes.c_void_p), ("w2", ctypes.c_void_p),
+        ("b2", ctypes.c_void_p), ("w3", ctypes.c_void_p), ("b3", ctypes.c_void_p),
+        ("w1t", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
+    ]
+
+
+class CsqBlock(ctypes.Structure):
+    _fields_ = [
+        ("din", ctypes.c_int), ("dout", ctypes.c_int),
+        ("wl", ctypes.c_void_p), ("bl", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("bs", ctypes.c_void_p),
+        ("wg", ctypes.c_void_p), ("bg", ctypes.c_void_p), ("wb", ctypes.c_void_p),
+        ("px", ctypes.c_void_p), ("qt", ctypes.c_void_p),
+    ]
+
+
+class Denoiser(ctypes.Structure):
+    _fields_ = [
+        ("nz", ctypes.c_int), ("nblocks", ctypes.c_int), ("residual", ctypes.c_int),
+        ("bmat", ctypes.c_void_p),
+        ("blocks", CsqBlock * 7),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_U64 = ctypes.c_uint64
+_SZ = ctypes.c_size_t
+
+_SIGS = {
+    "damc_abi_version": (_I, []),
+    "damc_error_string": (ctypes.c_char_p, [_I]),
+    "damc_generator_layer_packed_sizes": (_I, [ctypes.POINTER(Layer), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "damc_pack_generator_layer": (_I, [ctypes.POINTER(Layer), _P, _P, _P, _P]),
+    "damc_pack_ebm": (_I, [ctypes.POINTER(Ebm), _P, _P, _P]),
+    "damc_posterior_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
+    "damc_posterior_langevin": (_I, [ctypes.POINTER(Generator), ctypes.POINTER(Ebm), _P, _P, _I, _I, _F, _F, _I, _P,
+                                     _U64, _U64, _U64, _P, _P, _SZ, _P]),
+    "damc_likelihood_grad": (_I, [ctypes.POINTER(Generator), _P, _P, _I, _F, _P, _P, _SZ, _P]),
+    "damc_generator_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
+    "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P, _P]),
+    "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
+    "damc_z_update": (_I, [_P, _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P]),
+    "damc_philox_normal": (_I, [_P, _I, _I, _I, _U64, _U64, _U64, ctypes.c_uint32, _P]),
+    "damc_conv2d_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "damc_pack_conv2d": (_I, [_P, _I, _I, _I, _P, _P]),
+    "damc_instnorm_workspace_floats": (_SZ, [_I, _I, _I]),
+    "damc_instnorm_lrelu_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P]),
+    "damc_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _P, _P]),
+    "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
+    "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I]),
+    "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _I, _I, _P, _I, _P, _U64, _U64, _P, _I, _P, _SZ, _P]),
+    "damc_prof_enable": (_I, [_I]),
+    "damc_prof_reset": (_I, []),
+    "damc_prof_query": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),
+                             ctypes.POINTER(ctypes.c_double)]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+class DamcError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libdamc.so (raises if it was not built — there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DamcError(
+                "libdamc.so not found at %s: build it with `make -C diffusion-amortized-mcmc_amd/csrc` "
+                "(or __graft_entry__.build()); the HIP path has no fallback" % LIB_PATH)
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.damc_abi_version() != 1:
+            raise DamcError("libdamc ABI mismatch")
+        _lib = handle
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().damc_error_string(rc).decode()
+        raise DamcError("%s failed: %s (code %d)" % (what or "damc call", msg, rc))
+    return rc
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,139 @@
+"""Tensor-level Langevin API over libdamc (the functions behind src/MCMC.py).
+
+All functions run on the caller's current HIP stream, never synchronise the host (unless a
+diagnostics tensor is read by the caller), and update ``z`` in place.
+
+Noise: ``noise=None`` with ``with_noise`` draws xi in-kernel (Philox4x32-10) keyed by ``seed``
+and the chain's GLOBAL index ``chain_base + row`` and step ``step_offset + i``; passing
+``noise`` (n_steps, B, nz) injects values instead (parity tests).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+from .plans import ebm_plan, generator_plan
+
+
+def _f32c(t, name):
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise _lib.DamcError("%s must be a contiguous float32 tensor" % name)
+    if t.device.type != "cuda":
+        raise _lib.DamcError("%s must be on a ROCm device (got %s); the HIP path has no CPU fallback" % (name, t.device))
+    return t
+
+
+def new_seed():
+    """A Philox key drawn from torch's (seeded) CPU generator."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def posterior_langevin(z, x, netG, netE, n_steps, sigma, step, with_noise, noise=None, seed=None,
+                       step_offset=0, chain_base=0, diag=False):
+    """In-place n-step posterior Langevin (workspace/src/MCMC.py:48-74) on z (B, nz).
+
+    Returns a (n_steps, 4) diagnostics tensor {sum E, lik, |z|^2/2, mean grad} if diag else None.
+    """
+    _f32c(z, "z")
+    dev = z.device
+    x = x.to(device=dev, dtype=torch.float32).contiguous()
+    B = z.shape[0]
+    gp = generator_plan(netG)
+    if z.shape[1] != gp.nz or x.shape[0] != B or x.numel() != B * gp.nc * gp.h * gp.w:
+        raise _lib.DamcError("shape mismatch: z %s x %s for generator nz=%d out=(%d,%d,%d)"
+                             % (tuple(z.shape), tuple(x.shape), gp.nz, gp.nc, gp.h, gp.w))
+    gdesc = gp.refresh(dev)
+    edesc = ebm_plan(netE).refresh(dev) if netE is not None else None
+    ws, nbytes = gp.workspace(B)
+    if noise is not None:
+        noise = _f32c(noise.to(dev), "noise")
+        if noise.numel() < n_steps * B * gp.nz:
+            raise _lib.DamcError("noise must hold (n_steps, B, nz) values")
+    if seed is None:
+        seed = new_seed() if (with_noise and noise is None) else 0
+    dg = torch.zeros(max(n_steps, 1), 4, dtype=torch.float32, device=dev) if diag else None
+    check(_lib.lib().damc_posterior_langevin(
+        ctypes.byref(gdesc), ctypes.byref(edesc) if edesc is not None else None, ptr(z), ptr(x), B, int(n_steps),
+        float(sigma), float(step), int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base,
+        ptr(dg), ptr(ws), nbytes, _lib.stream_ptr(dev)), "damc_posterior_langevin")
+    return dg
+
+
+def likelihood_grad(z, x, netG, sigma):
+    """grad_z |G(z)-x|^2/(2 sigma^2) (per-op hook)."""
+    _f32c(z, "z")
+    dev = z.device
+    x = x.to(device=dev, dtype=torch.float32).contiguous()
+    gp = generator_plan(netG)
+    gdesc = gp.refresh(dev)
+    ws, nbytes = gp.workspace(z.shape[0])
+    g = torch.empty_like(z)
+    check(_lib.lib().damc_likelihood_grad(ctypes.byref(gdesc), ptr(z), ptr(x), z.shape[0], float(sigma), ptr(g),
+                                          ptr(ws), nbytes, _lib.stream_ptr(dev)), "damc_likelihood_grad")
+    return g
+
+
+def generator_forward(z, netG):
+    """x_hat = G(z) on the HIP path (NCHW, or (B, out) for MLP generators)."""
+    z = _f32c(z.detach().contiguous() if not z.is_contiguous() else z.detach(), "z")
+    dev = z.device
+    gp = generator_plan(netG)
+    gdesc = gp.refresh(dev)
+    ws, nbytes = gp.workspace(z.shape[0])
+    shape = (z.shape[0], gp.nc, gp.h, gp.w) if gp.is_conv else (z.shape[0], gp.nc)
+    out = torch.empty(shape, dtype=torch.float32, device=dev)
+    check(_lib.lib().damc_generator_forward(ctypes.byref(gdesc), ptr(z), z.shape[0], ptr(out), ptr(ws), nbytes,
+                                            _lib.stream_ptr(dev)), "damc_generator_forward")
+    return out
+
+
+def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, step_offset=0, chain_base=0,
+                   diag=False):
+    """In-place n-step prior Langevin (workspace/src/MCMC.py:27-46), one persistent launch.
+
+    Returns a (n_steps, 2) diagnostics tensor {sum E, |z|^2/2} if diag else None.
+    """
+    _f32c(z, "z")
+    dev = z.device
+    ep = ebm_plan(netE)
+    if z.shape[1] != ep.nz:
+        raise _lib.DamcError("z has %d dims, EBM expects %d" % (z.shape[1], ep.nz))
+    edesc = ep.refresh(dev)
+    B = z.shape[0]
+    if noise is not None:
+        noise = _f32c(noise.to(dev), "noise")
+    if seed is None:
+        seed = new_seed() if (with_noise and noise is None) else 0
+    dg = torch.zeros(max(n_steps, 1), 2, dtype=torch.float32, device=dev) if diag else None
+    check(_lib.lib().damc_prior_langevin(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
+                                         int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base, ptr(dg),
+                                         _lib.stream_ptr(dev)), "damc_prior_langevin")
+    return dg
+
+
+def ebm_energy_grad(z, netE):
+    _f32c(z, "z")
+    dev = z.device
+    edesc = ebm_plan(netE).refresh(dev)
+    e = torch.empty(z.shape[0], dtype=torch.float32, device=dev)
+    g = torch.empty_like(z)
+    check(_lib.lib().damc_ebm_energy_grad(ctypes.byref(edesc), ptr(z), z.shape[0], ptr(e), ptr(g),
+                                          _lib.stream_ptr(dev)), "damc_ebm_energy_grad")
+    return e, g
+
+
+def philox_normal(n_steps, batch, nz, seed, device, step_offset=0, chain_base=0, stream_id=0x51):
+    out = torch.empty(n_steps, batch, nz, dtype=torch.float32, device=device)
+    check(_lib.lib().damc_philox_normal(ptr(out), n_steps, batch, nz, seed, step_offset, chain_base, stream_id,
+                                        _lib.stream_ptr(device)), "damc_philox_normal")
+    return out
+
+
+def z_update(z, g, step, with_noise, noise=None, seed=0, step_index=0, chain_base=0):
+    _f32c(z, "z")
+    _f32c(g, "g")
+    check(_lib.lib().damc_z_update(ptr(z), ptr(g), z.shape[0], z.shape[1], float(step), int(bool(with_noise)),
+                                   ptr(noise), seed, step_index, chain_base, _lib.stream_ptr(z.device)),
+          "damc_z_update")
+    return z

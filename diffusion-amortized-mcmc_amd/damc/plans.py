@@ -1,0 +1,223 @@
+"""Device plans: turn the reference's nn.Modules into packed descriptors for libdamc.
+
+A plan reads the module structure once (layer kinds, shapes, activations) and, on every
+call, re-packs the live parameters into device buffers it owns (the nets are trained
+between Langevin calls, and EMA copies update through ``.data``, so nothing is cached
+across calls except the buffers themselves).
+
+Generator structure: ``_netG_*.gen`` = [ConvTranspose2d, LeakyReLU(.2)]* ConvTranspose2d, Tanh
+(workspace/src/diffusion_net.py:20-203), or the toy MLP ``G.net`` = [Linear, ReLU]* Linear
+(workspace/toy_example/toy_example.py:22-47).
+EBM structure: ``_netE.ebm`` = Linear, LeakyReLU(.2), Linear, LeakyReLU(.2), Linear
+(workspace/src/diffusion_net.py:207-223).
+"""
+import ctypes
+import weakref
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _act_of(mod):
+    if isinstance(mod, torch.nn.LeakyReLU):
+        return _lib.ACT_LRELU, float(mod.negative_slope)
+    if isinstance(mod, torch.nn.ReLU):
+        return _lib.ACT_LRELU, 0.0
+    if isinstance(mod, torch.nn.Tanh):
+        return _lib.ACT_TANH, 0.0
+    raise NotImplementedError("unsupported activation %r" % (mod,))
+
+
+def _require_plain_param(m):
+    if hasattr(m, "weight_orig"):
+        raise NotImplementedError("spectral-norm generators (use_spc_norm=True) are not supported by the HIP path")
+
+
+class GeneratorPlan:
+    """Packed generator for damc_posterior_langevin / damc_generator_forward."""
+
+    def __init__(self, G):
+        seq = G.gen if hasattr(G, "gen") else G.net
+        mods = list(seq)
+        specs = []  # (module, act, slope)
+        for m in mods:
+            if isinstance(m, (torch.nn.ConvTranspose2d, torch.nn.Linear)):
+                _require_plain_param(m)
+                specs.append([m, _lib.ACT_NONE, 0.0])
+            else:
+                if not specs:
+                    raise NotImplementedError("activation before the first layer")
+                specs[-1][1], specs[-1][2] = _act_of(m)
+        if not specs or len(specs) > _lib.MAX_LAYERS:
+            raise NotImplementedError("generator with %d layers" % len(specs))
+        self.modules = [s[0] for s in specs]
+        first = self.modules[0]
+        self.nz = first.in_channels if isinstance(first, torch.nn.ConvTranspose2d) else first.in_features
+        layers = []
+        h = 1
+        for i, (m, act, slope) in enumerate(specs):
+            last = i == len(specs) - 1
+            L = dict(act=act, slope=slope)
+            if isinstance(m, torch.nn.Linear):
+                L.update(kind=_lib.LAYER_LINEAR, cin=m.in_features, cout=m.out_features, k=1, stride=1, pad=0,
+                         hin=1, hout=1)
+            else:
+                k, s, p = m.kernel_size[0], m.stride[0], m.padding[0]
+                if m.kernel_size[0] != m.kernel_size[1] or m.stride[0] != m.stride[1] or m.padding[0] != m.padding[1]:
+                    raise NotImplementedError("non-square ConvTranspose2d")
+                if m.output_padding != (0, 0) or m.dilation != (1, 1) or m.groups != 1:
+                    raise NotImplementedError("ConvTranspose2d with output_padding/dilation/groups")
+                hout = (h - 1) * s - 2 * p + k
+                if i == 0:
+                    kind = _lib.LAYER_PROJ
+                elif last:
+                    kind = _lib.LAYER_SMALLC
+                else:
+                    kind = _lib.LAYER_UP2
+                L.update(kind=kind, cin=m.in_channels, cout=m.out_channels, k=k, stride=s, pad=p, hin=h, hout=hout)
+                h = hout
+            layers.append(L)
+        self.layers = layers
+        self.is_conv = layers[0]["kind"] != _lib.LAYER_LINEAR
+        last = layers[-1]
+        self.nc = last["cout"]
+        self.h = self.w = last["hout"]
+        self.device = None
+        self.buffers = None
+        self.desc = None
+
+    # --------------------------------------------------------------------------------
+    def _alloc(self, device):
+        L = _lib.lib()
+        self.device = device
+        self.buffers = []
+        desc = _lib.Generator()
+        desc.n_layers = len(self.layers)
+        desc.nz = self.nz
+        desc.nc, desc.h, desc.w = self.nc, self.h, self.w
+        for i, spec in enumerate(self.layers):
+            d = desc.layers[i]
+            d.kind = spec["kind"]
+            d.cin, d.cout, d.k = spec["cin"], spec["cout"], spec["k"]
+            d.stride, d.pad = spec["stride"], spec["pad"]
+            d.hin = d.win = spec["hin"]
+            d.hout = d.wout = spec["hout"]
+            d.act, d.slope = spec["act"], spec["slope"]
+            fwd, bwd = ctypes.c_size_t(), ctypes.c_size_t()
+            check(L.damc_generator_layer_packed_sizes(ctypes.byref(d), ctypes.byref(fwd), ctypes.byref(bwd)),
+                  "packed sizes")
+            wf = torch.empty(max(int(fwd.value), 1), dtype=torch.float32, device=device)
+            wb = torch.empty(max(int(bwd.value), 1), dtype=torch.float32, device=device)
+            self.buffers.append((wf, wb))
+            d.w_fwd = wf.data_ptr()
+            d.w_bwd = wb.data_ptr() if bwd.value else None
+        self.desc = desc
+
+    def refresh(self, device):
+        """(Re)pack the live parameters; returns the ctypes descriptor."""
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise _lib.DamcError("the HIP generator path needs CUDA (ROCm) tensors, got %s" % device)
+        if self.device != device or self.desc is None:
+            self._alloc(device)
+        L = _lib.lib()
+        stream = _lib.stream_ptr(device)
+        self._keep = []
+        for i, m in enumerate(self.modules):
+            w = m.weight.detach()
+            if w.device != device or w.dtype != torch.float32 or not w.is_contiguous():
+                w = w.to(device=device, dtype=torch.float32).contiguous()
+                self._keep.append(w)
+            wf, wb = self.buffers[i]
+            d = self.desc.layers[i]
+            check(L.damc_pack_generator_layer(ctypes.byref(d), ptr(w), ptr(wf),
+                                              ptr(wb) if d.w_bwd else None, stream), "pack generator layer")
+            if m.bias is not None:
+                b = m.bias.detach()
+                if b.device != device or b.dtype != torch.float32:
+                    b = b.to(device=device, dtype=torch.float32).contiguous()
+                    self._keep.append(b)
+                d.bias = b.data_ptr()
+            else:
+                d.bias = None
+        return self.desc
+
+    def workspace(self, batch):
+        L = _lib.lib()
+        nbytes = int(L.damc_posterior_workspace_bytes(ctypes.byref(self.desc), int(batch)))
+        if nbytes == 0:
+            raise _lib.DamcError("unsupported generator configuration for the HIP path")
+        key = (int(batch), str(self.device))
+        ws = getattr(self, "_ws", None)
+        if ws is None or ws[0] != key or ws[1].numel() < nbytes:
+            self._ws = (key, torch.empty(nbytes, dtype=torch.uint8, device=self.device))
+        return self._ws[1], nbytes
+
+
+class EbmPlan:
+    """_netE parameters + packed transposes."""
+
+    def __init__(self, E):
+        lin = [m for m in E.ebm if isinstance(m, torch.nn.Linear)]
+        acts = [m for m in E.ebm if not isinstance(m, torch.nn.Linear)]
+        if len(lin) != 3 or len(acts) != 2 or lin[2].out_features != 1:
+            raise NotImplementedError("unexpected _netE structure")
+        for m in lin:
+            _require_plain_param(m)
+        slopes = {float(a.negative_slope) for a in acts if isinstance(a, torch.nn.LeakyReLU)}
+        if len(slopes) != 1:
+            raise NotImplementedError("_netE activations must be LeakyReLU with one slope")
+        self.slope = slopes.pop()
+        self.lin = lin
+        self.nz, self.nh = lin[0].in_features, lin[0].out_features
+        self.device = None
+
+    def refresh(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise _lib.DamcError("the HIP EBM path needs CUDA (ROCm) tensors, got %s" % device)
+        self._keep = []
+
+        def dev(t):
+            t = t.detach()
+            if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(device=device, dtype=torch.float32).contiguous()
+                self._keep.append(t)
+            return t
+
+        (w1, b1), (w2, b2), (w3, b3) = [(dev(m.weight), dev(m.bias)) for m in self.lin]
+        if self.device != device:
+            self.w1t = torch.empty(self.nz * self.nh, dtype=torch.float32, device=device)
+            self.w2t = torch.empty(self.nh * self.nh, dtype=torch.float32, device=device)
+            self.device = device
+        d = _lib.Ebm()
+        d.nz, d.nh, d.slope = self.nz, self.nh, self.slope
+        d.w1, d.b1, d.w2, d.b2, d.w3, d.b3 = [t.data_ptr() for t in (w1, b1, w2, b2, w3, b3)]
+        d.w1t, d.w2t = self.w1t.data_ptr(), self.w2t.data_ptr()
+        self._params = (w1, b1, w2, b2, w3, b3)
+        check(_lib.lib().damc_pack_ebm(ctypes.byref(d), ptr(self.w1t), ptr(self.w2t), _lib.stream_ptr(device)),
+              "pack ebm")
+        self.desc = d
+        return d
+
+
+_GEN_PLANS = weakref.WeakKeyDictionary()
+_EBM_PLANS = weakref.WeakKeyDictionary()
+
+
+def generator_plan(G):
+    p = _GEN_PLANS.get(G)
+    if p is None:
+        p = GeneratorPlan(G)
+        _GEN_PLANS[G] = p
+    return p
+
+
+def ebm_plan(E):
+    p = _EBM_PLANS.get(E)
+    if p is None:
+        p = EbmPlan(E)
+        _EBM_PLANS[E] = p
+    return p

@@ -1,0 +1,188 @@
+/*
+ * damc.h — C ABI of libdamc.so, the MI355X (gfx950) diffusion-amortized Langevin inner loop.
+ *
+ * The reference (yuPeiyu98/Diffusion-Amortized-MCMC) has no native/FFI layer: its hot path is
+ * the Python call surface of workspace/src/MCMC.py and workspace/src/diffusion_net.py.  Each
+ * entry point below replaces the device work behind one of those Python functions; the
+ * Python mirror (diffusion-amortized-mcmc_amd/damc, bound with ctypes)
+ * keeps the reference's names and signatures.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer to caller-owned fp32 memory unless noted;
+ *   - images are NCHW exactly as the caller holds them; latents z are (B, nz) row-major;
+ *   - weights are passed once per call to damc_pack_* in PyTorch layouts and re-laid out
+ *     into caller-allocated packed buffers (no allocation inside the library);
+ *   - `stream` is a hipStream_t passed as void*; no host synchronisation happens inside
+ *     any call (everything is stream-ordered and graph-capturable);
+ *   - return 0 on success, otherwise a hipError_t value or one of DAMC_ERR_* (the Python
+ *     side raises RuntimeError with damc_error_string()).
+ *   - noise: with_noise != 0 and noise == NULL draws xi ~ N(0,1) in-kernel from
+ *     Philox4x32-10 keyed by (seed) with counter (dim/4, step + step_offset,
+ *     chain_base + chain, stream_id): a chain's noise depends on its GLOBAL index only, so
+ *     results are identical for any sharding of the batch over GPUs.  noise != NULL
+ *     injects (n_steps, B, nz) values instead (parity tests).
+ */
+#ifndef DAMC_H
+#define DAMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAMC_ABI_VERSION 1
+#define DAMC_MAX_LAYERS 10
+
+enum {
+  DAMC_OK = 0,
+  DAMC_ERR_ARG = 1001,       /* invalid shape / argument */
+  DAMC_ERR_WORKSPACE = 1002, /* workspace too small */
+  DAMC_ERR_UNSUPPORTED = 1003
+};
+
+/* Generator layer kinds (workspace/src/diffusion_net.py:20-203, toy_example.py:22-47) */
+enum {
+  DAMC_LAYER_PROJ = 1,   /* ConvTranspose2d on a 1x1 input (first layer): a GEMM z·W        */
+  DAMC_LAYER_UP2 = 2,    /* ConvTranspose2d k4 s2 p1 with Cout >= 8: phase-split implicit GEMM */
+  DAMC_LAYER_SMALLC = 3, /* last ConvTranspose2d with Cout <= 4 (to RGB / gray)             */
+  DAMC_LAYER_LINEAR = 4  /* nn.Linear (toy MLP generator)                                  */
+};
+enum { DAMC_ACT_NONE = 0, DAMC_ACT_LRELU = 1, DAMC_ACT_TANH = 2 };
+
+typedef struct {
+  int kind;
+  int cin, cout, k, stride, pad;
+  int hin, win, hout, wout;  /* spatial sizes (1 for PROJ input / LINEAR)                 */
+  int act;                   /* activation after this layer                               */
+  float slope;               /* LeakyReLU slope (ReLU = 0)                                */
+  const float* w_fwd;        /* packed forward weights  (damc_pack_generator_layer)       */
+  const float* w_bwd;        /* packed dgrad weights                                      */
+  const float* bias;         /* (cout) or NULL                                            */
+} damc_layer_t;
+
+typedef struct {
+  int n_layers;
+  int nz;                     /* latent size                                               */
+  int nc, h, w;               /* image shape (for LINEAR generators: nc = out features, h = w = 1) */
+  damc_layer_t layers[DAMC_MAX_LAYERS];
+} damc_generator_t;
+
+/* Latent EBM _netE: Linear(nz,nh) LReLU Linear(nh,nh) LReLU Linear(nh,1) (diffusion_net.py:207-223) */
+typedef struct {
+  int nz, nh;
+  float slope;
+  const float *w1, *b1, *w2, *b2, *w3, *b3;  /* PyTorch layouts: w1 (nh,nz), w2 (nh,nh), w3 (1,nh) */
+  const float *w1t, *w2t;                     /* packed transposes (damc_pack_ebm)                  */
+} damc_ebm_t;
+
+/* ---------------------------------------------------------------- library / packing */
+int damc_abi_version(void);
+const char* damc_error_string(int code);
+
+/* floats needed by the packed forward / dgrad buffers of one generator layer */
+int damc_generator_layer_packed_sizes(const damc_layer_t* layer, size_t* fwd_floats, size_t* bwd_floats);
+/* re-lay PyTorch weight (ConvT: (Cin,Cout,k,k); Linear: (out,in)) into layer->w_fwd / w_bwd */
+int damc_pack_generator_layer(const damc_layer_t* layer, const float* w_torch, float* w_fwd, float* w_bwd,
+                              void* stream);
+/* w1t (nz,nh) and w2t (nh,nh) from the PyTorch w1/w2 */
+int damc_pack_ebm(const damc_ebm_t* ebm, float* w1t, float* w2t, void* stream);
+
+/* ------------------------------------------------------------- posterior Langevin (a1) */
+/* workspace bytes for damc_posterior_langevin / damc_likelihood_grad / damc_generator_forward */
+size_t damc_posterior_workspace_bytes(const damc_generator_t* g, int batch);
+
+/* sample_langevin_post_z_with_prior (workspace/src/MCMC.py:48-74):
+ *   for i < n_steps:  z <- z - 0.5*step^2 * grad U(z) (+ step*xi),
+ *   U = |G(z)-x|^2/(2 sigma^2) + sum E(z) + |z|^2/2     (E omitted when ebm == NULL)
+ * z (B,nz) updated in place; x (B,nc,h,w) NCHW; diag (optional, n_steps*4 floats, zeroed by
+ * the call): per step {sum E, |G(z)-x|^2/(2sigma^2), |z|^2/2, mean(grad)} before the update. */
+int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
+                            int batch, int n_steps, float sigma, float step, int with_noise,
+                            const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                            float* diag, void* workspace, size_t workspace_bytes, void* stream);
+
+/* per-op hooks (parity tests): grad_z |G(z)-x|^2/(2 sigma^2) -> grad (B,nz) */
+int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int batch, float sigma,
+                         float* grad, void* workspace, size_t workspace_bytes, void* stream);
+/* x_hat = G(z) (B,nc,h,w) NCHW — gen_samples / gen_samples_with_diffusion_prior (MCMC.py:119-150) */
+int damc_generator_forward(const damc_generator_t* g, const float* z, int batch, float* x_hat,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
+/* ----------------------------------------------------------------- prior Langevin (a2) */
+/* sample_langevin_prior_z (MCMC.py:27-46): all n_steps in ONE persistent launch.
+ * diag (optional, n_steps*2 floats): {sum E, |z|^2/2} per step before the update. */
+int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps, float step, int with_noise,
+                        const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                        float* diag, void* stream);
+/* per-op hook: energy (B) and grad_z sum E (B,nz) */
+int damc_ebm_energy_grad(const damc_ebm_t* ebm, const float* z, int batch, float* energy, float* grad,
+                         void* stream);
+/* per-op hook: z <- z - 0.5 step^2 (g + z) (+ step xi) ; g (B,nz) */
+int damc_z_update(float* z, const float* g, int batch, int nz, float step, int with_noise, const float* noise,
+                  uint64_t seed, uint64_t step_index, uint64_t chain_base, void* stream);
+/* Philox N(0,1) draw used by every Langevin kernel (statistical tests) -> out (n_steps,B,nz) */
+int damc_philox_normal(float* out, int n_steps, int batch, int nz, uint64_t seed, uint64_t step_offset,
+                       uint64_t chain_base, uint32_t stream_id, void* stream);
+
+/* ---------------------------------------------------------------- Q amortizer (a8-a11) */
+/* generic fp32 MFMA implicit-GEMM conv (NHWC) + bias: encoder building block */
+int damc_conv2d_nhwc(const float* x, int batch, int hin, int win, int cin, const float* w_packed, const float* bias,
+                     int cout, int k, int stride, int pad, float* y, void* stream);
+/* pack Conv2d weight (Cout,Cin,k,k) -> (k,k,Cin,Cout) */
+int damc_pack_conv2d(const float* w_torch, int cout, int cin, int k, float* w_packed, void* stream);
+/* InstanceNorm2d(affine, eps) + LeakyReLU(slope), in place on NHWC (Welford partials merged with
+ * Chan's formula); workspace: damc_instnorm_workspace_floats() floats */
+size_t damc_instnorm_workspace_floats(int batch, int hw, int c);
+int damc_instnorm_lrelu_nhwc(float* y, int batch, int hw, int c, const float* gamma, const float* beta, float eps,
+                             float slope, float* workspace, void* stream);
+/* NCHW -> NHWC transpose (encoder input) */
+int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* stream);
+
+/* Dense fp32 MFMA GEMM: C(M,N) = act(A(M,K) · B(K,N) + bias) with B row-major (K,N) */
+int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc, int m,
+              int n, int k, int act, float slope, void* stream);
+
+/* Denoiser (Diffusion_UnetA, diffusion_net.py:417-533) reverse sweep (diffusion_net.py:595-622).
+ * Blocks are described by packed weights; see damc/amortizer.py for the packing order. */
+typedef struct {
+  int din, dout;
+  const float* wl;  /* _layer.0:      (din,dout) packed = W^T  */
+  const float* bl;  /*                (dout)                   */
+  const float* ws;  /* _skip:         (din,dout)               */
+  const float* bs;
+  const float* wg;  /* _hyper_gate:   (dout,dout) packed W^T   */
+  const float* bg;
+  const float* wb;  /* _hyper_bias:   (dout,dout) packed W^T   */
+  const float* px;  /* per-row xemb part of the ctx Linear (B,dout)  [step-invariant]       */
+  const float* qt;  /* per-step temb part of the ctx Linear (+bias) (n_steps,dout)         */
+} damc_csq_block_t;
+
+typedef struct {
+  int nz, nblocks;            /* 7 for Diffusion_UnetA                                      */
+  int residual;               /* diffusion_residual                                         */
+  const float* bmat;          /* p.B (nz, nz/2)                                             */
+  damc_csq_block_t blocks[7]; /* in0 in1 in2 mid0 out0 out1 out2                            */
+} damc_denoiser_t;
+
+/* per reverse step i (index k = n_interval-1-i): coefficients precomputed on the host from the
+ * fp32 logsnr schedule (diffusion_helper_func.py:36-70):
+ *   coef[k*6 + {0..5}] = {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std, is_last} */
+size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch);
+int damc_reverse_sweep(const damc_denoiser_t* d, float* zt, int batch, int n_steps, const float* coef,
+                       int with_noise, const float* noise, uint64_t seed, uint64_t chain_base, float* eps_log,
+                       int eps_log_steps, void* workspace, size_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------------------- profiling */
+/* optional per-kernel HIP-event timing (bench.py roofline): records events around each
+ * launch of the named kernel class on the launch stream; read back after a sync. */
+int damc_prof_enable(int on);
+int damc_prof_reset(void);
+/* total ms and launch count for kernel class `name` ("upconv_fwd", "upconv_dgrad", ...) */
+int damc_prof_query(const char* name, double* total_ms, long* launches, double* flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DAMC_H */

@@ -1,0 +1,105 @@
+"""pytest configuration.
+
+Markers: ``gpu`` — needs a ROCm device and libdamc.so (run on the MI355X box with -m gpu).
+
+Golden fixtures (tests/golden/*.npz) were captured from the REFERENCE implementation by
+tests/golden/make_golden.py (build container only).  Inputs are regenerated here from the
+counter-hash recipe (damc.synth) with the seeds below, which the capture script used too.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "diffusion-amortized-mcmc_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+# seeds shared with tests/golden/make_golden.py
+SEED_G, SEED_E, SEED_Q = 0, 10, 20
+SEED_X, SEED_Z0, SEED_POST, SEED_PRIOR, SEED_PRIOR_INIT, SEED_QN = 1, 2, 3, 4, 5, 6
+
+G_NAMES = ["svhn_w16", "cifar10_w16", "celeba64_w16", "celebaHQ_w8", "mnist_w16", "cifar10_full"]
+Q_NAMES = ["q_cifar10_s", "q_cifar10_small", "q_svhn_s", "q_celeba64_s", "q_celebaHQ_s", "q_mnist_s",
+           "q_cifar10_full"]
+# End-point tolerance (rel-L2) of a full reverse sweep: 2x the reference's own fp32 rounding spread,
+# measured as |fp64 oracle - reference golden| per case (n_interval 10-20 sweeps amplify rounding
+# through sqrt(1+e^-l) every step; 100-step 'large' sweeps are far better conditioned).
+Q_END_TOL = {"q_cifar10_s": 2e-2, "q_cifar10_small": 1.6e-1, "q_svhn_s": 5e-3, "q_celeba64_s": 1.1e-1,
+             "q_celebaHQ_s": 1.1e-1, "q_mnist_s": 1e-1, "q_cifar10_full": 2e-2}
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm) device and libdamc.so")
+
+
+def load_golden(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    meta = json.loads(str(d["meta"]))
+    return {k: d[k] for k in d.files if k != "meta"}, meta
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def build_g_case(name, device="cpu"):
+    """Nets + inputs of a golden generator case (drop-in classes, counter-hash weights)."""
+    import torch
+
+    from damc import synth
+    from src import diffusion_net as dn
+
+    rec, meta = load_golden(name)
+    G = getattr(dn, meta["ctor"])(nz=meta["nz"], ngf=meta["ngf"], nc=meta["nc"])
+    E = dn._netE(nz=meta["nz"])
+    synth.load_into(G, SEED_G)
+    synth.load_into(E, SEED_E)
+    G.to(device).eval()
+    E.to(device).eval()
+    B, nz, nc, H = meta["B"], meta["nz"], meta["nc"], meta["H"]
+    x = torch.from_numpy(synth.uniform_f32(SEED_X, 0, (B, nc, H, H))).to(device)
+    z0 = torch.from_numpy(synth.normal_f32(SEED_Z0, 0, (B, nz))).to(device)
+    post_noise = torch.from_numpy(np.stack([synth.normal_f32(SEED_POST, 100 + i, (B, nz)) for i in range(30)]))
+    zp0 = torch.from_numpy(np.concatenate([z0.cpu().numpy(), synth.normal_f32(SEED_PRIOR_INIT, 0, (B, nz))], 0))
+    prior_noise = torch.from_numpy(np.stack([synth.normal_f32(SEED_PRIOR, 100 + i, (2 * B, nz)) for i in range(60)]))
+    return dict(G=G, E=E, x=x, z0=z0, post_noise=post_noise.to(device), zp0=zp0.to(device),
+                prior_noise=prior_noise.to(device), rec=rec, meta=meta)
+
+
+def build_q_case(name, device="cpu"):
+    import torch
+
+    from damc import synth
+    from src import diffusion_net as dn
+
+    rec, meta = load_golden(name)
+    Q = dn._netQ_U(nc=meta["nc"], nz=meta["nz"], nxemb=meta["nxemb"], ntemb=meta["ntemb"], nif=meta["nif"],
+                   diffusion_residual=True, n_interval=meta["n_interval"], logsnr_min=meta["logsnr_min"],
+                   logsnr_max=meta["logsnr_max"], var_type=meta["var_type"], with_noise=True, cond_w=0.0,
+                   net_arch="A", dataset=meta["dataset"])
+    synth.load_into(Q, SEED_Q)
+    Q.to(device).eval()
+    B, nz, nc, H, n = meta["B"], meta["nz"], meta["nc"], meta["H"], meta["n_interval"]
+    x = torch.from_numpy(synth.uniform_f32(SEED_X, 0, (B, nc, H, H))).to(device)
+    zt0 = torch.from_numpy(synth.normal_f32(SEED_QN, 0, (B, nz))).to(device)
+    pe_noise = torch.from_numpy(synth.normal_f32(SEED_QN, 1, (B, nz))).to(device)
+    eps = torch.from_numpy(np.stack([synth.normal_f32(SEED_QN, 100 + i, (B, nz)) for i in range(max(n - 1, 1))]))
+    return dict(Q=Q, x=x, zt0=zt0, pe_noise=pe_noise, eps=eps.to(device), rec=rec, meta=meta)
+
+
+@pytest.fixture(scope="session")
+def gpu_device():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")

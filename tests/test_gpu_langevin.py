@@ -1,0 +1,194 @@
+"""GPU parity: the HIP Langevin path (libdamc via damc.langevin / src.MCMC) vs the reference's
+golden vectors and the oracle.
+
+Tolerances (fp32; SURVEY.md §4, ~4x the reference's own fp32-vs-fp64 / thread-count spread):
+  gradients rel-L2 <= 1e-5;  1 posterior step rel-L2(z) <= 1e-6;  10 no-noise steps <= 2e-4;
+  30 steps (injected noise) <= 2e-3;  recon MSE rel <= 1e-5;  60 prior steps <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import G_NAMES, build_g_case, load_golden, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lv(gpu_device):
+    from damc import langevin
+
+    return langevin
+
+
+@pytest.mark.parametrize("name", G_NAMES)
+def test_generator_forward(lv, gpu_device, name):
+    c = build_g_case(name, gpu_device)
+    xh = lv.generator_forward(c["z0"], c["G"]).cpu().numpy()
+    if "gen_x" in c["rec"]:
+        assert rel_l2(xh, c["rec"]["gen_x"]) < 1e-5
+    else:
+        assert rel_l2(xh[:, :, ::4, ::4], c["rec"]["gen_x_sub4"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", G_NAMES)
+def test_likelihood_and_ebm_gradients(lv, gpu_device, name):
+    c = build_g_case(name, gpu_device)
+    g = lv.likelihood_grad(c["z0"], c["x"], c["G"], c["meta"]["sigma"]).cpu().numpy()
+    assert rel_l2(g, c["rec"]["lik_grad0"]) < 1e-5
+    e, ge = lv.ebm_energy_grad(c["z0"], c["E"])
+    assert rel_l2(e.cpu().numpy(), c["rec"]["ebm_e"]) < 1e-5
+    assert rel_l2(ge.cpu().numpy(), c["rec"]["ebm_grad0"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", G_NAMES)
+def test_posterior_langevin_matches_reference(lv, gpu_device, name):
+    c = build_g_case(name, gpu_device)
+    m, rec = c["meta"], c["rec"]
+    z = c["z0"].clone()
+    lv.posterior_langevin(z, c["x"], c["G"], c["E"], 1, m["sigma"], m["step"], False)
+    assert rel_l2(z.cpu().numpy(), rec["post_z1"]) < 1e-6
+    z = c["z0"].clone()
+    lv.posterior_langevin(z, c["x"], c["G"], c["E"], 10, m["sigma"], m["step"], False)
+    assert rel_l2(z.cpu().numpy(), rec["post_z10"]) < 2e-4
+    mse = ((lv.generator_forward(z, c["G"]) - c["x"]) ** 2).mean(dim=(1, 2, 3)).cpu().numpy()
+    assert np.max(np.abs(mse - rec["recon_mse10"]) / rec["recon_mse10"]) < 1e-5
+    z = c["z0"].clone()
+    lv.posterior_langevin(z, c["x"], c["G"], c["E"], 30, m["sigma"], m["step"], True, noise=c["post_noise"])
+    assert rel_l2(z.cpu().numpy(), rec["post_z30"]) < 2e-3
+
+
+@pytest.mark.parametrize("name", ["cifar10_w16", "svhn_w16", "mnist_w16", "cifar10_full"])
+def test_prior_langevin_matches_reference(lv, gpu_device, name):
+    c = build_g_case(name, gpu_device)
+    z = c["zp0"].clone()
+    lv.prior_langevin(z, c["E"], 5, c["meta"]["prior_step"], False)
+    assert rel_l2(z.cpu().numpy(), c["rec"]["prior_z5"]) < 1e-6
+    z = c["zp0"].clone()
+    lv.prior_langevin(z, c["E"], 60, c["meta"]["prior_step"], True, noise=c["prior_noise"])
+    assert rel_l2(z.cpu().numpy(), c["rec"]["prior_z60"]) < 1e-4
+
+
+def test_toy_posterior_matches_reference(lv, gpu_device):
+    from damc import synth
+    from damc.toy import ToyG
+
+    rec, meta = load_golden("toy")
+    G = synth.load_into(ToyG(), 0).to(gpu_device)
+    B, nz = meta["B"], meta["nz"]
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, nz))).to(gpu_device)
+    x = torch.from_numpy(rec["x"]).to(gpu_device)
+    noise = torch.from_numpy(np.stack([synth.normal_f32(3, 100 + i, (B, nz))
+                                       for i in range(meta["steps"])])).to(gpu_device)
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, None, 1, meta["sigma"], meta["step"], True, noise=noise)
+    assert rel_l2(z.cpu().numpy(), rec["post_z1"]) < 1e-6
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, None, meta["steps"], meta["sigma"], meta["step"], True, noise=noise)
+    assert rel_l2(z.cpu().numpy(), rec["post_z1000"]) < 2e-3
+
+
+# ------------------------------------------------------------------ BASELINE-size checks
+def _cifar_full(device, B):
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=128, nc=3), 0).to(device).eval()
+    E = synth.load_into(dn._netE(nz=128), 10).to(device).eval()
+    x = torch.from_numpy(synth.uniform_f32(11, 0, (B, 3, 32, 32))).to(device)
+    z0 = torch.from_numpy(synth.normal_f32(12, 0, (B, 128))).to(device)
+    return G, E, x, z0
+
+
+def test_cifar_b128_step_vs_oracle(lv, gpu_device):
+    """BASELINE config (CIFAR-10, B=128, nz=128, ngf=128): one posterior step.
+
+    A few rows of this batch have ill-conditioned likelihood gradients: the fp32 CPU
+    restatement (= the reference's arithmetic) itself sits up to ~5e-4 from an fp64 evaluation
+    there.  The criterion is therefore accuracy-relative: the HIP result's distance to fp64 must
+    stay within 3x the fp32 reference arithmetic's distance to fp64 (+ a 1e-7 floor).
+    """
+    from oracle import damc_oracle as orc
+
+    G, E, x, z0 = _cifar_full(gpu_device, 128)
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, E, 1, 0.1, 0.1, False)
+    L32, P32 = orc.generator_layers(G), orc.ebm_params(E)
+    L64, P64 = orc.generator_layers(G, torch.float64), orc.ebm_params(E, torch.float64)
+    ref32 = orc.posterior_langevin(L32, P32, z0.cpu(), x.cpu(), 1, 0.1, 0.1).numpy()
+    ref64 = orc.posterior_langevin(L64, P64, z0.cpu().double(), x.cpu().double(), 1, 0.1, 0.1).numpy()
+    zg = z.cpu().numpy()
+    assert rel_l2(zg, ref64) <= 3 * rel_l2(ref32, ref64) + 1e-7
+    assert rel_l2(zg, ref32) < 2e-5
+    g = lv.likelihood_grad(z0, x, G, 0.1).cpu().numpy()
+    g32 = orc.likelihood_grad(L32, z0.cpu(), x.cpu(), 0.1)[0].numpy()
+    g64 = orc.likelihood_grad(L64, z0.cpu().double(), x.cpu().double(), 0.1)[0].numpy()
+    assert rel_l2(g, g64) <= 3 * rel_l2(g32, g64) + 1e-6
+
+
+def test_philox_noise_statistics(lv, gpu_device):
+    n = lv.philox_normal(4, 512, 128, seed=1234, device=gpu_device).double().cpu().numpy().ravel()
+    assert abs(n.mean()) < 5e-3 and abs(n.var() - 1.0) < 1e-2
+    from scipy import stats
+
+    assert stats.kstest(n[:200000], "norm").pvalue > 1e-3
+    # different chains / steps / seeds are different streams
+    a = lv.philox_normal(1, 2, 128, seed=1, device=gpu_device).cpu().numpy()
+    assert np.abs(a[0, 0] - a[0, 1]).max() > 0.1
+    b = lv.philox_normal(1, 2, 128, seed=2, device=gpu_device).cpu().numpy()
+    assert np.abs(a - b).max() > 0.1
+    # chain_base shifts the stream: chains [4, 8) of an 8-chain draw == a 4-chain draw at base 4
+    full = lv.philox_normal(3, 8, 100, seed=9, device=gpu_device).cpu().numpy()
+    part = lv.philox_normal(3, 4, 100, seed=9, device=gpu_device, chain_base=4).cpu().numpy()
+    assert np.array_equal(full[:, 4:], part)
+
+
+def test_sharded_chains_are_bitwise_identical(lv, gpu_device):
+    """Noise keyed by GLOBAL chain index: 2 shards of 4 chains == 1 batch of 8, bit for bit."""
+    G, E, x, z0 = _cifar_full(gpu_device, 8)
+    za = z0.clone()
+    lv.posterior_langevin(za, x, G, E, 5, 0.1, 0.1, True, seed=77)
+    zb = [z0[:4].clone(), z0[4:].clone()]
+    lv.posterior_langevin(zb[0], x[:4].contiguous(), G, E, 5, 0.1, 0.1, True, seed=77, chain_base=0)
+    lv.posterior_langevin(zb[1], x[4:].contiguous(), G, E, 5, 0.1, 0.1, True, seed=77, chain_base=4)
+    assert torch.equal(za, torch.cat(zb))
+    pa = torch.cat([z0, z0]).contiguous()
+    lv.prior_langevin(pa, E, 20, 0.4, True, seed=5)
+    pb = [torch.cat([z0, z0])[:10].clone(), torch.cat([z0, z0])[10:].clone()]
+    lv.prior_langevin(pb[0], E, 20, 0.4, True, seed=5, chain_base=0)
+    lv.prior_langevin(pb[1], E, 20, 0.4, True, seed=5, chain_base=10)
+    assert torch.equal(pa, torch.cat(pb))
+
+
+def test_dropin_mcmc_api(gpu_device):
+    """src.MCMC keeps the reference's call surface: in-place z, detach, requires_grad toggling."""
+    from src import MCMC
+
+    G, E, x, z0 = _cifar_full(gpu_device, 4)
+    z = z0.clone().requires_grad_(True)
+    out = MCMC.sample_langevin_post_z_with_prior(z=z, x=x, netG=G, netE=E, g_l_steps=3, g_llhd_sigma=0.1,
+                                                 g_l_with_noise=True, g_l_step_size=0.1, verbose=True)
+    assert out.data_ptr() == z.data_ptr() and not out.requires_grad
+    assert not torch.equal(out, z0)
+    assert all(p.requires_grad for p in G.parameters()) and all(p.requires_grad for p in E.parameters())
+    zn = torch.cat([z0, torch.randn_like(z0, requires_grad=True)], dim=0)
+    out = MCMC.sample_langevin_prior_z(z=zn, netE=E, e_l_steps=10, e_l_step_size=0.4, e_l_with_noise=True,
+                                       verbose=True)
+    assert out.shape == (8, 128) and torch.isfinite(out).all()
+    xs = MCMC.gen_samples(bs=16, nz=128, netE=E, netG=G, e_l_steps=5, e_l_step_size=0.4, e_l_with_noise=True)
+    assert xs.shape == (16, 3, 32, 32) and torch.isfinite(xs).all() and xs.abs().max() <= 1.0
+
+
+def test_verbose_diagnostics_match_oracle(lv, gpu_device):
+    """diag = {sum E, |G(z)-x|^2/(2s^2), |z|^2/2, mean grad} per step, as the reference logs them."""
+    from oracle import damc_oracle as orc
+
+    G, E, x, z0 = _cifar_full(gpu_device, 8)
+    z = z0.clone()
+    d = lv.posterior_langevin(z, x, G, E, 1, 0.1, 0.1, False, diag=True).cpu().numpy()[0]
+    L, P = orc.generator_layers(G), orc.ebm_params(E)
+    gl, lik, _ = orc.likelihood_grad(L, z0.cpu(), x.cpu(), 0.1)
+    e, ge = orc.ebm_energy_grad(P, z0.cpu())
+    want = [float(e.sum()), float(lik), float(0.5 * (z0.cpu() ** 2).sum()), float((gl + ge + z0.cpu()).mean())]
+    assert np.allclose(d[:3], want[:3], rtol=1e-4, atol=1e-4)
+    assert abs(d[3] - want[3]) < 1e-4 * max(1.0, abs(want[3]))
