@@ -90,6 +90,7 @@ __device__ __forceinline__ float sub_rn(float a, float b) { return __fsub_rn(a, 
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == DAMC_ACT_LRELU) return v > 0.f ? v : v * slope;
   if (act == DAMC_ACT_TANH) return tanhf(v);
+  if (act == DAMC_ACT_SILU) return v / (1.f + expf(-v));
   return v;
 }
 // derivative expressed through the post-activation value (sign(h) == sign(a) for LReLU)

@@ -50,14 +50,15 @@ class CsqBlock(ctypes.Structure):
         ("din", ctypes.c_int), ("dout", ctypes.c_int),
         ("wl", ctypes.c_void_p), ("bl", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("bs", ctypes.c_void_p),
         ("wg", ctypes.c_void_p), ("bg", ctypes.c_void_p), ("wb", ctypes.c_void_p),
-        ("px", ctypes.c_void_p), ("qt", ctypes.c_void_p),
     ]
 
 
 class Denoiser(ctypes.Structure):
     _fields_ = [
-        ("nz", ctypes.c_int), ("nblocks", ctypes.c_int), ("residual", ctypes.c_int),
+        ("nz", ctypes.c_int), ("ntemb", ctypes.c_int), ("nxemb", ctypes.c_int), ("residual", ctypes.c_int),
         ("bmat", ctypes.c_void_p),
+        ("tw1", ctypes.c_void_p), ("tb1", ctypes.c_void_p), ("tw2", ctypes.c_void_p), ("tb2", ctypes.c_void_p),
+        ("wctx_t", ctypes.c_void_p), ("wctx_x", ctypes.c_void_p), ("bctx", ctypes.c_void_p),
         ("blocks", CsqBlock * 7),
     ]
 
@@ -89,8 +90,9 @@ _SIGS = {
     "damc_instnorm_lrelu_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P]),
     "damc_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
-    "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I]),
-    "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _I, _I, _P, _I, _P, _U64, _U64, _P, _I, _P, _SZ, _P]),
+    "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
+    "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,
+                                _SZ, _P]),
     "damc_prof_enable": (_I, [_I]),
     "damc_prof_reset": (_I, []),
     "damc_prof_query": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),

@@ -1,0 +1,244 @@
+"""The amortizer Q on the HIP path: encoder (or prior embedding) + latent reverse sweep.
+
+Mirrors ``_netQ_U.forward`` (workspace/src/diffusion_net.py:585-622):
+  x given : xemb = encoder(x)                 -> Encoder_* on the MFMA conv engine + fused IN/LReLU
+  x None  : xemb = prior_emb(randn(b, nz))    -> two GEMMs (LeakyReLU 0.01 between)
+  zt = randn(b, nz) (host generator, as the reference) then n_interval reverse steps in libdamc.
+
+The per-step schedule scalars (logsnr_t/logsnr_s and the coefficients of pred_x_from_eps /
+diffusion_reverse, diffusion_helper_func.py:36-70) and the sinusoidal time embedding input
+(SinusoidalPosEmb, diffusion_net.py:447-461) are batch-invariant: they are evaluated once per
+call on the host in fp32 with the reference's own op sequence and handed to the kernels.
+"""
+import ctypes
+import math
+import weakref
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _dev(t, device):
+    t = t.detach()
+    if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.to(device=device, dtype=torch.float32).contiguous()
+    return t
+
+
+# ----------------------------------------------------------------------------- schedule
+def _schedule(t, lmin, lmax):
+    """logsnr_schedule_fn (diffusion_helper_func.py:41-50), fp32 op for op."""
+    lmin_t = lmin * torch.ones_like(t)
+    lmax_t = lmax * torch.ones_like(t)
+    b = torch.arctan(torch.exp(-0.5 * lmax_t))
+    a = torch.arctan(torch.exp(-0.5 * lmin_t)) - b
+    return -2.0 * torch.log(torch.tan(a * t + b))
+
+
+def step_tables(n_interval, logsnr_min, logsnr_max, var_type, ntemb):
+    """Host tables for the sweep: coef (n, 6) and the sinusoidal time-embedding input (n, ntemb)."""
+    coef = torch.zeros(n_interval, 6, dtype=torch.float32)
+    temb = torch.zeros(n_interval, ntemb, dtype=torch.float32)
+    half = ntemb // 2
+    freqs = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
+    for k, i in enumerate(reversed(range(n_interval))):
+        it = torch.ones(1, dtype=torch.float32) * float(i)
+        lt = _schedule(it / (n_interval - 1.0), logsnr_min, logsnr_max)
+        ls = _schedule(torch.clamp(it - 1.0, min=0.0) / (n_interval - 1.0), logsnr_min, logsnr_max)
+        c0 = torch.sqrt(1.0 + torch.exp(-lt))
+        c1 = torch.rsqrt(1.0 + torch.exp(lt))
+        alpha_st = torch.sqrt((1.0 + torch.exp(-lt)) / (1.0 + torch.exp(-ls)))
+        alpha_s = torch.sqrt(torch.sigmoid(ls))
+        r = torch.exp(lt - ls)
+        omr = -torch.expm1(lt - ls)
+        if var_type == "large":
+            var = omr * torch.sigmoid(-lt)
+        elif var_type == "small":
+            a_t, a_s = torch.sigmoid(lt), torch.sigmoid(ls)
+            var = (1.0 - a_s) / (1.0 - a_t) * (1 - a_t / a_s)
+        else:
+            raise NotImplementedError(var_type)
+        coef[k] = torch.cat([c0, c1, r * alpha_st, omr * alpha_s, torch.sqrt(var),
+                             torch.ones(1) if i == 0 else torch.zeros(1)])
+        li = torch.arctan(torch.exp(-0.5 * torch.clamp(lt, min=-20.0, max=20.0))) / (0.5 * math.pi)
+        li = li * (1000.0 / 1.0)  # SinusoidalPosEmb(max_time=1.) scales its input by 1000
+        e = li[:, None] * freqs[None, :]
+        temb[k] = torch.cat((e.sin(), e.cos()), dim=-1)[0]
+    return coef, temb
+
+
+# ------------------------------------------------------------------------------ encoder
+class EncoderPlan:
+    """Encoder_*.net = [Conv2d, InstanceNorm2d(affine), LeakyReLU(.2)]* Conv2d (diffusion_net.py:227-413)."""
+
+    def __init__(self, enc):
+        mods = list(enc.net)
+        self.stages = []  # (conv, norm or None, slope or None)
+        i = 0
+        while i < len(mods):
+            conv = mods[i]
+            if not isinstance(conv, torch.nn.Conv2d) or hasattr(conv, "weight_orig"):
+                raise NotImplementedError("unexpected encoder module %r" % (conv,))
+            norm, slope = None, None
+            if i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.InstanceNorm2d):
+                norm = mods[i + 1]
+                if not norm.affine or norm.track_running_stats:
+                    raise NotImplementedError("InstanceNorm2d must be affine without running stats")
+                slope = float(mods[i + 2].negative_slope)
+                i += 3
+            else:
+                i += 1
+            self.stages.append((conv, norm, slope))
+        self.nemb = enc.nemb
+
+    def forward(self, x):
+        L = _lib.lib()
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        B, C, H, W = x.shape
+        h = torch.empty(B, H, W, C, dtype=torch.float32, device=dev)
+        check(L.damc_nchw_to_nhwc(ptr(x), B, C, H * W, ptr(h), stream), "nchw_to_nhwc")
+        keep = []
+        for conv, norm, slope in self.stages:
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            cout, cin = conv.out_channels, conv.in_channels
+            w = _dev(conv.weight, dev)
+            wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
+            check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(wp), stream), "pack conv2d")
+            bias = _dev(conv.bias, dev) if conv.bias is not None else None
+            Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+            y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
+            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(bias), cout, k, s, p, ptr(y), stream),
+                  "conv2d")
+            keep += [w, wp, bias]
+            if norm is not None:
+                nws = int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout))
+                ws = torch.empty(max(nws, 1), dtype=torch.float32, device=dev)
+                g, b = _dev(norm.weight, dev), _dev(norm.bias, dev)
+                check(L.damc_instnorm_lrelu_nhwc(ptr(y), B, Ho * Wo, cout, ptr(g), ptr(b), float(norm.eps),
+                                                 slope, ptr(ws), stream), "instnorm")
+                keep += [ws, g, b]
+            h, H, W = y, Ho, Wo
+        return h.reshape(B, -1)
+
+
+# ----------------------------------------------------------------------------- denoiser
+class DenoiserPlan:
+    """Packed Diffusion_UnetA (diffusion_net.py:463-533)."""
+
+    def __init__(self, p):
+        self.p = p
+        self.blocks = list(p.in_layers) + list(p.mid_layers) + list(p.out_layers)
+        if len(self.blocks) != 7:
+            raise NotImplementedError("Diffusion_UnetA with %d blocks" % len(self.blocks))
+        self.nz, self.ntemb, self.nxemb = p.nz, p.ntemb, p.nxemb
+
+    def pack(self, device):
+        t = lambda w: _dev(w, device).t().contiguous()  # noqa: E731  W (out,in) -> W^T (in,out)
+        d = _lib.Denoiser()
+        d.nz, d.ntemb, d.nxemb, d.residual = self.nz, self.ntemb, self.nxemb, int(bool(self.p.residual))
+        keep = []
+        bmat = _dev(self.p.B, device)
+        tw1, tb1 = t(self.p.time_mlp[1].weight), _dev(self.p.time_mlp[1].bias, device)
+        tw2, tb2 = t(self.p.time_mlp[3].weight), _dev(self.p.time_mlp[3].bias, device)
+        ctx_w = [_dev(blk._layer_ctx[1].weight, device) for blk in self.blocks]
+        wctx_t = torch.cat([w[:, :self.ntemb] for w in ctx_w], dim=0).t().contiguous()
+        wctx_x = torch.cat([w[:, self.ntemb:] for w in ctx_w], dim=0).t().contiguous()
+        bctx = torch.cat([_dev(blk._layer_ctx[1].bias, device) for blk in self.blocks]).contiguous()
+        keep += [bmat, tw1, tb1, tw2, tb2, wctx_t, wctx_x, bctx]
+        d.bmat, d.tw1, d.tb1, d.tw2, d.tb2 = [x.data_ptr() for x in (bmat, tw1, tb1, tw2, tb2)]
+        d.wctx_t, d.wctx_x, d.bctx = wctx_t.data_ptr(), wctx_x.data_ptr(), bctx.data_ptr()
+        for j, blk in enumerate(self.blocks):
+            lin, skip = blk._layer[0], blk._skip
+            arrs = [t(lin.weight), _dev(lin.bias, device), t(skip.weight), _dev(skip.bias, device),
+                    t(blk._hyper_gate.weight), _dev(blk._hyper_gate.bias, device), t(blk._hyper_bias.weight)]
+            keep += arrs
+            b = d.blocks[j]
+            b.din, b.dout = lin.in_features, lin.out_features
+            b.wl, b.bl, b.ws, b.bs, b.wg, b.bg, b.wb = [x.data_ptr() for x in arrs]
+        self._keep = keep
+        return d
+
+
+_ENC = weakref.WeakKeyDictionary()
+_DEN = weakref.WeakKeyDictionary()
+
+
+def encoder_forward(enc, x):
+    plan = _ENC.get(enc)
+    if plan is None:
+        plan = _ENC[enc] = EncoderPlan(enc)
+    x = x.detach().to(dtype=torch.float32).contiguous()
+    if x.device.type != "cuda":
+        raise _lib.DamcError("encoder input must be on a ROCm device; the HIP path has no CPU fallback")
+    return plan.forward(x)
+
+
+def prior_embedding(Q, noise):
+    """prior_emb = Linear(nz,128) -> LeakyReLU(0.01) -> Linear(128,nxemb) (diffusion_net.py:577-581)."""
+    L = _lib.lib()
+    dev = noise.device
+    stream = _lib.stream_ptr(dev)
+    l1, act, l2 = Q.prior_emb[0], Q.prior_emb[1], Q.prior_emb[2]
+    w1, b1 = _dev(l1.weight, dev).t().contiguous(), _dev(l1.bias, dev)
+    w2, b2 = _dev(l2.weight, dev).t().contiguous(), _dev(l2.bias, dev)
+    B = noise.shape[0]
+    h = torch.empty(B, l1.out_features, dtype=torch.float32, device=dev)
+    out = torch.empty(B, l2.out_features, dtype=torch.float32, device=dev)
+    check(L.damc_gemm(ptr(noise), l1.in_features, ptr(w1), l1.out_features, ptr(b1), ptr(h), l1.out_features, B,
+                      l1.out_features, l1.in_features, _lib.ACT_LRELU, float(act.negative_slope), stream), "gemm")
+    check(L.damc_gemm(ptr(h), l2.in_features, ptr(w2), l2.out_features, ptr(b2), ptr(out), l2.out_features, B,
+                      l2.out_features, l2.in_features, _lib.ACT_NONE, 0.0, stream), "gemm")
+    return out
+
+
+def reverse_sweep(Q, xemb, zt, noise=None, seed=None, chain_base=0, eps_log_steps=0, with_noise=None):
+    """In-place latent reverse sweep on zt (B, nz); returns eps of the first eps_log_steps steps."""
+    dev = zt.device
+    plan = _DEN.get(Q.p)
+    if plan is None:
+        plan = _DEN[Q.p] = DenoiserPlan(Q.p)
+    d = plan.pack(dev)
+    n = int(Q.n_interval)
+    B = zt.shape[0]
+    coef, temb = step_tables(n, Q.logsnr_min, Q.logsnr_max, Q.var_type, plan.ntemb)
+    temb_d = temb.to(dev)
+    coef_h = coef.contiguous()
+    L = _lib.lib()
+    nbytes = int(L.damc_sweep_workspace_bytes(ctypes.byref(d), B, n))
+    if nbytes == 0:
+        raise _lib.DamcError("unsupported denoiser configuration for the HIP path")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    with_noise = bool(Q.with_noise) if with_noise is None else bool(with_noise)
+    if noise is not None:
+        noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item()) if with_noise and noise is None else 0
+    xemb = xemb.to(dtype=torch.float32).contiguous()
+    eps_log = torch.empty(max(eps_log_steps, 1), B, plan.nz, dtype=torch.float32, device=dev) if eps_log_steps else None
+    check(L.damc_reverse_sweep(ctypes.byref(d), ptr(xemb), ptr(zt), B, n, ptr(temb_d),
+                               coef_h.numpy().ctypes.data_as(ctypes.c_void_p), int(with_noise), ptr(noise), seed,
+                               chain_base, ptr(eps_log), int(eps_log_steps), ptr(ws), nbytes, _lib.stream_ptr(dev)),
+          "damc_reverse_sweep")
+    return eps_log
+
+
+def q_forward(Q, x=None, b=None, device=None, cond_w=-1):
+    """_netQ_U.forward on the HIP path (diffusion_net.py:585-622)."""
+    if cond_w is not None and cond_w > 0 and x is not None:
+        raise NotImplementedError("classifier-free guidance (cond_w > 0) is dead code in the reference drivers")
+    if x is not None:
+        assert b is None and device is None
+        b = len(x)
+        device = x.device
+        xemb = encoder_forward(Q.encoder, x)
+    else:
+        device = torch.device(device) if device is not None else torch.device("cuda")
+        xemb = prior_embedding(Q, torch.randn(b, Q.nz, device=device))
+    zt = torch.randn(b, Q.nz).to(device)
+    if zt.device.type != "cuda":
+        raise _lib.DamcError("the HIP sweep needs a ROCm device (got %s)" % zt.device)
+    reverse_sweep(Q, xemb, zt)
+    return zt

@@ -49,7 +49,7 @@ enum {
   DAMC_LAYER_SMALLC = 3, /* last ConvTranspose2d with Cout <= 4 (to RGB / gray)             */
   DAMC_LAYER_LINEAR = 4  /* nn.Linear (toy MLP generator)                                  */
 };
-enum { DAMC_ACT_NONE = 0, DAMC_ACT_LRELU = 1, DAMC_ACT_TANH = 2 };
+enum { DAMC_ACT_NONE = 0, DAMC_ACT_LRELU = 1, DAMC_ACT_TANH = 2, DAMC_ACT_SILU = 3 };
 
 typedef struct {
   int kind;
@@ -144,35 +144,45 @@ int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* 
 int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc, int m,
               int n, int k, int act, float slope, void* stream);
 
-/* Denoiser (Diffusion_UnetA, diffusion_net.py:417-533) reverse sweep (diffusion_net.py:595-622).
- * Blocks are described by packed weights; see damc/amortizer.py for the packing order. */
+/* Denoiser Diffusion_UnetA (diffusion_net.py:417-533) and its reverse sweep (diffusion_net.py:595-622).
+ * Seven ConcatSquashLinearSkipCtx blocks (in0 in1 in2 mid0 out0 out1 out2); every Linear weight is
+ * packed as W^T (in, out).  The ctx Linear of each block, Lc(SiLU(cat(temb, xemb))), is split into its
+ * step-invariant xemb part (computed once per sweep, (B, sum dout)) and its batch-invariant temb part
+ * (computed once per step for the whole batch, (n_steps, sum dout)); blocks are concatenated along
+ * the output axis in block order. */
 typedef struct {
   int din, dout;
-  const float* wl;  /* _layer.0:      (din,dout) packed = W^T  */
-  const float* bl;  /*                (dout)                   */
-  const float* ws;  /* _skip:         (din,dout)               */
-  const float* bs;
-  const float* wg;  /* _hyper_gate:   (dout,dout) packed W^T   */
-  const float* bg;
-  const float* wb;  /* _hyper_bias:   (dout,dout) packed W^T   */
-  const float* px;  /* per-row xemb part of the ctx Linear (B,dout)  [step-invariant]       */
-  const float* qt;  /* per-step temb part of the ctx Linear (+bias) (n_steps,dout)         */
+  const float *wl, *bl; /* _layer.0     (din, dout), (dout)  */
+  const float *ws, *bs; /* _skip        (din, dout), (dout)  */
+  const float *wg, *bg; /* _hyper_gate  (dout, dout), (dout) */
+  const float* wb;      /* _hyper_bias  (dout, dout), no bias */
 } damc_csq_block_t;
 
 typedef struct {
-  int nz, nblocks;            /* 7 for Diffusion_UnetA                                      */
-  int residual;               /* diffusion_residual                                         */
-  const float* bmat;          /* p.B (nz, nz/2)                                             */
-  damc_csq_block_t blocks[7]; /* in0 in1 in2 mid0 out0 out1 out2                            */
+  int nz, ntemb, nxemb, residual;
+  const float* bmat;               /* p.B (nz, nz/2)                                         */
+  const float *tw1, *tb1;          /* time_mlp[1]: (ntemb, ntemb) W^T, (ntemb)               */
+  const float *tw2, *tb2;          /* time_mlp[3]                                            */
+  const float* wctx_t;             /* (ntemb, sum dout): temb columns of every ctx Linear    */
+  const float* wctx_x;             /* (nxemb, sum dout): xemb columns of every ctx Linear    */
+  const float* bctx;               /* (sum dout)                                             */
+  damc_csq_block_t blocks[7];
 } damc_denoiser_t;
 
-/* per reverse step i (index k = n_interval-1-i): coefficients precomputed on the host from the
- * fp32 logsnr schedule (diffusion_helper_func.py:36-70):
- *   coef[k*6 + {0..5}] = {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std, is_last} */
-size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch);
-int damc_reverse_sweep(const damc_denoiser_t* d, float* zt, int batch, int n_steps, const float* coef,
-                       int with_noise, const float* noise, uint64_t seed, uint64_t chain_base, float* eps_log,
-                       int eps_log_steps, void* workspace, size_t workspace_bytes, void* stream);
+/* workspace bytes for damc_reverse_sweep */
+size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch, int n_steps);
+/* The reverse sweep (n_steps = n_interval denoiser evaluations, i = n_steps-1 .. 0, k = n_steps-1-i):
+ *   eps = p(zt, l_t, xemb); pred = c0 * (zt - eps * c1); zt <- last ? pred : c2*zt + c3*pred (+ c4*xi)
+ * temb_in (n_steps, ntemb): SinusoidalPosEmb of the step's logsnr input (host, fp32, as the reference);
+ * coef (n_steps, 6), a HOST pointer: {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std,
+ * is_last} (diffusion_helper_func.py:36-70, evaluated on the host in fp32 like the reference; the
+ * scalars travel by value in each step's kernel arguments);
+ * noise (n_steps-1, B, nz) injected or NULL for Philox; eps_log (optional) receives eps of the
+ * first eps_log_steps steps. zt (B, nz) is updated in place; xemb (B, nxemb). */
+int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int batch, int n_steps,
+                       const float* temb_in, const float* coef, int with_noise, const float* noise, uint64_t seed,
+                       uint64_t chain_base, float* eps_log, int eps_log_steps, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------------------- profiling */
 /* optional per-kernel HIP-event timing (bench.py roofline): records events around each
