@@ -154,7 +154,7 @@ def main():
 
     classes = {}
     for name in ("upconv_fwd", "upconv_dgrad", "proj_fwd", "proj_dgrad", "smallc_fwd", "smallc_dgrad",
-                 "posterior_update", "prior_chain"):
+                 "posterior_update", "slab_sum", "prior_chain"):
         ms, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         _lib.check(L.damc_prof_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
         if n.value:

@@ -50,6 +50,7 @@ __device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* ene
     const float bj = e.b1[j];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = bj;
+#pragma unroll 8
     for (int k = 0; k < nz; ++k) {
       const float w = e.w1t[(long)k * nh + j];
 #pragma unroll
@@ -65,6 +66,7 @@ __device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* ene
     const float bj = e.b2[j];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = bj;
+#pragma unroll 8
     for (int k = 0; k < nh; ++k) {
       const float w = e.w2t[(long)k * nh + j];
 #pragma unroll
@@ -94,6 +96,7 @@ __device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* ene
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll 8
     for (int j = 0; j < nh; ++j) {
       const float w = e.w2[(long)j * nh + k];
 #pragma unroll
@@ -108,6 +111,7 @@ __device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* ene
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll 8
     for (int j = 0; j < nh; ++j) {
       const float w = e.w1[(long)j * nz + c];
 #pragma unroll
@@ -294,8 +298,10 @@ __global__ void philox_normal_kernel(float* out, int n_steps, int B, int nz, uin
   out[i] = n4[c & 3];
 }
 
-constexpr int RP = 4;  // rows per workgroup, prior chain
-constexpr int RU = 8;  // rows per workgroup, posterior update
+// rows per workgroup: per step a workgroup streams all four weight panels (~0.5 MB, L2-resident) once,
+// so few rows per workgroup = more workgroups in flight = lower latency for these tiny batches
+constexpr int RP = 2;  // prior chain
+constexpr int RU = 2;  // posterior update
 
 }  // namespace
 

@@ -1,23 +1,42 @@
 // gemm.hip — fp32 MFMA implicit-GEMM engine for the generator / encoder convolutions.
 //
-// Tile 128x128x16, 256 threads = 4 waves in a 2x2 grid, each wave 64x64 = 2x2 tiles of
-// v_mfma_f32_32x32x2_f32 (exact fp32: a k-ordered fmaf chain per output, no xf32 on gfx950).
-// Operands are staged global -> registers -> LDS (k-major images so every MFMA operand read is
-// one conflict-free ds_read_b32 of 32 consecutive floats per half-wave), double-buffered with one
-// barrier per K-tile: the next tile's global loads are issued before the current tile's MFMAs.
-// Blocks are remapped so each XCD owns a contiguous run of tiles (shared A rows stay in its L2).
+// Block tile (64*MT) x 128 x BK, 256 threads = 4 waves in a 2x2 grid; a wave owns (32*MT) x 64 =
+// MT x 2 tiles of v_mfma_f32_32x32x2_f32 (exact fp32: a k-ordered fmaf chain per output; gfx950
+// has no xf32).  Operands are staged global -> registers -> LDS (k-major images: every MFMA operand
+// read is one conflict-free ds_read_b32 of 32 consecutive floats per half-wave), double-buffered
+// with one barrier per K-tile.  Schedule per tile: all fragments of the tile -> registers, store the
+// next tile into the other LDS buffer, issue the global loads of the tile after that, then the
+// tile's MFMAs back to back (the loads land under them).  Gather addresses are 32-bit element
+// offsets off the tensor base (every tensor here has < 2^31 elements).  Blocks are remapped so each
+// XCD owns a contiguous run of tiles (shared A rows stay in its L2).
+//
+// Config (BK, OCC, MT): K-tile depth, workgroups per CU for the launch bounds, MFMA tiles per wave
+// along M.  tools/gemm_bench.hip A/B-tests them on the generator's convolutions.
 #include "gemm.h"
 
 namespace damc {
 
-constexpr int BM = 128, BN = 128, BK = 16;
-constexpr int LDA_S = BM + 2;  // 4*LDA_S == 8 (mod 32): the transposing ds_write_b32 of A is conflict-free
-constexpr int LDB_S = BN;
+constexpr int BN = 128;
 
-template <int AM, int EPI, int OM, bool BVEC>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
-  __shared__ float As[2][BK * LDA_S];
-  __shared__ float Bs[2][BK * LDB_S];
+template <int BK, int MT>
+struct TileCfg {
+  static constexpr int BM = 64 * MT;
+  // A is written transposed with ds_write_b32: lanes (a_kq, m) of a half-wave must hit 32 banks
+  static constexpr int LDA = (BK == 16) ? BM + 2 : BM + 1;
+  static constexpr int LDB = BN;
+  static constexpr int AQ = BK / 4;              // float4 slots per A row
+  static constexpr int AROWS_V = BM * BK / 1024; // A float4 loads per thread (vector path)
+  static constexpr int AROWS_S = BM * BK / 256;  // A scalar loads per thread
+  static constexpr int BROWS_V = BK / 8;         // B float4 loads per thread
+  static constexpr int BROWS_S = BK / 2;         // B scalar loads per thread
+};
+
+template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT>
+__global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
+  typedef TileCfg<BK, MT> C;
+  constexpr int BM = C::BM;
+  __shared__ float As[2][BK * C::LDA];
+  __shared__ float Bs[2][BK * C::LDB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -50,38 +69,44 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
   }
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  // ---- per-thread A rows (vector paths: 2 rows x one float4 of k; scalar path: 8 rows x 1 k)
-  const int a_kq = tid & 3;       // float4 slot within the 16-wide k tile
-  const int a_ml = tid >> 2;      // 0..63 (+64)
-  const int s_kk = tid & 15;      // scalar path k
-  const int s_ml = tid >> 4;      // 0..15 (+16*j)
-  constexpr int AROWS = (AM == A_CONV_SCALAR) ? 8 : 2;
-  int a_b[AROWS], a_iy[AROWS], a_ix[AROWS];
-  bool a_ok[AROWS];
-  const long hwq = (long)p.Hq * p.Wq;
+  // ---- per-thread A rows
+  const int a_kq = tid % C::AQ;  // float4 slot within the k tile (vector paths)
+  const int a_ml = tid / C::AQ;  // rows a_ml + AVSTEP*j
+  constexpr int AVSTEP = 256 / C::AQ;
+  const int s_kk = tid % BK;     // scalar path k
+  const int s_ml = tid / BK;     // rows s_ml + ASSTEP*j
+  constexpr int ASSTEP = 256 / BK;
+  constexpr int AROWS = (AM == A_CONV_SCALAR) ? C::AROWS_S : C::AROWS_V;
+  int a_pix[AROWS], a_iy[AROWS], a_ix[AROWS];  // first pixel of the sample / top-left input tap
+  const int hwq = p.Hq * p.Wq;
+  const int hwin = p.Hin * p.Win;
 #pragma unroll
   for (int j = 0; j < AROWS; ++j) {
-    const int m = m0 + ((AM == A_CONV_SCALAR) ? (s_ml + 16 * j) : (a_ml + 64 * j));
-    a_ok[j] = m < p.M;
+    const int m = m0 + ((AM == A_CONV_SCALAR) ? (s_ml + ASSTEP * j) : (a_ml + AVSTEP * j));
+    const bool ok = m < p.M;
     if (AM == A_DENSE) {
-      a_b[j] = m;
-      a_iy[j] = 0;
+      a_pix[j] = m * (int)p.lda;
+      a_iy[j] = ok ? 0 : -0x40000000;  // poisons the row bound check
       a_ix[j] = 0;
     } else {
-      const int mm = a_ok[j] ? m : 0;
-      const int b = (int)(mm / hwq);
-      const int r = (int)(mm - b * hwq);
+      const int mm = ok ? m : 0;
+      const int b = mm / hwq;
+      const int r = mm - b * hwq;
       const int qy = r / p.Wq, qx = r - qy * p.Wq;
-      a_b[j] = b;
-      a_iy[j] = qy * p.stride - pad_y;
+      a_pix[j] = b * hwin;
+      a_iy[j] = ok ? qy * p.stride - pad_y : -0x40000000;
       a_ix[j] = qx * p.stride - pad_x;
     }
   }
+  // when Cg is a multiple of BK a whole K-tile sits inside one filter tap: the tap decomposition
+  // is then tile-uniform (scalar) instead of a per-lane division
+  const bool tap_uniform = (AM == A_CONV) && (p.Cg % BK == 0);
+  const unsigned Hin = (unsigned)p.Hin, Win = (unsigned)p.Win;
 
-  f32x4 ra[2];
-  float rs[8];
-  f32x4 rb[2];
-  float rbs[8];
+  f32x4 ra[C::AROWS_V];
+  float rs[C::AROWS_S];
+  f32x4 rb[C::BROWS_V];
+  float rbs[C::BROWS_S];
 
   auto load_a = [&](int k0) {
     if (AM == A_CONV_SCALAR) {
@@ -95,33 +120,38 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
         kx = tap - ky * p.kw;
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < C::AROWS_S; ++j) {
         const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
-        const bool ok = kin && a_ok[j] && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-        rs[j] = ok ? p.A[(((long)a_b[j] * p.Hin + iy) * p.Win + ix) * p.Cg + ci] : 0.f;
+        const bool ok = kin && (unsigned)iy < Hin && (unsigned)ix < Win;
+        rs[j] = ok ? p.A[(a_pix[j] + iy * p.Win + ix) * p.Cg + ci] : 0.f;
       }
     } else {
       const int k = k0 + 4 * a_kq;
       const bool kin = k < kend;
       if (AM == A_DENSE) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          ra[j] = (kin && a_ok[j]) ? *reinterpret_cast<const f32x4*>(p.A + (long)a_b[j] * p.lda + k)
-                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < C::AROWS_V; ++j) {
+          ra[j] = (kin && a_iy[j] == 0) ? *reinterpret_cast<const f32x4*>(p.A + (a_pix[j] + k))
+                                        : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       } else {
         int ky = 0, kx = 0, ci = 0;
-        if (kin) {
+        if (tap_uniform) {
+          const int tap = k0 / p.Cg;
+          ci = k0 - tap * p.Cg + 4 * a_kq;
+          ky = tap / p.kw;
+          kx = tap - ky * p.kw;
+        } else if (kin) {
           const int tap = k / p.Cg;
           ci = k - tap * p.Cg;
           ky = tap / p.kw;
           kx = tap - ky * p.kw;
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < C::AROWS_V; ++j) {
           const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
-          const bool ok = kin && a_ok[j] && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-          ra[j] = ok ? *reinterpret_cast<const f32x4*>(p.A + (((long)a_b[j] * p.Hin + iy) * p.Win + ix) * p.Cg + ci)
+          const bool ok = kin && (unsigned)iy < Hin && (unsigned)ix < Win;
+          ra[j] = ok ? *reinterpret_cast<const f32x4*>(p.A + ((a_pix[j] + iy * p.Win + ix) * p.Cg + ci))
                      : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -131,36 +161,37 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
     float* as = As[buf];
     if (AM == A_CONV_SCALAR) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) as[s_kk * LDA_S + s_ml + 16 * j] = rs[j];
+      for (int j = 0; j < C::AROWS_S; ++j) as[s_kk * C::LDA + s_ml + ASSTEP * j] = rs[j];
     } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ml = a_ml + 64 * j;
-        as[(4 * a_kq + 0) * LDA_S + ml] = ra[j].x;
-        as[(4 * a_kq + 1) * LDA_S + ml] = ra[j].y;
-        as[(4 * a_kq + 2) * LDA_S + ml] = ra[j].z;
-        as[(4 * a_kq + 3) * LDA_S + ml] = ra[j].w;
+      for (int j = 0; j < C::AROWS_V; ++j) {
+        const int ml = a_ml + AVSTEP * j;
+        as[(4 * a_kq + 0) * C::LDA + ml] = ra[j].x;
+        as[(4 * a_kq + 1) * C::LDA + ml] = ra[j].y;
+        as[(4 * a_kq + 2) * C::LDA + ml] = ra[j].z;
+        as[(4 * a_kq + 3) * C::LDA + ml] = ra[j].w;
       }
     }
   };
-  // B tile: 16 k-rows x 128 n
-  const int b_row = tid >> 5, b_c4 = tid & 31;   // vector path
-  const int bs_n = tid & 127, bs_row = tid >> 7; // scalar path
+  // B tile: BK k-rows x 128 n
+  const int b_row = tid >> 5, b_c4 = tid & 31;    // vector path: 8 rows per pass
+  const int bs_n = tid & 127, bs_row = tid >> 7;  // scalar path: 2 rows per pass
+  const int ldb = (int)p.ldb;
   auto load_b = [&](int k0) {
     if (BVEC) {
+      const int n = n0 + 4 * b_c4;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < C::BROWS_V; ++j) {
         const int k = k0 + b_row + 8 * j;
-        const int n = n0 + 4 * b_c4;
-        rb[j] = (k < kend && n < p.N) ? *reinterpret_cast<const f32x4*>(Bg + (long)k * p.ldb + n)
+        rb[j] = (k < kend && n < p.N) ? *reinterpret_cast<const f32x4*>(Bg + (k * ldb + n))
                                       : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
+      const int n = n0 + bs_n;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < C::BROWS_S; ++j) {
         const int k = k0 + bs_row + 2 * j;
-        const int n = n0 + bs_n;
-        rbs[j] = (k < kend && n < p.N) ? Bg[(long)k * p.ldb + n] : 0.f;
+        rbs[j] = (k < kend && n < p.N) ? Bg[k * ldb + n] : 0.f;
       }
     }
   };
@@ -168,16 +199,17 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
     float* bs = Bs[buf];
     if (BVEC) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) *reinterpret_cast<f32x4*>(bs + (b_row + 8 * j) * LDB_S + 4 * b_c4) = rb[j];
+      for (int j = 0; j < C::BROWS_V; ++j)
+        *reinterpret_cast<f32x4*>(bs + (b_row + 8 * j) * C::LDB + 4 * b_c4) = rb[j];
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bs[(bs_row + 2 * j) * LDB_S + bs_n] = rbs[j];
+      for (int j = 0; j < C::BROWS_S; ++j) bs[(bs_row + 2 * j) * C::LDB + bs_n] = rbs[j];
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[MT][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -188,34 +220,43 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
     load_b(kbeg);
     store_a(0);
     store_b(0);
+    if (nk > 1) {
+      load_a(kbeg + BK);
+      load_b(kbeg + BK);
+    }
   }
   __syncthreads();
 
   const int lrow = lane & 31, lk = lane >> 5;
+  const int am0 = wm * (32 * MT) + lrow, bn0 = wn * 64 + lrow;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_a(kbeg + (kt + 1) * BK);
-      load_b(kbeg + (kt + 1) * BK);
-    }
     const float* as = As[cur];
     const float* bs = Bs[cur];
+    float fa[BK / 2][MT], fb[BK / 2][2];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a0 = as[(kk + lk) * LDA_S + wm * 64 + lrow];
-      const float a1 = as[(kk + lk) * LDA_S + wm * 64 + 32 + lrow];
-      const float b0 = bs[(kk + lk) * LDB_S + wn * 64 + lrow];
-      const float b1 = bs[(kk + lk) * LDB_S + wn * 64 + 32 + lrow];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    for (int s2 = 0; s2 < BK / 2; ++s2) {
+      const int kk = 2 * s2 + lk;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) fa[s2][i] = as[kk * C::LDA + am0 + 32 * i];
+      fb[s2][0] = bs[kk * C::LDB + bn0];
+      fb[s2][1] = bs[kk * C::LDB + bn0 + 32];
     }
-    if (more) {
+    if (kt + 1 < nk) {
       store_a(cur ^ 1);
       store_b(cur ^ 1);
+      if (kt + 2 < nk) {
+        load_a(kbeg + (kt + 2) * BK);
+        load_b(kbeg + (kt + 2) * BK);
+      }
     }
+#pragma unroll
+    for (int s2 = 0; s2 < BK / 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][0], acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][1], acc[i][1], 0, 0, 0);
+      }
     __syncthreads();
   }
 
@@ -223,15 +264,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
   float* Cz = p.C;
   if (OM == O_DENSE) Cz += (long)z * p.c_zstride;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int m = m0 + wm * (32 * MT) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= p.M) continue;
       long rowoff;
       if (OM == O_PHASE) {
-        const int b = (int)(m / hwq);
-        const int rr = (int)(m - b * hwq);
+        const int b = m / hwq;
+        const int rr = m - b * hwq;
         const int qy = rr / p.Wq, qx = rr - qy * p.Wq;
         rowoff = (((long)b * p.Hout + 2 * qy + py) * p.Wout + 2 * qx + px) * p.ldc;
       } else {
@@ -262,16 +303,31 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs p) {
   }
 }
 
-template <int AM, int EPI, int OM, bool BV>
+template <int AM, int EPI, int OM, bool BV, int BK, int OCC, int MT>
 static void launch_t(const GemmArgs& a, int zdim, hipStream_t s) {
-  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  const int bm = 64 * MT;
+  const int ntm = (a.M + bm - 1) / bm, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, zdim);
-  hipLaunchKernelGGL((gemm_f32_kernel<AM, EPI, OM, BV>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_f32_kernel<AM, EPI, OM, BV, BK, OCC, MT>), grid, dim3(256), 0, s, a);
 }
+
+// tile configuration used by the library (tools/gemm_bench.hip A/B-tests alternatives)
+#ifndef DAMC_GEMM_BK
+#define DAMC_GEMM_BK 32  // measured best on the B=128 generator convs (profiles/r01/gemm_bench.txt)
+#endif
+#ifndef DAMC_GEMM_OCC
+#define DAMC_GEMM_OCC 2
+#endif
+#ifndef DAMC_GEMM_MT
+#define DAMC_GEMM_MT 2
+#endif
 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return DAMC_ERR_ARG;
+  // 32-bit element offsets inside the kernel
+  const double a_elems = (am == A_DENSE) ? (double)a.M * a.lda : (double)a.Hin * a.Win * a.Cg * ((double)a.M / ((double)a.Hq * a.Wq) + 1);
+  if (a_elems >= 2147483647.0 || (double)a.K * a.ldb >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
   const bool bvec = (a.ldb % 4 == 0) && (a.N % 4 == 0) && ((uintptr_t)a.B % 16 == 0);
   if (am == A_DENSE && (a.lda % 4 != 0 || a.K % 4 != 0 || (uintptr_t)a.A % 16 != 0)) am = A_CONV_SCALAR;
   if (am == A_CONV && (a.Cg % 4 != 0 || (uintptr_t)a.A % 16 != 0)) am = A_CONV_SCALAR;
@@ -281,10 +337,11 @@ int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const 
     b.Cg = (int)a.lda;
   }
   ProfScope ps(prof_name, flops, s);
+  constexpr int BKc = DAMC_GEMM_BK, OCCc = DAMC_GEMM_OCC, MTc = DAMC_GEMM_MT;
 #define DAMC_G(AM_, EPI_, OM_)                                                          \
   if (am == AM_ && epi == EPI_ && om == OM_) {                                          \
-    if (bvec) launch_t<AM_, EPI_, OM_, true>(b, zdim, s);                               \
-    else launch_t<AM_, EPI_, OM_, false>(b, zdim, s);                                   \
+    if (bvec) launch_t<AM_, EPI_, OM_, true, BKc, OCCc, MTc>(b, zdim, s);               \
+    else launch_t<AM_, EPI_, OM_, false, BKc, OCCc, MTc>(b, zdim, s);                   \
     return (int)hipGetLastError();                                                      \
   }
   DAMC_G(A_DENSE, EPI_STORE, O_DENSE)
@@ -307,6 +364,7 @@ int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const 
 
 }  // namespace damc
 
+#ifndef DAMC_GEMM_NO_C_API
 extern "C" int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc,
                          int m, int n, int k, int act, float slope, void* stream) {
   damc::GemmArgs g;
@@ -327,3 +385,4 @@ extern "C" int damc_gemm(const float* a, int lda, const float* b, int ldb, const
   return damc::launch_gemm(g, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "gemm", 2.0 * m * n * k,
                            as_stream(stream));
 }
+#endif

@@ -191,8 +191,324 @@ __global__ __launch_bounds__(256) void smallc_dgrad_kernel(float* h, int B, int 
   }
 }
 
+// ---- register-resident variants (the BASELINE shapes): a group of G = Cin/CH lanes owns one pixel,
+// lane g holds channels [g*CH, g*CH+CH) and ALL their weights (K*K*CH*NC floats) in VGPRs for the
+// whole launch; activations move as float4/float2 channel vectors (one coalesced 16*G-byte row per
+// group), the NC partial dots are reduced across the group with xor-shuffles.
+template <int CH>
+struct VecT;
+template <>
+struct VecT<4> {
+  typedef f32x4 T;
+};
+template <>
+struct VecT<2> {
+  typedef float __attribute__((ext_vector_type(2))) T;
+};
+
+template <int NC, int K, int S, int CH>
+__global__ __launch_bounds__(256) void smallc_fwd_reg_kernel(const float* __restrict__ h, int B, int Hin, int Win,
+                                                             int Cin, int pad, int Hout, int Wout,
+                                                             const float* __restrict__ wpk,
+                                                             const float* __restrict__ bias, const float* x,
+                                                             float inv_s2, float* delta, float* xhat,
+                                                             float* sqerr_sum) {
+  typedef typename VecT<CH>::T V;
+  __shared__ float red[4];
+  const int G = Cin / CH, P = 64 / G;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane % G, sub = lane / G;
+  const int ci0 = g * CH;
+  float w[K * K][CH][NC];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int o = 0; o < NC; ++o) w[t][c][o] = wpk[((long)t * Cin + ci0 + c) * NC + o];
+  float bo[NC];
+#pragma unroll
+  for (int o = 0; o < NC; ++o) bo[o] = bias ? bias[o] : 0.f;
+  const long npix = (long)B * Hout * Wout;
+  float sq_local = 0.f;
+  const long step = (long)gridDim.x * 4 * P;
+  for (long pix0 = ((long)blockIdx.x * 4 + wave) * P; pix0 < npix; pix0 += step) {
+    const long pix = pix0 + sub;
+    const bool live = pix < npix;
+    const long pp = live ? pix : 0;
+    const int b = (int)(pp / ((long)Hout * Wout));
+    const int rem = (int)(pp - (long)b * Hout * Wout);
+    const int oy = rem / Wout, ox = rem - oy * Wout;
+    static_assert(S == 1, "stride-2 output layers use smallc_fwd_s2_kernel");
+    // all K*K taps are loaded unconditionally (border taps clamped + zero-weighted) so the loads
+    // issue back to back instead of serialising their latency behind per-tap branches
+    V hv[K * K];
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int iy = oy + pad - ky;
+      const int iyc = min(max(iy, 0), Hin - 1);
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const int ix = ox + pad - kx;
+        const int ixc = min(max(ix, 0), Win - 1);
+        hv[ky * K + kx] = *reinterpret_cast<const V*>(h + (((long)b * Hin + iyc) * Win + ixc) * Cin + ci0);
+        const float m = (iy == iyc && ix == ixc) ? 1.f : 0.f;
+        hv[ky * K + kx] *= m;
+      }
+    }
+    float acc[NC];
+#pragma unroll
+    for (int o = 0; o < NC; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int t = 0; t < K * K; ++t)
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[o] = fmaf(hv[t][c], w[t][c][o], acc[o]);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+      if (off < G)
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[o] += __shfl_xor(acc[o], off, 64);
+    if (g == 0 && live) {
+#pragma unroll
+      for (int o = 0; o < NC; ++o) {
+        const float t = tanhf(acc[o] + bo[o]);
+        const long nchw = (((long)b * NC + o) * Hout + oy) * Wout + ox;
+        if (xhat) xhat[nchw] = t;
+        if (delta) {
+          const float r = t - x[nchw];
+          delta[pix * NC + o] = r * inv_s2 * (1.f - t * t);
+          sq_local += r * r;
+        }
+      }
+    }
+  }
+  if (sqerr_sum) {
+    sq_local = wave_sum(sq_local);
+    if (lane == 0) red[wave] = sq_local;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
+// k4 s2 p1 forward: a pixel group owns the output QUAD (2qy+py, 2qx+px), py,px in {0,1}, whose 16
+// taps are exactly the 3x3 input neighbourhood (qy+dy, qx+dx) with ky = 1 + py - 2dy (0..3), so each
+// input vector is loaded once and every tap index is a compile-time constant.
+template <int NC, int CH>
+__global__ __launch_bounds__(256) void smallc_fwd_s2_kernel(const float* __restrict__ h, int B, int Hin, int Win,
+                                                            int Cin, const float* __restrict__ wpk,
+                                                            const float* __restrict__ bias, const float* x,
+                                                            float inv_s2, float* delta, float* xhat,
+                                                            float* sqerr_sum) {
+  typedef typename VecT<CH>::T V;
+  constexpr int K = 4;
+  __shared__ float red[4];
+  const int G = Cin / CH, P = 64 / G;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane % G, sub = lane / G;
+  const int ci0 = g * CH;
+  const int Hout = 2 * Hin, Wout = 2 * Win;
+  float w[K * K][CH][NC];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int o = 0; o < NC; ++o) w[t][c][o] = wpk[((long)t * Cin + ci0 + c) * NC + o];
+  float bo[NC];
+#pragma unroll
+  for (int o = 0; o < NC; ++o) bo[o] = bias ? bias[o] : 0.f;
+  const long nq = (long)B * Hin * Win;
+  float sq_local = 0.f;
+  const long step = (long)gridDim.x * 4 * P;
+  for (long q0 = ((long)blockIdx.x * 4 + wave) * P; q0 < nq; q0 += step) {
+    const long q = q0 + sub;
+    const bool live = q < nq;
+    const long qq = live ? q : 0;
+    const int b = (int)(qq / ((long)Hin * Win));
+    const int rem = (int)(qq - (long)b * Hin * Win);
+    const int qy = rem / Win, qx = rem - qy * Win;
+    V hv[3][3];
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = qy + dy, iyc = min(max(iy, 0), Hin - 1);
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = qx + dx, ixc = min(max(ix, 0), Win - 1);
+        V v = *reinterpret_cast<const V*>(h + (((long)b * Hin + iyc) * Win + ixc) * Cin + ci0);
+        v *= (iy == iyc && ix == ixc) ? 1.f : 0.f;
+        hv[dy + 1][dx + 1] = v;
+      }
+    }
+    float acc[2][2][NC];
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+      for (int px = 0; px < 2; ++px) {
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[py][px][o] = 0.f;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+          const int ky = 1 + py - 2 * dy;
+          if (ky < 0 || ky > 3) continue;  // compile-time
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int kx = 1 + px - 2 * dx;
+            if (kx < 0 || kx > 3) continue;
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+              for (int o = 0; o < NC; ++o)
+                acc[py][px][o] = fmaf(hv[dy + 1][dx + 1][c], w[ky * K + kx][c][o], acc[py][px][o]);
+          }
+        }
+      }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+      if (off < G)
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+          for (int px = 0; px < 2; ++px)
+#pragma unroll
+            for (int o = 0; o < NC; ++o) acc[py][px][o] += __shfl_xor(acc[py][px][o], off, 64);
+    if (g == 0 && live) {
+#pragma unroll
+      for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          const int oy = 2 * qy + py, ox = 2 * qx + px;
+          const long pix = ((long)b * Hout + oy) * Wout + ox;
+#pragma unroll
+          for (int o = 0; o < NC; ++o) {
+            const float t = tanhf(acc[py][px][o] + bo[o]);
+            const long nchw = (((long)b * NC + o) * Hout + oy) * Wout + ox;
+            if (xhat) xhat[nchw] = t;
+            if (delta) {
+              const float r = t - x[nchw];
+              delta[pix * NC + o] = r * inv_s2 * (1.f - t * t);
+              sq_local += r * r;
+            }
+          }
+        }
+    }
+  }
+  if (sqerr_sum) {
+    sq_local = wave_sum(sq_local);
+    if (lane == 0) red[wave] = sq_local;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
+template <int NC, int K, int S, int CH>
+__global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, int Hin, int Win, int Cin, int pad,
+                                                               int Hout, int Wout, const float* __restrict__ wpk,
+                                                               const float* __restrict__ delta, int mask_act,
+                                                               float mask_slope) {
+  typedef typename VecT<CH>::T V;
+  const int G = Cin / CH, P = 64 / G;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane % G, sub = lane / G;
+  const int ci0 = g * CH;
+  float w[K * K][CH][NC];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int o = 0; o < NC; ++o) w[t][c][o] = wpk[((long)t * Cin + ci0 + c) * NC + o];
+  const long npix = (long)B * Hin * Win;
+  const long step = (long)gridDim.x * 4 * P;
+  for (long pix0 = ((long)blockIdx.x * 4 + wave) * P; pix0 < npix; pix0 += step) {
+    const long pix = pix0 + sub;
+    if (pix >= npix) continue;
+    const int b = (int)(pix / ((long)Hin * Win));
+    const int rem = (int)(pix - (long)b * Hin * Win);
+    const int iy = rem / Win, ix = rem - iy * Win;
+    V* hp = reinterpret_cast<V*>(h + pix * Cin + ci0);
+    V hv = *hp;  // issued first: its latency overlaps the delta gathers
+    float d[K * K][NC];
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int oy = iy * S - pad + ky;
+      const int oyc = min(max(oy, 0), Hout - 1);
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const int ox = ix * S - pad + kx;
+        const int oxc = min(max(ox, 0), Wout - 1);
+        const float* dp = delta + (((long)b * Hout + oyc) * Wout + oxc) * NC;
+        const float m = (oy == oyc && ox == oxc) ? 1.f : 0.f;
+#pragma unroll
+        for (int o = 0; o < NC; ++o) d[ky * K + kx][o] = dp[o] * m;
+      }
+    }
+    float acc[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int t = 0; t < K * K; ++t)
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[c] = fmaf(d[t][o], w[t][c][o], acc[c]);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) hv[c] = acc[c] * act_grad_from_out(hv[c], mask_act, mask_slope);
+    *hp = hv;
+  }
+}
+
+bool smallc_reg_ok(const damc_layer_t& L) {
+  if (L.cout != 1 && L.cout != 3) return false;
+  if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
+  const int CH = L.k == 3 ? 4 : 2;
+  if (L.cin % CH) return false;
+  const int G = L.cin / CH;
+  return G <= 64 && (64 % G) == 0;
+}
+
+// dispatch of a register-resident instantiation (caller checked smallc_reg_ok)
+template <int NC>
+bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, float* h_out, int B, const float* x,
+                         float inv_s2, float* delta, const float* delta_in, float* xhat, float* sqerr, int mask_act,
+                         float mask_slope, hipStream_t s) {
+  const int CH = L.k == 3 ? 4 : 2;
+  if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
+  if (L.cin % CH) return false;
+  const int G = L.cin / CH;
+  if (G > 64 || (64 % G)) return false;
+  const int P = 64 / G;
+  const long npix = (fwd && L.k == 3) ? (long)B * L.hout * L.wout : (long)B * L.hin * L.win;
+  const int grid = (int)std::max<long>(1, std::min<long>((npix + 4L * P - 1) / (4L * P), 1024));
+  if (fwd) {
+    if (L.k == 3)
+      hipLaunchKernelGGL((smallc_fwd_reg_kernel<NC, 3, 1, 4>), dim3(grid), dim3(256), 0, s, h_in, B, L.hin, L.win,
+                         L.cin, L.pad, L.hout, L.wout, L.w_fwd, L.bias, x, inv_s2, delta, xhat, sqerr);
+    else
+      hipLaunchKernelGGL((smallc_fwd_s2_kernel<NC, 2>), dim3(grid), dim3(256), 0, s, h_in, B, L.hin, L.win, L.cin,
+                         L.w_fwd, L.bias, x, inv_s2, delta, xhat, sqerr);
+  } else {
+    if (L.k == 3)
+      hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 3, 1, 4>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
+                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope);
+    else
+      hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
+                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope);
+  }
+  return true;
+}
+
 int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta, float* xhat,
                float* sqerr, hipStream_t s) {
+  if (smallc_reg_ok(L)) {
+    ProfScope ps("smallc_fwd", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
+    if (L.cout == 3)
+      smallc_reg_dispatch<3>(true, L, h, nullptr, B, x, inv_s2, delta, nullptr, xhat, sqerr, 0, 0.f, s);
+    else
+      smallc_reg_dispatch<1>(true, L, h, nullptr, B, x, inv_s2, delta, nullptr, xhat, sqerr, 0, 0.f, s);
+    return (int)hipGetLastError();
+  }
   const size_t sm = (size_t)L.k * L.k * L.cin * L.cout * sizeof(float);
   const long npix = (long)B * L.hout * L.wout;
   const int grid = (int)std::min<long>((npix + 3) / 4, 2048);
@@ -213,6 +529,16 @@ int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, flo
 
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
                  hipStream_t s) {
+  if (smallc_reg_ok(L)) {
+    ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
+    if (L.cout == 3)
+      smallc_reg_dispatch<3>(false, L, nullptr, h, B, nullptr, 0.f, nullptr, delta, nullptr, nullptr, mask_act,
+                             mask_slope, s);
+    else
+      smallc_reg_dispatch<1>(false, L, nullptr, h, B, nullptr, 0.f, nullptr, delta, nullptr, nullptr, mask_act,
+                             mask_slope, s);
+    return (int)hipGetLastError();
+  }
   const size_t sm = (size_t)L.k * L.k * L.cin * L.cout * sizeof(float);
   const long npix = (long)B * L.hin * L.win;
   const int grid = (int)std::min<long>((npix + 3) / 4, 2048);
@@ -231,12 +557,28 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
   return (int)hipGetLastError();
 }
 
-__global__ void slab_sum_kernel(const float* slabs, int nslab, long n, float* out) {
+// fixed-order (deterministic) reduction of the split-K slabs: one thread per element, loads unrolled
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slabs, int nslab, long n,
+                                                       float* __restrict__ out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float acc = 0.f;
-  for (int k = 0; k < nslab; ++k) acc += slabs[(long)k * n + i];
+  int k = 0;
+  for (; k + 8 <= nslab; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slabs[(long)(k + u) * n + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < nslab; ++k) acc += slabs[(long)k * n + i];
   out[i] = acc;
+}
+
+int slab_sum(const float* slabs, int nslab, long n, float* out, hipStream_t s) {
+  ProfScope ps("slab_sum", 0.0, s);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slabs, nslab, n, out);
+  return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------------------- plan helpers
@@ -289,6 +631,7 @@ struct Workspace {
   std::vector<float*> h;  // activations (NHWC), one per layer except the final one
   float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
   float* slabs;           // split-K partial gradients
+  float* glik;            // their fixed-order sum: grad of the likelihood term (B, nz)
   int nslab;
   size_t bytes;
 };
@@ -311,9 +654,11 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   const long K0 = (long)L0.hout * L0.wout * L0.cout;
   const int S = (g->n_layers == 1) ? 1 : proj_slices(K0);
   float* sl = take((long)S * B * g->nz);
+  float* gl = take((long)B * g->nz);
   if (w) {
     w->delta = d;
     w->slabs = sl;
+    w->glik = gl;
     w->nslab = S;
     w->bytes = off;
   }
@@ -582,8 +927,7 @@ extern "C" int damc_likelihood_grad(const damc_generator_t* g, const float* z, c
   }
   if ((rc = backward(g, B, ws, s))) return rc;
   const long n = (long)B * g->nz;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws.slabs, ws.nslab, n, grad);
-  return (int)hipGetLastError();
+  return slab_sum(ws.slabs, ws.nslab, n, grad, s);
 }
 
 extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
@@ -605,8 +949,9 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
     if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s))) return rc;
     if ((rc = backward(g, B, ws, s))) return rc;
     const float* nz_i = noise ? noise + (size_t)i * B * g->nz : nullptr;
-    rc = damc_launch_posterior_update(ebm, z, ws.slabs, ws.nslab, (long)B * g->nz, B, g->nz, step, with_noise, nz_i,
-                                      seed, step_offset + i, chain_base, dg, s);
+    if ((rc = slab_sum(ws.slabs, ws.nslab, (long)B * g->nz, ws.glik, s))) return rc;
+    rc = damc_launch_posterior_update(ebm, z, ws.glik, 1, (long)B * g->nz, B, g->nz, step, with_noise, nz_i, seed,
+                                      step_offset + i, chain_base, dg, s);
     if (rc) return rc;
   }
   return 0;

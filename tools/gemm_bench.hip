@@ -1,0 +1,126 @@
+// gemm_bench.hip — A/B the implicit-GEMM tile configurations on the four CIFAR-10 B=128 generator
+// convolutions (upconv fwd L2/L3, upconv dgrad L3/L2), interleaved in one process (guide §5.4 r24).
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DDAMC_GEMM_NO_C_API tools/gemm_bench.hip -o gemm_bench
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../diffusion-amortized-mcmc_amd/csrc/gemm.hip"
+
+namespace damc_prof {
+bool enabled() { return false; }
+int begin(const char*, double, hipStream_t) { return -1; }
+void end(int, hipStream_t) {}
+}  // namespace damc_prof
+
+using namespace damc;
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e = (x);                                                    \
+    if (e != hipSuccess) {                                                 \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+static float* rnd(size_t n, unsigned seed) {
+  std::vector<float> h(n);
+  unsigned s = seed;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    h[i] = ((s >> 8) * (1.0f / 16777216.0f)) * 2.f - 1.f;
+  }
+  float* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+struct Shape {
+  const char* name;
+  GemmArgs a;
+  bool phase;
+  double flops;
+};
+
+template <int BK, int OCC, int MT>
+void run(const Shape& sh, hipStream_t s) {
+  if (sh.phase)
+    launch_t<A_CONV, EPI_BIAS_ACT, O_PHASE, true, BK, OCC, MT>(sh.a, 4, s);
+  else
+    launch_t<A_CONV, EPI_MASK, O_DENSE, true, BK, OCC, MT>(sh.a, 1, s);
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 128;
+  const int ngf = 128;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  // activations (NHWC) and packed weights for the CIFAR generator
+  float* h1 = rnd((size_t)B * 8 * 8 * 8 * ngf, 1);
+  float* h2 = rnd((size_t)B * 16 * 16 * 4 * ngf, 2);
+  float* h3 = rnd((size_t)B * 32 * 32 * 2 * ngf, 3);
+  float* d3 = rnd((size_t)B * 32 * 32 * 2 * ngf, 4);
+  float* d2 = rnd((size_t)B * 16 * 16 * 4 * ngf, 5);
+  float* w2 = rnd((size_t)16 * 8 * ngf * 4 * ngf, 6);
+  float* w3 = rnd((size_t)16 * 4 * ngf * 2 * ngf, 7);
+  float* o1 = rnd((size_t)B * 8 * 8 * 8 * ngf, 8);
+  float* o2 = rnd((size_t)B * 16 * 16 * 4 * ngf, 9);
+  float* o3 = rnd((size_t)B * 32 * 32 * 2 * ngf, 10);
+  float* bias = rnd(1024, 11);
+  std::vector<Shape> shapes;
+  auto up = [&](const char* nm, float* in, int H, int cin, int cout, float* w, float* out) {
+    GemmArgs a;
+    a.A = in; a.Hin = H; a.Win = H; a.Cg = cin; a.Hq = H; a.Wq = H; a.kw = 2; a.stride = 1;
+    a.B = w; a.ldb = cout; a.b_zstride = 4L * cin * cout; a.C = out; a.ldc = cout;
+    a.M = B * H * H; a.N = cout; a.K = 4 * cin; a.Hout = 2 * H; a.Wout = 2 * H;
+    a.bias = bias; a.bias_mod = cout; a.act = DAMC_ACT_LRELU; a.slope = 0.2f;
+    shapes.push_back({nm, a, true, 2.0 * B * 4 * H * H * (double)cout * 4 * cin});
+  };
+  auto dg = [&](const char* nm, float* din, int Hout, int cout, int cin, float* w, float* out) {
+    GemmArgs a;
+    a.A = din; a.Hin = Hout; a.Win = Hout; a.Cg = cout; a.Hq = Hout / 2; a.Wq = Hout / 2; a.kw = 4; a.stride = 2;
+    a.pad_y = 1; a.pad_x = 1; a.B = w; a.ldb = cin; a.C = out; a.ldc = cin;
+    a.M = B * (Hout / 2) * (Hout / 2); a.N = cin; a.K = 16 * cout; a.k_per_z = a.K;
+    a.mask = out; a.mask_act = DAMC_ACT_LRELU; a.mask_slope = 0.2f;
+    shapes.push_back({nm, a, false, 2.0 * a.M * (double)a.N * a.K});
+  };
+  up("L2 fwd  8->16 1024->512", h1, 8, 8 * ngf, 4 * ngf, w2, o2);
+  up("L3 fwd 16->32  512->256", h2, 16, 4 * ngf, 2 * ngf, w3, o3);
+  dg("L3 dgrad 32->16 256->512", d3, 32, 2 * ngf, 4 * ngf, w3, o2);
+  dg("L2 dgrad 16->8  512->1024", d2, 16, 4 * ngf, 8 * ngf, w2, o1);
+
+  typedef void (*RunFn)(const Shape&, hipStream_t);
+  struct V { const char* name; RunFn fn; };
+  V vars[] = {{"BK16/2/MT2", run<16, 2, 2>}, {"BK32/2/MT2", run<32, 2, 2>}, {"BK16/1/MT4", run<16, 1, 4>},
+              {"BK16/2/MT4", run<16, 2, 4>}};
+  const int NV = sizeof(vars) / sizeof(vars[0]);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int rounds = 5, reps = 10;
+  std::vector<std::vector<float>> best(shapes.size(), std::vector<float>(NV, 1e30f));
+  for (int r = 0; r < rounds; ++r)
+    for (size_t si = 0; si < shapes.size(); ++si)
+      for (int v = 0; v < NV; ++v) {
+        vars[v].fn(shapes[si], s);  // warm
+        CK(hipEventRecord(e0, s));
+        for (int k = 0; k < reps; ++k) vars[v].fn(shapes[si], s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        if (ms < best[si][v]) best[si][v] = ms;
+      }
+  CK(hipGetLastError());
+  printf("B=%d  best-of-%d ms (TFLOP/s)\n", B, rounds);
+  for (size_t si = 0; si < shapes.size(); ++si) {
+    printf("%-28s", shapes[si].name);
+    for (int v = 0; v < NV; ++v)
+      printf("  %s %.3f (%.1f)", vars[v].name, best[si][v], shapes[si].flops / (best[si][v] * 1e-3) / 1e12);
+    printf("\n");
+  }
+  return 0;
+}
