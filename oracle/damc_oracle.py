@@ -69,10 +69,20 @@ def ebm_params(E, dtype=torch.float32):
 def _apply_act(a, act):
     kind, slope = act
     if kind == "lrelu":
-        return torch.where(a > 0, a, a * slope)
+        return F.leaky_relu(a, slope)
     if kind == "tanh":
         return torch.tanh(a)
     return a
+
+
+def _act_backward(d, h, act):
+    """d * act'(.) expressed through the post-activation h (single fused ATen pass, as autograd)."""
+    kind, slope = act
+    if kind == "lrelu":
+        return torch.ops.aten.leaky_relu_backward(d, h, slope, True)
+    if kind == "tanh":
+        return torch.ops.aten.tanh_backward(d, h)
+    return d
 
 
 def _act_grad_from_out(h, act):
@@ -106,12 +116,20 @@ def generator_vjp(layers, hs, delta_last):
     for i in range(len(layers) - 1, -1, -1):
         L = layers[i]
         if L["kind"] == "convT":
-            dh = F.conv2d(d, L["W"], None, stride=L["stride"], padding=L["pad"])
+            # input gradient of the transposed conv (= conv2d(d, W, stride, pad)), through ATen's
+            # convolution_backward — the kernel the reference's autograd dispatches to, so the CPU
+            # baseline times the same arithmetic the reference runs (no autograd graph involved)
+            inp = hs[i - 1] if i > 0 else None
+            if inp is None:
+                inp = torch.empty(d.shape[0], L["W"].shape[0], 1, 1, dtype=d.dtype)
+            dh = torch.ops.aten.convolution_backward(
+                d, inp, L["W"], None, [L["stride"]] * 2, [L["pad"]] * 2, [1, 1], True, [0, 0], 1,
+                [True, False, False])[0]
         else:
             dh = d @ L["W"]
         if i == 0:
             return dh.reshape(len(dh), -1)
-        d = dh * _act_grad_from_out(hs[i - 1], layers[i - 1]["act"])
+        d = _act_backward(dh, hs[i - 1], layers[i - 1]["act"])
     raise AssertionError
 
 
