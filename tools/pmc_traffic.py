@@ -18,8 +18,9 @@ CLASSES = [
     (r"gemm_f32_kernel<1, 1, 1", "upconv_fwd"),
     (r"gemm_f32_kernel<0, 1, 0", "proj_fwd"),
     (r"gemm_f32_kernel<0, 0, 0", "proj_dgrad"),
-    (r"smallc_fwd_kernel", "smallc_fwd"),
-    (r"smallc_dgrad_kernel", "smallc_dgrad"),
+    (r"smallc_fwd", "smallc_fwd"),
+    (r"smallc_dgrad", "smallc_dgrad"),
+    (r"slab_sum_kernel", "slab_sum"),
     (r"posterior_update_kernel", "posterior_update"),
     (r"prior_chain_kernel", "prior_chain"),
 ]
