@@ -60,8 +60,9 @@ __global__ void pack_up2_kernel(const float* w, int cin, int cout, float* wf, fl
   wf[((((long)phase * 2 + ty) * 2 + tx) * cin + ci) * cout + co] = v;
   wb[(((long)ky * 4 + kx) * cout + co) * cin + ci] = v;
 }
-// SMALLC: [ky][kx][ci][co]
-__global__ void pack_smallc_kernel(const float* w, int cin, int cout, int k, float* wf) {
+// SMALLC: fwd [ky][kx][ci][co]; bwd (the two-stage projection) [(ky*k+kx)*cout + co][ci] (rows padded
+// to a multiple of 32 with zeros by the caller's memset)
+__global__ void pack_smallc_kernel(const float* w, int cin, int cout, int k, float* wf, float* wb) {
   const long n = (long)cin * cout * k * k;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -73,6 +74,7 @@ __global__ void pack_smallc_kernel(const float* w, int cin, int cout, int k, flo
   const int co = (int)(t % cout);
   const int ci = (int)(t / cout);
   wf[(((long)ky * k + kx) * cin + ci) * cout + co] = w[i];
+  if (wb) wb[((long)(ky * k + kx) * cout + co) * cin + ci] = w[i];
 }
 // LINEAR: w (out,in): fwd = W^T (in,out), bwd = W (out,in)
 __global__ void pack_linear_kernel(const float* w, int in, int out, float* wf, float* wb) {
@@ -499,8 +501,144 @@ bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, flo
   return true;
 }
 
+// ---- two-stage output-layer forward -------------------------------------------------------
+// Stage 1 (MFMA): per INPUT pixel p the per-tap projections P[p][n], n = (ky*K + kx)*NC + co,
+//   P = h (npix x Cin) . Wp^T,  Wp packed [NTILE*32][Cin] (rows n >= K*K*NC are zero).
+// A wave owns 32 pixels x 32 columns per 32-column tile (v_mfma_f32_32x32x2_f32).  Operands come
+// straight from L2 as float4: lane (i = l&31, h = l>>5) loads h[p_i][8j + 4h .. +3] and
+// Wp[n_i][8j + 4h .. +3]; element t of those feeds k-step 4j + t, i.e. half h covers
+// k = 8j + 4h + t — the same bijection of k for A and B, so the sum is unchanged.
+template <int NTILE>
+__global__ __launch_bounds__(256) void smallc_proj_kernel(const float* __restrict__ h, long npix, int Cin,
+                                                          const float* __restrict__ wp, float* __restrict__ P) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long p0 = ((long)blockIdx.x * 4 + wave) * 32;
+  if (p0 >= npix) return;
+  const int i = lane & 31, hh = lane >> 5;
+  const long pi = min(p0 + i, npix - 1);
+  const float* hrow = h + pi * Cin + 4 * hh;
+  f32x16 acc[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const float* wrow[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) wrow[t] = wp + (long)(32 * t + i) * Cin + 4 * hh;
+#pragma unroll 2
+  for (int j = 0; j < Cin; j += 8) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(hrow + j);
+    f32x4 b[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) b[t] = *reinterpret_cast<const f32x4*>(wrow[t] + j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], b[t][e], acc[t], 0, 0, 0);
+  }
+  // C layout: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const int ldp = NTILE * 32;
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long p = p0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (p < npix) P[p * ldp + 32 * t + i] = acc[t][r];
+    }
+}
+
+// Stage 2: out[b,oy,ox,co] = bias + sum over the valid taps of P[input pixel][tap*NC + co], then tanh,
+// x_hat (NCHW) and the residual delta = (x_hat - x)/s^2 * (1 - x_hat^2) (NHWC).  One thread per output pixel.
+template <int NC, int K, int S>
+__global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restrict__ P, int ldp, int B, int Hin,
+                                                            int Win, int pad, int Hout, int Wout,
+                                                            const float* __restrict__ bias, const float* x,
+                                                            float inv_s2, float* delta, float* xhat,
+                                                            float* sqerr_sum) {
+  __shared__ float red[4];
+  const long npix = (long)B * Hout * Wout;
+  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float sq = 0.f;
+  if (pix < npix) {
+    const int b = (int)(pix / ((long)Hout * Wout));
+    const int rem = (int)(pix - (long)b * Hout * Wout);
+    const int oy = rem / Wout, ox = rem - oy * Wout;
+    float acc[NC];
+#pragma unroll
+    for (int o = 0; o < NC; ++o) acc[o] = bias ? bias[o] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int ty = oy + pad - ky;
+      if (ty < 0 || (S == 2 && (ty & 1))) continue;
+      const int iy = ty / S;
+      if (iy >= Hin) continue;
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const int tx = ox + pad - kx;
+        if (tx < 0 || (S == 2 && (tx & 1))) continue;
+        const int ix = tx / S;
+        if (ix >= Win) continue;
+        const float* pp = P + (((long)b * Hin + iy) * Win + ix) * ldp + (ky * K + kx) * NC;
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[o] += pp[o];
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < NC; ++o) {
+      const float t = tanhf(acc[o]);
+      const long nchw = (((long)b * NC + o) * Hout + oy) * Wout + ox;
+      if (xhat) xhat[nchw] = t;
+      if (delta) {
+        const float r = t - x[nchw];
+        delta[pix * NC + o] = r * inv_s2 * (1.f - t * t);
+        sq += r * r;
+      }
+    }
+  }
+  if (sqerr_sum) {
+    sq = wave_sum(sq);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
+int smallc_ntile(const damc_layer_t& L) { return (L.k * L.k * L.cout + 31) / 32; }
+
+bool smallc_twostage_ok(const damc_layer_t& L) {
+  if (L.cout != 1 && L.cout != 3) return false;
+  if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
+  return L.cin % 8 == 0 && smallc_ntile(L) <= 2 && L.w_bwd != nullptr;
+}
+
+int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta,
+                        float* xhat, float* sqerr, float* Pbuf, hipStream_t s) {
+  ProfScope ps("smallc_fwd", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
+  const long npin = (long)B * L.hin * L.win;
+  const int nt = smallc_ntile(L);
+  const int g1 = (int)((npin + 127) / 128);
+  if (nt == 1)
+    hipLaunchKernelGGL((smallc_proj_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
+  else
+    hipLaunchKernelGGL((smallc_proj_kernel<2>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
+  const long npout = (long)B * L.hout * L.wout;
+  const int g2 = (int)((npout + 255) / 256);
+#define SG(NC_, K_, S_)                                                                                             \
+  hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2), dim3(256), 0, s, Pbuf, nt * 32, B, L.hin, L.win, \
+                     L.pad, L.hout, L.wout, L.bias, x, inv_s2, delta, xhat, sqerr)
+  if (L.cout == 3) {
+    if (L.k == 3) SG(3, 3, 1); else SG(3, 4, 2);
+  } else {
+    if (L.k == 3) SG(1, 3, 1); else SG(1, 4, 2);
+  }
+#undef SG
+  return (int)hipGetLastError();
+}
+
 int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta, float* xhat,
-               float* sqerr, hipStream_t s) {
+               float* sqerr, float* Pbuf, hipStream_t s) {
+  if (Pbuf && smallc_twostage_ok(L)) return smallc_fwd_twostage(L, h, B, x, inv_s2, delta, xhat, sqerr, Pbuf, s);
   if (smallc_reg_ok(L)) {
     ProfScope ps("smallc_fwd", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
     if (L.cout == 3)
@@ -632,6 +770,7 @@ struct Workspace {
   float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
   float* slabs;           // split-K partial gradients
   float* glik;            // their fixed-order sum: grad of the likelihood term (B, nz)
+  float* pbuf;            // per-tap projections of the output layer (two-stage forward)
   int nslab;
   size_t bytes;
 };
@@ -655,10 +794,12 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   const int S = (g->n_layers == 1) ? 1 : proj_slices(K0);
   float* sl = take((long)S * B * g->nz);
   float* gl = take((long)B * g->nz);
+  float* pb = (F.kind == DAMC_LAYER_SMALLC) ? take((long)B * F.hin * F.win * smallc_ntile(F) * 32) : nullptr;
   if (w) {
     w->delta = d;
     w->slabs = sl;
     w->glik = gl;
+    w->pbuf = pb;
     w->nslab = S;
     w->bytes = off;
   }
@@ -727,7 +868,8 @@ int forward_final(const damc_generator_t* g, int B, const float* z, const float*
   const damc_layer_t& F = g->layers[n - 1];
   const float* hin = n >= 2 ? ws.h[n - 2] : z;
   if (F.kind == DAMC_LAYER_SMALLC)
-    return smallc_fwd(F, hin, B, want_delta ? x : nullptr, inv_s2, want_delta ? ws.delta : nullptr, xhat, sqerr, s);
+    return smallc_fwd(F, hin, B, want_delta ? x : nullptr, inv_s2, want_delta ? ws.delta : nullptr, xhat, sqerr,
+                      ws.pbuf, s);
   // LINEAR final layer
   GemmArgs a;
   a.A = hin;
@@ -851,7 +993,7 @@ extern "C" int damc_generator_layer_packed_sizes(const damc_layer_t* L, size_t* 
       return 0;
     case DAMC_LAYER_SMALLC:
       *fwd = n;
-      *bwd = 0;
+      *bwd = (size_t)smallc_ntile(*L) * 32 * L->cin;  // two-stage projection layout
       return 0;
   }
   return DAMC_ERR_ARG;
@@ -872,7 +1014,8 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, wf, wb);
       break;
     case DAMC_LAYER_SMALLC:
-      hipLaunchKernelGGL(pack_smallc_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf);
+      if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));
+      hipLaunchKernelGGL(pack_smallc_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf, wb);
       break;
     case DAMC_LAYER_LINEAR:
       if (!wb) return DAMC_ERR_ARG;
