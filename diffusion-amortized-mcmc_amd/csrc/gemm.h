@@ -16,6 +16,8 @@ enum OMode { O_DENSE = 0, O_PHASE = 1 };
 //                   2x2 conv with pad (1-py, 1-px) and row m = (b,qy,qx) is stored at output pixel
 //                   (b, 2qy+py, 2qx+px) of a Hout x Wout NHWC map; B advanced by z*b_zstride
 //   O_DENSE       : blockIdx.z = split-K slice: k in [z*k_per_z, (z+1)*k_per_z), C advanced by z*c_zstride
+//   b_kmajor      : B is stored transposed, Bt[n*ldb + k] (k contiguous).  Only the K-major convolution
+//                   engine reads this layout: A_CONV with conv_kmajor_ok(Cg), no split-K.
 struct GemmArgs {
   const float* A = nullptr;
   long lda = 0;
@@ -39,7 +41,13 @@ struct GemmArgs {
   float* xhat = nullptr;
   float* sqerr = nullptr;       // EPI_RESID: accumulates |t - x|^2 * inv_s2 / 2 (diagnostics)
   int Hout = 1, Wout = 1;
+  int b_kmajor = 0;
 };
+
+// The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
+// channel count is a multiple of its K tile; weight packers pick the B layout with this predicate.
+constexpr int KM_BK = 32;
+inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);

@@ -12,6 +12,9 @@
 //
 // Config (BK, OCC, MT): K-tile depth, workgroups per CU for the launch bounds, MFMA tiles per wave
 // along M.  tools/gemm_bench.hip A/B-tests them on the generator's convolutions.
+#include <algorithm>
+#include <cstdlib>
+
 #include "gemm.h"
 
 namespace damc {
@@ -31,7 +34,69 @@ struct TileCfg {
   static constexpr int BROWS_S = BK / 2;         // B scalar loads per thread
 };
 
-template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT>
+// ---- epilogue: lane holds col = lane&31, rows (r&3) + 8(r>>2) + 4(lane>>5) of each 32x32 tile
+// output row offset of GEMM row m (O_PHASE: pixel (b, 2qy+py, 2qx+px) of the Hout x Wout map)
+template <int OM>
+__device__ __forceinline__ long gemm_row_offset(const GemmArgs& p, int m, int py, int px) {
+  if (OM == O_PHASE) {
+    const int hwq = p.Hq * p.Wq;
+    const int b = m / hwq;
+    const int rr = m - b * hwq;
+    const int qy = rr / p.Wq, qx = rr - qy * p.Wq;
+    return (((long)b * p.Hout + 2 * qy + py) * p.Wout + 2 * qx + px) * p.ldc;
+  }
+  return (long)m * p.ldc;
+}
+
+// rowtab: optional per-block table of gemm_row_offset for rows m0 .. m0 + 32*MT*2 - 1
+template <int EPI, int OM, int MT>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[MT][2], int m0, int n0, int wm,
+                                              int wn, int lane, int z, int py, int px,
+                                              const long* rowtab = nullptr) {
+  const int lrow = lane & 31;
+  float* Cz = p.C;
+  if (OM == O_DENSE) Cz += (long)z * p.c_zstride;
+  const bool bias_wrap = p.bias_mod < p.N;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ml = wm * (32 * MT) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int m = m0 + ml;
+      if (m >= p.M) continue;
+      const long rowoff = rowtab ? rowtab[ml] : gemm_row_offset<OM>(p, m, py, px);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + j * 32 + lrow;
+        if (n >= p.N) continue;
+        float v = acc[i][j][r];
+        const long idx = rowoff + n;
+        if (EPI == EPI_BIAS_ACT) {
+          if (p.bias) v += p.bias[bias_wrap ? n % p.bias_mod : n];
+          v = act_apply(v, p.act, p.slope);
+        } else if (EPI == EPI_MASK) {
+          v *= act_grad_from_out(p.mask[idx], p.mask_act, p.mask_slope);
+        } else if (EPI == EPI_RESID) {
+          if (p.bias) v += p.bias[n % p.bias_mod];
+          const float t = act_apply(v, p.act, p.slope);
+          if (p.xhat) p.xhat[idx] = t;
+          const float res = t - p.xres[idx];
+          if (p.sqerr) atomicAdd(p.sqerr, 0.5f * p.inv_s2 * res * res);
+          v = res * p.inv_s2 * act_grad_from_out(t, p.act, p.slope);
+        }
+        Cz[idx] = v;
+      }
+    }
+  }
+}
+
+// XCD-aware bijective remap: consecutive work-group ids land on one XCD (dispatch is round-robin over 8)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT, int SCHED>
 __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
   typedef TileCfg<BK, MT> C;
   constexpr int BM = C::BM;
@@ -44,10 +109,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
   const int wm = wave >> 1, wn = wave & 1;
 
   // ---- XCD-aware tile remap (bijective for any grid size)
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntn = (p.N + BN - 1) / BN;
   const int tm = wgid / ntn, tn = wgid - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -242,73 +304,437 @@ __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
       fb[s2][0] = bs[kk * C::LDB + bn0];
       fb[s2][1] = bs[kk * C::LDB + bn0 + 32];
     }
-    if (kt + 1 < nk) {
-      store_a(cur ^ 1);
-      store_b(cur ^ 1);
-      if (kt + 2 < nk) {
-        load_a(kbeg + (kt + 2) * BK);
-        load_b(kbeg + (kt + 2) * BK);
+    auto mfma_steps = [&](int s_lo, int s_hi) {
+#pragma unroll
+      for (int s2 = 0; s2 < BK / 2; ++s2) {
+        if (s2 < s_lo || s2 >= s_hi) continue;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][0], acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][1], acc[i][1], 0, 0, 0);
+        }
       }
+    };
+    auto stage_next = [&]() {
+      if (kt + 1 < nk) {
+        store_a(cur ^ 1);
+        store_b(cur ^ 1);
+        if (kt + 2 < nk) {
+          load_a(kbeg + (kt + 2) * BK);
+          load_b(kbeg + (kt + 2) * BK);
+        }
+      }
+    };
+    if (SCHED == 0) {
+      stage_next();
+      mfma_steps(0, BK / 2);
+    } else if (SCHED == 1) {
+      // keep the MFMA block before the barrier (hipcc otherwise hoists the barrier and its
+      // lgkmcnt(0) above the MFMAs, serialising the LDS writes in front of them)
+      stage_next();
+      mfma_steps(0, BK / 2);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      // first half of the MFMAs, then the LDS writes + next global loads, then the second half
+      mfma_steps(0, BK / 4);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_next();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_steps(BK / 4, BK / 2);
+      __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int s2 = 0; s2 < BK / 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][0], acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][i], fb[s2][1], acc[i][1], 0, 0, 0);
-      }
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds col = lane&31, rows (r&3) + 8(r>>2) + 4(lane>>5) of each 32x32 tile
-  float* Cz = p.C;
-  if (OM == O_DENSE) Cz += (long)z * p.c_zstride;
+  gemm_epilogue<EPI, OM, MT>(p, acc, m0, n0, wm, wn, lane, z, py, px);
+}
+
+// ================================================================================================
+// K-major convolution engine (A_CONV with Cg % 32 == 0, B packed [n][k]).
+//
+// Both operands are staged k-contiguous: a global float4 (4 consecutive channels of one pixel, or 4
+// consecutive k of one weight row) -> one ds_write_b128 -> the MFMA fragments come back as
+// ds_read_b128 through a k-permutation (MFMA step s of k-quad q uses k = 8q + 4(lane>>5) + s, the same
+// bijection on A and B, so every lane's 4 consecutive steps are one 16-B read).  Rows are padded to
+// 36 floats: any 16 consecutive rows then cover all 64 banks, which makes both the b128 reads (16-lane
+// groups of rows) and the b128 writes (8-lane groups along one row) conflict-free.
+// Since a 32-wide K tile never straddles a filter tap, the tap walk is a scalar counter; each A row
+// carries a bitmask of the taps that land inside the image (computed once), and every load is a
+// buffer load whose offset is pushed out of the descriptor's range when the tap is padding, so the
+// hardware returns zeros -- no per-load bounds arithmetic or exec-mask branches in the K loop.
+constexpr int KM_BM = 128;
+constexpr int KM_RS = KM_BK + 4;
+constexpr unsigned KM_OOB = 0xF0000000u;  // any offset >= the descriptor size reads as zero
+
+// PIPE 0: per tile {fragments of tile kt -> regs, stage tile kt+1, load tile kt+2, MFMAs, barrier}.
+// PIPE 1: fragments register-prefetched one tile ahead; per tile {barrier, fragments of kt+1 -> regs,
+//         stage tile kt+2, load tile kt+3, MFMAs of kt} so the MFMA operands are resident when the
+//         barrier releases and the LDS traffic runs under the MFMAs.
+#ifndef DAMC_KM_PIPE
+#define DAMC_KM_PIPE 3
+#endif
+// DBG (timing experiments only, wrong results): 1 = every row loads the same cache lines,
+// 2 = no global loads in the K loop
+template <int EPI, int OM, int PIPE = DAMC_KM_PIPE, int DBG = 0>
+__global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
+  constexpr int BK = KM_BK, RS = KM_RS, BM = KM_BM, MT = 2;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * RS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * RS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = (p.N + BN - 1) / BN;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int z = blockIdx.z;
+
+  int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
+  const float* Bg = p.B;
+  if (OM == O_PHASE) {
+    py = z >> 1;
+    px = z & 1;
+    pad_y = 1 - py;
+    pad_x = 1 - px;
+    Bg += (long)z * p.b_zstride;
+  }
+  const int Cg = p.Cg, kw = p.kw, Win = p.Win;
+  const int nk = p.K / BK;
+  const int kh = p.K / Cg / kw;
+  const int hwq = p.Hq * p.Wq;
+  const int nimg = (p.M + hwq - 1) / hwq;
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, nimg * p.Hin * Win * Cg * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Bg, (short)0, p.N * (int)p.ldb * 4, 0x00020000);
+
+  // ---- per-thread rows: A rows / B rows (tid>>3) + 32j, float4 slot tid&7 of the K tile
+  const int q4 = tid & 7, r0 = tid >> 3;
+  int abase[4];
+  unsigned amask[4], boff[4];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + r0 + 32 * j;
+    unsigned msk = 0;
+    int base = 0;
+    if (m < p.M) {
+      const int b = m / hwq;
+      const int r = m - b * hwq;
+      const int qy = r / p.Wq, qx = r - qy * p.Wq;
+      const int iy0 = qy * p.stride - pad_y, ix0 = qx * p.stride - pad_x;
+      base = ((b * p.Hin + iy0) * Win + ix0) * Cg;
+      for (int ky = 0; ky < kh; ++ky)
+        for (int kx = 0; kx < kw; ++kx)
+          if ((unsigned)(iy0 + ky) < (unsigned)p.Hin && (unsigned)(ix0 + kx) < (unsigned)Win)
+            msk |= 1u << (ky * kw + kx);
+    }
+    abase[j] = base * 4 + q4 * 16;
+    amask[j] = msk;
+    boff[j] = (unsigned)((n0 + r0 + 32 * j) * (int)p.ldb * 4 + q4 * 16);  // rows >= N fall out of range
+    if (DBG == 1) {
+      abase[j] = q4 * 16;
+      amask[j] = 0xFFFFFFFFu;
+      boff[j] = q4 * 16;
+    }
+  }
+
+  // ---- scalar tap walk over the K tiles still to be loaded
+  int tap = 0, tky = 0, tkx = 0, ci0 = 0;
+  unsigned aoff[4];
+  auto set_tap = [&]() {
+    const int toff = DBG == 1 ? 0 : (tky * Win + tkx) * Cg * 4;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * (32 * MT) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m >= p.M) continue;
-      long rowoff;
-      if (OM == O_PHASE) {
-        const int b = m / hwq;
-        const int rr = m - b * hwq;
-        const int qy = rr / p.Wq, qx = rr - qy * p.Wq;
-        rowoff = (((long)b * p.Hout + 2 * qy + py) * p.Wout + 2 * qx + px) * p.ldc;
-      } else {
-        rowoff = (long)m * p.ldc;
+    for (int j = 0; j < 4; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
+  };
+  set_tap();
+  f32x4 ra[4], rb[4];
+  auto load_ab = [&](int k0) {
+    if (DBG == 2) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      ra[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)aoff[j], DBG == 1 ? 0 : ci0 * 4, 0));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      rb[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)boff[j], DBG == 1 ? 0 : k0 * 4, 0));
+    ci0 += BK;
+    if (ci0 == Cg) {
+      ci0 = 0;
+      ++tap;
+      if (++tkx == kw) {
+        tkx = 0;
+        ++tky;
       }
+      set_tap();
+    }
+  };
+  // branch-free form for the interleaved pipelines (one basic block per K step): a tile past the end
+  // of K loads nothing (every offset out of range) and the tap walk advances with selects
+  auto load_ab_nb = [&](int k0) {
+    const bool live = k0 < p.K;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + j * 32 + lrow;
-        if (n >= p.N) continue;
-        float v = acc[i][j][r];
-        const long idx = rowoff + n;
-        if (EPI == EPI_BIAS_ACT) {
-          if (p.bias) v += p.bias[n % p.bias_mod];
-          v = act_apply(v, p.act, p.slope);
-        } else if (EPI == EPI_MASK) {
-          v *= act_grad_from_out(p.mask[idx], p.mask_act, p.mask_slope);
-        } else if (EPI == EPI_RESID) {
-          if (p.bias) v += p.bias[n % p.bias_mod];
-          const float t = act_apply(v, p.act, p.slope);
-          if (p.xhat) p.xhat[idx] = t;
-          const float res = t - p.xres[idx];
-          if (p.sqerr) atomicAdd(p.sqerr, 0.5f * p.inv_s2 * res * res);
-          v = res * p.inv_s2 * act_grad_from_out(t, p.act, p.slope);
+    for (int j = 0; j < 4; ++j)
+      ra[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(live ? aoff[j] : KM_OOB), ci0 * 4, 0));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      rb[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)(live ? boff[j] : KM_OOB), k0 * 4, 0));
+    ci0 += BK;
+    const int wrap = ci0 == Cg;
+    ci0 = wrap ? 0 : ci0;
+    tap = min(tap + wrap, 31);
+    tkx += wrap;
+    const int wx = tkx == kw;
+    tkx = wx ? 0 : tkx;
+    tky += wx;
+    set_tap();
+  };
+  auto store_ab = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *reinterpret_cast<f32x4*>(&As[buf][(r0 + 32 * j) * RS + 4 * q4]) = ra[j];
+      *reinterpret_cast<f32x4*>(&Bs[buf][(r0 + 32 * j) * RS + 4 * q4]) = rb[j];
+    }
+  };
+
+  f32x16 acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lrow = lane & 31, lk = lane >> 5;
+  const int afr = (wm * 64 + lrow) * RS + 4 * lk, bfr = (wn * 64 + lrow) * RS + 4 * lk;
+  auto read_frags = [&](int buf, f32x4 (&fa)[4][MT], f32x4 (&fb)[4][2]) {
+    const float* as = As[buf];
+    const float* bs = Bs[buf];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) fa[q][i] = *reinterpret_cast<const f32x4*>(as + afr + 32 * i * RS + 8 * q);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[q][j] = *reinterpret_cast<const f32x4*>(bs + bfr + 32 * j * RS + 8 * q);
+    }
+  };
+  auto mfma_tile = [&](const f32x4 (&fa)[4][MT], const f32x4 (&fb)[4][2]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][s2], fb[q][0][s2], acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][s2], fb[q][1][s2], acc[i][1], 0, 0, 0);
         }
-        Cz[idx] = v;
+  };
+
+  constexpr int SG_MFMA = 0x8, SG_VMEM_RD = 0x20, SG_DS_RD = 0x100, SG_DS_WR = 0x200;
+  if (PIPE == 0 || PIPE == 2) {  // PIPE >= 3: the prefetch structure below
+    if (nk > 0) {
+      load_ab(0);
+      store_ab(0);
+      if (nk > 1) load_ab(BK);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      f32x4 fa[4][MT], fb[4][2];
+      if (PIPE == 0) {
+        read_frags(cur, fa, fb);
+        if (kt + 1 < nk) {
+          store_ab(cur ^ 1);
+          if (kt + 2 < nk) load_ab((kt + 2) * BK);
+        }
+        mfma_tile(fa, fb);
+      } else {
+        // stores past the last tile land in the buffer nobody reads again; loads past K are empty
+        read_frags(cur, fa, fb);
+        store_ab(cur ^ 1);
+        load_ab_nb((kt + 2) * BK);
+        mfma_tile(fa, fb);
+        // the first k-quad's 4 fragments, then the remaining reads, stores and loads one per MFMA
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 4, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_WR, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_VMEM_RD, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 36, 0);
+      }
+      __syncthreads();
+    }
+  } else {
+    // prologue: tiles 0 and 1 staged, tile 2 in flight, fragments of tile 0 resident
+    if (nk > 0) {
+      load_ab(0);
+      store_ab(0);
+      if (nk > 1) {
+        load_ab(BK);
+        store_ab(1);
+        if (nk > 2) load_ab(2 * BK);
       }
     }
+    __syncthreads();
+    f32x4 f0a[4][MT], f0b[4][2], f1a[4][MT], f1b[4][2];
+    if (nk > 0) read_frags(0, f0a, f0b);
+    auto step = [&](int kt, const f32x4 (&fca)[4][MT], const f32x4 (&fcb)[4][2], f32x4 (&fna)[4][MT],
+                    f32x4 (&fnb)[4][2]) {
+      __syncthreads();
+      if (PIPE == 1) {
+        if (kt + 1 < nk) read_frags((kt + 1) & 1, fna, fnb);
+        if (kt + 2 < nk) {
+          store_ab(kt & 1);
+          if (kt + 3 < nk) load_ab((kt + 3) * BK);
+        }
+        mfma_tile(fca, fcb);
+      } else {
+        read_frags((kt + 1) & 1, fna, fnb);
+        store_ab(kt & 1);
+        load_ab_nb((kt + 3) * BK);
+        mfma_tile(fca, fcb);
+        // one LDS read / LDS write / global load per MFMA gap, so every wave always has MFMAs ready
+        if (PIPE == 3) {  // 16 reads, 8 writes, 8 loads on the first 32 MFMAs
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_WR, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_VMEM_RD, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 32, 0);
+        } else if (PIPE == 4) {  // the same order spread over all 64 MFMAs
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_WR, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_VMEM_RD, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          }
+        } else {  // PIPE 5: global loads first (they have the longest latency), then reads, then writes
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_WR, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_VMEM_RD, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 32, 0);
+        }
+      }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, f0a, f0b, f1a, f1b);
+      if (kt + 1 < nk) step(kt + 1, f1a, f1b, f0a, f0b);
+    }
+  }
+  if (OM == O_PHASE) {
+    // one row-offset division per row instead of one per (row, lane): table in the (drained) A buffer
+    long* rowtab = reinterpret_cast<long*>(&As[0][0]);
+    __syncthreads();
+    if (tid < BM) rowtab[tid] = gemm_row_offset<OM>(p, m0 + tid, py, px);
+    __syncthreads();
+    gemm_epilogue<EPI, OM, MT>(p, acc, m0, n0, wm, wn, lane, z, py, px, rowtab);
+  } else {
+    gemm_epilogue<EPI, OM, MT>(p, acc, m0, n0, wm, wn, lane, z, py, px);
   }
 }
 
-template <int AM, int EPI, int OM, bool BV, int BK, int OCC, int MT>
+template <int EPI, int OM, int PIPE = DAMC_KM_PIPE, int DBG = 0>
+static void launch_km_t(const GemmArgs& a, int zdim, hipStream_t s) {
+  const int ntm = (a.M + KM_BM - 1) / KM_BM, ntn = (a.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_km_kernel<EPI, OM, PIPE, DBG>), dim3(ntm * ntn, 1, zdim), dim3(256), 0, s, a);
+}
+
+// K-major dispatch; splits the batch so every launch's gathered tensor stays below 2^31 bytes
+static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
+  const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
+  if (!conv_kmajor_ok(a.Cg) || taps * a.Cg != a.K || a.kw <= 0 || taps % a.kw != 0 || taps > 32) return DAMC_ERR_ARG;
+  if ((om == O_PHASE && zdim != 4) || (om == O_DENSE && (zdim != 1 || a.k_per_z < a.K))) return DAMC_ERR_ARG;
+  if (a.ldb < a.K || ((uintptr_t)a.A | (uintptr_t)a.B) % 16 != 0 || (a.ldb % 4) != 0) return DAMC_ERR_ARG;
+  if ((double)a.N * a.ldb * 4 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
+  const long hwq = (long)a.Hq * a.Wq;
+  if (a.M % hwq != 0) return DAMC_ERR_ARG;
+  const long img = (long)a.Hin * a.Win * a.Cg;  // floats per gathered image
+  const long nimg = a.M / hwq;
+  // DAMC_KM_CHUNK_BYTES lowers the per-launch limit (tests exercise the chunked path on small inputs)
+  static const long lim = [] {
+    const char* e = getenv("DAMC_KM_CHUNK_BYTES");
+    const long v = e ? atol(e) : 0;
+    return (v > 0 && v < 2147483647L) ? v : 2147483647L;
+  }();
+  const long per = (lim / 4 - 1) / img;
+  if (per < 1) return DAMC_ERR_UNSUPPORTED;
+  const long cimg = (om == O_PHASE) ? (long)a.Hout * a.Wout * a.ldc : hwq * a.ldc;  // output floats per image
+  for (long b0 = 0; b0 < nimg; b0 += per) {
+    const long nb = std::min(per, nimg - b0);
+    GemmArgs c = a;
+    c.A = a.A + b0 * img;
+    c.C = a.C + b0 * cimg;
+    if (a.mask) c.mask = a.mask + b0 * cimg;
+    c.M = (int)(nb * hwq);
+#define DAMC_KM(E_, O_)                \
+  if (epi == E_ && om == O_) {         \
+    launch_km_t<E_, O_>(c, zdim, s);   \
+    continue;                          \
+  }
+    DAMC_KM(EPI_BIAS_ACT, O_PHASE)
+    DAMC_KM(EPI_MASK, O_DENSE)
+    DAMC_KM(EPI_BIAS_ACT, O_DENSE)
+    DAMC_KM(EPI_STORE, O_DENSE)
+#undef DAMC_KM
+    return DAMC_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+#ifndef DAMC_GEMM_SCHED
+#define DAMC_GEMM_SCHED 0  // hipcc's own placement measured best (profiles/r01/gemm_bench.txt)
+#endif
+template <int AM, int EPI, int OM, bool BV, int BK, int OCC, int MT, int SCHED = DAMC_GEMM_SCHED>
 static void launch_t(const GemmArgs& a, int zdim, hipStream_t s) {
   const int bm = 64 * MT;
   const int ntm = (a.M + bm - 1) / bm, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, zdim);
-  hipLaunchKernelGGL((gemm_f32_kernel<AM, EPI, OM, BV, BK, OCC, MT>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_f32_kernel<AM, EPI, OM, BV, BK, OCC, MT, SCHED>), grid, dim3(256), 0, s, a);
 }
 
 // tile configuration used by the library (tools/gemm_bench.hip A/B-tests alternatives)
@@ -325,6 +751,11 @@ static void launch_t(const GemmArgs& a, int zdim, hipStream_t s) {
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return DAMC_ERR_ARG;
+  if (a.b_kmajor) {
+    if (am != A_CONV) return DAMC_ERR_ARG;
+    ProfScope ps(prof_name, flops, s);
+    return launch_gemm_km(a, epi, om, zdim, s);
+  }
   // 32-bit element offsets inside the kernel
   const double a_elems = (am == A_DENSE) ? (double)a.M * a.lda : (double)a.Hin * a.Win * a.Cg * ((double)a.M / ((double)a.Hq * a.Wq) + 1);
   if (a_elems >= 2147483647.0 || (double)a.K * a.ldb >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;

@@ -41,7 +41,9 @@ __global__ void pack_proj_kernel(const float* w, int cin, int cout, int k, float
 }
 // UP2 (k4 s2 p1): fwd [phase(py,px)][ty][tx][ci][co] = W[ci][co][3-py-2ty][3-px-2tx];
 //                 bwd [ky][kx][co][ci] = W[ci][co][ky][kx]
-__global__ void pack_up2_kernel(const float* w, int cin, int cout, float* wf, float* wb) {
+// or, for the K-major engine (conv_kmajor_ok of the gathered channel count), the same matrices
+// transposed to [n][k]: fwd [phase][co][ty][tx][ci], bwd [ci][ky][kx][co]
+__global__ void pack_up2_kernel(const float* w, int cin, int cout, int km_f, int km_b, float* wf, float* wb) {
   const long n = (long)cin * cout * 16;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -57,8 +59,14 @@ __global__ void pack_up2_kernel(const float* w, int cin, int cout, float* wf, fl
   const int py = (3 - ky) & 1, ty = (3 - ky - py) >> 1;
   const int px = (3 - kx) & 1, tx = (3 - kx - px) >> 1;
   const int phase = py * 2 + px;
-  wf[((((long)phase * 2 + ty) * 2 + tx) * cin + ci) * cout + co] = v;
-  wb[(((long)ky * 4 + kx) * cout + co) * cin + ci] = v;
+  if (km_f)
+    wf[(((long)phase * cout + co) * 4 + ty * 2 + tx) * cin + ci] = v;
+  else
+    wf[((((long)phase * 2 + ty) * 2 + tx) * cin + ci) * cout + co] = v;
+  if (km_b)
+    wb[(((long)ci * 4 + ky) * 4 + kx) * cout + co] = v;
+  else
+    wb[(((long)ky * 4 + kx) * cout + co) * cin + ci] = v;
 }
 // SMALLC: fwd [ky][kx][ci][co]; bwd (the two-stage projection) [(ky*k+kx)*cout + co][ci] (rows padded
 // to a multiple of 32 with zeros by the caller's memset)
@@ -846,7 +854,8 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.kw = 2;
       a.stride = 1;
       a.B = L.w_fwd;
-      a.ldb = L.cout;
+      a.b_kmajor = damc::conv_kmajor_ok(L.cin);
+      a.ldb = a.b_kmajor ? 4L * L.cin : L.cout;
       a.b_zstride = 4L * L.cin * L.cout;
       a.ldc = L.cout;
       a.M = B * L.hin * L.win;
@@ -924,7 +933,8 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
       a.pad_y = 1;
       a.pad_x = 1;
       a.B = L.w_bwd;
-      a.ldb = L.cin;
+      a.b_kmajor = damc::conv_kmajor_ok(L.cout);
+      a.ldb = a.b_kmajor ? 16L * L.cout : L.cin;
       a.C = out;
       a.ldc = L.cin;
       a.M = B * L.hin * L.win;
@@ -1011,7 +1021,8 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       break;
     case DAMC_LAYER_UP2:
       if (!wb || L->k != 4) return DAMC_ERR_ARG;
-      hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, wf, wb);
+      hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, (int)damc::conv_kmajor_ok(L->cin),
+                         (int)damc::conv_kmajor_ok(L->cout), wf, wb);
       break;
     case DAMC_LAYER_SMALLC:
       if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));

@@ -192,3 +192,31 @@ def test_verbose_diagnostics_match_oracle(lv, gpu_device):
     want = [float(e.sum()), float(lik), float(0.5 * (z0.cpu() ** 2).sum()), float((gl + ge + z0.cpu()).mean())]
     assert np.allclose(d[:3], want[:3], rtol=1e-4, atol=1e-4)
     assert abs(d[3] - want[3]) < 1e-4 * max(1.0, abs(want[3]))
+
+
+def test_kmajor_batch_chunking_is_bitwise(lv, gpu_device, tmp_path):
+    """The K-major conv engine splits the batch when a gathered tensor would reach 2^31 bytes (the
+    full-width CelebA-HQ dgrad at B=64 does).  A child process forced to ~3 MB chunks
+    (DAMC_KM_CHUNK_BYTES) must reproduce the unchunked forward and gradient bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import PKG, REPO
+
+    G, E, x, z0 = _cifar_full(gpu_device, 8)
+    g = lv.likelihood_grad(z0, x, G, 0.1).cpu().numpy()
+    xh = lv.generator_forward(z0, G).cpu().numpy()
+    out = str(tmp_path / "chunked.npz")
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path[:0] = [{os.path.join(REPO, 'tests')!r}, {PKG!r}, {REPO!r}]\n"
+        "import test_gpu_langevin as t\n"
+        "from damc import langevin as lv\n"
+        "G, E, x, z0 = t._cifar_full('cuda:0', 8)\n"
+        f"np.savez({out!r}, g=lv.likelihood_grad(z0, x, G, 0.1).cpu().numpy(),"
+        " xh=lv.generator_forward(z0, G).cpu().numpy())\n")
+    env = dict(os.environ, DAMC_KM_CHUNK_BYTES=str(3 << 20))
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=600)
+    r = np.load(out)
+    assert np.array_equal(r["g"], g) and np.array_equal(r["xh"], xh)

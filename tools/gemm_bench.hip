@@ -1,6 +1,11 @@
 // gemm_bench.hip — A/B the implicit-GEMM tile configurations on the four CIFAR-10 B=128 generator
 // convolutions (upconv fwd L2/L3, upconv dgrad L3/L2), interleaved in one process (guide §5.4 r24).
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DDAMC_GEMM_NO_C_API tools/gemm_bench.hip -o gemm_bench
+#ifndef KMCHK
+#define KMCHK 0
+#endif
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -42,14 +47,42 @@ struct Shape {
   GemmArgs a;
   bool phase;
   double flops;
+  float* bt;  // weights transposed per phase to [n][k] for the K-major engine
 };
 
-template <int BK, int OCC, int MT>
+// per-phase transpose of B[K][N] (ldb = N) into Bt[N][K]
+static float* transpose_b(const float* dB, int nz, int K, int N) {
+  std::vector<float> h((size_t)nz * K * N), t((size_t)nz * K * N);
+  CK(hipMemcpy(h.data(), dB, h.size() * 4, hipMemcpyDeviceToHost));
+  for (int z = 0; z < nz; ++z)
+    for (int k = 0; k < K; ++k)
+      for (int n = 0; n < N; ++n) t[((size_t)z * N + n) * K + k] = h[((size_t)z * K + k) * N + n];
+  float* d;
+  CK(hipMalloc(&d, t.size() * 4));
+  CK(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+template <int PIPE, int DBG = 0>
+void run_km(const Shape& sh, hipStream_t s) {
+  static_assert(PIPE >= 0 && PIPE <= 5, "pipe");
+  GemmArgs a = sh.a;
+  a.B = sh.bt;
+  a.b_kmajor = 1;
+  a.ldb = a.K;
+  a.b_zstride = (long)a.N * a.K;
+  if (sh.phase)
+    launch_km_t<EPI_BIAS_ACT, O_PHASE, PIPE, DBG>(a, 4, s);
+  else
+    launch_km_t<EPI_MASK, O_DENSE, PIPE, DBG>(a, 1, s);
+}
+
+template <int BK, int OCC, int MT, int SCHED>
 void run(const Shape& sh, hipStream_t s) {
   if (sh.phase)
-    launch_t<A_CONV, EPI_BIAS_ACT, O_PHASE, true, BK, OCC, MT>(sh.a, 4, s);
+    launch_t<A_CONV, EPI_BIAS_ACT, O_PHASE, true, BK, OCC, MT, SCHED>(sh.a, 4, s);
   else
-    launch_t<A_CONV, EPI_MASK, O_DENSE, true, BK, OCC, MT>(sh.a, 1, s);
+    launch_t<A_CONV, EPI_MASK, O_DENSE, true, BK, OCC, MT, SCHED>(sh.a, 1, s);
 }
 
 int main(int argc, char** argv) {
@@ -76,7 +109,7 @@ int main(int argc, char** argv) {
     a.B = w; a.ldb = cout; a.b_zstride = 4L * cin * cout; a.C = out; a.ldc = cout;
     a.M = B * H * H; a.N = cout; a.K = 4 * cin; a.Hout = 2 * H; a.Wout = 2 * H;
     a.bias = bias; a.bias_mod = cout; a.act = DAMC_ACT_LRELU; a.slope = 0.2f;
-    shapes.push_back({nm, a, true, 2.0 * B * 4 * H * H * (double)cout * 4 * cin});
+    shapes.push_back({nm, a, true, 2.0 * B * 4 * H * H * (double)cout * 4 * cin, transpose_b(w, 4, 4 * cin, cout)});
   };
   auto dg = [&](const char* nm, float* din, int Hout, int cout, int cin, float* w, float* out) {
     GemmArgs a;
@@ -84,7 +117,7 @@ int main(int argc, char** argv) {
     a.pad_y = 1; a.pad_x = 1; a.B = w; a.ldb = cin; a.C = out; a.ldc = cin;
     a.M = B * (Hout / 2) * (Hout / 2); a.N = cin; a.K = 16 * cout; a.k_per_z = a.K;
     a.mask = out; a.mask_act = DAMC_ACT_LRELU; a.mask_slope = 0.2f;
-    shapes.push_back({nm, a, false, 2.0 * a.M * (double)a.N * a.K});
+    shapes.push_back({nm, a, false, 2.0 * a.M * (double)a.N * a.K, transpose_b(w, 1, a.K, a.N)});
   };
   up("L2 fwd  8->16 1024->512", h1, 8, 8 * ngf, 4 * ngf, w2, o2);
   up("L3 fwd 16->32  512->256", h2, 16, 4 * ngf, 2 * ngf, w3, o3);
@@ -93,9 +126,48 @@ int main(int argc, char** argv) {
 
   typedef void (*RunFn)(const Shape&, hipStream_t);
   struct V { const char* name; RunFn fn; };
-  V vars[] = {{"BK16/2/MT2", run<16, 2, 2>}, {"BK32/2/MT2", run<32, 2, 2>}, {"BK16/1/MT4", run<16, 1, 4>},
-              {"BK16/2/MT4", run<16, 2, 4>}};
+  V vars[] = {{"BK32/2/MT2/s0", run<32, 2, 2, 0>}, {"KM/p0", run_km<0>}, {"KM/p2", run_km<2>},
+              {"KM/p3", run_km<3>}, {"KM/p4", run_km<4>}, {"KM/p5", run_km<5>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
+  // correctness: the K-major engine against the generic engine on the same problem (own output and
+  // mask buffers; the k order differs, so agreement is to fp32 rounding, not bitwise)
+  for (size_t si = 0; si < shapes.size(); ++si) {
+    Shape sh = shapes[si];
+    const GemmArgs& a0 = sh.a;
+    const size_t nout = sh.phase ? (size_t)B * a0.Hout * a0.Wout * a0.ldc : (size_t)a0.M * a0.ldc;
+    float *c1, *c2;
+    CK(hipMalloc(&c1, nout * 4));
+    CK(hipMalloc(&c2, nout * 4));
+    float* mk = rnd(nout, 99);
+    Shape s1 = sh;
+    s1.a.C = c1;
+    s1.a.mask = mk;
+    run<32, 2, 2, 0>(s1, s);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> h1(nout), h2(nout);
+    CK(hipMemcpy(h1.data(), c1, nout * 4, hipMemcpyDeviceToHost));
+    void (*kms[6])(const Shape&, hipStream_t) = {run_km<0>, run_km<1>, run_km<2>, run_km<3>, run_km<4>, run_km<5>};
+    printf("check %-28s max|generic-km|", sh.name);
+    for (int v = 0; v < 6; ++v) {
+      Shape s2 = sh;
+      s2.a.C = c2;
+      s2.a.mask = mk;
+      CK(hipMemset(c2, 0, nout * 4));
+      kms[v](s2, s);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(h2.data(), c2, nout * 4, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (size_t i = 0; i < nout; ++i) {
+        md = std::max(md, (double)std::fabs(h1[i] - h2[i]));
+        mx = std::max(mx, (double)std::fabs(h1[i]));
+      }
+      printf("  p%d %.2e", v, md / mx);
+    }
+    printf("  (relative to max|c|)\n");
+    CK(hipFree(c1));
+    CK(hipFree(c2));
+    CK(hipFree(mk));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
