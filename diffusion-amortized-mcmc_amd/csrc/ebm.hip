@@ -5,24 +5,30 @@
 //   grad_z E = W1^T [ lrelu'(a1) * W2^T ( lrelu'(a2) * w3 ) ]
 // A workgroup owns R chains (rows).  Rows are independent, so the chains never communicate:
 // the prior kernel runs every step with z resident in LDS.  At R <= 8 rows per workgroup the
-// three FC layers are tiny-M GEMMs; on the VALU each weight element is loaded once per step
-// (coalesced across the 256 lanes) and reused R times from registers.
+// FC layers are tiny-M GEMMs bound by latency, not FLOPs: each layer splits its K axis over the
+// 1024-thread workgroup (float4 weight columns x strided k-groups, all loads of a thread in flight
+// at once) and adds the k-group partials in a fixed order in LDS.
 #include "common.h"
 
 namespace {
 
+constexpr int EBM_THREADS = 1024;  // 16 waves: the K axis of every layer is split over the workgroup
+
 struct EbmSmem {
-  float* zs;  // [R][nz]
-  float* h1;  // [R][nh]  lrelu(a1)
-  float* h2;  // [R][nh]  lrelu(a2)
-  float* g2;  // [R][nh]
-  float* g1;  // [R][nh]
-  float* gz;  // [R][nz]
-  float* red; // [8]
+  float* zs;   // [R][nz]
+  float* h1;   // [R][nh]  lrelu(a1)
+  float* h2;   // [R][nh]  lrelu(a2)
+  float* g2;   // [R][nh]
+  float* g1;   // [R][nh]
+  float* gz;   // [R][nz]
+  float* red;  // [32]
+  float* part; // [G][R][N] k-group partial sums, G*N <= 4*EBM_THREADS (+ scalar-path slack)
 };
 
+__host__ __device__ inline size_t ebm_part_floats(int R) { return (size_t)R * (4 * EBM_THREADS + 4 * 256); }
+
 __host__ __device__ inline size_t ebm_smem_floats(int R, int nz, int nh) {
-  return (size_t)R * nz * 2 + (size_t)R * nh * 4 + 8;
+  return (size_t)R * nz * 2 + (size_t)R * nh * 4 + 32 + ebm_part_floats(R);
 }
 
 __device__ inline EbmSmem ebm_carve(float* base, int R, int nz, int nh) {
@@ -34,93 +40,105 @@ __device__ inline EbmSmem ebm_carve(float* base, int R, int nz, int nh) {
   s.g1 = s.g2 + R * nh;
   s.gz = s.g1 + R * nh;
   s.red = s.gz + R * nz;
+  s.part = s.red + 32;
   return s;
 }
 
+// One fully connected layer for R rows: y[r][n] = sum_k W[k*N + n] x[r][k]  (W k-major, n contiguous).
+// Thread t owns the float4 column group nq = t % NQ and the k-group kg = t / NQ (k = kg, kg+G, ...), so
+// each thread's ~K/G weight loads are independent and all in flight at once; the G partial sums are
+// then added in k-group order by fin(r, n, sum) (a fixed order: deterministic, batch-independent).
+// Ends with a barrier.
+template <int R, typename Fin>
+__device__ __forceinline__ void fc_rows(const float* __restrict__ W, int K, int N, const float* x, float* part,
+                                        Fin fin) {
+  const int tid = threadIdx.x;
+  const bool v4 = (N & 3) == 0;
+  const int NQ = v4 ? (N >> 2) : N;  // column groups (float4, or scalar when N % 4 != 0)
+  const int G = EBM_THREADS / NQ;
+  const int nq = tid % NQ, kg = tid / NQ;
+  if (kg < G) {
+    if (v4) {
+      f32x4 acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k = kg; k < K; k += G) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(W + (long)k * N + 4 * nq);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float xv = x[r * K + k];
+          acc[r].x = fmaf(w.x, xv, acc[r].x);
+          acc[r].y = fmaf(w.y, xv, acc[r].y);
+          acc[r].z = fmaf(w.z, xv, acc[r].z);
+          acc[r].w = fmaf(w.w, xv, acc[r].w);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) *reinterpret_cast<f32x4*>(part + ((long)kg * R + r) * N + 4 * nq) = acc[r];
+    } else {
+      float acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = 0.f;
+      for (int k = kg; k < K; k += G) {
+        const float w = W[(long)k * N + nq];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = fmaf(w, x[r * K + k], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) part[((long)kg * R + r) * N + nq] = acc[r];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < R * N; i += EBM_THREADS) {
+    float sum = part[i];
+    for (int g = 1; g < G; ++g) sum += part[(long)g * R * N + i];
+    fin(i / N, i - (i / N) * N, sum);
+  }
+  __syncthreads();
+}
+
 // Computes gz = grad_z sum_r E(z_r) for the R rows in s.zs; if energy != nullptr also writes
-// per-row energies (valid rows only).  All 256 threads participate; ends with a barrier.
+// per-row energies (valid rows only).  All EBM_THREADS threads participate; ends with a barrier.
 template <int R>
 __device__ void ebm_rows(const damc_ebm_t& e, EbmSmem& s, int nvalid, float* energy_rows) {
-  const int tid = threadIdx.x;
   const int nz = e.nz, nh = e.nh;
   const float sl = e.slope;
-  // layer 1: a1 = W1 z + b1   (w1t is (nz, nh): lane j streams column j)
-  for (int j = tid; j < nh; j += blockDim.x) {
-    float acc[R];
-    const float bj = e.b1[j];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = bj;
-#pragma unroll 8
-    for (int k = 0; k < nz; ++k) {
-      const float w = e.w1t[(long)k * nh + j];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.zs[r * nz + k], acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) s.h1[r * nh + j] = acc[r] > 0.f ? acc[r] : acc[r] * sl;
-  }
-  __syncthreads();
-  // layer 2: a2 = W2 h1 + b2 ; g2 = w3 * lrelu'(a2)
-  for (int j = tid; j < nh; j += blockDim.x) {
-    float acc[R];
-    const float bj = e.b2[j];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = bj;
-#pragma unroll 8
-    for (int k = 0; k < nh; ++k) {
-      const float w = e.w2t[(long)k * nh + j];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.h1[r * nh + k], acc[r]);
-    }
-    const float w3 = e.w3[j];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool pos = acc[r] > 0.f;
-      s.h2[r * nh + j] = pos ? acc[r] : acc[r] * sl;
-      s.g2[r * nh + j] = pos ? w3 : w3 * sl;
-    }
-  }
-  __syncthreads();
+  const float* b1 = e.b1;
+  const float* b2 = e.b2;
+  const float* w3 = e.w3;
+  float* h1 = s.h1;
+  float* h2 = s.h2;
+  float* g2 = s.g2;
+  float* g1 = s.g1;
+  float* gz = s.gz;
+  // layer 1: a1 = W1 z + b1 ; h1 = lrelu(a1)      (w1t is (nz, nh))
+  fc_rows<R>(e.w1t, nz, nh, s.zs, s.part, [&](int r, int j, float v) {
+    v += b1[j];
+    h1[r * nh + j] = v > 0.f ? v : v * sl;
+  });
+  // layer 2: a2 = W2 h1 + b2 ; h2 = lrelu(a2) ; g2 = w3 * lrelu'(a2)     (w2t is (nh, nh))
+  fc_rows<R>(e.w2t, nh, nh, h1, s.part, [&](int r, int j, float v) {
+    v += b2[j];
+    const bool pos = v > 0.f;
+    h2[r * nh + j] = pos ? v : v * sl;
+    g2[r * nh + j] = pos ? w3[j] : w3[j] * sl;
+  });
   // energies (optional): e_r = w3 . h2_r + b3, one wave per row
   if (energy_rows) {
-    const int wave = tid >> 6, lane = tid & 63;
-    for (int r = wave; r < R; r += blockDim.x / 64) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int r = wave; r < R; r += EBM_THREADS / 64) {
       float v = 0.f;
-      for (int j = lane; j < nh; j += 64) v = fmaf(e.w3[j], s.h2[r * nh + j], v);
+      for (int j = lane; j < nh; j += 64) v = fmaf(w3[j], h2[r * nh + j], v);
       v = wave_sum(v);
       if (lane == 0 && r < nvalid) energy_rows[r] = v + e.b3[0];
     }
   }
-  // layer 2 backward: g1 = (W2^T g2) * lrelu'(a1)   (w2 is (nh, nh) row-major: lane k streams column k)
-  for (int k = tid; k < nh; k += blockDim.x) {
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < nh; ++j) {
-      const float w = e.w2[(long)j * nh + k];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.g2[r * nh + j], acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) s.g1[r * nh + k] = s.h1[r * nh + k] > 0.f ? acc[r] : acc[r] * sl;
-  }
-  __syncthreads();
-  // layer 1 backward: gz = W1^T g1   (w1 is (nh, nz))
-  for (int c = tid; c < nz; c += blockDim.x) {
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < nh; ++j) {
-      const float w = e.w1[(long)j * nz + c];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, s.g1[r * nh + j], acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) s.gz[r * nz + c] = acc[r];
-  }
-  __syncthreads();
+  // layer 2 backward: g1 = (W2^T g2) * lrelu'(a1)      (w2 is (nh, nh) = [j][k])
+  fc_rows<R>(e.w2, nh, nh, g2, s.part, [&](int r, int k, float v) {
+    g1[r * nh + k] = h1[r * nh + k] > 0.f ? v : v * sl;
+  });
+  // layer 1 backward: gz = W1^T g1                     (w1 is (nh, nz) = [j][c])
+  fc_rows<R>(e.w1, nh, nz, g1, s.part, [&](int r, int c, float v) { gz[r * nz + c] = v; });
 }
 
 __device__ __forceinline__ float noise_at(const float* noise, long noise_idx, int with_noise, uint64_t seed,
@@ -147,7 +165,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // ---- posterior update: g = sum_s lik_slab[s] + grad E + z ; z <- (z - c1 g) + step xi
 template <int R>
-__global__ __launch_bounds__(256) void posterior_update_kernel(damc_ebm_t e, int use_ebm, float* z, const float* slabs,
+__global__ __launch_bounds__(EBM_THREADS) void posterior_update_kernel(damc_ebm_t e, int use_ebm, float* z, const float* slabs,
                                                                 int nslab, long slab_stride, int B, int nz, float c1,
                                                                 float step, int with_noise, const float* noise,
                                                                 uint64_t seed, uint64_t step_idx, uint64_t chain_base,
@@ -204,7 +222,7 @@ __global__ __launch_bounds__(256) void posterior_update_kernel(damc_ebm_t e, int
 
 // ---- prior chain: every step in one launch, z resident in LDS
 template <int R>
-__global__ __launch_bounds__(256) void prior_chain_kernel(damc_ebm_t e, float* z, int B, int n_steps, float c1, float step,
+__global__ __launch_bounds__(EBM_THREADS) void prior_chain_kernel(damc_ebm_t e, float* z, int B, int n_steps, float c1, float step,
                                                            int with_noise, const float* noise, uint64_t seed,
                                                            uint64_t step_offset, uint64_t chain_base, float* diag) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -253,7 +271,7 @@ __global__ __launch_bounds__(256) void prior_chain_kernel(damc_ebm_t e, float* z
 }
 
 template <int R>
-__global__ __launch_bounds__(256) void ebm_energy_grad_kernel(damc_ebm_t e, const float* z, int B, float* energy,
+__global__ __launch_bounds__(EBM_THREADS) void ebm_energy_grad_kernel(damc_ebm_t e, const float* z, int B, float* energy,
                                                                float* grad) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nz = e.nz;
@@ -303,6 +321,13 @@ __global__ void philox_normal_kernel(float* out, int n_steps, int B, int nz, uin
 constexpr int RP = 2;  // prior chain
 constexpr int RU = 2;  // posterior update
 
+// fc_rows needs every layer width <= EBM_THREADS (one column group per thread at least) and the
+// carved LDS within the default 64 KB dynamic allocation
+bool ebm_shape_ok(int R, int nz, int nh) {
+  return nz > 0 && nz <= EBM_THREADS && nh >= 0 && nh <= EBM_THREADS &&
+         ebm_smem_floats(R, nz, nh) * sizeof(float) <= 65536;
+}
+
 }  // namespace
 
 // host helpers used by generator.hip
@@ -316,10 +341,11 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
     use_ebm = 1;
     if (ev.nz != nz) return DAMC_ERR_ARG;
   }
+  if (!ebm_shape_ok(RU, nz, use_ebm ? ev.nh : 0)) return DAMC_ERR_UNSUPPORTED;
   const float c1 = (float)(0.5 * (double)step * (double)step);
   const size_t sm = ebm_smem_floats(RU, nz, use_ebm ? ev.nh : 0) * sizeof(float);
   ProfScope ps("posterior_update", 0.0, s);
-  hipLaunchKernelGGL((posterior_update_kernel<RU>), dim3((B + RU - 1) / RU), dim3(256), sm, s, ev, use_ebm, z, slabs,
+  hipLaunchKernelGGL((posterior_update_kernel<RU>), dim3((B + RU - 1) / RU), dim3(EBM_THREADS), sm, s, ev, use_ebm, z, slabs,
                      nslab, slab_stride, B, nz, c1, step, with_noise, noise, seed, step_idx, chain_base, diag);
   return (int)hipGetLastError();
 }
@@ -331,13 +357,14 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
                                    float* diag, void* stream) {
   if (!e || !z || B <= 0 || n_steps < 0) return DAMC_ERR_ARG;
   if (!e->w1t || !e->w2t) return DAMC_ERR_ARG;
+  if (!ebm_shape_ok(RP, e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
   if (n_steps == 0) return 0;
   const float c1 = (float)(0.5 * (double)step * (double)step);
   const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
   ProfScope ps("prior_chain", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
-  hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(256), sm, s, *e, z, B, n_steps, c1, step,
+  hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, s, *e, z, B, n_steps, c1, step,
                      with_noise, noise, seed, step_offset, chain_base, diag);
   return (int)hipGetLastError();
 }
@@ -345,8 +372,9 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
 extern "C" int damc_ebm_energy_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad,
                                     void* stream) {
   if (!e || !z || !grad || B <= 0) return DAMC_ERR_ARG;
+  if (!ebm_shape_ok(RP, e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
-  hipLaunchKernelGGL((ebm_energy_grad_kernel<RP>), dim3((B + RP - 1) / RP), dim3(256), sm, as_stream(stream), *e, z, B,
+  hipLaunchKernelGGL((ebm_energy_grad_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, as_stream(stream), *e, z, B,
                      energy, grad);
   return (int)hipGetLastError();
 }

@@ -7,8 +7,8 @@
 
 namespace {
 
-// (Cout,Cin,k,k) -> [(ky,kx,ci)][co]
-__global__ void pack_conv_kernel(const float* w, int cout, int cin, int k, float* wp) {
+// (Cout,Cin,k,k) -> [(ky,kx,ci)][co], or [co][(ky,kx,ci)] for the K-major engine (km)
+__global__ void pack_conv_kernel(const float* w, int cout, int cin, int k, int km, float* wp) {
   const long n = (long)cout * cin * k * k;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -19,7 +19,11 @@ __global__ void pack_conv_kernel(const float* w, int cout, int cin, int k, float
   t /= k;
   const int ci = (int)(t % cin);
   const int co = (int)(t / cin);
-  wp[(((long)ky * k + kx) * cin + ci) * cout + co] = w[i];
+  const long kk = ((long)ky * k + kx) * cin + ci;
+  if (km)
+    wp[(long)co * k * k * cin + kk] = w[i];
+  else
+    wp[kk * cout + co] = w[i];
 }
 
 __global__ void nchw_to_nhwc_kernel(const float* x, int B, int C, int HW, float* y) {
@@ -123,7 +127,7 @@ extern "C" int damc_pack_conv2d(const float* w, int cout, int cin, int k, float*
   if (!w || !wp || cout <= 0 || cin <= 0 || k <= 0) return DAMC_ERR_ARG;
   const long n = (long)cout * cin * k * k;
   hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), w, cout, cin,
-                     k, wp);
+                     k, (int)damc::conv_kmajor_ok(cin), wp);
   return (int)hipGetLastError();
 }
 
@@ -152,7 +156,8 @@ extern "C" int damc_conv2d_nhwc(const float* x, int B, int hin, int win, int cin
   a.pad_y = pad;
   a.pad_x = pad;
   a.B = wp;
-  a.ldb = cout;
+  a.b_kmajor = damc::conv_kmajor_ok(cin);
+  a.ldb = a.b_kmajor ? (long)k * k * cin : cout;
   a.C = y;
   a.ldc = cout;
   a.M = B * hout * wout;

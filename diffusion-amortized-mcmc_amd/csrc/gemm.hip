@@ -401,8 +401,11 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
     Bg += (long)z * p.b_zstride;
   }
   const int Cg = p.Cg, kw = p.kw, Win = p.Win;
-  const int nk = p.K / BK;
   const int kh = p.K / Cg / kw;
+  // O_DENSE: blockIdx.z is a split-K slice [kbeg, kend) (k_per_z a multiple of BK)
+  const int kbeg = (OM == O_DENSE) ? z * p.k_per_z : 0;
+  const int kend = (OM == O_DENSE) ? min(p.K, kbeg + p.k_per_z) : p.K;
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   const int hwq = p.Hq * p.Wq;
   const int nimg = (p.M + hwq - 1) / hwq;
   const __amdgpu_buffer_rsrc_t rsA =
@@ -441,7 +444,8 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
   }
 
   // ---- scalar tap walk over the K tiles still to be loaded
-  int tap = 0, tky = 0, tkx = 0, ci0 = 0;
+  int tap = kbeg / Cg, ci0 = kbeg - (kbeg / Cg) * Cg;
+  int tky = tap / kw, tkx = tap - (tap / kw) * kw;
   unsigned aoff[4];
   auto set_tap = [&]() {
     const int toff = DBG == 1 ? 0 : (tky * Win + tkx) * Cg * 4;
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
   // branch-free form for the interleaved pipelines (one basic block per K step): a tile past the end
   // of K loads nothing (every offset out of range) and the tap walk advances with selects
   auto load_ab_nb = [&](int k0) {
-    const bool live = k0 < p.K;
+    const bool live = k0 < kend;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       ra[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(live ? aoff[j] : KM_OOB), ci0 * 4, 0));
@@ -533,9 +537,9 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
   constexpr int SG_MFMA = 0x8, SG_VMEM_RD = 0x20, SG_DS_RD = 0x100, SG_DS_WR = 0x200;
   if (PIPE == 0 || PIPE == 2) {  // PIPE >= 3: the prefetch structure below
     if (nk > 0) {
-      load_ab(0);
+      load_ab(kbeg);
       store_ab(0);
-      if (nk > 1) load_ab(BK);
+      if (nk > 1) load_ab(kbeg + BK);
     }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
@@ -545,14 +549,14 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
         read_frags(cur, fa, fb);
         if (kt + 1 < nk) {
           store_ab(cur ^ 1);
-          if (kt + 2 < nk) load_ab((kt + 2) * BK);
+          if (kt + 2 < nk) load_ab(kbeg + (kt + 2) * BK);
         }
         mfma_tile(fa, fb);
       } else {
         // stores past the last tile land in the buffer nobody reads again; loads past K are empty
         read_frags(cur, fa, fb);
         store_ab(cur ^ 1);
-        load_ab_nb((kt + 2) * BK);
+        load_ab_nb(kbeg + (kt + 2) * BK);
         mfma_tile(fa, fb);
         // the first k-quad's 4 fragments, then the remaining reads, stores and loads one per MFMA
         __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 4, 0);
@@ -578,12 +582,12 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
   } else {
     // prologue: tiles 0 and 1 staged, tile 2 in flight, fragments of tile 0 resident
     if (nk > 0) {
-      load_ab(0);
+      load_ab(kbeg);
       store_ab(0);
       if (nk > 1) {
-        load_ab(BK);
+        load_ab(kbeg + BK);
         store_ab(1);
-        if (nk > 2) load_ab(2 * BK);
+        if (nk > 2) load_ab(kbeg + 2 * BK);
       }
     }
     __syncthreads();
@@ -596,13 +600,13 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
         if (kt + 1 < nk) read_frags((kt + 1) & 1, fna, fnb);
         if (kt + 2 < nk) {
           store_ab(kt & 1);
-          if (kt + 3 < nk) load_ab((kt + 3) * BK);
+          if (kt + 3 < nk) load_ab(kbeg + (kt + 3) * BK);
         }
         mfma_tile(fca, fcb);
       } else {
         read_frags((kt + 1) & 1, fna, fnb);
         store_ab(kt & 1);
-        load_ab_nb((kt + 3) * BK);
+        load_ab_nb(kbeg + (kt + 3) * BK);
         mfma_tile(fca, fcb);
         // one LDS read / LDS write / global load per MFMA gap, so every wave always has MFMAs ready
         if (PIPE == 3) {  // 16 reads, 8 writes, 8 loads on the first 32 MFMAs
@@ -688,7 +692,10 @@ static void launch_km_t(const GemmArgs& a, int zdim, hipStream_t s) {
 static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
   const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
   if (!conv_kmajor_ok(a.Cg) || taps * a.Cg != a.K || a.kw <= 0 || taps % a.kw != 0 || taps > 32) return DAMC_ERR_ARG;
-  if ((om == O_PHASE && zdim != 4) || (om == O_DENSE && (zdim != 1 || a.k_per_z < a.K))) return DAMC_ERR_ARG;
+  if (om == O_PHASE && zdim != 4) return DAMC_ERR_ARG;
+  if (om == O_DENSE && (a.k_per_z <= 0 || a.k_per_z % KM_BK != 0 ||
+                        (long)zdim * a.k_per_z < a.K || (long)(zdim - 1) * a.k_per_z >= a.K))
+    return DAMC_ERR_ARG;
   if (a.ldb < a.K || ((uintptr_t)a.A | (uintptr_t)a.B) % 16 != 0 || (a.ldb % 4) != 0) return DAMC_ERR_ARG;
   if ((double)a.N * a.ldb * 4 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
   const long hwq = (long)a.Hq * a.Wq;

@@ -771,7 +771,8 @@ int proj_slices(long K) {
   if (s > 512) s = 512;
   return (int)s;
 }
-int proj_k_per(long K, int S) { return (int)(((K + S - 1) / S + 15) / 16 * 16); }
+// slice length: a multiple of the K-major engine's K tile (depends on K only, never on the batch)
+int proj_k_per(long K, int S) { return (int)(((K + S - 1) / S + 31) / 32 * 32); }
 
 struct Workspace {
   std::vector<float*> h;  // activations (NHWC), one per layer except the final one
@@ -831,7 +832,23 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
     a.slope = L.slope;
     a.C = ws.h[i];
     int rc;
-    if (L.kind == DAMC_LAYER_PROJ || L.kind == DAMC_LAYER_LINEAR) {
+    if (L.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok(L.cin)) {
+      // z . W as a 1x1 "convolution" on the K-major engine; its B operand [(oy,ox,co)][ci] is the
+      // dgrad packing
+      const int N = L.hout * L.wout * L.cout;
+      a.A = (i == 0) ? z : ws.h[i - 1];
+      a.Cg = L.cin;
+      a.B = L.w_bwd;
+      a.b_kmajor = 1;
+      a.ldb = L.cin;
+      a.ldc = N;
+      a.M = B;
+      a.N = N;
+      a.K = L.cin;
+      a.k_per_z = a.K;
+      rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
+                             2.0 * B * (double)N * L.cin, s);
+    } else if (L.kind == DAMC_LAYER_PROJ || L.kind == DAMC_LAYER_LINEAR) {
       const int N = L.hout * L.wout * L.cout;
       a.A = (i == 0) ? z : ws.h[i - 1];
       a.lda = L.cin;
@@ -974,6 +991,13 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
   a.lda = K;
   a.B = L0.w_bwd;
   a.ldb = L0.cin;
+  const bool km = L0.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok((int)K);
+  if (km) {  // 1x1 "convolution" with Cg = K; B operand [ci][(oy,ox,co)] is the forward packing
+    a.Cg = (int)K;
+    a.B = L0.w_fwd;
+    a.b_kmajor = 1;
+    a.ldb = K;
+  }
   a.C = ws.slabs;
   a.ldc = L0.cin;
   a.c_zstride = (long)B * L0.cin;
@@ -984,7 +1008,7 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
   const int S = (int)((K + a.k_per_z - 1) / a.k_per_z);
   // slices beyond S (when rounding shrank the count) must contribute zeros
   if (S < ws.nslab) DAMC_CHECK(hipMemsetAsync(ws.slabs, 0, sizeof(float) * ws.nslab * (size_t)B * L0.cin, s));
-  return damc::launch_gemm(a, damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, S, "proj_dgrad",
+  return damc::launch_gemm(a, km ? damc::A_CONV : damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, S, "proj_dgrad",
                            2.0 * B * (double)K * L0.cin, s);
 }
 

@@ -130,7 +130,8 @@ int damc_philox_normal(float* out, int n_steps, int batch, int nz, uint64_t seed
 /* generic fp32 MFMA implicit-GEMM conv (NHWC) + bias: encoder building block */
 int damc_conv2d_nhwc(const float* x, int batch, int hin, int win, int cin, const float* w_packed, const float* bias,
                      int cout, int k, int stride, int pad, float* y, void* stream);
-/* pack Conv2d weight (Cout,Cin,k,k) -> (k,k,Cin,Cout) */
+/* pack Conv2d weight (Cout,Cin,k,k) into the engine's layout (same element count; opaque to callers):
+ * (Cout, k,k,Cin) for the K-major engine when Cin % 32 == 0, else (k,k,Cin,Cout) */
 int damc_pack_conv2d(const float* w_torch, int cout, int cin, int k, float* w_packed, void* stream);
 /* InstanceNorm2d(affine, eps) + LeakyReLU(slope), in place on NHWC (Welford partials merged with
  * Chan's formula); workspace: damc_instnorm_workspace_floats() floats */
