@@ -90,6 +90,72 @@ def cpu_baseline(budget_s=12.0):
                        "fp32 oracle restatement, %.1f s" % (n, 2 * n, el))
 
 
+def event_ms(fn, reps=5):
+    """Median wall time of fn() in ms, HIP events on the current stream (the library launches there)."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return sorted(ts)[len(ts) // 2]
+
+
+def langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank):
+    """the posterior (a1) and prior (a2) legs of the block timed separately."""
+    def post():
+        zbuf.copy_(z0)
+        lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=7, chain_base=rank * B)
+
+    def prior():
+        lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=8, chain_base=rank * 2 * B)
+
+    tp, tq = event_ms(post), event_ms(prior)
+    return {"posterior_ms_per_langevin_step": round(tp / POST_STEPS, 4),
+            "posterior_z_steps_per_s": round(B * POST_STEPS / (tp / 1e3), 1),
+            "prior_ms_per_langevin_step": round(tq / PRIOR_STEPS, 4),
+            "prior_z_steps_per_s": round(2 * B * PRIOR_STEPS / (tq / 1e3), 1)}
+
+
+def amortizer_bench(device):
+    """Q(x) = encoder + 100-step reverse sweep, CIFAR-10 B=128 with the
+    reference's training defaults (train_gen_recon.py:360-380: nif 64, nxemb 1024, ntemb 128,
+    n_interval 100, logsnr [-5.1, 9.8], var 'large', residual, noise on)."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    n_int = 100
+    Q = dn._netQ_U(nc=3, nz=NZ, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=n_int,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                   dataset="cifar10")
+    synth.load_into(Q, 20)
+    Q.to(device).eval()
+    for p in Q.parameters():
+        p.requires_grad_(False)
+    x = torch.from_numpy(synth.uniform_f32(31, 0, (B, 3, 32, 32))).to(device)
+    zt = torch.from_numpy(synth.normal_f32(32, 0, (B, NZ))).to(device)
+    xemb = amortizer.encoder_forward(Q.encoder, x)
+    zw = torch.empty_like(zt)
+
+    def sweep():
+        zw.copy_(zt)
+        amortizer.reverse_sweep(Q, xemb, zw, seed=5)
+
+    t_enc = event_ms(lambda: amortizer.encoder_forward(Q.encoder, x))
+    t_sw = event_ms(sweep)
+    t_q = event_ms(lambda: amortizer.q_forward(Q, x=x))
+    enc_flop = 2.0 * B * 110.8e6        # SURVEY.md §8(a) a10: 110.8 M MAC / sample
+    sweep_flop = 2.0 * B * 3.146e6 * n_int  # reference-algorithm FLOP (a9: 3.146 M MAC / sample / step)
+    return {"config": "cifar10 Q(x) B=128, nif 64, nxemb 1024, ntemb 128, 100 steps",
+            "q_forward_ms": round(t_q, 3), "encoder_ms": round(t_enc, 3), "sweep_ms": round(t_sw, 3),
+            "us_per_denoise_step": round(1e3 * t_sw / n_int, 2),
+            "encoder_tflops": round(enc_flop / (t_enc / 1e3) / 1e12, 2),
+            "sweep_reference_equivalent_tflops": round(sweep_flop / (t_sw / 1e3) / 1e12, 2)}
+
+
 def traffic_from_profiles(kernel_class):
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
@@ -107,6 +173,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-extras", action="store_true", help="skip the per-leg and amortizer timings")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,6 +227,12 @@ def main():
         if n.value:
             classes[name] = dict(total_ms=ms.value, launches=n.value, flops=fl.value)
 
+    extras = None
+    if not args.no_extras:
+        # outside the timed region: does not enter `value`
+        extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
+        extras["amortizer"] = amortizer_bench(device)
+
     t_max = elapsed
     if dist:
         t = torch.tensor([elapsed], device=device)
@@ -210,8 +283,12 @@ def main():
                                for k, v in classes.items()},
             "prior_us_per_step": round(1e3 * classes["prior_chain"]["total_ms"] / classes["prior_chain"]["launches"]
                                        / PRIOR_STEPS, 2) if "prior_chain" in classes else None,
+            "batch_iterations_per_s": round(args.steps / t_max, 3),
             "cpu_baseline": None,
         }
+        if extras:
+            out["langevin_legs"] = {k: v for k, v in extras.items() if k != "amortizer"}
+            out["amortizer"] = extras["amortizer"]
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_budget)
             out["cpu_baseline"] = cb

@@ -17,7 +17,18 @@
 
 namespace {
 
-constexpr int TM = 16, TN = 32;
+constexpr int TM = 16, TN = 16;     // output tile of one workgroup
+constexpr int CSQ_THREADS = 512;    // 8 waves: two per product (l, s, g, b), each over half of K
+constexpr int CSQ_CH = 8;           // k-groups (16 k each) whose loads one wave keeps in flight
+
+// LDS row stride of a [TM][K] operand image: a multiple of 64 plus 8 floats, which makes the
+// ds_read_b128 fragment reads (rows m = lane&15, k-quads lane>>4) conflict-free
+__host__ __device__ inline int csq_ld(int k) { return (k + 63) / 64 * 64 + 8; }
+
+// emb_nz > 0 (block in0): room for the Fourier matrix B (nz, nz/2) as well
+__host__ __device__ inline size_t csq_smem_bytes(int din, int dout, int emb_nz = 0) {
+  return sizeof(float) * ((size_t)TM * (csq_ld(din) + csq_ld(dout)) + 8 * TM * TN + (size_t)emb_nz * (emb_nz / 2));
+}
 
 struct CsqArgs {
   const float* srcA;  // block input source 1 (B, wa)
@@ -29,7 +40,7 @@ struct CsqArgs {
   const float* bmat;  // (nz, nz/2)
   int nz;
   int din, dout, B;
-  const float *wl, *bl, *ws, *bs, *wg, *bg, *wb;
+  const float *wl, *bl, *ws, *bs, *wg, *bg, *wb;  // PyTorch Linear layout (out, in): k contiguous
   const float* px;    // (B, ldpx) at this block's column offset
   int ldpx;
   const float* qt;    // (ldpx) row of this step at this block's column offset
@@ -46,98 +57,142 @@ struct CsqArgs {
   float* eps_log;      // (B, nz) or null
 };
 
-__global__ __launch_bounds__(256) void csq_block_kernel(CsqArgs a) {
+// One ConcatSquashLinear block (diffusion_net.py:417-460) for a 16 x 16 output tile:
+//   out = (x Wl^T + bl) * sigmoid(c Wg^T + bg) + c Wb^T + (x Ws^T + bs),   c = SiLU(px + qt)
+// x (16 x din) and c (16 x dout) are staged in LDS.  Wave w computes product w>>1 over half w&1 of
+// its K on v_mfma_f32_16x16x4_f32 through a k-permutation (MFMA step s of k-group g uses
+// k = 16g + 4(lane>>4) + s), so each lane's operands for 4 steps are one 16-B LDS read (x / c) and one
+// 16-B global read of a weight row; a wave issues CSQ_CH groups of loads before their MFMAs.  The
+// eight partial tiles are added in a fixed order in the epilogue.
+__global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int din = a.din, dout = a.dout;
-  const int ldx = din + 2, ldcs = dout + 2;  // row strides = 2 (mod 32): conflict-free fragment reads
-  float* xs = sm;                            // [TM][ldx]
-  float* cs = xs + TM * ldx;                 // [TM][ldcs]
-  float* red = cs + TM * ldcs;               // [4][TM][TN]
+  const int ldx = csq_ld(din), ldcs = csq_ld(dout);
+  float* xs = sm;                 // [TM][ldx]
+  float* cs = xs + TM * ldx;      // [TM][ldcs]
+  float* red = cs + TM * ldcs;    // [8][TM][TN]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  const int kx16 = (din + 15) & ~15, kc16 = (dout + 15) & ~15;
 
-  // ---- stage x (block input) for the 16 rows
+  // ---- stage x (block input) for the 16 rows; columns [din, kx16) zero.  Staging is float4 and
+  // unrolled so that a thread's global loads are in flight together (this kernel is latency-bound)
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   if (a.emb_mode) {
-    const int half = a.nz >> 1;
-    const float two_pi = 6.28318548f;  // fp32(2*pi), as the reference's 2*np.pi*tensor
-    for (int i = tid; i < TM * half; i += 256) {
-      const int r = i / half, j = i - r * half;
+    const int half = a.nz >> 1, nzq = a.nz >> 2;
+    float* bm = red + 8 * TM * TN;  // [nz][half]
+    const int nbq = (a.nz * half) >> 2;
+#pragma unroll 4
+    for (int i = tid; i < nbq; i += CSQ_THREADS)
+      *reinterpret_cast<f32x4*>(bm + 4 * i) = *reinterpret_cast<const f32x4*>(a.bmat + 4 * (long)i);
+    // z rows -> xs[:, 2*half : 2*half + nz] (also the embedding's operand, read back from LDS)
+#pragma unroll 4
+    for (int i = tid; i < TM * nzq; i += CSQ_THREADS) {
+      const int r = i / nzq, k = 4 * (i - r * nzq);
       const int row = r0 + r;
-      float s = 0.f;
-      if (row < a.B) {
-        const float* zr = a.z + (long)row * a.nz;
-        for (int k = 0; k < a.nz; ++k) s = fmaf(zr[k], a.bmat[(long)k * half + j], s);
-      }
-      const float p = two_pi * s;
-      xs[r * ldx + j] = row < a.B ? sinf(p) : 0.f;
-      xs[r * ldx + half + j] = row < a.B ? cosf(p) : 0.f;
+      const f32x4 v = row < a.B ? *reinterpret_cast<const f32x4*>(a.z + (long)row * a.nz + k) : zero4;
+      *reinterpret_cast<f32x4*>(xs + r * ldx + 2 * half + k) = v;
     }
-    for (int i = tid; i < TM * a.nz; i += 256) {
-      const int r = i / a.nz, k = i - r * a.nz;
-      const int row = r0 + r;
-      xs[r * ldx + 2 * half + k] = row < a.B ? a.z[(long)row * a.nz + k] : 0.f;
+    for (int i = tid; i < TM * (kx16 - din); i += CSQ_THREADS) {
+      const int r = i / (kx16 - din);
+      xs[r * ldx + din + (i - r * (kx16 - din))] = 0.f;
+    }
+    __syncthreads();
+    const float two_pi = 6.28318548f;  // fp32(2*pi), as the reference's 2*np.pi*tensor
+    for (int i = tid; i < TM * half; i += CSQ_THREADS) {
+      const int r = i / half, j = i - r * half;
+      const float* zr = xs + r * ldx + 2 * half;
+      float sdot = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < a.nz; ++k) sdot = fmaf(zr[k], bm[k * half + j], sdot);
+      const float ph = two_pi * sdot;
+      const bool ok = r0 + r < a.B;
+      xs[r * ldx + j] = ok ? sinf(ph) : 0.f;
+      xs[r * ldx + half + j] = ok ? cosf(ph) : 0.f;
     }
   } else {
-    for (int i = tid; i < TM * din; i += 256) {
-      const int r = i / din, k = i - r * din;
+    const int q16 = kx16 >> 2;
+#pragma unroll 4
+    for (int i = tid; i < TM * q16; i += CSQ_THREADS) {
+      const int r = i / q16, k = 4 * (i - r * q16);
       const int row = r0 + r;
-      float v = 0.f;
-      if (row < a.B) v = k < a.wa ? a.srcA[(long)row * a.wa + k] : a.srcB[(long)row * a.wb_ + (k - a.wa)];
-      xs[r * ldx + k] = v > 0.f ? v : 0.01f * v;
+      f32x4 v = zero4;
+      if (row < a.B && k < din)
+        v = k < a.wa ? *reinterpret_cast<const f32x4*>(a.srcA + (long)row * a.wa + k)
+                     : *reinterpret_cast<const f32x4*>(a.srcB + (long)row * a.wb_ + (k - a.wa));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.01f * v[e];
+      *reinterpret_cast<f32x4*>(xs + r * ldx + k) = v;
     }
   }
-  // ---- stage c = SiLU(px + qt)
-  for (int i = tid; i < TM * dout; i += 256) {
-    const int r = i / dout, n = i - r * dout;
-    const int row = r0 + r;
-    float v = 0.f;
-    if (row < a.B) {
-      const float u = a.px[(long)row * a.ldpx + n] + a.qt[n];
-      v = u / (1.f + expf(-u));
+  // ---- stage c = SiLU(px + qt); columns [dout, kc16) zero
+  {
+    const int q16 = kc16 >> 2;
+#pragma unroll 4
+    for (int i = tid; i < TM * q16; i += CSQ_THREADS) {
+      const int r = i / q16, n = 4 * (i - r * q16);
+      const int row = r0 + r;
+      f32x4 v = zero4;
+      if (row < a.B && n < dout) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(a.px + (long)row * a.ldpx + n) +
+                        *reinterpret_cast<const f32x4*>(a.qt + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = u[e] / (1.f + expf(-u[e]));
+      }
+      *reinterpret_cast<f32x4*>(cs + r * ldcs + n) = v;
     }
-    cs[r * ldcs + n] = v;
   }
   __syncthreads();
 
-  // ---- wave w: product w over its K; two 16x16 column tiles
-  const float* As = (wave < 2) ? xs : cs;
-  const int lda_s = (wave < 2) ? ldx : ldcs;
-  const int K = (wave < 2) ? din : dout;
-  const float* W = wave == 0 ? a.wl : wave == 1 ? a.ws : wave == 2 ? a.wg : a.wb;
-  const int am = lane & 15, ak = lane >> 4;
+  // ---- wave w: product w>>1 over k-groups [g_lo, g_hi) (half w&1)
+  const int prod = wave >> 1, hf = wave & 1;
+  const float* As = (prod < 2) ? xs : cs;
+  const int lda_s = (prod < 2) ? ldx : ldcs;
+  const int K = (prod < 2) ? din : dout;
+  const float* W = prod == 0 ? a.wl : prod == 1 ? a.ws : prod == 2 ? a.wg : a.wb;
+  const int ng = (K + 15) >> 4, gh = (ng + 1) >> 1;
+  const int g_lo = hf * gh, g_hi = min(ng, g_lo + gh);
+  const int m = lane & 15, q = lane >> 4;
+  const int n = n0 + m;
+  const bool nok = n < dout;
+  const float* Wn = W + (long)(nok ? n : 0) * K;
+  const float* Am = As + m * lda_s + 4 * q;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  const int nA = n0 + am, nB = n0 + 16 + am;
-  const bool okA = nA < dout, okB = nB < dout;
-#pragma unroll 4
-  for (int k0 = 0; k0 < K; k0 += 4) {
-    const int k = k0 + ak;
-    const float av = As[am * lda_s + k];
-    const float* wr = W + (long)k * dout;
-    const float b0 = okA ? wr[nA] : 0.f;
-    const float b1 = okB ? wr[nB] : 0.f;
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc1, 0, 0, 0);
+  for (int g0 = g_lo; g0 < g_hi; g0 += CSQ_CH) {
+    f32x4 bw[CSQ_CH], av[CSQ_CH];
+#pragma unroll
+    for (int c = 0; c < CSQ_CH; ++c) {
+      const int g = g0 + c;
+      const int k = 16 * g + 4 * q;
+      const bool ok = g < g_hi;
+      bw[c] = (ok && nok && k < K) ? *reinterpret_cast<const f32x4*>(Wn + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      av[c] = ok ? *reinterpret_cast<const f32x4*>(Am + 16 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < CSQ_CH; ++c) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][0], bw[c][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][1], bw[c][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][2], bw[c][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][3], bw[c][3], acc1, 0, 0, 0);
+    }
   }
   // C layout 16x16x4: col = lane & 15, row = (lane >> 4) * 4 + reg
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = (lane >> 4) * 4 + r;
-    red[(wave * TM + row) * TN + (lane & 15)] = acc0[r];
-    red[(wave * TM + row) * TN + 16 + (lane & 15)] = acc1[r];
-  }
+  for (int r = 0; r < 4; ++r) red[(wave * TM + q * 4 + r) * TN + m] = acc0[r] + acc1[r];
   __syncthreads();
 
   // ---- combine: out = (l + bl) * sigmoid(g + bg) + b + (s + bs)
-  for (int i = tid; i < TM * TN; i += 256) {
+  for (int i = tid; i < TM * TN; i += CSQ_THREADS) {
     const int r = i / TN, c = i - r * TN;
     const int row = r0 + r, col = n0 + c;
     if (row >= a.B || col >= dout) continue;
-    const float l = red[(0 * TM + r) * TN + c] + a.bl[col];
-    const float s = red[(1 * TM + r) * TN + c] + a.bs[col];
-    const float g = red[(2 * TM + r) * TN + c] + a.bg[col];
-    const float bb = red[(3 * TM + r) * TN + c];
+    auto P = [&](int p) { return red[((2 * p) * TM + r) * TN + c] + red[((2 * p + 1) * TM + r) * TN + c]; };
+    const float l = P(0) + a.bl[col];
+    const float sk = P(1) + a.bs[col];
+    const float g = P(2) + a.bg[col];
+    const float bb = P(3);
     const float gate = 1.f / (1.f + expf(-g));
-    const float o = l * gate + bb + s;
+    const float o = l * gate + bb + sk;
     if (!a.final_) {
       a.out[(long)row * dout + col] = o;
       continue;
@@ -220,7 +275,9 @@ int validate(const damc_denoiser_t* d) {
     const damc_csq_block_t& b = d->blocks[j];
     if (b.din != din[j] || b.dout != dout[j]) return DAMC_ERR_ARG;
     if (!b.wl || !b.bl || !b.ws || !b.bs || !b.wg || !b.bg || !b.wb) return DAMC_ERR_ARG;
-    if (b.din > 1024 || b.dout > 512) return DAMC_ERR_UNSUPPORTED;
+    // float4 weight rows / LDS images / staging need every width % 4 == 0; the operand images must fit
+    if ((b.din & 3) || (b.dout & 3) || (nz & 3)) return DAMC_ERR_UNSUPPORTED;
+    if (csq_smem_bytes(b.din, b.dout, j == 0 ? nz : 0) > 160 * 1024) return DAMC_ERR_UNSUPPORTED;
   }
   return 0;
 }
@@ -300,6 +357,11 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
       return rc;
   }
 
+  // the widest blocks (din 4w) need more than the default 64 KB of dynamic LDS
+  static const bool lds_ok = hipFuncSetAttribute((const void*)csq_block_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!lds_ok) return DAMC_ERR_UNSUPPORTED;
+
   // ---- the sweep: 7 fused block launches per step
   int coloff[7];
   {
@@ -370,9 +432,9 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
         a.zt = zt;
         a.eps_log = (eps_log && k < eps_log_steps) ? eps_log + (size_t)k * B * d->nz : nullptr;
       }
-      const size_t sm = sizeof(float) * ((size_t)TM * (b.din + 2) + (size_t)TM * (b.dout + 2) + 4 * TM * TN);
+      const size_t sm = csq_smem_bytes(b.din, b.dout, j == 0 ? d->nz : 0);
       dim3 grid((B + TM - 1) / TM, (b.dout + TN - 1) / TN);
-      hipLaunchKernelGGL(csq_block_kernel, grid, dim3(256), sm, s, a);
+      hipLaunchKernelGGL(csq_block_kernel, grid, dim3(CSQ_THREADS), sm, s, a);
     }
     if (!last) ++noisy_k;
     DAMC_LAUNCH_CHECK();

@@ -40,13 +40,14 @@ int begin(const char* name, double flops, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
   Rec r{name ? name : "?", flops, take_event(), take_event()};
   if (!r.a || !r.b) return -1;
-  hipEventRecord(r.a, s);
+  if (hipEventRecord(r.a, s) != hipSuccess) return -1;
   g_recs.push_back(r);
   return (int)g_recs.size() - 1;
 }
 void end(int slot, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (slot >= 0 && slot < (int)g_recs.size()) hipEventRecord(g_recs[slot].b, s);
+  // a failed record leaves the slot's end event unset; damc_prof_query then returns that error
+  if (slot >= 0 && slot < (int)g_recs.size()) (void)hipEventRecord(g_recs[slot].b, s);
 }
 }  // namespace damc_prof
 

@@ -153,8 +153,9 @@ int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bia
  * the output axis in block order. */
 typedef struct {
   int din, dout;
-  const float *wl, *bl; /* _layer.0     (din, dout), (dout)  */
-  const float *ws, *bs; /* _skip        (din, dout), (dout)  */
+  /* PyTorch nn.Linear layout (out, in), k contiguous */
+  const float *wl, *bl; /* _layer.0     (dout, din), (dout)  */
+  const float *ws, *bs; /* _skip        (dout, din), (dout)  */
   const float *wg, *bg; /* _hyper_gate  (dout, dout), (dout) */
   const float* wb;      /* _hyper_bias  (dout, dout), no bias */
 } damc_csq_block_t;
