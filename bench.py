@@ -28,6 +28,8 @@ sys.path.insert(0, os.path.join(HERE, "diffusion-amortized-mcmc_amd"))
 import torch  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 (= f32 MFMA rate), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, no sparsity), MI355X_MICROARCH.md
+LIMB_PRODUCTS = 6          # limb engine: 6 bf16 MFMA products per fp32 product (csrc/gemm.hip)
 B, NZ, NGF = 128, 128, 128
 POST_STEPS, PRIOR_STEPS = 30, 60
 SIGMA, S_POST, S_PRIOR = 0.1, 0.1, 0.4
@@ -174,7 +176,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extras", action="store_true", help="skip the per-leg and amortizer timings")
+    ap.add_argument("--exact-fp32", action="store_true",
+                    help="run the generator convolutions on the fp32-MFMA engine instead of the limb engine")
     args = ap.parse_args()
+    if args.exact_fp32:
+        os.environ["DAMC_EXACT_FP32"] = "1"
+    limb = os.environ.get("DAMC_EXACT_FP32", "0") != "1"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -221,7 +228,7 @@ def main():
 
     classes = {}
     for name in ("upconv_fwd", "upconv_dgrad", "proj_fwd", "proj_dgrad", "smallc_fwd", "smallc_dgrad",
-                 "posterior_update", "slab_sum", "prior_chain"):
+                 "posterior_update", "slab_sum", "prior_chain", "split_x3"):
         ms, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         _lib.check(L.damc_prof_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
         if n.value:
@@ -247,6 +254,7 @@ def main():
         avg_s = c["total_ms"] / c["launches"] / 1e3
         flops_per_launch = c["flops"] / c["launches"]
         achieved = flops_per_launch / avg_s / 1e12
+        peak = PEAK_BF16_TFLOPS / LIMB_PRODUCTS if limb else PEAK_FP32_TFLOPS
         traffic = traffic_from_profiles(dom)
         gemm_ms = sum(classes[k]["total_ms"] for k in classes if k.startswith(("upconv", "proj")))
         gemm_fl = sum(classes[k]["flops"] for k in classes if k.startswith(("upconv", "proj")))
@@ -272,11 +280,19 @@ def main():
                 "parallelism": "dp%d (chains sharded, no collective)" % world,
             },
             "roofline": {
-                "bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
                 "traffic": traffic,
+                "peak_basis": ("limb engine: fp32 FLOP at the bf16 dense MFMA peak %.0f / %d limb products "
+                               "(executed bf16 MFMA %.0f TFLOP/s)" % (PEAK_BF16_TFLOPS, LIMB_PRODUCTS,
+                                                                       achieved * LIMB_PRODUCTS)) if limb
+                              else "fp32 MFMA dense peak",
             },
+            "gemm_arith": ("fp32 operands as 3 bf16 limbs, 6 limb products per fp32 product on "
+                           "v_mfma_f32_32x32x16_bf16, fp32 accumulation; error vs fp64 equal to the fp32-MFMA "
+                           "engine's (profiles/r01/gemm_bench.txt)") if limb
+                          else "fp32 v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains)",
             "posterior_tflops_effective": round(post_flops_step * POST_STEPS * args.steps / t_max / 1e12, 2),
             "gemm_classes_tflops": round(gemm_fl / (gemm_ms / 1e3) / 1e12, 2) if gemm_ms else None,
             "kernel_classes": {k: dict(avg_ms=round(v["total_ms"] / v["launches"], 4), launches=v["launches"])

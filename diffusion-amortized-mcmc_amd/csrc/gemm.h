@@ -42,12 +42,19 @@ struct GemmArgs {
   float* sqerr = nullptr;       // EPI_RESID: accumulates |t - x|^2 * inv_s2 / 2 (diagnostics)
   int Hout = 1, Wout = 1;
   int b_kmajor = 0;
+  // limb engine (gemm_x3_kernel): A and B as x3 bf16 limb tensors (see gemm.hip); when A3 is set the
+  // fp32 A / B pointers are not read
+  const unsigned short* A3 = nullptr;
+  const unsigned short* B3 = nullptr;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
 // channel count is a multiple of its K tile; weight packers pick the B layout with this predicate.
 constexpr int KM_BK = 32;
 inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
+
+// fp32 [n/C rows][C] -> x3 limb layout [rows][C/8][3][8] bf16 (n % 8 == 0, 16-B aligned)
+int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);

@@ -733,6 +733,271 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   return (int)hipGetLastError();
 }
 
+// ================================================================================================
+// Limb engine: fp32-accurate convolution GEMM on bf16 MFMA.
+//
+// Every fp32 operand value a is carried as three bf16 limbs a = a0 + a1 + a2 (RNE splits: a0 = bf16(a),
+// a1 = bf16(a - a0), a2 = bf16(a - a0 - a1); both subtractions are exact, so the limbs hold all 24
+// significand bits).  A product a*b is the sum of the six limb products with i + j <= 2; the dropped
+// three are below 2^-23 |ab|.  Each limb product is exact in the MFMA (8 x 8 significand bits) and the
+// sum is accumulated in fp32 by v_mfma_f32_32x32x16_bf16, smallest terms first.  Error against fp64 is
+// the fp32 GEMM's (tools/gemm_bench.hip prints both), at 16/6 of the fp32-MFMA rate per clock.
+//
+// "x3" tensor layout: a row of C channels is C/8 octets, each octet stored as [limb][8] bf16 (48 B), so
+// a 32-channel K tile of one row is 192 contiguous bytes.  The A operand is an NHWC x3 map gathered by
+// the same tap walk as the K-major engine (a K tile never straddles a tap, padding taps read zero
+// through an out-of-range buffer offset); B is x3 over K, [n][K/8][3][8].
+//
+// Block 256 x 128, 8 waves (4 along M x 2 along N), each wave 64 x 64 = 2 x 2 accumulators of 32 x 32.
+// LDS rows are 208 B (192 + 16 pad: any 16 consecutive rows cover all 64 banks for ds_read_b128),
+// double-buffered: 2 x 384 rows x 208 B = 159,744 B, one workgroup per CU.
+constexpr int X3_BM = 256, X3_BN = 128, X3_BK = 32, X3_ROWB = 208;
+constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
+constexpr int X3_AJ = X3_BM * X3_CHUNKS / 512, X3_BJ = X3_BN * X3_CHUNKS / 512;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int EPI, int OM>
+__global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (X3_BM + X3_BN) * X3_ROWB];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = (p.N + X3_BN - 1) / X3_BN;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * X3_BM, n0 = tn * X3_BN;
+  const int z = blockIdx.z;
+
+  int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
+  const unsigned short* Bg = p.B3;
+  if (OM == O_PHASE) {
+    py = z >> 1;
+    px = z & 1;
+    pad_y = 1 - py;
+    pad_x = 1 - px;
+    Bg += (long)z * p.b_zstride * 3;
+  }
+  const int Cg = p.Cg, kw = p.kw, Win = p.Win;
+  const int kh = p.K / Cg / kw;
+  const int nk = p.K / X3_BK;
+  const int hwq = p.Hq * p.Wq;
+  const int nimg = (p.M + hwq - 1) / hwq;
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A3, (short)0, nimg * p.Hin * Win * Cg * 6, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Bg, (short)0, p.N * p.K * 6, 0x00020000);
+
+  // ---- per-thread chunks: chunk id = tid + 512 j -> (row id / 12, 16-B chunk id % 12)
+  int abase[X3_AJ];
+  unsigned amask[X3_AJ], boff[X3_BJ];
+  int alds[X3_AJ], blds[X3_BJ];
+#pragma unroll
+  for (int j = 0; j < X3_AJ; ++j) {
+    const int id = tid + 512 * j, row = id / X3_CHUNKS, ch = id - row * X3_CHUNKS;
+    const int m = m0 + row;
+    unsigned msk = 0;
+    int base = 0;
+    if (m < p.M) {
+      const int b = m / hwq;
+      const int r = m - b * hwq;
+      const int qy = r / p.Wq, qx = r - qy * p.Wq;
+      const int iy0 = qy * p.stride - pad_y, ix0 = qx * p.stride - pad_x;
+      base = ((b * p.Hin + iy0) * Win + ix0) * Cg;
+      for (int ky = 0; ky < kh; ++ky)
+        for (int kx = 0; kx < kw; ++kx)
+          if ((unsigned)(iy0 + ky) < (unsigned)p.Hin && (unsigned)(ix0 + kx) < (unsigned)Win)
+            msk |= 1u << (ky * kw + kx);
+    }
+    abase[j] = base * 6 + ch * 16;
+    amask[j] = msk;
+    alds[j] = row * X3_ROWB + ch * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < X3_BJ; ++j) {
+    const int id = tid + 512 * j, row = id / X3_CHUNKS, ch = id - row * X3_CHUNKS;
+    boff[j] = (unsigned)((n0 + row) * p.K * 6 + ch * 16);  // rows >= N fall out of range
+    blds[j] = (X3_BM + row) * X3_ROWB + ch * 16;
+  }
+
+  int tap = 0, ci0 = 0, tky = 0, tkx = 0;
+  unsigned aoff[X3_AJ];
+  auto set_tap = [&]() {
+    const int toff = (tky * Win + tkx) * Cg * 6;
+#pragma unroll
+    for (int j = 0; j < X3_AJ; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
+  };
+  set_tap();
+  u32x4 ra[X3_AJ], rb[X3_BJ];
+  auto load_ab = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < X3_AJ; ++j)
+      ra[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)aoff[j], ci0 * 6, 0));
+#pragma unroll
+    for (int j = 0; j < X3_BJ; ++j)
+      rb[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)boff[j], k0 * 6, 0));
+    ci0 += X3_BK;
+    if (ci0 == Cg) {
+      ci0 = 0;
+      ++tap;
+      if (++tkx == kw) {
+        tkx = 0;
+        ++tky;
+      }
+      set_tap();
+    }
+  };
+  auto store_ab = [&](int buf) {
+    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB;
+#pragma unroll
+    for (int j = 0; j < X3_AJ; ++j) *reinterpret_cast<u32x4*>(base + alds[j]) = ra[j];
+#pragma unroll
+    for (int j = 0; j < X3_BJ; ++j) *reinterpret_cast<u32x4*>(base + blds[j]) = rb[j];
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // fragment of k16 step s, lane half h: octet 2s + h of the row, limb l at +16 l
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int afr = (wm * 64 + lrow) * X3_ROWB + lh * 48;
+  const int bfr = (X3_BM + wn * 64 + lrow) * X3_ROWB + lh * 48;
+
+  if (nk > 0) {
+    load_ab(0);
+    store_ab(0);
+    if (nk > 1) load_ab(X3_BK);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
+    bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+          fa[s][t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 32 * X3_ROWB + s * 96 + l * 16);
+          fb[s][t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 32 * X3_ROWB + s * 96 + l * 16);
+        }
+    if (kt + 1 < nk) {
+      store_ab((kt + 1) & 1);
+      if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][2], fb[s][j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][1], c, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
+        }
+    __syncthreads();
+  }
+  if (OM == O_PHASE) {
+    long* rowtab = reinterpret_cast<long*>(smem);
+    if (tid < X3_BM) rowtab[tid] = gemm_row_offset<OM>(p, m0 + tid, py, px);
+    __syncthreads();
+    gemm_epilogue<EPI, OM, 2>(p, acc, m0, n0, wm, wn, lane, z, py, px, rowtab);
+  } else {
+    gemm_epilogue<EPI, OM, 2>(p, acc, m0, n0, wm, wn, lane, z, py, px);
+  }
+}
+
+template <int EPI, int OM>
+static void launch_x3_t(const GemmArgs& a, int zdim, hipStream_t s) {
+  const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
+  hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
+}
+
+// fp32 [rows][C] -> x3 [rows][C/8][3][8]; one thread per channel octet
+__global__ void split_x3_kernel(const float* __restrict__ x, long n8, unsigned short* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
+  const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
+  const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 b0 = (__bf16)v[e];
+    const float r1 = v[e] - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)r2;
+  }
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * i;
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
+int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
+  if (n % 8 != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0) return DAMC_ERR_ARG;
+  const long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, y);
+  return (int)hipGetLastError();
+}
+
+// limb-engine dispatch (A3 / B3 set, A_CONV geometry as the K-major engine); splits the batch so every
+// launch's gathered x3 tensor stays below 2^31 bytes
+static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
+  const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
+  if (!a.A3 || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 || taps % a.kw != 0 || taps > 32)
+    return DAMC_ERR_ARG;
+  if ((om == O_PHASE) != (zdim == 4) || (om == O_DENSE && zdim != 1)) return DAMC_ERR_ARG;
+  if (((uintptr_t)a.A3 | (uintptr_t)a.B3) % 16 != 0) return DAMC_ERR_ARG;
+  if ((double)a.N * a.K * 6 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
+  const long hwq = (long)a.Hq * a.Wq;
+  if (a.M % hwq != 0) return DAMC_ERR_ARG;
+  const long img = (long)a.Hin * a.Win * a.Cg;  // elements per gathered image
+  const long nimg = a.M / hwq;
+  static const long lim = [] {
+    const char* e = getenv("DAMC_KM_CHUNK_BYTES");
+    const long v = e ? atol(e) : 0;
+    return (v > 0 && v < 2147483647L) ? v : 2147483647L;
+  }();
+  const long per = (lim / 6 - 1) / img;
+  if (per < 1) return DAMC_ERR_UNSUPPORTED;
+  const long cimg = (om == O_PHASE) ? (long)a.Hout * a.Wout * a.ldc : hwq * a.ldc;
+  for (long b0 = 0; b0 < nimg; b0 += per) {
+    const long nb = std::min(per, nimg - b0);
+    GemmArgs c = a;
+    c.A3 = a.A3 + b0 * img * 3;
+    c.C = a.C + b0 * cimg;
+    if (a.mask) c.mask = a.mask + b0 * cimg;
+    c.M = (int)(nb * hwq);
+#define DAMC_X3(E_, O_)                \
+  if (epi == E_ && om == O_) {         \
+    launch_x3_t<E_, O_>(c, zdim, s);   \
+    continue;                          \
+  }
+    DAMC_X3(EPI_BIAS_ACT, O_PHASE)
+    DAMC_X3(EPI_MASK, O_DENSE)
+    DAMC_X3(EPI_BIAS_ACT, O_DENSE)
+    DAMC_X3(EPI_STORE, O_DENSE)
+#undef DAMC_X3
+    return DAMC_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
 #ifndef DAMC_GEMM_SCHED
 #define DAMC_GEMM_SCHED 0  // hipcc's own placement measured best (profiles/r01/gemm_bench.txt)
 #endif
@@ -758,6 +1023,11 @@ static void launch_t(const GemmArgs& a, int zdim, hipStream_t s) {
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return DAMC_ERR_ARG;
+  if (a.A3) {
+    if (am != A_CONV) return DAMC_ERR_ARG;
+    ProfScope ps(prof_name, flops, s);
+    return launch_gemm_x3(a, epi, om, zdim, s);
+  }
   if (a.b_kmajor) {
     if (am != A_CONV) return DAMC_ERR_ARG;
     ProfScope ps(prof_name, flops, s);

@@ -8,6 +8,7 @@
 //   bwd : SMALLC dgrad * lrelu'  ->  UP2 dgrad (stride-2 conv implicit GEMM) * lrelu'
 //         -> PROJ dgrad (split-K GEMM into slabs)  ->  fused EBM grad + slab sum + z update
 // dgrad outputs overwrite the activation they are masked with (same thread reads h, writes dh).
+#include <cstdlib>
 #include <vector>
 
 #include "gemm.h"
@@ -774,8 +775,30 @@ int proj_slices(long K) {
 // slice length: a multiple of the K-major engine's K tile (depends on K only, never on the batch)
 int proj_k_per(long K, int S) { return (int)(((K + S - 1) / S + 31) / 32 * 32); }
 
+// Limb engine (gemm.hip, fp32-accurate bf16 MFMA) for the UP2 convolutions whose gathered channel
+// count is a multiple of 32.  Packed weights and workspaces always carry the x3 copies such a layer
+// can use; damc_set_exact_fp32(1) (or DAMC_EXACT_FP32=1 at load) routes the launches to the fp32-MFMA
+// K-major engine instead.
+int g_exact_fp32 = [] {
+  const char* e = getenv("DAMC_EXACT_FP32");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
+bool x3_fwd_cap(const damc_layer_t& L) { return L.kind == DAMC_LAYER_UP2 && L.cin % damc::KM_BK == 0; }
+bool x3_bwd_cap(const damc_layer_t& L) { return L.kind == DAMC_LAYER_UP2 && L.cout % damc::KM_BK == 0; }
+bool x3_fwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_fwd_cap(L); }
+bool x3_bwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_bwd_cap(L); }
+size_t up2_floats(const damc_layer_t& L) { return (size_t)L.cin * L.cout * 16; }
+// x3 copy of a packed weight matrix, stored behind its fp32 packing (n floats, 16-B aligned)
+const unsigned short* x3_of(const float* w, size_t n) { return reinterpret_cast<const unsigned short*>(w + n); }
+// activation j needs an x3 copy when layer j+1 consumes it in the forward pass, or layer j consumes its
+// gradient (stored in the same buffer) in the backward pass
+bool h_needs_x3(const damc_generator_t* g, int j) {
+  return (j + 1 < g->n_layers && x3_fwd_cap(g->layers[j + 1])) || (j >= 1 && x3_bwd_cap(g->layers[j]));
+}
+
 struct Workspace {
   std::vector<float*> h;  // activations (NHWC), one per layer except the final one
+  std::vector<unsigned short*> h3;  // x3 limb copies of h (limb engine operands) or nullptr
   float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
   float* slabs;           // split-K partial gradients
   float* glik;            // their fixed-order sum: grad of the likelihood term (B, nz)
@@ -791,10 +814,18 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
     off += ((size_t)floats * sizeof(float) + 255) / 256 * 256;
     return p;
   };
-  if (w) w->h.clear();
+  if (w) {
+    w->h.clear();
+    w->h3.clear();
+  }
   for (int i = 0; i + 1 < g->n_layers; ++i) {
     float* p = take(act_floats(g->layers[i], B));
     if (w) w->h.push_back(p);
+  }
+  for (int i = 0; i + 1 < g->n_layers; ++i) {
+    unsigned short* p = nullptr;
+    if (h_needs_x3(g, i)) p = reinterpret_cast<unsigned short*>(take(act_floats(g->layers[i], B) * 3 / 2));
+    if (w) w->h3.push_back(p);
   }
   const damc_layer_t& F = g->layers[g->n_layers - 1];
   float* d = take(act_floats(F, B));
@@ -880,9 +911,17 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.K = 4 * L.cin;
       a.Hout = L.hout;
       a.Wout = L.wout;
+      if (x3_fwd(L)) {
+        a.A3 = ws.h3[i - 1];
+        a.B3 = x3_of(L.w_fwd, up2_floats(L));
+      }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
     if (rc) return rc;
+    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {
+      ProfScope ps("split_x3", 0.0, s);
+      if ((rc = damc::launch_split_x3(ws.h[i], act_floats(L, B), ws.h3[i], s))) return rc;
+    }
   }
   return 0;
 }
@@ -938,6 +977,7 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
     if (L.kind == DAMC_LAYER_SMALLC) {
       rc = smallc_dgrad(L, out, B, d, P.act, P.slope, s);
     } else if (L.kind == DAMC_LAYER_UP2) {
+      const bool x3 = x3_bwd(L);
       GemmArgs a;
       a.A = d;
       a.Hin = L.hout;
@@ -961,6 +1001,10 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
       a.mask = out;
       a.mask_act = P.act;
       a.mask_slope = P.slope;
+      if (x3) {
+        a.A3 = ws.h3[i];
+        a.B3 = x3_of(L.w_bwd, up2_floats(L));
+      }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_MASK, damc::O_DENSE, 1, "upconv_dgrad", conv_flops(L, B), s);
     } else {  // LINEAR hidden/final
       GemmArgs a;
@@ -981,6 +1025,10 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
                              2.0 * B * (double)L.cin * L.cout, s);
     }
     if (rc) return rc;
+    if (x3_bwd(P)) {  // the next dgrad reads this gradient through the limb engine
+      ProfScope ps("split_x3", 0.0, s);
+      if ((rc = damc::launch_split_x3(out, act_floats(P, B), ws.h3[i - 1], s))) return rc;
+    }
     d = out;
   }
   // first layer: dz = dA0 . W0^T  (split-K into slabs)
@@ -1019,8 +1067,12 @@ extern "C" int damc_generator_layer_packed_sizes(const damc_layer_t* L, size_t* 
   if (!L || !fwd || !bwd) return DAMC_ERR_ARG;
   const size_t n = (size_t)L->cin * L->cout * (L->kind == DAMC_LAYER_LINEAR ? 1 : (size_t)L->k * L->k);
   switch (L->kind) {
-    case DAMC_LAYER_PROJ:
     case DAMC_LAYER_UP2:
+      // fp32 packing, then (limb engine) its x3 copy: 3 bf16 per element = 1.5 floats
+      *fwd = n + (x3_fwd_cap(*L) ? n * 3 / 2 : 0);
+      *bwd = n + (x3_bwd_cap(*L) ? n * 3 / 2 : 0);
+      return 0;
+    case DAMC_LAYER_PROJ:
     case DAMC_LAYER_LINEAR:
       *fwd = n;
       *bwd = n;
@@ -1047,6 +1099,8 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       if (!wb || L->k != 4) return DAMC_ERR_ARG;
       hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, (int)damc::conv_kmajor_ok(L->cin),
                          (int)damc::conv_kmajor_ok(L->cout), wf, wb);
+      if (x3_fwd_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wf, n, reinterpret_cast<unsigned short*>(wf + n), s));
+      if (x3_bwd_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wb, n, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_SMALLC:
       if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));
@@ -1060,6 +1114,12 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       return DAMC_ERR_ARG;
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int damc_set_exact_fp32(int on) {
+  const int prev = g_exact_fp32;
+  g_exact_fp32 = on ? 1 : 0;
+  return prev;
 }
 
 extern "C" size_t damc_posterior_workspace_bytes(const damc_generator_t* g, int B) {

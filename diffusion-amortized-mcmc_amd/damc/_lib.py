@@ -75,6 +75,7 @@ _SIGS = {
     "damc_generator_layer_packed_sizes": (_I, [ctypes.POINTER(Layer), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "damc_pack_generator_layer": (_I, [ctypes.POINTER(Layer), _P, _P, _P, _P]),
     "damc_pack_ebm": (_I, [ctypes.POINTER(Ebm), _P, _P, _P]),
+    "damc_set_exact_fp32": (_I, [_I]),
     "damc_posterior_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
     "damc_posterior_langevin": (_I, [ctypes.POINTER(Generator), ctypes.POINTER(Ebm), _P, _P, _I, _I, _F, _F, _I, _P,
                                      _U64, _U64, _U64, _P, _P, _SZ, _P]),
@@ -125,6 +126,21 @@ def lib():
             raise DamcError("libdamc ABI mismatch")
         _lib = handle
     return _lib
+
+
+class exact_fp32:
+    """Context manager: run the generator convolutions on the fp32-MFMA engine instead of the limb engine."""
+
+    def __init__(self, on=True):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = lib().damc_set_exact_fp32(1 if self.on else 0)
+        return self
+
+    def __exit__(self, *exc):
+        lib().damc_set_exact_fp32(self.prev)
+        return False
 
 
 def check(rc, what=""):

@@ -86,6 +86,12 @@ int damc_generator_layer_packed_sizes(const damc_layer_t* layer, size_t* fwd_flo
 /* re-lay PyTorch weight (ConvT: (Cin,Cout,k,k); Linear: (out,in)) into layer->w_fwd / w_bwd */
 int damc_pack_generator_layer(const damc_layer_t* layer, const float* w_torch, float* w_fwd, float* w_bwd,
                               void* stream);
+/* Generator convolutions whose gathered channel count is a multiple of 32 run on the limb engine by
+ * default: fp32 operands split into 3 bf16 limbs, 6 limb products per fp32 product on bf16 MFMA, fp32
+ * accumulation (error vs fp64 equal to fp32 MFMA's).  on != 0 selects the fp32-MFMA engine
+ * (v_mfma_f32_32x32x2_f32) for later launches; returns the previous setting.  Initial value: env
+ * DAMC_EXACT_FP32=1.  Packed weights / workspaces are sized for either engine. */
+int damc_set_exact_fp32(int on);
 /* w1t (nz,nh) and w2t (nh,nh) from the PyTorch w1/w2 */
 int damc_pack_ebm(const damc_ebm_t* ebm, float* w1t, float* w2t, void* stream);
 

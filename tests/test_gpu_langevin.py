@@ -220,3 +220,33 @@ def test_kmajor_batch_chunking_is_bitwise(lv, gpu_device, tmp_path):
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=600)
     r = np.load(out)
     assert np.array_equal(r["g"], g) and np.array_equal(r["xh"], xh)
+
+
+def test_limb_engine_as_accurate_as_fp32_mfma(lv, gpu_device):
+    """The limb engine (fp32 operands as 3 bf16 limbs, 6 limb products on bf16 MFMA, fp32 accumulate)
+    against the fp32-MFMA engine, both measured against an fp64 evaluation of the same CIFAR-10
+    full-width generator: the limb path must be as close to fp64 as exact fp32 arithmetic is
+    (within 1.5x), on the likelihood gradient, the forward image and one posterior step."""
+    from damc import _lib
+    from oracle import damc_oracle as orc
+
+    G, E, x, z0 = _cifar_full(gpu_device, 32)
+    L64 = orc.generator_layers(G, torch.float64)
+    P64 = orc.ebm_params(E, torch.float64)
+    g64 = orc.likelihood_grad(L64, z0.cpu().double(), x.cpu().double(), 0.1)[0].numpy()
+    x64 = orc.generator_sample(L64, z0.cpu().double()).numpy()
+    z64 = orc.posterior_langevin(L64, P64, z0.cpu().double(), x.cpu().double(), 1, 0.1, 0.1).numpy()
+
+    def run():
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 1, 0.1, 0.1, False)
+        return (lv.likelihood_grad(z0, x, G, 0.1).cpu().numpy(), lv.generator_forward(z0, G).cpu().numpy(),
+                z.cpu().numpy())
+
+    limb = run()
+    with _lib.exact_fp32():
+        exact = run()
+    assert _lib.lib().damc_set_exact_fp32(0) == 0  # the context restored the default engine
+    for got, ex, ref in zip(limb, exact, (g64, x64, z64)):
+        e_limb, e_exact = rel_l2(got, ref), rel_l2(ex, ref)
+        assert e_limb <= 1.5 * e_exact + 1e-7, (e_limb, e_exact)
