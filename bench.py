@@ -176,6 +176,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extras", action="store_true", help="skip the per-leg and amortizer timings")
+    ap.add_argument("--no-live-prof", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--exact-fp32", action="store_true",
                     help="run the generator convolutions on the fp32-MFMA engine instead of the limb engine")
     args = ap.parse_args()
@@ -212,7 +213,9 @@ def main():
         one_block(lv, G, E, x, z0, zbuf, pbuf, 1000 + i, rank)
     L = _lib.lib()
     L.damc_prof_reset()
-    L.damc_prof_enable(1)
+    # live HIP events only around the dominant kernel classes (every event pair costs the stream a gap)
+    L.damc_prof_select(b"upconv_fwd,upconv_dgrad")
+    L.damc_prof_enable(0 if args.no_live_prof else 1)
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -226,13 +229,25 @@ def main():
     # per-class kernel time from the live HIP events
     import ctypes
 
-    classes = {}
-    for name in ("upconv_fwd", "upconv_dgrad", "proj_fwd", "proj_dgrad", "smallc_fwd", "smallc_dgrad",
-                 "posterior_update", "slab_sum", "prior_chain", "split_x3"):
-        ms, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
-        _lib.check(L.damc_prof_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
-        if n.value:
-            classes[name] = dict(total_ms=ms.value, launches=n.value, flops=fl.value)
+    def query():
+        out = {}
+        for name in ("upconv_fwd", "upconv_dgrad", "proj_fwd", "proj_dgrad", "smallc_fwd", "smallc_dgrad",
+                     "posterior_update", "slab_sum", "prior_chain", "split_x3"):
+            ms, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
+            _lib.check(L.damc_prof_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
+            if n.value:
+                out[name] = dict(total_ms=ms.value, launches=n.value, flops=fl.value)
+        return out
+
+    classes = query()
+    # every kernel class, from one more (untimed) block with events around every launch
+    L.damc_prof_reset()
+    L.damc_prof_select(None)
+    L.damc_prof_enable(1)
+    one_block(lv, G, E, x, z0, zbuf, pbuf, 3000, rank)
+    torch.cuda.synchronize(device)
+    L.damc_prof_enable(0)
+    breakdown = query()
 
     extras = None
     if not args.no_extras:
@@ -250,14 +265,14 @@ def main():
         zsteps = world * B * POST_STEPS * args.steps
         value = zsteps / t_max
         dom = max(("upconv_fwd", "upconv_dgrad"), key=lambda k: classes.get(k, {}).get("total_ms", 0.0))
-        c = classes[dom]
+        c = classes.get(dom, dict(total_ms=float("nan"), launches=1, flops=float("nan")))
         avg_s = c["total_ms"] / c["launches"] / 1e3
         flops_per_launch = c["flops"] / c["launches"]
         achieved = flops_per_launch / avg_s / 1e12
         peak = PEAK_BF16_TFLOPS / LIMB_PRODUCTS if limb else PEAK_FP32_TFLOPS
         traffic = traffic_from_profiles(dom)
-        gemm_ms = sum(classes[k]["total_ms"] for k in classes if k.startswith(("upconv", "proj")))
-        gemm_fl = sum(classes[k]["flops"] for k in classes if k.startswith(("upconv", "proj")))
+        gemm_ms = sum(breakdown[k]["total_ms"] for k in breakdown if k.startswith(("upconv", "proj"))) or None
+        gemm_fl = sum(breakdown[k]["flops"] for k in breakdown if k.startswith(("upconv", "proj")))
         post_flops_step = 4.0 * B * 1089.2e6  # 4 * B * MAC_G per posterior step
         out = {
             "metric": "Langevin z-steps/sec (B=128, z_dim=128, CIFAR-10)",
@@ -296,9 +311,10 @@ def main():
             "posterior_tflops_effective": round(post_flops_step * POST_STEPS * args.steps / t_max / 1e12, 2),
             "gemm_classes_tflops": round(gemm_fl / (gemm_ms / 1e3) / 1e12, 2) if gemm_ms else None,
             "kernel_classes": {k: dict(avg_ms=round(v["total_ms"] / v["launches"], 4), launches=v["launches"])
-                               for k, v in classes.items()},
-            "prior_us_per_step": round(1e3 * classes["prior_chain"]["total_ms"] / classes["prior_chain"]["launches"]
-                                       / PRIOR_STEPS, 2) if "prior_chain" in classes else None,
+                               for k, v in breakdown.items()},
+            "prior_us_per_step": round(1e3 * breakdown["prior_chain"]["total_ms"]
+                                       / breakdown["prior_chain"]["launches"] / PRIOR_STEPS, 2)
+            if "prior_chain" in breakdown else None,
             "batch_iterations_per_s": round(args.steps / t_max, 3),
             "cpu_baseline": None,
         }

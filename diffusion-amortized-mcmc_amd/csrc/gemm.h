@@ -46,6 +46,8 @@ struct GemmArgs {
   // fp32 A / B pointers are not read
   const unsigned short* A3 = nullptr;
   const unsigned short* B3 = nullptr;
+  // limb engine output: an x3 copy of the epilogue result (C may then be null: fp32 not stored)
+  unsigned short* C3 = nullptr;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered

@@ -48,6 +48,25 @@ __device__ __forceinline__ long gemm_row_offset(const GemmArgs& p, int m, int py
   return (long)m * p.ldc;
 }
 
+// one output element: epilogue arithmetic + store (idx = row offset + n)
+template <int EPI>
+__device__ __forceinline__ void epi_element(const GemmArgs& p, float* Cz, long idx, int n, bool bias_wrap, float v) {
+  if (EPI == EPI_BIAS_ACT) {
+    if (p.bias) v += p.bias[bias_wrap ? n % p.bias_mod : n];
+    v = act_apply(v, p.act, p.slope);
+  } else if (EPI == EPI_MASK) {
+    v *= act_grad_from_out(p.mask[idx], p.mask_act, p.mask_slope);
+  } else if (EPI == EPI_RESID) {
+    if (p.bias) v += p.bias[n % p.bias_mod];
+    const float t = act_apply(v, p.act, p.slope);
+    if (p.xhat) p.xhat[idx] = t;
+    const float res = t - p.xres[idx];
+    if (p.sqerr) atomicAdd(p.sqerr, 0.5f * p.inv_s2 * res * res);
+    v = res * p.inv_s2 * act_grad_from_out(t, p.act, p.slope);
+  }
+  Cz[idx] = v;
+}
+
 // rowtab: optional per-block table of gemm_row_offset for rows m0 .. m0 + 32*MT*2 - 1
 template <int EPI, int OM, int MT>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[MT][2], int m0, int n0, int wm,
@@ -69,22 +88,32 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[M
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + wn * 64 + j * 32 + lrow;
         if (n >= p.N) continue;
-        float v = acc[i][j][r];
-        const long idx = rowoff + n;
-        if (EPI == EPI_BIAS_ACT) {
-          if (p.bias) v += p.bias[bias_wrap ? n % p.bias_mod : n];
-          v = act_apply(v, p.act, p.slope);
-        } else if (EPI == EPI_MASK) {
-          v *= act_grad_from_out(p.mask[idx], p.mask_act, p.mask_slope);
-        } else if (EPI == EPI_RESID) {
-          if (p.bias) v += p.bias[n % p.bias_mod];
-          const float t = act_apply(v, p.act, p.slope);
-          if (p.xhat) p.xhat[idx] = t;
-          const float res = t - p.xres[idx];
-          if (p.sqerr) atomicAdd(p.sqerr, 0.5f * p.inv_s2 * res * res);
-          v = res * p.inv_s2 * act_grad_from_out(t, p.act, p.slope);
-        }
-        Cz[idx] = v;
+        epi_element<EPI>(p, Cz, rowoff + n, n, bias_wrap, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+// the same for a wave's 4 x 4 grid of 16x16 accumulators (col = lane&15, row = 4(lane>>4) + r)
+template <int EPI, int OM>
+__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, f32x4 (&acc)[4][4], int m0, int n0, int wm, int wn,
+                                                int lane, int z, int py, int px, const long* rowtab) {
+  float* Cz = p.C;
+  if (OM == O_DENSE) Cz += (long)z * p.c_zstride;
+  const bool bias_wrap = p.bias_mod < p.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ml = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+      const int m = m0 + ml;
+      if (m >= p.M) continue;
+      const long rowoff = rowtab ? rowtab[ml] : gemm_row_offset<OM>(p, m, py, px);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (n >= p.N) continue;
+        epi_element<EPI>(p, Cz, rowoff + n, n, bias_wrap, acc[i][j][r]);
       }
     }
   }
@@ -748,17 +777,42 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
 // the same tap walk as the K-major engine (a K tile never straddles a tap, padding taps read zero
 // through an out-of-range buffer offset); B is x3 over K, [n][K/8][3][8].
 //
-// Block 256 x 128, 8 waves (4 along M x 2 along N), each wave 64 x 64 = 2 x 2 accumulators of 32 x 32.
-// LDS rows are 208 B (192 + 16 pad: any 16 consecutive rows cover all 64 banks for ds_read_b128),
-// double-buffered: 2 x 384 rows x 208 B = 159,744 B, one workgroup per CU.
-constexpr int X3_BM = 256, X3_BN = 128, X3_BK = 32, X3_ROWB = 208;
+// Block 256 x 128, 8 waves (4 along M x 2 along N), each wave 64 x 64 of accumulators.
+// LDS rows are the 192 B of a K tile, unpadded, with the four 48-B octets of row r stored at octet
+// position q ^ ((r >> 1) & 3): the ds_read_b128 lane groups of a 16x16x32 fragment read ({0-3,12-15,
+// 20-27}, ...) then hit 16 distinct 4-bank groups, and the staging writes are lane-linear (each thread
+// stores the PHYSICAL chunk id % 12 of row id / 12 and gathers the matching logical chunk), so 8-lane
+// write groups are contiguous.  Double-buffered: 2 x 384 rows x 192 B = 147,456 B, one workgroup per CU.
+constexpr int X3_BM = 256, X3_BN = 128, X3_BK = 32, X3_ROWB = 192;
+__device__ __forceinline__ int x3_swz(int row) { return (row >> 1) & 3; }
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
 constexpr int X3_AJ = X3_BM * X3_CHUNKS / 512, X3_BJ = X3_BN * X3_CHUNKS / 512;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int EPI, int OM>
+// V: variant bits (tools/gemm_bench.hip A/B): 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
+// wave, 2 = s_setprio(1) around the MFMA cluster, 4 = LDS-DMA staging (buffer_load ... lds straight into
+// the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write)
+#ifndef DAMC_X3_VARIANT
+#define DAMC_X3_VARIANT 5  // measured best (profiles/r01/gemm_bench.txt)
+#endif
+// RNE limb split of 8 consecutive values: v = h + m + l (to 24 significand bits)
+__device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 b0 = (__bf16)v[e];
+    const float r1 = v[e] - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)r2;
+  }
+}
+
+template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
+  constexpr bool M16 = (V & 1) != 0;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (X3_BM + X3_BN) * X3_ROWB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -810,14 +864,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
           if ((unsigned)(iy0 + ky) < (unsigned)p.Hin && (unsigned)(ix0 + kx) < (unsigned)Win)
             msk |= 1u << (ky * kw + kx);
     }
-    abase[j] = base * 6 + ch * 16;
+    const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;  // logical octet of physical chunk ch
+    abase[j] = base * 6 + q * 48 + limb * 16;
     amask[j] = msk;
     alds[j] = row * X3_ROWB + ch * 16;
   }
 #pragma unroll
   for (int j = 0; j < X3_BJ; ++j) {
     const int id = tid + 512 * j, row = id / X3_CHUNKS, ch = id - row * X3_CHUNKS;
-    boff[j] = (unsigned)((n0 + row) * p.K * 6 + ch * 16);  // rows >= N fall out of range
+    const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;
+    boff[j] = (unsigned)((n0 + row) * p.K * 6 + q * 48 + limb * 16);  // rows >= N fall out of range
     blds[j] = (X3_BM + row) * X3_ROWB + ch * 16;
   }
 
@@ -855,21 +911,56 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < X3_BJ; ++j) *reinterpret_cast<u32x4*>(base + blds[j]) = rb[j];
   };
+  // LDS-DMA form: chunk id -> LDS byte 16 id, so each wave-instruction fills 1 KiB at a wave-uniform base
+  typedef __attribute__((address_space(3))) void* lds_t;
+  const int wbase = (tid & ~63) * 16;
+  auto dma_ab = [&](int k0, int buf) {
+    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
+#pragma unroll
+    for (int j = 0; j < X3_AJ; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+#pragma unroll
+    for (int j = 0; j < X3_BJ; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
+                                               k0 * 6, 0, 0);
+    ci0 += X3_BK;
+    if (ci0 == Cg) {
+      ci0 = 0;
+      ++tap;
+      if (++tkx == kw) {
+        tkx = 0;
+        ++tky;
+      }
+      set_tap();
+    }
+  };
 
   f32x16 acc[2][2];
+  f32x4 acc16[4][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment of k16 step s, lane half h: octet 2s + h of the row, limb l at +16 l
-  const int lrow = lane & 31, lh = lane >> 5;
-  const int afr = (wm * 64 + lrow) * X3_ROWB + lh * 48;
-  const int bfr = (X3_BM + wn * 64 + lrow) * X3_ROWB + lh * 48;
+  // 32x32x16: fragment of k16 step s, lane half h = octet 2s + h of the row, limb l at +16 l
+  // 16x16x32: lane quarter q = octet q of the row (the whole 32-deep K tile in one MFMA)
+  // (tile bases are multiples of 16 rows, so the row swizzle is a function of lrow alone)
+  const int lrow = M16 ? (lane & 15) : (lane & 31), loct = M16 ? (lane >> 4) : (lane >> 5);
+  const int sw = x3_swz(lrow);
+  const int afr = (wm * 64 + lrow) * X3_ROWB, bfr = (X3_BM + wn * 64 + lrow) * X3_ROWB;
+  const int oct16 = (loct ^ sw) * 48;                                         // 16x16x32
+  const int oct32[2] = {((loct) ^ sw) * 48, ((2 + loct) ^ sw) * 48};          // 32x32x16, k16 step s
 
-  if (nk > 0) {
+  constexpr bool DMA = (V & 4) != 0;
+  if (DMA) {
+    if (nk > 0) dma_ab(0, 0);
+  } else if (nk > 0) {
     load_ab(0);
     store_ab(0);
     if (nk > 1) load_ab(X3_BK);
@@ -877,50 +968,145 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
-    bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
+    // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
+    // barrier at the end of this tile (its vmcnt(0)) lands it
+    if (DMA && kt + 1 < nk) dma_ab((kt + 1) * X3_BK, (kt + 1) & 1);
+    if (M16) {
+      bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int l = 0; l < 3; ++l) {
-          fa[s][t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 32 * X3_ROWB + s * 96 + l * 16);
-          fb[s][t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 32 * X3_ROWB + s * 96 + l * 16);
+          fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
+          fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
         }
-    if (kt + 1 < nk) {
-      store_ab((kt + 1) & 1);
-      if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+      if (!DMA && kt + 1 < nk) {
+        store_ab((kt + 1) & 1);
+        if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+      }
+      if (V & 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 c = acc16[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+        }
+      if (V & 2) __builtin_amdgcn_s_setprio(0);
+    } else {
+      bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int l = 0; l < 3; ++l) {
+            fa[s][t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 32 * X3_ROWB + oct32[s] + l * 16);
+            fb[s][t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 32 * X3_ROWB + oct32[s] + l * 16);
+          }
+      if (!DMA && kt + 1 < nk) {
+        store_ab((kt + 1) & 1);
+        if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+      }
+      if (V & 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][2], fb[s][j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][1], c, 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
+          }
+      if (V & 2) __builtin_amdgcn_s_setprio(0);
     }
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][2], fb[s][j][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][1], c, 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
-        }
     __syncthreads();
   }
-  if (OM == O_PHASE) {
-    long* rowtab = reinterpret_cast<long*>(smem);
-    if (tid < X3_BM) rowtab[tid] = gemm_row_offset<OM>(p, m0 + tid, py, px);
-    __syncthreads();
-    gemm_epilogue<EPI, OM, 2>(p, acc, m0, n0, wm, wn, lane, z, py, px, rowtab);
+  // ---- epilogue through LDS: the block's 256 x 128 fp32 tile, then one thread per (row, channel octet):
+  // 2 x 16-B fp32 stores and (C3) 3 x 16-B limb stores per octet, each row's 128 channels contiguous
+  constexpr int TS = X3_BN + 4;  // tile row stride (floats): 4-row groups of a 16x16 store land 16 banks apart
+  static_assert(X3_BM * TS * 4 + X3_BM * 8 <= 2 * (X3_BM + X3_BN) * X3_ROWB, "epilogue tile exceeds the LDS");
+  float* tile = reinterpret_cast<float*>(smem);
+  long* rowtab = reinterpret_cast<long*>(smem + X3_BM * TS * 4);
+  if (tid < X3_BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
+  if (M16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 64 + j * 16 + (lane & 15)] = acc16[i][j][r];
   } else {
-    gemm_epilogue<EPI, OM, 2>(p, acc, m0, n0, wm, wn, lane, z, py, px);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          tile[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TS + wn * 64 + j * 32 + (lane & 31)] =
+              acc[i][j][r];
+  }
+  __syncthreads();
+  float* Cz = p.C;
+  if (OM == O_DENSE && Cz) Cz += (long)z * p.c_zstride;
+#pragma unroll 2
+  for (int it = 0; it < X3_BM * X3_BN / 8 / 512; ++it) {
+    const int id = tid + 512 * it, row = id >> 4, oct = id & 15;
+    const int n = n0 + oct * 8;
+    const long rowoff = rowtab[row];
+    if (rowoff < 0 || n >= p.N) continue;
+    const long idx = rowoff + n;
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8);
+    const f32x4 t1 = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8 + 4);
+    float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    if (EPI == EPI_BIAS_ACT) {
+      if (p.bias) {
+        const int nb = p.bias_mod < p.N ? n % p.bias_mod : n;
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + nb);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + nb + 4);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bb[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_apply(v[e], p.act, p.slope);
+    } else if (EPI == EPI_MASK) {
+      const f32x4 k0 = *reinterpret_cast<const f32x4*>(p.mask + idx);
+      const f32x4 k1 = *reinterpret_cast<const f32x4*>(p.mask + idx + 4);
+      const float kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= act_grad_from_out(kk[e], p.mask_act, p.mask_slope);
+    }
+    if (Cz) {
+      *reinterpret_cast<f32x4*>(Cz + idx) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(Cz + idx + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+    if (p.C3) {
+      bf16x8 h, m, l;
+      split3_octet(v, h, m, l);
+      bf16x8* o = reinterpret_cast<bf16x8*>(p.C3 + 3 * idx);
+      o[0] = h;
+      o[1] = m;
+      o[2] = l;
+    }
   }
 }
 
-template <int EPI, int OM>
+template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 static void launch_x3_t(const GemmArgs& a, int zdim, hipStream_t s) {
   const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
-  hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
 }
 
 // fp32 [rows][C] -> x3 [rows][C/8][3][8]; one thread per channel octet
@@ -931,16 +1117,7 @@ __global__ void split_x3_kernel(const float* __restrict__ x, long n8, unsigned s
   const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
   const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
   bf16x8 h, m, l;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 b0 = (__bf16)v[e];
-    const float r1 = v[e] - (float)b0;
-    const __bf16 b1 = (__bf16)r1;
-    const float r2 = r1 - (float)b1;
-    h[e] = b0;
-    m[e] = b1;
-    l[e] = (__bf16)r2;
-  }
+  split3_octet(v, h, m, l);
   bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * i;
   o[0] = h;
   o[1] = m;
@@ -962,7 +1139,12 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   if (!a.A3 || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 || taps % a.kw != 0 || taps > 32)
     return DAMC_ERR_ARG;
   if ((om == O_PHASE) != (zdim == 4) || (om == O_DENSE && zdim != 1)) return DAMC_ERR_ARG;
-  if (((uintptr_t)a.A3 | (uintptr_t)a.B3) % 16 != 0) return DAMC_ERR_ARG;
+  if (((uintptr_t)a.A3 | (uintptr_t)a.B3 | (uintptr_t)a.C | (uintptr_t)a.C3 | (uintptr_t)a.mask) % 16 != 0)
+    return DAMC_ERR_ARG;
+  if (!a.C && !a.C3) return DAMC_ERR_ARG;
+  // octet epilogue: 8 consecutive channels per thread, 16-B aligned rows and bias
+  if (a.N % 8 != 0 || a.ldc % 8 != 0 || (a.bias && ((uintptr_t)a.bias % 16 != 0 || a.bias_mod % 8 != 0)))
+    return DAMC_ERR_UNSUPPORTED;
   if ((double)a.N * a.K * 6 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
   const long hwq = (long)a.Hq * a.Wq;
   if (a.M % hwq != 0) return DAMC_ERR_ARG;
@@ -980,7 +1162,8 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
     c.A3 = a.A3 + b0 * img * 3;
-    c.C = a.C + b0 * cimg;
+    if (a.C) c.C = a.C + b0 * cimg;
+    if (a.C3) c.C3 = a.C3 + b0 * cimg * 3;
     if (a.mask) c.mask = a.mask + b0 * cimg;
     c.M = (int)(nb * hwq);
 #define DAMC_X3(E_, O_)                \

@@ -417,7 +417,7 @@ template <int NC, int K, int S, int CH>
 __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, int Hin, int Win, int Cin, int pad,
                                                                int Hout, int Wout, const float* __restrict__ wpk,
                                                                const float* __restrict__ delta, int mask_act,
-                                                               float mask_slope) {
+                                                               float mask_slope, unsigned short* __restrict__ h3) {
   typedef typename VecT<CH>::T V;
   const int G = Cin / CH, P = 64 / G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -466,7 +466,28 @@ __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, 
         for (int o = 0; o < NC; ++o) acc[c] = fmaf(d[t][o], w[t][c][o], acc[c]);
 #pragma unroll
     for (int c = 0; c < CH; ++c) hv[c] = acc[c] * act_grad_from_out(hv[c], mask_act, mask_slope);
-    *hp = hv;
+    if (h3) {
+      // limbs only (the limb engine reads this gradient); h keeps the activation.  x3 layout:
+      // pixel row of 3*Cin bf16, channel octet o at 24 o, limb l at + 8 l
+      unsigned short* q = h3 + pix * 3 * Cin + (ci0 >> 3) * 24 + (ci0 & 7);
+      typedef unsigned short U __attribute__((ext_vector_type(CH)));
+      U lh, lm, ll;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const __bf16 b0 = (__bf16)hv[c];
+        const float r1 = hv[c] - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        const __bf16 b2 = (__bf16)(r1 - (float)b1);
+        lh[c] = __builtin_bit_cast(unsigned short, b0);
+        lm[c] = __builtin_bit_cast(unsigned short, b1);
+        ll[c] = __builtin_bit_cast(unsigned short, b2);
+      }
+      *reinterpret_cast<U*>(q) = lh;
+      *reinterpret_cast<U*>(q + 8) = lm;
+      *reinterpret_cast<U*>(q + 16) = ll;
+    } else {
+      *hp = hv;
+    }
   }
 }
 
@@ -483,7 +504,7 @@ bool smallc_reg_ok(const damc_layer_t& L) {
 template <int NC>
 bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, float* h_out, int B, const float* x,
                          float inv_s2, float* delta, const float* delta_in, float* xhat, float* sqerr, int mask_act,
-                         float mask_slope, hipStream_t s) {
+                         float mask_slope, hipStream_t s, unsigned short* h3 = nullptr) {
   const int CH = L.k == 3 ? 4 : 2;
   if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
   if (L.cin % CH) return false;
@@ -502,10 +523,10 @@ bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, flo
   } else {
     if (L.k == 3)
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 3, 1, 4>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
-                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope);
+                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
     else
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
-                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope);
+                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
   }
   return true;
 }
@@ -674,16 +695,20 @@ int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, flo
   return (int)hipGetLastError();
 }
 
+// the register-resident dgrad can write its gradient as x3 limbs (channel groups never straddle an octet)
+bool smallc_x3_ok(const damc_layer_t& L) { return smallc_reg_ok(L) && L.cin % 8 == 0; }
+
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
-                 hipStream_t s) {
+                 unsigned short* h3, hipStream_t s) {
+  if (h3 && !smallc_x3_ok(L)) return DAMC_ERR_ARG;
   if (smallc_reg_ok(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
     if (L.cout == 3)
       smallc_reg_dispatch<3>(false, L, nullptr, h, B, nullptr, 0.f, nullptr, delta, nullptr, nullptr, mask_act,
-                             mask_slope, s);
+                             mask_slope, s, h3);
     else
       smallc_reg_dispatch<1>(false, L, nullptr, h, B, nullptr, 0.f, nullptr, delta, nullptr, nullptr, mask_act,
-                             mask_slope, s);
+                             mask_slope, s, h3);
     return (int)hipGetLastError();
   }
   const size_t sm = (size_t)L.k * L.k * L.cin * L.cout * sizeof(float);
@@ -783,8 +808,12 @@ int g_exact_fp32 = [] {
   const char* e = getenv("DAMC_EXACT_FP32");
   return (e && e[0] == '1') ? 1 : 0;
 }();
-bool x3_fwd_cap(const damc_layer_t& L) { return L.kind == DAMC_LAYER_UP2 && L.cin % damc::KM_BK == 0; }
-bool x3_bwd_cap(const damc_layer_t& L) { return L.kind == DAMC_LAYER_UP2 && L.cout % damc::KM_BK == 0; }
+bool x3_fwd_cap(const damc_layer_t& L) {
+  return L.kind == DAMC_LAYER_UP2 && L.cin % damc::KM_BK == 0 && L.cout % 8 == 0;
+}
+bool x3_bwd_cap(const damc_layer_t& L) {
+  return L.kind == DAMC_LAYER_UP2 && L.cout % damc::KM_BK == 0 && L.cin % 8 == 0;
+}
 bool x3_fwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_fwd_cap(L); }
 bool x3_bwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_bwd_cap(L); }
 size_t up2_floats(const damc_layer_t& L) { return (size_t)L.cin * L.cout * 16; }
@@ -914,11 +943,12 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       if (x3_fwd(L)) {
         a.A3 = ws.h3[i - 1];
         a.B3 = x3_of(L.w_fwd, up2_floats(L));
+        if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) a.C3 = ws.h3[i];  // the next layer's operand
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
     if (rc) return rc;
-    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {
+    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1]) && !(L.kind == DAMC_LAYER_UP2 && x3_fwd(L))) {
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(ws.h[i], act_floats(L, B), ws.h3[i], s))) return rc;
     }
@@ -974,8 +1004,10 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
     const damc_layer_t& P = g->layers[i - 1];
     float* out = ws.h[i - 1];  // dgrad overwrites the activation it is masked with
     int rc;
+    bool x3_out = false;  // the gradient went straight into its x3 copy
     if (L.kind == DAMC_LAYER_SMALLC) {
-      rc = smallc_dgrad(L, out, B, d, P.act, P.slope, s);
+      x3_out = x3_bwd(P) && smallc_x3_ok(L);
+      rc = smallc_dgrad(L, out, B, d, P.act, P.slope, x3_out ? ws.h3[i - 1] : nullptr, s);
     } else if (L.kind == DAMC_LAYER_UP2) {
       const bool x3 = x3_bwd(L);
       GemmArgs a;
@@ -1004,6 +1036,11 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
       if (x3) {
         a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
+        if (x3_bwd(P)) {  // only the next dgrad reads this gradient: limbs only, the fp32 activation stays
+          a.C3 = ws.h3[i - 1];
+          a.C = nullptr;
+          x3_out = true;
+        }
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_MASK, damc::O_DENSE, 1, "upconv_dgrad", conv_flops(L, B), s);
     } else {  // LINEAR hidden/final
@@ -1025,7 +1062,7 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
                              2.0 * B * (double)L.cin * L.cout, s);
     }
     if (rc) return rc;
-    if (x3_bwd(P)) {  // the next dgrad reads this gradient through the limb engine
+    if (x3_bwd(P) && !x3_out) {  // the next dgrad reads this gradient through the limb engine
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(out, act_floats(P, B), ws.h3[i - 1], s))) return rc;
     }

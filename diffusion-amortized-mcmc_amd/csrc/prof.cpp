@@ -21,6 +21,7 @@ std::mutex g_mu;
 bool g_on = false;
 std::vector<Rec> g_recs;
 std::vector<hipEvent_t> g_pool;
+std::vector<std::string> g_select;  // recorded classes (empty = all)
 
 hipEvent_t take_event() {
   if (!g_pool.empty()) {
@@ -38,6 +39,11 @@ namespace damc_prof {
 bool enabled() { return g_on; }
 int begin(const char* name, double flops, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_select.empty()) {
+    bool hit = false;
+    for (const std::string& c : g_select) hit = hit || (name && c == name);
+    if (!hit) return -1;
+  }
   Rec r{name ? name : "?", flops, take_event(), take_event()};
   if (!r.a || !r.b) return -1;
   if (hipEventRecord(r.a, s) != hipSuccess) return -1;
@@ -53,6 +59,23 @@ void end(int slot, hipStream_t s) {
 
 extern "C" int damc_prof_enable(int on) {
   g_on = on != 0;
+  return 0;
+}
+
+extern "C" int damc_prof_select(const char* classes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_select.clear();
+  if (!classes) return 0;
+  std::string cur;
+  for (const char* c = classes;; ++c) {
+    if (*c == ',' || *c == 0) {
+      if (!cur.empty()) g_select.push_back(cur);
+      cur.clear();
+      if (*c == 0) break;
+    } else {
+      cur += *c;
+    }
+  }
   return 0;
 }
 

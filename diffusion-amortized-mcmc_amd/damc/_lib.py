@@ -96,6 +96,7 @@ _SIGS = {
                                 _SZ, _P]),
     "damc_prof_enable": (_I, [_I]),
     "damc_prof_reset": (_I, []),
+    "damc_prof_select": (_I, [ctypes.c_char_p]),
     "damc_prof_query": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),
                              ctypes.POINTER(ctypes.c_double)]),
 }

@@ -196,6 +196,8 @@ int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, i
 /* optional per-kernel HIP-event timing (bench.py roofline): records events around each
  * launch of the named kernel class on the launch stream; read back after a sync. */
 int damc_prof_enable(int on);
+/* record only the comma-separated kernel classes in `classes` (NULL: every class) */
+int damc_prof_select(const char* classes);
 int damc_prof_reset(void);
 /* total ms and launch count for kernel class `name` ("upconv_fwd", "upconv_dgrad", ...) */
 int damc_prof_query(const char* name, double* total_ms, long* launches, double* flops);

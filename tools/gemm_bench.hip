@@ -70,15 +70,16 @@ static unsigned short* split_dev(const float* d, size_t n) {
   return y;
 }
 
+template <int V>
 static void run_x3(const Shape& sh, hipStream_t s) {
   GemmArgs a = sh.a;
   a.A3 = sh.a3;
   a.B3 = sh.b3;
   a.b_zstride = (long)a.N * a.K;
   if (sh.phase)
-    launch_x3_t<EPI_BIAS_ACT, O_PHASE>(a, 4, s);
+    launch_x3_t<EPI_BIAS_ACT, O_PHASE, V>(a, 4, s);
   else
-    launch_x3_t<EPI_MASK, O_DENSE>(a, 1, s);
+    launch_x3_t<EPI_MASK, O_DENSE, V>(a, 1, s);
 }
 
 static std::vector<float> to_host(const float* d, size_t n) {
@@ -233,7 +234,8 @@ int main(int argc, char** argv) {
     sh.a3 = split_dev(a.A, na);
     sh.b3 = split_dev(sh.bt, (size_t)(sh.phase ? 4 : 1) * a.N * a.K);
   }
-  V vars[] = {{"KM/p3", run_km<3>}, {"X3", run_x3}};
+  V vars[] = {{"KM/p3", run_km<3>}, {"X3/v3", run_x3<3>}, {"X3/v5", run_x3<5>}, {"X3/v7", run_x3<7>},
+              {"X3/v4", run_x3<4>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
