@@ -958,6 +958,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int oct32[2] = {((loct) ^ sw) * 48, ((2 + loct) ^ sw) * 48};          // 32x32x16, k16 step s
 
   constexpr bool DMA = (V & 4) != 0;
+  {
+  constexpr bool DMA = (V & 4) != 0;
   if (DMA) {
     if (nk > 0) dma_ab(0, 0);
   } else if (nk > 0) {
@@ -1031,6 +1033,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       if (V & 2) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
+  }
   }
   // ---- epilogue through LDS: the block's 256 x 128 fp32 tile, then one thread per (row, channel octet):
   // 2 x 16-B fp32 stores and (C3) 3 x 16-B limb stores per octet, each row's 128 channels contiguous

@@ -491,6 +491,115 @@ __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, 
   }
 }
 
+// k3 s1 p1 output-layer dgrad (CIFAR-10): a block owns R input rows of one image and stages the
+// (R+2) x (W+2) x NC delta window (zero border) in LDS once, so the 9 taps read LDS broadcasts instead
+// of per-pixel global gathers; lanes own 4 channels of a pixel and each wave walks its pixels UNR at a
+// time (UNR activation loads in flight).  Output: the masked gradient as fp32 in place, or (h3) as x3
+// limbs only, lane pairs exchanging halves so every store is a whole 16-B limb octet.
+template <int NC, int UNR>
+__global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict__ h, int Hin, int Win, int Cin,
+                                                              int R, const float* __restrict__ wpk,
+                                                              const float* __restrict__ delta, int mask_act,
+                                                              float mask_slope, unsigned short* __restrict__ h3) {
+  extern __shared__ float dl[];  // [(R+2)][(Win+2)][NC]
+  constexpr int K = 3, CH = 4;
+  const int G = Cin / CH, P = 64 / G;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane % G, sub = lane / G;
+  const int ci0 = g * CH;
+  const int b = blockIdx.y, y0 = blockIdx.x * R;
+  const int rows = min(R, Hin - y0);
+  const int W2 = Win + 2;
+  // delta window rows y0-1 .. y0+rows (output pixel (oy, ox) at [oy - y0 + 1][ox + 1])
+  for (int i = threadIdx.x; i < (R + 2) * W2 * NC; i += 256) {
+    const int o = i % NC, c = (i / NC) % W2, r = i / (NC * W2);
+    const int oy = y0 - 1 + r, ox = c - 1;
+    dl[i] = (oy >= 0 && oy < Hin && ox >= 0 && ox < Win && r < rows + 2)
+                ? delta[(((long)b * Hin + oy) * Win + ox) * NC + o]
+                : 0.f;
+  }
+  float w[K * K][CH][NC];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int o = 0; o < NC; ++o) w[t][c][o] = wpk[((long)t * Cin + ci0 + c) * NC + o];
+  __syncthreads();
+  const int npix = rows * Win;
+  const long pbase = ((long)b * Hin + y0) * Win;
+  for (int p0 = wave * P * UNR; p0 < npix; p0 += 4 * P * UNR) {
+    f32x4 hv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pl = p0 + u * P + sub;
+      hv[u] = pl < npix ? *reinterpret_cast<const f32x4*>(h + (pbase + pl) * Cin + ci0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pl = p0 + u * P + sub;
+      if (p0 + u * P >= npix) break;  // wave-uniform
+      const int iy = pl / Win, ix = pl - iy * Win;
+      float acc[CH] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          // output pixel (iy - 1 + ky, ix - 1 + kx) -> window [iy + ky][ix + kx]
+          const float* dp = dl + ((min(iy, rows - 1) + ky) * W2 + ix + kx) * NC;
+#pragma unroll
+          for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int o = 0; o < NC; ++o) acc[c] = fmaf(dp[o], w[ky * K + kx][c][o], acc[c]);
+        }
+      float v[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) v[c] = acc[c] * act_grad_from_out(hv[u][c], mask_act, mask_slope);
+      const bool live = pl < npix;
+      const long pix = pbase + pl;
+      if (!h3) {
+        if (live) *reinterpret_cast<f32x4*>(h + pix * Cin + ci0) = f32x4{v[0], v[1], v[2], v[3]};
+        continue;
+      }
+      // limbs of the 4 channels, packed 2 per dword; partner lane (g ^ 1) holds the other half octet
+      unsigned lh[2], lm[2], ll[2];
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        unsigned short hh[2], mm[2], lo[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float x = v[2 * c2 + e];
+          const __bf16 b0 = (__bf16)x;
+          const float r1 = x - (float)b0;
+          const __bf16 b1 = (__bf16)r1;
+          hh[e] = __builtin_bit_cast(unsigned short, b0);
+          mm[e] = __builtin_bit_cast(unsigned short, b1);
+          lo[e] = __builtin_bit_cast(unsigned short, (__bf16)(r1 - (float)b1));
+        }
+        lh[c2] = hh[0] | ((unsigned)hh[1] << 16);
+        lm[c2] = mm[0] | ((unsigned)mm[1] << 16);
+        ll[c2] = lo[0] | ((unsigned)lo[1] << 16);
+      }
+      unsigned ph[2], pm[2], pq[2];
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        ph[c2] = __shfl_xor(lh[c2], 1, 64);
+        pm[c2] = __shfl_xor(lm[c2], 1, 64);
+        pq[c2] = __shfl_xor(ll[c2], 1, 64);
+      }
+      if (!live) continue;
+      typedef unsigned u4 __attribute__((ext_vector_type(4)));
+      u4* q = reinterpret_cast<u4*>(h3 + pix * 3 * Cin + (ci0 >> 3) * 24);
+      if ((g & 1) == 0) {
+        q[0] = u4{lh[0], lh[1], ph[0], ph[1]};
+        q[2] = u4{ll[0], ll[1], pq[0], pq[1]};
+      } else {
+        q[1] = u4{pm[0], pm[1], lm[0], lm[1]};
+      }
+    }
+  }
+}
+
 bool smallc_reg_ok(const damc_layer_t& L) {
   if (L.cout != 1 && L.cout != 3) return false;
   if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
@@ -701,6 +810,19 @@ bool smallc_x3_ok(const damc_layer_t& L) { return smallc_reg_ok(L) && L.cin % 8 
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
                  unsigned short* h3, hipStream_t s) {
   if (h3 && !smallc_x3_ok(L)) return DAMC_ERR_ARG;
+  if (smallc_reg_ok(L) && L.k == 3 && L.stride == 1 && L.pad == 1 && L.hout == L.hin && L.wout == L.win) {
+    ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
+    const int R = 4;
+    const dim3 grid((unsigned)((L.hin + R - 1) / R), (unsigned)B);
+    const size_t sm = sizeof(float) * (R + 2) * (L.win + 2) * L.cout;
+    if (L.cout == 3)
+      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
+                         delta, mask_act, mask_slope, h3);
+    else
+      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<1, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
+                         delta, mask_act, mask_slope, h3);
+    return (int)hipGetLastError();
+  }
   if (smallc_reg_ok(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
     if (L.cout == 3)
@@ -815,6 +937,11 @@ bool x3_bwd_cap(const damc_layer_t& L) {
   return L.kind == DAMC_LAYER_UP2 && L.cout % damc::KM_BK == 0 && L.cin % 8 == 0;
 }
 bool x3_fwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_fwd_cap(L); }
+// first layer z.W as a 1x1 convolution on the limb engine (z split into limbs per call)
+bool x3_proj_cap(const damc_layer_t& L) {
+  return L.kind == DAMC_LAYER_PROJ && L.cin % damc::KM_BK == 0 && L.cout % 8 == 0;
+}
+bool x3_proj(const damc_layer_t& L) { return !g_exact_fp32 && x3_proj_cap(L); }
 bool x3_bwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_bwd_cap(L); }
 size_t up2_floats(const damc_layer_t& L) { return (size_t)L.cin * L.cout * 16; }
 // x3 copy of a packed weight matrix, stored behind its fp32 packing (n floats, 16-B aligned)
@@ -828,6 +955,7 @@ bool h_needs_x3(const damc_generator_t* g, int j) {
 struct Workspace {
   std::vector<float*> h;  // activations (NHWC), one per layer except the final one
   std::vector<unsigned short*> h3;  // x3 limb copies of h (limb engine operands) or nullptr
+  unsigned short* z3;               // x3 limbs of z (limb-engine first layer) or nullptr
   float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
   float* slabs;           // split-K partial gradients
   float* glik;            // their fixed-order sum: grad of the likelihood term (B, nz)
@@ -864,7 +992,10 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   float* sl = take((long)S * B * g->nz);
   float* gl = take((long)B * g->nz);
   float* pb = (F.kind == DAMC_LAYER_SMALLC) ? take((long)B * F.hin * F.win * smallc_ntile(F) * 32) : nullptr;
+  unsigned short* z3 =
+      x3_proj_cap(L0) ? reinterpret_cast<unsigned short*>(take((long)B * g->nz * 3 / 2 + 4)) : nullptr;
   if (w) {
+    w->z3 = z3;
     w->delta = d;
     w->slabs = sl;
     w->glik = gl;
@@ -892,7 +1023,31 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
     a.slope = L.slope;
     a.C = ws.h[i];
     int rc;
-    if (L.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok(L.cin)) {
+    bool wrote_x3 = false;  // the epilogue already wrote ws.h3[i]
+    if (x3_proj(L) && i == 0) {
+      // z . W on the limb engine: z -> limbs, 1x1 "convolution" against the x3 copy of the dgrad
+      // packing [(oy,ox,co)][ci]; the epilogue writes the next layer's limbs too
+      const int N = L.hout * L.wout * L.cout;
+      {
+        ProfScope ps("split_x3", 0.0, s);
+        if ((rc = damc::launch_split_x3(z, (long)B * L.cin, ws.z3, s))) return rc;
+      }
+      a.A = z;
+      a.A3 = ws.z3;
+      a.B3 = x3_of(L.w_bwd, (size_t)L.cin * N);
+      a.Cg = L.cin;
+      a.ldc = N;
+      a.M = B;
+      a.N = N;
+      a.K = L.cin;
+      a.k_per_z = a.K;
+      if (g->n_layers > 1 && x3_fwd(g->layers[1])) {
+        a.C3 = ws.h3[0];
+        wrote_x3 = true;
+      }
+      rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
+                             2.0 * B * (double)N * L.cin, s);
+    } else if (L.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok(L.cin)) {
       // z . W as a 1x1 "convolution" on the K-major engine; its B operand [(oy,ox,co)][ci] is the
       // dgrad packing
       const int N = L.hout * L.wout * L.cout;
@@ -943,12 +1098,15 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       if (x3_fwd(L)) {
         a.A3 = ws.h3[i - 1];
         a.B3 = x3_of(L.w_fwd, up2_floats(L));
-        if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) a.C3 = ws.h3[i];  // the next layer's operand
+        if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {  // the next layer's operand
+          a.C3 = ws.h3[i];
+          wrote_x3 = true;
+        }
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
     if (rc) return rc;
-    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1]) && !(L.kind == DAMC_LAYER_UP2 && x3_fwd(L))) {
+    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1]) && !wrote_x3) {
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(ws.h[i], act_floats(L, B), ws.h3[i], s))) return rc;
     }
@@ -1110,6 +1268,9 @@ extern "C" int damc_generator_layer_packed_sizes(const damc_layer_t* L, size_t* 
       *bwd = n + (x3_bwd_cap(*L) ? n * 3 / 2 : 0);
       return 0;
     case DAMC_LAYER_PROJ:
+      *fwd = n;
+      *bwd = n + (x3_proj_cap(*L) ? n * 3 / 2 : 0);
+      return 0;
     case DAMC_LAYER_LINEAR:
       *fwd = n;
       *bwd = n;
@@ -1131,6 +1292,7 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
     case DAMC_LAYER_PROJ:
       if (!wb) return DAMC_ERR_ARG;
       hipLaunchKernelGGL(pack_proj_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf, wb);
+      if (x3_proj_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wb, n, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_UP2:
       if (!wb || L->k != 4) return DAMC_ERR_ARG;
