@@ -305,7 +305,7 @@ def main():
                               else "fp32 MFMA dense peak",
             },
             "gemm_arith": ("fp32 operands as 3 bf16 limbs, 6 limb products per fp32 product on "
-                           "v_mfma_f32_32x32x16_bf16, fp32 accumulation; error vs fp64 equal to the fp32-MFMA "
+                           "v_mfma_f32_16x16x32_bf16, fp32 accumulation; error vs fp64 equal to the fp32-MFMA "
                            "engine's (profiles/r01/gemm_bench.txt)") if limb
                           else "fp32 v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains)",
             "posterior_tflops_effective": round(post_flops_step * POST_STEPS * args.steps / t_max / 1e12, 2),

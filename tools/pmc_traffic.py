@@ -14,6 +14,10 @@ import sys
 from collections import defaultdict
 
 CLASSES = [
+    (r"gemm_x3_kernel<2, 0", "upconv_dgrad"),
+    (r"gemm_x3_kernel<1, 1", "upconv_fwd"),
+    (r"gemm_x3_kernel<1, 0", "proj_fwd"),
+    (r"split_x3_kernel", "split_x3"),
     (r"gemm_km_kernel<2, 0", "upconv_dgrad"),
     (r"gemm_km_kernel<1, 1", "upconv_fwd"),
     (r"gemm_f32_kernel<1, 2, 0", "upconv_dgrad"),
