@@ -48,6 +48,10 @@ struct GemmArgs {
   const unsigned short* B3 = nullptr;
   // limb engine output: an x3 copy of the epilogue result (C may then be null: fp32 not stored)
   unsigned short* C3 = nullptr;
+  // limb engine: sign bits of the epilogue result (bit e of byte idx/8 = out[idx + e] > 0), and for
+  // EPI_MASK the LReLU' mask read from such bits instead of from the fp32 `mask`
+  unsigned char* sgn = nullptr;
+  const unsigned char* mask_sgn = nullptr;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered

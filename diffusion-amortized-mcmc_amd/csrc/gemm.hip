@@ -1085,11 +1085,23 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = act_apply(v[e], p.act, p.slope);
     } else if (EPI == EPI_MASK) {
-      const f32x4 k0 = *reinterpret_cast<const f32x4*>(p.mask + idx);
-      const f32x4 k1 = *reinterpret_cast<const f32x4*>(p.mask + idx + 4);
-      const float kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+      if (p.mask_sgn) {  // LReLU' from the sign bits of the activation: 1 where it was > 0, else slope
+        const unsigned bits = p.mask_sgn[idx >> 3];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= act_grad_from_out(kk[e], p.mask_act, p.mask_slope);
+        for (int e = 0; e < 8; ++e) v[e] *= ((bits >> e) & 1u) ? 1.f : p.mask_slope;
+      } else {
+        const f32x4 k0 = *reinterpret_cast<const f32x4*>(p.mask + idx);
+        const f32x4 k1 = *reinterpret_cast<const f32x4*>(p.mask + idx + 4);
+        const float kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= act_grad_from_out(kk[e], p.mask_act, p.mask_slope);
+      }
+    }
+    if (p.sgn) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= (v[e] > 0.f ? 1u : 0u) << e;
+      p.sgn[idx >> 3] = (unsigned char)bits;
     }
     if (Cz) {
       *reinterpret_cast<f32x4*>(Cz + idx) = f32x4{v[0], v[1], v[2], v[3]};
@@ -1145,6 +1157,8 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   if (((uintptr_t)a.A3 | (uintptr_t)a.B3 | (uintptr_t)a.C | (uintptr_t)a.C3 | (uintptr_t)a.mask) % 16 != 0)
     return DAMC_ERR_ARG;
   if (!a.C && !a.C3) return DAMC_ERR_ARG;
+  if (epi == EPI_MASK && !a.mask && !a.mask_sgn) return DAMC_ERR_ARG;
+  if (a.mask_sgn && a.mask_act != DAMC_ACT_LRELU) return DAMC_ERR_ARG;
   // octet epilogue: 8 consecutive channels per thread, 16-B aligned rows and bias
   if (a.N % 8 != 0 || a.ldc % 8 != 0 || (a.bias && ((uintptr_t)a.bias % 16 != 0 || a.bias_mod % 8 != 0)))
     return DAMC_ERR_UNSUPPORTED;
@@ -1167,6 +1181,8 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     c.A3 = a.A3 + b0 * img * 3;
     if (a.C) c.C = a.C + b0 * cimg;
     if (a.C3) c.C3 = a.C3 + b0 * cimg * 3;
+    if (a.sgn) c.sgn = a.sgn + b0 * cimg / 8;
+    if (a.mask_sgn) c.mask_sgn = a.mask_sgn + b0 * cimg / 8;
     if (a.mask) c.mask = a.mask + b0 * cimg;
     c.M = (int)(nb * hwq);
 #define DAMC_X3(E_, O_)                \

@@ -500,21 +500,25 @@ template <int NC, int UNR>
 __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict__ h, int Hin, int Win, int Cin,
                                                               int R, const float* __restrict__ wpk,
                                                               const float* __restrict__ delta, int mask_act,
-                                                              float mask_slope, unsigned short* __restrict__ h3) {
-  extern __shared__ float dl[];  // [(R+2)][(Win+2)][NC]
+                                                              float mask_slope, unsigned short* __restrict__ h3,
+                                                              const unsigned char* __restrict__ hbits) {
+  extern __shared__ __attribute__((aligned(16))) float dl[];  // [(R+2)][(Win+2)][4]
+  __shared__ __attribute__((aligned(16))) unsigned char stg_all[4][UNR * 1536];  // per-wave x3 staging
   constexpr int K = 3, CH = 4;
   const int G = Cin / CH, P = 64 / G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned char* stg = stg_all[wave];
   const int g = lane % G, sub = lane / G;
   const int ci0 = g * CH;
   const int b = blockIdx.y, y0 = blockIdx.x * R;
   const int rows = min(R, Hin - y0);
   const int W2 = Win + 2;
   // delta window rows y0-1 .. y0+rows (output pixel (oy, ox) at [oy - y0 + 1][ox + 1])
-  for (int i = threadIdx.x; i < (R + 2) * W2 * NC; i += 256) {
-    const int o = i % NC, c = (i / NC) % W2, r = i / (NC * W2);
+  // window cells padded to 4 floats: one ds_read_b128 broadcast per tap
+  for (int i = threadIdx.x; i < (R + 2) * W2 * 4; i += 256) {
+    const int o = i & 3, c = (i >> 2) % W2, r = (i >> 2) / W2;
     const int oy = y0 - 1 + r, ox = c - 1;
-    dl[i] = (oy >= 0 && oy < Hin && ox >= 0 && ox < Win && r < rows + 2)
+    dl[i] = (o < NC && oy >= 0 && oy < Hin && ox >= 0 && ox < Win && r < rows + 2)
                 ? delta[(((long)b * Hin + oy) * Win + ox) * NC + o]
                 : 0.f;
   }
@@ -529,16 +533,24 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
   const int npix = rows * Win;
   const long pbase = ((long)b * Hin + y0) * Win;
   for (int p0 = wave * P * UNR; p0 < npix; p0 += 4 * P * UNR) {
+    // the LReLU' mask source: the fp32 activation, or (hbits) its sign bits (nibble of this lane's 4 channels)
     f32x4 hv[UNR];
+    unsigned mb[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int pl = p0 + u * P + sub;
-      hv[u] = pl < npix ? *reinterpret_cast<const f32x4*>(h + (pbase + pl) * Cin + ci0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (hbits) {
+        mb[u] = pl < npix ? (hbits[((pbase + pl) * Cin + ci0) >> 3] >> (ci0 & 4)) & 15u : 0u;
+        hv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        mb[u] = 0u;
+        hv[u] = pl < npix ? *reinterpret_cast<const f32x4*>(h + (pbase + pl) * Cin + ci0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int pl = p0 + u * P + sub;
-      if (p0 + u * P >= npix) break;  // wave-uniform
+      if (p0 + u * P >= npix) break;  // wave-uniform (the flush below stores only the valid pixels)
       const int iy = pl / Win, ix = pl - iy * Win;
       float acc[CH] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -546,22 +558,23 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
           // output pixel (iy - 1 + ky, ix - 1 + kx) -> window [iy + ky][ix + kx]
-          const float* dp = dl + ((min(iy, rows - 1) + ky) * W2 + ix + kx) * NC;
+          const f32x4 dv = *reinterpret_cast<const f32x4*>(dl + ((min(iy, rows - 1) + ky) * W2 + ix + kx) * 4);
 #pragma unroll
           for (int c = 0; c < CH; ++c)
 #pragma unroll
-            for (int o = 0; o < NC; ++o) acc[c] = fmaf(dp[o], w[ky * K + kx][c][o], acc[c]);
+            for (int o = 0; o < NC; ++o) acc[c] = fmaf(dv[o], w[ky * K + kx][c][o], acc[c]);
         }
       float v[CH];
 #pragma unroll
-      for (int c = 0; c < CH; ++c) v[c] = acc[c] * act_grad_from_out(hv[u][c], mask_act, mask_slope);
+      for (int c = 0; c < CH; ++c)
+        v[c] = acc[c] * (hbits ? (((mb[u] >> c) & 1u) ? 1.f : mask_slope) : act_grad_from_out(hv[u][c], mask_act, mask_slope));
       const bool live = pl < npix;
       const long pix = pbase + pl;
       if (!h3) {
         if (live) *reinterpret_cast<f32x4*>(h + pix * Cin + ci0) = f32x4{v[0], v[1], v[2], v[3]};
         continue;
       }
-      // limbs of the 4 channels, packed 2 per dword; partner lane (g ^ 1) holds the other half octet
+      // limbs of the 4 channels (2 per dword) into this wave's LDS image of the iteration's x3 rows
       unsigned lh[2], lm[2], ll[2];
 #pragma unroll
       for (int c2 = 0; c2 < 2; ++c2) {
@@ -580,22 +593,24 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
         lm[c2] = mm[0] | ((unsigned)mm[1] << 16);
         ll[c2] = lo[0] | ((unsigned)lo[1] << 16);
       }
-      unsigned ph[2], pm[2], pq[2];
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        ph[c2] = __shfl_xor(lh[c2], 1, 64);
-        pm[c2] = __shfl_xor(lm[c2], 1, 64);
-        pq[c2] = __shfl_xor(ll[c2], 1, 64);
-      }
-      if (!live) continue;
+      typedef unsigned u2 __attribute__((ext_vector_type(2)));
+      unsigned char* q = stg + (u * P + sub) * 6 * Cin + (ci0 >> 3) * 48 + (ci0 & 4) * 2;
+      *reinterpret_cast<u2*>(q) = u2{lh[0], lh[1]};
+      *reinterpret_cast<u2*>(q + 16) = u2{lm[0], lm[1]};
+      *reinterpret_cast<u2*>(q + 32) = u2{ll[0], ll[1]};
+    }
+    if (h3) {
+      // the iteration's UNR*P consecutive pixels are one contiguous x3 span: 16-B chunks, 1 KiB per
+      // wave-instruction
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int nv = (int)min((long)UNR * P, (long)npix - p0);
+      const int nchunk = nv * 3 * Cin / 8;
       typedef unsigned u4 __attribute__((ext_vector_type(4)));
-      u4* q = reinterpret_cast<u4*>(h3 + pix * 3 * Cin + (ci0 >> 3) * 24);
-      if ((g & 1) == 0) {
-        q[0] = u4{lh[0], lh[1], ph[0], ph[1]};
-        q[2] = u4{ll[0], ll[1], pq[0], pq[1]};
-      } else {
-        q[1] = u4{pm[0], pm[1], lm[0], lm[1]};
-      }
+      u4* dst = reinterpret_cast<u4*>(h3 + (pbase + p0) * 3 * Cin);
+      for (int c = lane; c < nchunk; c += 64) dst[c] = reinterpret_cast<const u4*>(stg)[c];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -664,7 +679,7 @@ __global__ __launch_bounds__(256) void smallc_proj_kernel(const float* __restric
   const float* wrow[NTILE];
 #pragma unroll
   for (int t = 0; t < NTILE; ++t) wrow[t] = wp + (long)(32 * t + i) * Cin + 4 * hh;
-#pragma unroll 2
+#pragma unroll 8
   for (int j = 0; j < Cin; j += 8) {
     const f32x4 a = *reinterpret_cast<const f32x4*>(hrow + j);
     f32x4 b[NTILE];
@@ -807,20 +822,29 @@ int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, flo
 // the register-resident dgrad can write its gradient as x3 limbs (channel groups never straddle an octet)
 bool smallc_x3_ok(const damc_layer_t& L) { return smallc_reg_ok(L) && L.cin % 8 == 0; }
 
+// k3 s1 p1 output layer handled by smallc_dgrad_k3_kernel (reads sign bits / writes limbs)
+bool smallc_k3(const damc_layer_t& L) {
+  return L.kind == DAMC_LAYER_SMALLC && L.k == 3 && L.stride == 1 && L.pad == 1 && L.hout == L.hin &&
+         L.wout == L.win && (L.cout == 1 || L.cout == 3) && L.cin % 8 == 0 && L.cin / 4 <= 64 &&
+         64 % (L.cin / 4) == 0;
+}
+
+
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
-                 unsigned short* h3, hipStream_t s) {
+                 unsigned short* h3, const unsigned char* hbits_in, hipStream_t s) {
   if (h3 && !smallc_x3_ok(L)) return DAMC_ERR_ARG;
-  if (smallc_reg_ok(L) && L.k == 3 && L.stride == 1 && L.pad == 1 && L.hout == L.hin && L.wout == L.win) {
+  if (hbits_in && (!smallc_k3(L) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
+  if (smallc_k3(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
     const int R = 4;
     const dim3 grid((unsigned)((L.hin + R - 1) / R), (unsigned)B);
-    const size_t sm = sizeof(float) * (R + 2) * (L.win + 2) * L.cout;
+    const size_t sm = sizeof(float) * (R + 2) * (L.win + 2) * 4;
     if (L.cout == 3)
       hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
-                         delta, mask_act, mask_slope, h3);
+                         delta, mask_act, mask_slope, h3, hbits_in);
     else
       hipLaunchKernelGGL((smallc_dgrad_k3_kernel<1, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
-                         delta, mask_act, mask_slope, h3);
+                         delta, mask_act, mask_slope, h3, hbits_in);
     return (int)hipGetLastError();
   }
   if (smallc_reg_ok(L)) {
@@ -952,8 +976,25 @@ bool h_needs_x3(const damc_generator_t* g, int j) {
   return (j + 1 < g->n_layers && x3_fwd_cap(g->layers[j + 1])) || (j >= 1 && x3_bwd_cap(g->layers[j]));
 }
 
+// Activation j as sign bits: its producer is a limb-engine epilogue with LReLU, and the kernel that
+// masks the next gradient with it (limb dgrad of layer j+1, or the k3 output-layer dgrad) reads bits.
+bool hbits_cap(const damc_generator_t* g, int j) {
+  if (j + 1 >= g->n_layers) return false;
+  const damc_layer_t& L = g->layers[j];
+  const damc_layer_t& N = g->layers[j + 1];
+  const bool prod = (j == 0) ? x3_proj_cap(L) : x3_fwd_cap(L);
+  return prod && L.act == DAMC_ACT_LRELU && (x3_bwd_cap(N) || smallc_k3(N));
+}
+bool hbits(const damc_generator_t* g, int j) { return !g_exact_fp32 && hbits_cap(g, j); }
+// the fp32 activation j is stored unless sign bits carry the mask and the next layer's forward gathers
+// limbs (the output layer's forward reads fp32)
+bool h_f32(const damc_generator_t* g, int j) {
+  return !(hbits(g, j) && j + 1 < g->n_layers && x3_fwd(g->layers[j + 1]));
+}
+
 struct Workspace {
   std::vector<float*> h;  // activations (NHWC), one per layer except the final one
+  std::vector<unsigned char*> hb;  // sign bits of h (LReLU' masks) or nullptr
   std::vector<unsigned short*> h3;  // x3 limb copies of h (limb engine operands) or nullptr
   unsigned short* z3;               // x3 limbs of z (limb-engine first layer) or nullptr
   float* delta;           // final-layer pre-activation gradient (NHWC / row-major)
@@ -983,6 +1024,12 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
     unsigned short* p = nullptr;
     if (h_needs_x3(g, i)) p = reinterpret_cast<unsigned short*>(take(act_floats(g->layers[i], B) * 3 / 2));
     if (w) w->h3.push_back(p);
+  }
+  if (w) w->hb.clear();
+  for (int i = 0; i + 1 < g->n_layers; ++i) {
+    unsigned char* p = nullptr;
+    if (hbits_cap(g, i)) p = reinterpret_cast<unsigned char*>(take(act_floats(g->layers[i], B) / 32 + 4));
+    if (w) w->hb.push_back(p);
   }
   const damc_layer_t& F = g->layers[g->n_layers - 1];
   float* d = take(act_floats(F, B));
@@ -1045,6 +1092,8 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
         a.C3 = ws.h3[0];
         wrote_x3 = true;
       }
+      if (hbits(g, 0)) a.sgn = ws.hb[0];
+      if (!h_f32(g, 0)) a.C = nullptr;
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
                              2.0 * B * (double)N * L.cin, s);
     } else if (L.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok(L.cin)) {
@@ -1102,6 +1151,8 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
           a.C3 = ws.h3[i];
           wrote_x3 = true;
         }
+        if (hbits(g, i)) a.sgn = ws.hb[i];
+        if (!h_f32(g, i)) a.C = nullptr;
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
@@ -1165,7 +1216,8 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
     bool x3_out = false;  // the gradient went straight into its x3 copy
     if (L.kind == DAMC_LAYER_SMALLC) {
       x3_out = x3_bwd(P) && smallc_x3_ok(L);
-      rc = smallc_dgrad(L, out, B, d, P.act, P.slope, x3_out ? ws.h3[i - 1] : nullptr, s);
+      rc = smallc_dgrad(L, out, B, d, P.act, P.slope, x3_out ? ws.h3[i - 1] : nullptr,
+                        hbits(g, i - 1) ? ws.hb[i - 1] : nullptr, s);
     } else if (L.kind == DAMC_LAYER_UP2) {
       const bool x3 = x3_bwd(L);
       GemmArgs a;
@@ -1194,6 +1246,10 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
       if (x3) {
         a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
+        if (hbits(g, i - 1)) {
+          a.mask_sgn = ws.hb[i - 1];
+          a.mask = nullptr;
+        }
         if (x3_bwd(P)) {  // only the next dgrad reads this gradient: limbs only, the fp32 activation stays
           a.C3 = ws.h3[i - 1];
           a.C = nullptr;

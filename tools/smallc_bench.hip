@@ -1,0 +1,103 @@
+// smallc_bench.hip — A/B the output-layer (to-RGB) kernels at the CIFAR-10 B=128 shape (256 ch @ 32x32
+// -> 3 ch, k3 s1 p1): the dgrad (fp32 mask / sign-bit mask, fp32 / limb output) and the two-stage
+// forward, timed in one process.
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DDAMC_GEMM_NO_C_API tools/smallc_bench.hip -o tools/smallc_bench
+#include <cstdio>
+#include <vector>
+
+#include "../diffusion-amortized-mcmc_amd/csrc/gemm.hip"
+#include "../diffusion-amortized-mcmc_amd/csrc/generator.hip"
+
+namespace damc_prof {
+bool enabled() { return false; }
+int begin(const char*, double, hipStream_t) { return -1; }
+void end(int, hipStream_t) {}
+}  // namespace damc_prof
+int damc_launch_posterior_update(const damc_ebm_t*, float*, const float*, int, long, int, int, float, int,
+                                 const float*, uint64_t, uint64_t, uint64_t, float*, hipStream_t) {
+  return 0;
+}
+
+#define CK(x)                                                                             \
+  do {                                                                                    \
+    hipError_t e = (x);                                                                   \
+    if (e != hipSuccess) {                                                                \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);        \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+static float* rnd(size_t n, unsigned seed) {
+  std::vector<float> h(n);
+  unsigned s = seed;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    h[i] = ((s >> 8) * (1.0f / 16777216.0f)) * 2.f - 1.f;
+  }
+  float* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+int main() {
+  const int B = 128, C = 256, H = 32;
+  const long npix = (long)B * H * H;
+  damc_layer_t L{};
+  L.kind = DAMC_LAYER_SMALLC;
+  L.cin = C; L.cout = 3; L.k = 3; L.stride = 1; L.pad = 1; L.hin = L.win = L.hout = L.wout = H;
+  L.act = DAMC_ACT_TANH;
+  float* wt = rnd((size_t)C * 3 * 9, 1);
+  float *wf, *wb;
+  CK(hipMalloc(&wf, C * 27 * 4));
+  CK(hipMalloc(&wb, 32 * C * 4));
+  L.w_fwd = wf; L.w_bwd = wb;
+  L.bias = rnd(3, 2);
+  CK((hipError_t)damc_pack_generator_layer(&L, wt, wf, wb, nullptr));
+  float* h = rnd(npix * C, 3);
+  float* x = rnd(npix * 3, 4);
+  float* delta = rnd(npix * 3, 5);
+  float* pbuf;
+  CK(hipMalloc(&pbuf, npix * 32 * 4));
+  unsigned short* h3;
+  CK(hipMalloc(&h3, npix * C * 6));
+  unsigned char* bits;
+  CK(hipMalloc(&bits, npix * C / 8));
+  CK(hipMemset(bits, 0x5a, npix * C / 8));
+  float* hcopy;
+  CK(hipMalloc(&hcopy, npix * C * 4));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto timeit = [&](const char* name, double bytes, auto fn) {
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+      fn();
+      CK(hipEventRecord(e0, s));
+      for (int k = 0; k < 20; ++k) fn();
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = std::min(best, ms / 20);
+    }
+    printf("%-40s %8.1f us  %6.2f TB/s\n", name, best * 1e3, bytes / (best * 1e-3) / 1e12);
+  };
+  const double act = (double)npix * C * 4;
+  timeit("fwd two-stage", act, [&] {
+    smallc_fwd(L, h, B, x, 100.f, delta, nullptr, nullptr, pbuf, s);
+  });
+  timeit("dgrad fp32 mask, fp32 out", 2 * act, [&] {
+    smallc_dgrad(L, hcopy, B, delta, DAMC_ACT_LRELU, 0.2f, nullptr, nullptr, s);
+  });
+  timeit("dgrad fp32 mask, limb out", act * 2.5, [&] {
+    smallc_dgrad(L, h, B, delta, DAMC_ACT_LRELU, 0.2f, h3, nullptr, s);
+  });
+  timeit("dgrad bit mask, limb out", act * 1.5 + act / 32, [&] {
+    smallc_dgrad(L, h, B, delta, DAMC_ACT_LRELU, 0.2f, h3, bits, s);
+  });
+  CK(hipGetLastError());
+  return 0;
+}
