@@ -158,6 +158,53 @@ def amortizer_bench(device):
             "sweep_reference_equivalent_tflops": round(sweep_flop / (t_sw / 1e3) / 1e12, 2)}
 
 
+def g_update_bench(device, with_torch=True):
+    """SURVEY.md §8(f) row 1, the G update of a training iteration (train_gen_recon.py:222-231) at the bench
+    config: x_hat = G(z); sum((x_hat - x)^2, [1,2,3]).mean().backward() with the drop-in _netG_cifar10
+    (HIP forward + HIP training backward), and the same with the stock PyTorch modules (G.gen, MIOpen fp32:
+    the reference's own GPU implementation of this step).  FLOP = 3 x 2 B MAC_G (forward, dgrad, wgrad)."""
+    import ctypes
+
+    from damc import _lib, synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=NZ, ngf=NGF, nc=3), 0).to(device).train()
+    z = torch.from_numpy(synth.normal_f32(41, 0, (B, NZ))).to(device)
+    x = torch.from_numpy(synth.uniform_f32(42, 0, (B, 3, 32, 32))).to(device)
+
+    def step_hip():
+        G.zero_grad(set_to_none=True)
+        torch.sum((G(z) - x) ** 2, dim=[1, 2, 3]).mean().backward()
+
+    def step_torch():
+        G.zero_grad(set_to_none=True)
+        torch.sum((G.gen(z.reshape(B, NZ, 1, 1)) - x) ** 2, dim=[1, 2, 3]).mean().backward()
+
+    L = _lib.lib()
+    t_hip = event_ms(step_hip)
+    L.damc_prof_reset()
+    L.damc_prof_select(b"wgrad_up2")
+    L.damc_prof_enable(1)
+    step_hip()
+    torch.cuda.synchronize()
+    L.damc_prof_enable(0)
+    L.damc_prof_select(None)
+    tot, n, fl = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
+    L.damc_prof_query(b"wgrad_up2", ctypes.byref(tot), ctypes.byref(n), ctypes.byref(fl))
+    flop = 3 * 2.0 * B * 1089.2e6
+    out = {"config": "cifar10 _netG_cifar10 ngf=128, B=128: forward + loss + backward (weights and biases)",
+           "hip_ms": round(t_hip, 3), "hip_tflops": round(flop / (t_hip / 1e3) / 1e12, 2)}
+    if n.value:
+        out["wgrad_up2_avg_ms"] = round(tot.value / n.value, 4)
+        out["wgrad_up2_tflops"] = round(fl.value / (tot.value / 1e3) / 1e12, 2)
+    if with_torch:
+        print("bench: timing the stock PyTorch G update (MIOpen may tune on first use)", file=sys.stderr, flush=True)
+        t_torch = event_ms(step_torch, reps=3)
+        out["torch_miopen_ms"] = round(t_torch, 3)
+        out["speedup_vs_torch"] = round(t_torch / t_hip, 2)
+    return out
+
+
 def traffic_from_profiles(kernel_class):
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
@@ -175,7 +222,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-extras", action="store_true", help="skip the per-leg and amortizer timings")
+    ap.add_argument("--no-extras", action="store_true", help="skip the per-leg, amortizer and G-update timings")
+    ap.add_argument("--no-torch-g", action="store_true", help="skip the stock-PyTorch G-update comparison")
     ap.add_argument("--no-live-prof", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--exact-fp32", action="store_true",
                     help="run the generator convolutions on the fp32-MFMA engine instead of the limb engine")
@@ -254,6 +302,7 @@ def main():
         # outside the timed region: does not enter `value`
         extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
         extras["amortizer"] = amortizer_bench(device)
+        extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
 
     t_max = elapsed
     if dist:
@@ -319,8 +368,9 @@ def main():
             "cpu_baseline": None,
         }
         if extras:
-            out["langevin_legs"] = {k: v for k, v in extras.items() if k != "amortizer"}
+            out["langevin_legs"] = {k: v for k, v in extras.items() if k not in ("amortizer", "g_update")}
             out["amortizer"] = extras["amortizer"]
+            out["g_update"] = extras["g_update"]
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_budget)
             out["cpu_baseline"] = cb

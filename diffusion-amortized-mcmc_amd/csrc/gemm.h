@@ -6,7 +6,7 @@ namespace damc {
 
 enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_SCALAR = 2 };
 enum Epi { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_MASK = 2, EPI_RESID = 3 };
-enum OMode { O_DENSE = 0, O_PHASE = 1 };
+enum OMode { O_DENSE = 0, O_PHASE = 1, O_WGRAD = 2 };
 
 // C[M,N] (+)= A[M,K] · B[K,N], K reduced in fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fmaf chains).
 //   A_DENSE       : A[m*lda + k]
@@ -16,6 +16,13 @@ enum OMode { O_DENSE = 0, O_PHASE = 1 };
 //                   2x2 conv with pad (1-py, 1-px) and row m = (b,qy,qx) is stored at output pixel
 //                   (b, 2qy+py, 2qx+px) of a Hout x Wout NHWC map; B advanced by z*b_zstride
 //   O_DENSE       : blockIdx.z = split-K slice: k in [z*k_per_z, (z+1)*k_per_z), C advanced by z*c_zstride
+//   O_WGRAD       : (limb engine only) weight gradient of a generator layer over pixel-major transposed
+//                   operands (wgrad.hip): A = x3 [Cg][K] input channels, K = (qy, qx, n) with n fastest over
+//                   wg_bp (a multiple of 32) samples; GEMM row m = (tap, ci) with tap = (ty, tx) on a kw x kw
+//                   grid reads A row ci shifted by (ty - pad_y, tx - pad_x) pixels (zero outside the
+//                   Hin x Win grid); B = x3 [N][K] (per phase: + ph * b_zstride).  blockIdx.z = phase *
+//                   slices + split-K slice; wg_phases = 4 (k4 s2 p1 ConvT, pad = 1 - phase) or 1 (no
+//                   shift); C advanced by z * c_zstride (EPI_STORE only)
 //   b_kmajor      : B is stored transposed, Bt[n*ldb + k] (k contiguous).  Only the K-major convolution
 //                   engine reads this layout: A_CONV with conv_kmajor_ok(Cg), no split-K.
 struct GemmArgs {
@@ -52,6 +59,8 @@ struct GemmArgs {
   // EPI_MASK the LReLU' mask read from such bits instead of from the fp32 `mask`
   unsigned char* sgn = nullptr;
   const unsigned char* mask_sgn = nullptr;
+  // O_WGRAD geometry (see above)
+  int wg_phases = 1, wg_bp = 0;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
@@ -61,6 +70,9 @@ inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
 
 // fp32 [n/C rows][C] -> x3 limb layout [rows][C/8][3][8] bf16 (n % 8 == 0, 16-B aligned)
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
+
+// O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
+int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);
 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);

@@ -833,13 +833,29 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     pad_x = 1 - px;
     Bg += (long)z * p.b_zstride * 3;
   }
+  int kbeg = 0, kend = p.K;
+  if constexpr (OM == O_WGRAD) {  // z = phase * slices + split-K slice
+    const int nsl = gridDim.z / p.wg_phases;
+    const int ph = z / nsl, sl = z - ph * nsl;
+    if (p.wg_phases == 4) {
+      py = ph >> 1;
+      px = ph & 1;
+      pad_y = 1 - py;
+      pad_x = 1 - px;
+    } else {
+      pad_y = pad_x = 0;
+    }
+    Bg += (long)ph * p.b_zstride * 3;
+    kbeg = sl * p.k_per_z;
+    kend = min(p.K, kbeg + p.k_per_z);
+  }
   const int Cg = p.Cg, kw = p.kw, Win = p.Win;
   const int kh = p.K / Cg / kw;
-  const int nk = p.K / X3_BK;
+  const int nk = (OM == O_WGRAD) ? max(kend - kbeg, 0) / X3_BK : p.K / X3_BK;
   const int hwq = p.Hq * p.Wq;
   const int nimg = (p.M + hwq - 1) / hwq;
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A3, (short)0, nimg * p.Hin * Win * Cg * 6, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.A3, (short)0, (OM == O_WGRAD) ? Cg * p.K * 6 : nimg * p.Hin * Win * Cg * 6, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)Bg, (short)0, p.N * p.K * 6, 0x00020000);
 
@@ -853,7 +869,18 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     const int m = m0 + row;
     unsigned msk = 0;
     int base = 0;
-    if (m < p.M) {
+    if constexpr (OM == O_WGRAD) {
+      // row m = (tap, ci): A row ci shifted by (dy, dx) pixels = (dy * Win + dx) * wg_bp elements; the shift
+      // is packed into the mask word ((dy+1) | (dx+1) << 2), all-ones for rows beyond M
+      msk = 0xFFFFFFFFu;
+      if (m < p.M) {
+        const int t = m / Cg, ci = m - t * Cg;
+        const int ty = t / kw, tx = t - ty * kw;
+        const int dy = ty - pad_y, dx = tx - pad_x;
+        base = ci * p.K + (dy * Win + dx) * p.wg_bp;
+        msk = (unsigned)(dy + 1) | ((unsigned)(dx + 1) << 2);
+      }
+    } else if (m < p.M) {
       const int b = m / hwq;
       const int r = m - b * hwq;
       const int qy = r / p.Wq, qx = r - qy * p.Wq;
@@ -916,22 +943,39 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int wbase = (tid & ~63) * 16;
   auto dma_ab = [&](int k0, int buf) {
     unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
+    if constexpr (OM == O_WGRAD) {
+      // the K tile is 32 samples of ONE pixel (wg_bp % 32 == 0): a chunk is live when its shifted pixel
+      // lies inside the grid
+      const int pix = k0 / p.wg_bp;
+      const int qy = pix / Win, qx = pix - qy * Win;
 #pragma unroll
-    for (int j = 0; j < X3_AJ; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+      for (int j = 0; j < X3_AJ; ++j) {
+        const int dy = (int)(amask[j] & 3u) - 1, dx = (int)((amask[j] >> 2) & 3u) - 1;
+        const bool live = amask[j] != 0xFFFFFFFFu && (unsigned)(qy + dy) < (unsigned)p.Hin &&
+                          (unsigned)(qx + dx) < (unsigned)Win;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16,
+                                                 live ? (int)(abase[j] + k0 * 6) : (int)KM_OOB, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < X3_AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+    }
 #pragma unroll
     for (int j = 0; j < X3_BJ; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
                                                k0 * 6, 0, 0);
-    ci0 += X3_BK;
-    if (ci0 == Cg) {
-      ci0 = 0;
-      ++tap;
-      if (++tkx == kw) {
-        tkx = 0;
-        ++tky;
+    if constexpr (OM != O_WGRAD) {
+      ci0 += X3_BK;
+      if (ci0 == Cg) {
+        ci0 = 0;
+        ++tap;
+        if (++tkx == kw) {
+          tkx = 0;
+          ++tky;
+        }
+        set_tap();
       }
-      set_tap();
     }
   };
 
@@ -960,8 +1004,9 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool DMA = (V & 4) != 0;
   {
   constexpr bool DMA = (V & 4) != 0;
+  static_assert(OM != O_WGRAD || DMA, "O_WGRAD runs on the LDS-DMA staging path only");
   if (DMA) {
-    if (nk > 0) dma_ab(0, 0);
+    if (nk > 0) dma_ab(kbeg, 0);
   } else if (nk > 0) {
     load_ab(0);
     store_ab(0);
@@ -972,7 +1017,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
     // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
     // barrier at the end of this tile (its vmcnt(0)) lands it
-    if (DMA && kt + 1 < nk) dma_ab((kt + 1) * X3_BK, (kt + 1) & 1);
+    if (DMA && kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
     if (M16) {
       bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
 #pragma unroll
@@ -1062,7 +1107,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   __syncthreads();
   float* Cz = p.C;
-  if (OM == O_DENSE && Cz) Cz += (long)z * p.c_zstride;
+  if ((OM == O_DENSE || OM == O_WGRAD) && Cz) Cz += (long)z * p.c_zstride;
 #pragma unroll 2
   for (int it = 0; it < X3_BM * X3_BN / 8 / 512; ++it) {
     const int id = tid + 512 * it, row = id >> 4, oct = id & 15;
@@ -1197,6 +1242,25 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
 #undef DAMC_X3
     return DAMC_ERR_UNSUPPORTED;
   }
+  return (int)hipGetLastError();
+}
+
+// O_WGRAD: A3 [Cg][K] and B3 [wg_phases][N][K] pixel-major x3 operands, C = fp32 slabs
+// [wg_phases * slices][M][ldc] (EPI_STORE); slice length k_per_z (a multiple of 32)
+int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s) {
+  if (!a.A3 || !a.B3 || !a.C || a.C3 || a.sgn || a.M <= 0 || a.N <= 0 || a.K <= 0 || slices < 1) return DAMC_ERR_ARG;
+  if (a.wg_phases != 1 && a.wg_phases != 4) return DAMC_ERR_ARG;
+  if (a.wg_bp <= 0 || a.wg_bp % X3_BK != 0 || a.K % a.wg_bp != 0 || a.K / a.wg_bp != a.Hin * a.Win)
+    return DAMC_ERR_ARG;
+  if (a.k_per_z <= 0 || a.k_per_z % X3_BK != 0 || (long)a.k_per_z * slices < a.K) return DAMC_ERR_ARG;
+  if (a.kw < 1 || a.kw > 2 || a.M != a.kw * a.kw * a.Cg || (a.wg_phases == 1 && a.kw != 1)) return DAMC_ERR_ARG;
+  if (a.N % 8 != 0 || a.ldc % 8 != 0 || a.ldc < a.N || a.c_zstride < (long)a.M * a.ldc) return DAMC_ERR_ARG;
+  if (((uintptr_t)a.A3 | (uintptr_t)a.B3 | (uintptr_t)a.C) % 16 != 0) return DAMC_ERR_ARG;
+  if ((double)a.Cg * a.K * 6 >= 2147483647.0 || (double)a.N * a.K * 6 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
+  const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
+  ProfScope ps(prof_name, flops, s);
+  hipLaunchKernelGGL((gemm_x3_kernel<EPI_STORE, O_WGRAD>), dim3(ntm * ntn, 1, a.wg_phases * slices), dim3(512), 0, s,
+                     a);
   return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "gemm.h"
+#include "wgrad.h"
 
 using damc::GemmArgs;
 
@@ -1204,11 +1205,12 @@ int forward_final(const damc_generator_t* g, int B, const float* z, const float*
                            2.0 * B * (double)F.cout * F.cin, s);
 }
 
-// backward from ws.delta to the PROJ/first-layer split-K slabs
-int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
-  const int n = g->n_layers;
-  const float* d = ws.delta;  // gradient w.r.t. the pre-activation of layer i (current)
-  for (int i = n - 1; i >= 1; --i) {
+// input gradient of layer i >= 1 from d (the gradient w.r.t. its pre-activation), masked with the
+// activation derivative of layer i-1: the result (the pre-activation gradient of layer i-1) overwrites
+// ws.h[i-1] and/or, when only a limb-engine dgrad reads it, ws.h3[i-1] (*x3_only = true)
+int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const float* d, bool* x3_only,
+                hipStream_t s) {
+  {
     const damc_layer_t& L = g->layers[i];
     const damc_layer_t& P = g->layers[i - 1];
     float* out = ws.h[i - 1];  // dgrad overwrites the activation it is masked with
@@ -1280,9 +1282,13 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(out, act_floats(P, B), ws.h3[i - 1], s))) return rc;
     }
-    d = out;
+    *x3_only = x3_out;
   }
-  // first layer: dz = dA0 . W0^T  (split-K into slabs)
+  return 0;
+}
+
+// first layer: dz = dA0 . W0^T  (split-K into slabs); d = the fp32 pre-activation gradient of layer 0
+int dz_slabs(const damc_generator_t* g, int B, Workspace& ws, const float* d, hipStream_t s) {
   const damc_layer_t& L0 = g->layers[0];
   const long K = (long)L0.hout * L0.wout * L0.cout;
   GemmArgs a;
@@ -1309,6 +1315,200 @@ int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
   if (S < ws.nslab) DAMC_CHECK(hipMemsetAsync(ws.slabs, 0, sizeof(float) * ws.nslab * (size_t)B * L0.cin, s));
   return damc::launch_gemm(a, km ? damc::A_CONV : damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, S, "proj_dgrad",
                            2.0 * B * (double)K * L0.cin, s);
+}
+
+// backward from ws.delta to the PROJ/first-layer split-K slabs
+int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
+  const float* d = ws.delta;  // gradient w.r.t. the pre-activation of layer i (current)
+  for (int i = g->n_layers - 1; i >= 1; --i) {
+    bool x3_only = false;
+    int rc = dgrad_layer(g, B, ws, i, d, &x3_only, s);
+    if (rc) return rc;
+    d = ws.h[i - 1];
+  }
+  return dz_slabs(g, B, ws, d, s);
+}
+
+// ------------------------------------------------------------------ training backward (weight gradients)
+// The G update of a training iteration (workspace/train_gen_recon.py:222-231): after the forward above,
+// dL/dx_hat -> per-layer dL/dW, dL/db (and optionally dL/dz).  Layer i's weight gradient is taken before
+// its input gradient overwrites the activation buffers it reads.  k4 s2 p1 and first-layer weight
+// gradients run on the limb engine (gemm.hip O_WGRAD) over pixel-major transposes (wgrad.hip) of the layer
+// input and of the pre-activation gradient, the latter split into the 4 output phases; batches are padded
+// to Bp = a multiple of 32 samples with zeros.
+struct TrainWs {
+  unsigned short* tin;  // transposed layer input, x3 [Cin][pixels][Bp]
+  unsigned short* tdl;  // transposed pre-activation gradient, x3 [phase][Cout][pixels][Bp]
+  float* wslab;         // O_WGRAD split-K slabs
+  float* part;          // bias partial sums / output-layer wgrad partials
+  float* ctmp;          // column-sum scratch
+};
+
+int bp_of(int B) { return (B + 31) / 32 * 32; }
+
+// split-K of a k4 s2 p1 weight gradient: >= 512 workgroups; slice length a multiple of 32 (depends on the
+// shape and Bp only)
+void up2_wgrad_split(const damc_layer_t& L, int Bp, int* S, int* kper) {
+  const long M = 4L * L.cin, N = L.cout, K = (long)L.hin * L.win * Bp;
+  const long base = ((M + 255) / 256) * ((N + 127) / 128) * 4;
+  const long nkt = K / 32;
+  long sl = std::max(1L, std::min((512 + base - 1) / base, nkt));
+  const long kp = (nkt + sl - 1) / sl * 32;
+  *kper = (int)kp;
+  *S = (int)((K + kp - 1) / kp);
+}
+
+size_t carve_train(const damc_generator_t* g, int B, char* base, TrainWs* t) {
+  const int Bp = bp_of(B);
+  size_t tin = 0, tdl = 0, wslab = 0, part = 0, ctmp = 0;
+  for (int i = 0; i < g->n_layers; ++i) {
+    const damc_layer_t& L = g->layers[i];
+    const size_t nb = Bp / 32;
+    if (L.kind == DAMC_LAYER_UP2) {
+      const size_t P = (size_t)L.hin * L.win;
+      int S, kp;
+      up2_wgrad_split(L, Bp, &S, &kp);
+      tin = std::max(tin, (size_t)L.cin * P * Bp);
+      tdl = std::max(tdl, 4 * (size_t)L.cout * P * Bp);
+      wslab = std::max(wslab, 4 * (size_t)S * 4 * L.cin * L.cout);
+      part = std::max(part, 4 * P * nb * L.cout);
+      ctmp = std::max(ctmp, damc::colsum_tmp_floats((long)(4 * P * nb), L.cout));
+    } else if (L.kind == DAMC_LAYER_PROJ) {
+      const size_t Pd = (size_t)L.hout * L.wout;
+      tin = std::max(tin, (size_t)L.cin * Bp);
+      tdl = std::max(tdl, (size_t)L.cout * Pd * Bp);
+      part = std::max(part, Pd * nb * L.cout);
+      ctmp = std::max(ctmp, damc::colsum_tmp_floats((long)(Pd * nb), L.cout));
+    } else if (L.kind == DAMC_LAYER_SMALLC) {
+      part = std::max(part, damc::smallc_wgrad_part_floats(L, B));
+      ctmp = std::max(ctmp, damc::colsum_tmp_floats((long)B * L.hout * L.wout, L.cout));
+    } else {
+      ctmp = std::max(ctmp, damc::colsum_tmp_floats(B, L.cout));
+    }
+  }
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) / 256 * 256;
+    return p;
+  };
+  char* p_tin = take(tin * 6);
+  char* p_tdl = take(tdl * 6);
+  char* p_ws = take(wslab * 4);
+  char* p_part = take(part * 4);
+  char* p_ct = take(ctmp * 4);
+  if (t) {
+    t->tin = reinterpret_cast<unsigned short*>(p_tin);
+    t->tdl = reinterpret_cast<unsigned short*>(p_tdl);
+    t->wslab = reinterpret_cast<float*>(p_ws);
+    t->part = reinterpret_cast<float*>(p_part);
+    t->ctmp = reinterpret_cast<float*>(p_ct);
+  }
+  return off;
+}
+
+int train_backward(const damc_generator_t* g, int B, const float* z, const float* xhat, const float* gx,
+                   const damc_generator_grads_t* gr, float* gz, Workspace& ws, TrainWs& tw, hipStream_t s) {
+  const int n = g->n_layers;
+  const damc_layer_t& F = g->layers[n - 1];
+  const int Bp = bp_of(B), nb = Bp / 32;
+  int rc;
+  {
+    ProfScope ps("out_delta", 0.0, s);
+    const int hw = F.kind == DAMC_LAYER_LINEAR ? 1 : F.hout * F.wout;
+    if ((rc = damc::launch_out_delta(gx, xhat, B, F.cout, hw, F.act, ws.delta, s))) return rc;
+  }
+  const float* d = ws.delta;  // pre-activation gradient of layer i: fp32 ...
+  bool d_x3 = false;          // ... or (when a limb dgrad wrote it) only the limbs in ws.h3[i]
+  for (int i = n - 1; i >= 0; --i) {
+    const damc_layer_t& L = g->layers[i];
+    float* dW = gr->w[i];
+    float* db = L.bias ? gr->b[i] : nullptr;
+    const float* in32 = i ? ws.h[i - 1] : z;
+    if (L.kind == DAMC_LAYER_SMALLC) {
+      if (i == 0 || !h_f32(g, i - 1) || d_x3) return DAMC_ERR_UNSUPPORTED;
+      if (dW && (rc = damc::launch_smallc_wgrad(L, in32, d, B, tw.part, dW, s))) return rc;
+      if (db && (rc = damc::launch_colsum(d, (long)B * L.hout * L.wout, L.cout, L.cout, db, tw.ctmp, s))) return rc;
+    } else if (L.kind == DAMC_LAYER_LINEAR) {
+      if (d_x3 || (i > 0 && !h_f32(g, i - 1))) return DAMC_ERR_UNSUPPORTED;
+      if (dW && (rc = damc::launch_linear_wgrad(d, in32, B, L.cout, L.cin, dW, s))) return rc;
+      if (db && (rc = damc::launch_colsum(d, B, L.cout, L.cout, db, tw.ctmp, s))) return rc;
+    } else {
+      const bool up2 = L.kind == DAMC_LAYER_UP2;
+      const int hq = up2 ? L.hin : 1, wq = up2 ? L.win : 1;
+      const long P = (long)hq * wq;
+      // layer input, pixel-major (the limbs the forward gathered, else fp32)
+      const unsigned short* in3 = (up2 && x3_fwd(L)) ? ws.h3[i - 1] : nullptr;
+      if (up2 && !in3 && !h_f32(g, i - 1)) return DAMC_ERR_UNSUPPORTED;
+      if (dW && (rc = damc::launch_transpose_x3(in3 ? nullptr : in32, in3, B, hq, wq, L.cin, hq, wq, 1, 1, 0, 0, Bp,
+                                                tw.tin, nullptr, s)))
+        return rc;
+      const float* d32 = d_x3 ? nullptr : d;
+      const unsigned short* d3 = d_x3 ? ws.h3[i] : nullptr;
+      if (up2) {  // the 4 output phases of the gradient, each on the input grid
+        for (int ph = 0; ph < 4; ++ph) {
+          rc = damc::launch_transpose_x3(d32, d3, B, L.hout, L.wout, L.cout, L.hin, L.win, 2, 2, ph >> 1, ph & 1, Bp,
+                                         tw.tdl + (size_t)ph * L.cout * P * Bp * 3,
+                                         db ? tw.part + (size_t)ph * P * nb * L.cout : nullptr, s);
+          if (rc) return rc;
+        }
+      } else {  // PROJ: rows (co, output pixel) = the PyTorch (Cin, Cout, k, k) column order
+        rc = damc::launch_transpose_x3(d32, d3, B, L.hout, L.wout, L.cout, L.hout, L.wout, 1, 1, 0, 0, Bp, tw.tdl,
+                                       db ? tw.part : nullptr, s);
+        if (rc) return rc;
+      }
+      if (dW) {
+        GemmArgs a;
+        a.A3 = tw.tin;
+        a.B3 = tw.tdl;
+        a.Cg = L.cin;
+        a.Hin = hq;
+        a.Win = wq;
+        a.K = (int)(P * Bp);
+        a.wg_bp = Bp;
+        if (up2) {
+          int S, kp;
+          up2_wgrad_split(L, Bp, &S, &kp);
+          a.kw = 2;
+          a.wg_phases = 4;
+          a.M = 4 * L.cin;
+          a.N = L.cout;
+          a.ldc = L.cout;
+          a.c_zstride = (long)a.M * a.N;
+          a.b_zstride = (long)L.cout * a.K;
+          a.k_per_z = kp;
+          a.C = tw.wslab;
+          if ((rc = damc::launch_wgrad_x3(a, S, "wgrad_up2", conv_flops(L, B), s))) return rc;
+          if ((rc = damc::launch_up2_wgrad_reduce(tw.wslab, S, L.cin, L.cout, dW, s))) return rc;
+        } else {
+          a.kw = 1;
+          a.wg_phases = 1;
+          a.M = L.cin;
+          a.N = L.cout * L.hout * L.wout;
+          a.ldc = a.N;
+          a.c_zstride = (long)a.M * a.N;
+          a.k_per_z = a.K;
+          a.C = dW;
+          if ((rc = damc::launch_wgrad_x3(a, 1, "wgrad_proj", 2.0 * B * (double)a.M * a.N, s))) return rc;
+        }
+      }
+      if (db) {
+        const long rows = (up2 ? 4 * P : (long)L.hout * L.wout) * nb;
+        if ((rc = damc::launch_colsum(tw.part, rows, L.cout, L.cout, db, tw.ctmp, s))) return rc;
+      }
+    }
+    if (i >= 1) {
+      bool x3o = false;
+      if ((rc = dgrad_layer(g, B, ws, i, d, &x3o, s))) return rc;
+      d = ws.h[i - 1];
+      d_x3 = x3o;
+    } else if (gz) {
+      if (n < 2 || d_x3) return DAMC_ERR_UNSUPPORTED;
+      if ((rc = dz_slabs(g, B, ws, d, s))) return rc;
+      if ((rc = slab_sum(ws.slabs, ws.nslab, (long)B * g->nz, gz, s))) return rc;
+    }
+  }
+  return 0;
 }
 
 }  // namespace
@@ -1448,4 +1648,45 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
     if (rc) return rc;
   }
   return 0;
+}
+
+// ------------------------------------------------------------------------------------ training (G update)
+extern "C" size_t damc_generator_train_workspace_bytes(const damc_generator_t* g, int B) {
+  if (validate(g) || B <= 0) return 0;
+  return carve(g, B, nullptr, nullptr) + carve_train(g, B, nullptr, nullptr);
+}
+
+static int setup_train(const damc_generator_t* g, int B, void* wsp, size_t wsb, Workspace* ws, TrainWs* tw) {
+  int rc = validate(g);
+  if (rc) return rc;
+  if (B <= 0) return DAMC_ERR_ARG;
+  const size_t n0 = carve(g, B, nullptr, nullptr);
+  const size_t n1 = carve_train(g, B, nullptr, nullptr);
+  if (!wsp || wsb < n0 + n1) return DAMC_ERR_WORKSPACE;
+  carve(g, B, reinterpret_cast<char*>(wsp), ws);
+  carve_train(g, B, reinterpret_cast<char*>(wsp) + n0, tw);
+  return 0;
+}
+
+extern "C" int damc_generator_train_forward(const damc_generator_t* g, const float* z, int B, float* xhat, void* wsp,
+                                            size_t wsb, void* stream) {
+  Workspace ws;
+  TrainWs tw;
+  int rc = setup_train(g, B, wsp, wsb, &ws, &tw);
+  if (rc) return rc;
+  if (!z || !xhat) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
+  return forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s);
+}
+
+extern "C" int damc_generator_train_backward(const damc_generator_t* g, const float* z, const float* xhat,
+                                             const float* grad_xhat, int B, const damc_generator_grads_t* grads,
+                                             float* grad_z, void* wsp, size_t wsb, void* stream) {
+  Workspace ws;
+  TrainWs tw;
+  int rc = setup_train(g, B, wsp, wsb, &ws, &tw);
+  if (rc) return rc;
+  if (!z || !xhat || !grad_xhat || !grads) return DAMC_ERR_ARG;
+  return train_backward(g, B, z, xhat, grad_xhat, grads, grad_z, ws, tw, as_stream(stream));
 }

@@ -1,0 +1,320 @@
+// wgrad.hip — generator weight / bias gradients: the device side of the G update of a training iteration
+// (workspace/train_gen_recon.py:222-231: x_hat = G(z); sum((x_hat - x)^2).mean().backward()).
+//
+// The k4 s2 p1 and first-layer weight gradients are GEMMs over pixels and samples; they run on the limb
+// engine (gemm.hip, O_WGRAD) over PIXEL-MAJOR transposed operands written here: [channel][pixel][sample]
+// with the sample index fastest, so a 32-deep K tile is 32 samples of one pixel and a filter tap is a
+// pixel shift of a whole K tile (no per-element masks, 16-B aligned limb loads).  The output layer
+// (Cout <= 4) has N = k*k*Cout <= 64 and reads one large activation once: a direct kernel with the
+// gradient window in LDS and the Cin channels across threads.
+#include <algorithm>
+
+#include "gemm.h"
+#include "wgrad.h"
+
+namespace damc {
+
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
+
+// ---------------------------------------------------------------------------------------- transpose
+// grid (Hq*Wq, Bp/32, ceil(C/64)), 256 threads: a 32-sample x 64-channel tile of one pixel through LDS
+template <bool X3>
+__global__ __launch_bounds__(256) void transpose_x3_kernel(const float* __restrict__ src32,
+                                                           const unsigned short* __restrict__ src3, int B, int H,
+                                                           int W, int C, int Wq, int sy, int sx, int oy, int ox,
+                                                           int Bp, int P, unsigned short* __restrict__ dst,
+                                                           float* __restrict__ part) {
+  __shared__ float tile[64][33];
+  const int pq = blockIdx.x, nb = blockIdx.y, cb = blockIdx.z;
+  const int qy = pq / Wq, qx = pq - qy * Wq;
+  const int y = sy * qy + oy, x = sx * qx + ox;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + 256 * i;
+    const int nl = e >> 6, cl = e & 63;
+    const int n = nb * 32 + nl, c = cb * 64 + cl;
+    float v = 0.f;
+    if (n < B && c < C) {
+      const long pix = ((long)n * H + y) * W + x;
+      if (X3) {  // octet [limb][8]: the three limbs sum back to the fp32 value exactly
+        const long o = (pix * C + (c & ~7)) * 3 + (c & 7);
+        v = (bf16_bits_to_f32(src3[o]) + bf16_bits_to_f32(src3[o + 8])) + bf16_bits_to_f32(src3[o + 16]);
+      } else {
+        v = src32[pix * C + c];
+      }
+    }
+    tile[cl][nl] = v;
+  }
+  __syncthreads();
+  {
+    const int cl = tid >> 2, oct = tid & 3;
+    const int c = cb * 64 + cl;
+    if (c < C) {
+      wg_bf16x8 h, m, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // RNE limb split, as the engine's own split (gemm.hip split3_octet)
+        const float v = tile[cl][oct * 8 + e];
+        const __bf16 b0 = (__bf16)v;
+        const float r1 = v - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        h[e] = b0;
+        m[e] = b1;
+        l[e] = (__bf16)(r1 - (float)b1);
+      }
+      wg_bf16x8* o = reinterpret_cast<wg_bf16x8*>(dst + (((long)c * P + pq) * Bp + nb * 32 + oct * 8) * 3);
+      o[0] = h;
+      o[1] = m;
+      o[2] = l;
+    }
+  }
+  if (part && tid < 64) {
+    const int c = cb * 64 + tid;
+    if (c < C) {
+      float sum = 0.f;
+#pragma unroll 8
+      for (int n = 0; n < 32; ++n) sum += tile[tid][n];
+      part[((long)pq * (Bp / 32) + nb) * C + c] = sum;
+    }
+  }
+}
+
+int launch_transpose_x3(const float* src32, const unsigned short* src3, int B, int H, int W, int C, int Hq, int Wq,
+                        int sy, int sx, int oy, int ox, int Bp, unsigned short* dst, float* part, hipStream_t s) {
+  if ((!src32) == (!src3) || !dst || B <= 0 || C <= 0 || Hq <= 0 || Wq <= 0 || Bp < B || Bp % 32 != 0)
+    return DAMC_ERR_ARG;
+  if (src3 && C % 8 != 0) return DAMC_ERR_ARG;
+  if ((uintptr_t)dst % 16 != 0) return DAMC_ERR_ARG;
+  if (sy * (Hq - 1) + oy >= H || sx * (Wq - 1) + ox >= W || oy < 0 || ox < 0) return DAMC_ERR_ARG;
+  const dim3 grid((unsigned)(Hq * Wq), (unsigned)(Bp / 32), (unsigned)((C + 63) / 64));
+  ProfScope ps("wgrad_transpose", 0.0, s);
+  if (src3)
+    hipLaunchKernelGGL(transpose_x3_kernel<true>, grid, dim3(256), 0, s, nullptr, src3, B, H, W, C, Wq, sy, sx, oy,
+                       ox, Bp, Hq * Wq, dst, part);
+  else
+    hipLaunchKernelGGL(transpose_x3_kernel<false>, grid, dim3(256), 0, s, src32, nullptr, B, H, W, C, Wq, sy, sx, oy,
+                       ox, Bp, Hq * Wq, dst, part);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ k4 s2 p1 slab reduce
+// one thread per (ci, co): the 16 taps, each a fixed-order sum over the split-K slices; tap (ky, kx)
+// comes from phase (py, px) = ((ky+1)&1, (kx+1)&1) and GEMM row (ty, tx) with ky = 3 - py - 2 ty
+__global__ __launch_bounds__(256) void up2_wgrad_reduce_kernel(const float* __restrict__ slabs, int S, int Cin,
+                                                               int Cout, float* __restrict__ dW) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Cin * Cout) return;
+  const int ci = (int)(i / Cout), co = (int)(i - (long)ci * Cout);
+  const long M = 4L * Cin;
+  float out[16];
+#pragma unroll
+  for (int ky = 0; ky < 4; ++ky) {
+    const int py = (ky + 1) & 1, ty = (3 - ky - py) >> 1;
+#pragma unroll
+    for (int kx = 0; kx < 4; ++kx) {
+      const int px = (kx + 1) & 1, tx = (3 - kx - px) >> 1;
+      const int ph = py * 2 + px, t = ty * 2 + tx;
+      const float* sp = slabs + ((long)ph * S * M + (long)t * Cin + ci) * Cout + co;
+      float acc = 0.f;
+      for (int sl = 0; sl < S; ++sl) acc += sp[(long)sl * M * Cout];
+      out[ky * 4 + kx] = acc;
+    }
+  }
+  f32x4* o = reinterpret_cast<f32x4*>(dW + i * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = f32x4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+}
+
+int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float* dW, hipStream_t s) {
+  if (!slabs || !dW || S < 1 || Cin <= 0 || Cout <= 0 || (uintptr_t)dW % 16 != 0) return DAMC_ERR_ARG;
+  const long n = (long)Cin * Cout;
+  ProfScope ps("wgrad_reduce", 0.0, s);
+  hipLaunchKernelGGL(up2_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slabs, S, Cin,
+                     Cout, dW);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------------- column sums
+// grid (ceil(C/64), row blocks), 256 threads = 4 row lanes x 64 channels; fixed-order combine
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, long R, int C, long ld,
+                                                     long rows_per, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const long r0 = (long)blockIdx.y * rows_per;
+  const long r1 = min(R, r0 + rows_per);
+  float sum = 0.f;
+  if (c < C)
+    for (long r = r0 + rl; r < r1; r += 4) sum += X[r * ld + c];
+  red[rl][cl] = sum;
+  __syncthreads();
+  if (rl == 0 && c < C) out[(long)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
+static int colsum_blocks(long R) { return R <= 4096 ? 1 : (int)std::min<long>(256, (R + 1023) / 1024); }
+
+size_t colsum_tmp_floats(long R, int C) { return (size_t)colsum_blocks(R) * C; }
+
+int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s) {
+  if (!X || !out || R <= 0 || C <= 0 || ld < C) return DAMC_ERR_ARG;
+  ProfScope ps("bias_grad", 0.0, s);
+  const int nrb = colsum_blocks(R);
+  const unsigned gx = (unsigned)((C + 63) / 64);
+  if (nrb == 1) {
+    hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, X, R, C, ld, R, out);
+    return (int)hipGetLastError();
+  }
+  if (!tmp) return DAMC_ERR_ARG;
+  const long per = (R + nrb - 1) / nrb;
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, (unsigned)nrb), dim3(256), 0, s, X, R, C, ld, per, tmp);
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, (const float*)tmp, (long)nrb, C, (long)C,
+                     (long)nrb, out);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ output-layer wgrad
+// grid (row blocks of R input rows, B): dw = the delta window [S(R-1)+K rows][Wd = S(Win-1)+K][NC] in LDS
+// (zero outside the map); each thread owns input channels and accumulates all K*K*NC taps
+template <int NC, int K>
+__global__ __launch_bounds__(256) void smallc_wgrad_kernel(const float* __restrict__ h, const float* __restrict__ delta,
+                                                           int Hin, int Win, int Cin, int S, int pad, int Hout,
+                                                           int Wout, int R, int Wd, float* __restrict__ part) {
+  extern __shared__ float dw[];
+  const int rb = blockIdx.x, n = blockIdx.y, nrb = gridDim.x;
+  const int iy0 = rb * R;
+  const int rows = min(R, Hin - iy0);
+  const int nrows = S * (R - 1) + K;
+  const int oy0 = S * iy0 - pad;
+  for (int i = threadIdx.x; i < nrows * Wd * NC; i += blockDim.x) {
+    const int o = i % NC, rc = i / NC;
+    const int r = rc / Wd, cc = rc - r * Wd;
+    const int oy = oy0 + r, ox = cc - pad;
+    float v = 0.f;
+    if (oy >= 0 && oy < Hout && ox >= 0 && ox < Wout) v = delta[(((long)n * Hout + oy) * Wout + ox) * NC + o];
+    dw[i] = v;
+  }
+  __syncthreads();
+  constexpr int T = K * K * NC;
+  for (int ci = threadIdx.x; ci < Cin; ci += blockDim.x) {
+    float acc[T];
+#pragma unroll
+    for (int j = 0; j < T; ++j) acc[j] = 0.f;
+    for (int yy = 0; yy < rows; ++yy) {
+      const float* hr = h + ((long)n * Hin + iy0 + yy) * Win * Cin + ci;
+      const float* wr = dw + (S * yy) * Wd * NC;
+      for (int ix = 0; ix < Win; ++ix) {
+        const float hv = hr[(long)ix * Cin];
+        const float* w0 = wr + S * ix * NC;
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+            for (int o = 0; o < NC; ++o) acc[(ky * K + kx) * NC + o] += hv * w0[(ky * Wd + kx) * NC + o];
+      }
+    }
+    float* pp = part + (long)(n * nrb + rb) * T * Cin + ci;
+#pragma unroll
+    for (int j = 0; j < T; ++j) pp[(long)j * Cin] = acc[j];
+  }
+}
+
+// dW[ci][o][ky][kx] = fixed-order sum over the partial blocks; one thread per (tap*NC + o, ci)
+template <int NC, int K>
+__global__ __launch_bounds__(256) void smallc_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int Cin,
+                                                                  float* __restrict__ dW) {
+  constexpr int T = K * K * NC;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)T * Cin) return;
+  const int j = (int)(i / Cin), ci = (int)(i - (long)j * Cin);
+  float sum = 0.f;
+  for (int b = 0; b < nblk; ++b) sum += part[(long)b * T * Cin + i];
+  const int o = j % NC, t = j / NC;
+  dW[((long)ci * NC + o) * (K * K) + t] = sum;
+}
+
+static int smallc_rows(const damc_layer_t& L) {
+  int R = 8;
+  const int Wd = L.stride * (L.win - 1) + L.k;
+  while (R > 1 && (size_t)(L.stride * (R - 1) + L.k) * Wd * L.cout * sizeof(float) > 40960) R /= 2;
+  return R;
+}
+
+size_t smallc_wgrad_part_floats(const damc_layer_t& L, int B) {
+  const int R = smallc_rows(L);
+  return (size_t)B * ((L.hin + R - 1) / R) * L.k * L.k * L.cout * L.cin;
+}
+
+int launch_smallc_wgrad(const damc_layer_t& L, const float* h, const float* delta, int B, float* part, float* dW,
+                        hipStream_t s) {
+  if (!h || !delta || !part || !dW || B <= 0) return DAMC_ERR_ARG;
+  const int R = smallc_rows(L);
+  const int Wd = L.stride * (L.win - 1) + L.k;
+  const size_t sm = (size_t)(L.stride * (R - 1) + L.k) * Wd * L.cout * sizeof(float);
+  if (sm > 65536) return DAMC_ERR_UNSUPPORTED;
+  const int nrb = (L.hin + R - 1) / R;
+  const dim3 grid((unsigned)nrb, (unsigned)B);
+  const long nout = (long)L.k * L.k * L.cout * L.cin;
+  const dim3 rgrid((unsigned)((nout + 255) / 256));
+  ProfScope ps("smallc_wgrad", 2.0 * B * L.hin * L.win * L.cin * L.k * L.k * L.cout, s);
+#define SW(NC_, K_)                                                                                                 \
+  if (L.cout == NC_ && L.k == K_) {                                                                                 \
+    hipLaunchKernelGGL((smallc_wgrad_kernel<NC_, K_>), grid, dim3(256), sm, s, h, delta, L.hin, L.win, L.cin,       \
+                       L.stride, L.pad, L.hout, L.wout, R, Wd, part);                                               \
+    hipLaunchKernelGGL((smallc_wgrad_reduce_kernel<NC_, K_>), rgrid, dim3(256), 0, s, (const float*)part, B * nrb, \
+                       L.cin, dW);                                                                                  \
+    return (int)hipGetLastError();                                                                                  \
+  }
+  SW(3, 3) SW(3, 4) SW(1, 3) SW(1, 4) SW(2, 3) SW(2, 4) SW(4, 3) SW(4, 4)
+#undef SW
+  return DAMC_ERR_UNSUPPORTED;
+}
+
+// --------------------------------------------------------------------------------- output delta
+__global__ __launch_bounds__(256) void out_delta_kernel(const float* __restrict__ g, const float* __restrict__ xhat,
+                                                        int NC, int HW, long n, int act, float* __restrict__ delta) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long b = i / ((long)NC * HW);
+  const long r = i - b * NC * HW;
+  const int o = (int)(r / HW), p = (int)(r - (long)o * HW);
+  float d = g[i];
+  if (act == DAMC_ACT_TANH) {
+    const float t = xhat[i];
+    d = d * (1.f - t * t);
+  }
+  delta[(b * HW + p) * NC + o] = d;
+}
+
+int launch_out_delta(const float* g, const float* xhat, int B, int NC, int HW, int act, float* delta, hipStream_t s) {
+  if (!g || !delta || B <= 0 || NC <= 0 || HW <= 0) return DAMC_ERR_ARG;
+  if (act != DAMC_ACT_NONE && act != DAMC_ACT_TANH) return DAMC_ERR_UNSUPPORTED;
+  if (act == DAMC_ACT_TANH && !xhat) return DAMC_ERR_ARG;
+  const long n = (long)B * NC * HW;
+  hipLaunchKernelGGL(out_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, xhat, NC, HW, n, act,
+                     delta);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------- Linear wgrad
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ d, const float* __restrict__ h,
+                                                           int B, int nout, int nin, float* __restrict__ dW) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)nout * nin) return;
+  const int o = (int)(i / nin), k = (int)(i - (long)o * nin);
+  float sum = 0.f;
+  for (int n = 0; n < B; ++n) sum += d[(long)n * nout + o] * h[(long)n * nin + k];
+  dW[i] = sum;
+}
+
+int launch_linear_wgrad(const float* d, const float* h, int B, int nout, int nin, float* dW, hipStream_t s) {
+  if (!d || !h || !dW || B <= 0 || nout <= 0 || nin <= 0) return DAMC_ERR_ARG;
+  const long n = (long)nout * nin;
+  ProfScope ps("linear_wgrad", 2.0 * B * n, s);
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, h, B, nout, nin, dW);
+  return (int)hipGetLastError();
+}
+
+}  // namespace damc

@@ -36,6 +36,10 @@ class Generator(ctypes.Structure):
     ]
 
 
+class GeneratorGrads(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p * MAX_LAYERS), ("b", ctypes.c_void_p * MAX_LAYERS)]
+
+
 class Ebm(ctypes.Structure):
     _fields_ = [
         ("nz", ctypes.c_int), ("nh", ctypes.c_int), ("slope", ctypes.c_float),
@@ -81,6 +85,10 @@ _SIGS = {
                                      _U64, _U64, _U64, _P, _P, _SZ, _P]),
     "damc_likelihood_grad": (_I, [ctypes.POINTER(Generator), _P, _P, _I, _F, _P, _P, _SZ, _P]),
     "damc_generator_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
+    "damc_generator_train_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
+    "damc_generator_train_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
+    "damc_generator_train_backward": (_I, [ctypes.POINTER(Generator), _P, _P, _P, _I, ctypes.POINTER(GeneratorGrads),
+                                           _P, _P, _SZ, _P]),
     "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P, _P]),
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_z_update": (_I, [_P, _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P]),

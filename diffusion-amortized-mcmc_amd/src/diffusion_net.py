@@ -2,11 +2,12 @@
 
 Same class names, constructor signatures and ``state_dict`` keys/order as the reference, so
 reference checkpoints load unchanged (workspace/train_gen_recon.py:284-294).  The nets are
-built from compact spec tables.  ``forward`` of G / E / encoders / denoiser stays stock
-PyTorch (autograd is needed by the training updates, which are outside the hot path);
-the hot path — Langevin sampling and the amortizer's reverse sweep — runs on the HIP
-kernels: ``_netQ_U.forward`` dispatches to ``damc.amortizer`` and ``src.MCMC`` to
-``damc.langevin``.
+built from compact spec tables.  The hot path — Langevin sampling and the amortizer's
+reverse sweep — runs on the HIP kernels: ``_netQ_U.forward`` dispatches to
+``damc.amortizer`` and ``src.MCMC`` to ``damc.langevin``.  ``_netG_*.forward`` on ROCm
+tensors runs on libdamc too, with a HIP backward for the G update (``damc.training``).
+``forward`` of E / encoders / denoiser stays stock PyTorch (their training updates are
+outside the hot path).
 """
 import math
 
@@ -50,9 +51,17 @@ class _GeneratorBase(nn.Module):
     def __init__(self, nz, ngf, nc, use_spc_norm=False):
         super().__init__()
         self.nz = nz
+        self._spc = bool(use_spc_norm)
         self.gen = _deconv_stack(nz, ngf, nc, _G_TOPOLOGY[self.TOPOLOGY], use_spc_norm)
 
     def forward(self, z):
+        # ROCm tensors run on libdamc: the forward, and under autograd the training backward
+        # (damc.training: dL/dW, dL/db, dL/dz for the G update, train_gen_recon.py:222-231).
+        # Spectral-norm generators (use_spc_norm=True, default False) are outside the HIP path.
+        if z.is_cuda and not self._spc:
+            from damc.training import generator_apply
+
+            return generator_apply(self, z)
         return self.gen(z.reshape(z.shape[0], self.nz, 1, 1))
 
 

@@ -116,6 +116,28 @@ int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float*
 int damc_generator_forward(const damc_generator_t* g, const float* z, int batch, float* x_hat,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------- generator training step */
+/* The G update of a training iteration (workspace/train_gen_recon.py:222-231):
+ *   x_hat = G(z); g_loss = sum((x_hat - x)^2, [1,2,3]).mean(); g_loss.backward()
+ * damc_generator_train_forward computes x_hat (NCHW) and keeps in the workspace what the backward reads;
+ * damc_generator_train_backward then maps grad_xhat = dL/dx_hat (NCHW, from the caller's autograd) to the
+ * weight and bias gradients of every layer (PyTorch layouts: ConvTranspose2d (Cin, Cout, k, k), Linear
+ * (out, in); WRITTEN, not accumulated; NULL entries are skipped) and, if grad_z != NULL, dL/dz (B, nz).
+ * The two calls must use the same descriptor, batch and workspace, with no other call on that workspace in
+ * between.  ConvT weight gradients run on the limb engine (fp32-accurate bf16 MFMA) whatever
+ * damc_set_exact_fp32 says; layer inputs and gradients with a batch that is not a multiple of 32 are
+ * zero-padded to one. */
+typedef struct {
+  float* w[DAMC_MAX_LAYERS];
+  float* b[DAMC_MAX_LAYERS];
+} damc_generator_grads_t;
+size_t damc_generator_train_workspace_bytes(const damc_generator_t* g, int batch);
+int damc_generator_train_forward(const damc_generator_t* g, const float* z, int batch, float* x_hat, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+int damc_generator_train_backward(const damc_generator_t* g, const float* z, const float* x_hat,
+                                  const float* grad_xhat, int batch, const damc_generator_grads_t* grads,
+                                  float* grad_z, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ----------------------------------------------------------------- prior Langevin (a2) */
 /* sample_langevin_prior_z (MCMC.py:27-46): all n_steps in ONE persistent launch.
  * diag (optional, n_steps*2 floats): {sum E, |z|^2/2} per step before the update. */

@@ -133,6 +133,35 @@ def generator_vjp(layers, hs, delta_last):
     raise AssertionError
 
 
+def generator_train_grads(layers, z, grad_xhat):
+    """The G update's gradients (workspace/train_gen_recon.py:222-231: x_hat = G(z), loss.backward()):
+    given dL/dx_hat, per layer (dL/dW, dL/db) and dL/dz.  Explicit backward through ATen's
+    convolution_backward (the kernel the reference's autograd dispatches to for ConvTranspose2d,
+    diffusion_net.py:20-203) and the Linear identities (toy G, toy_example.py:22-47)."""
+    hs = generator_forward(layers, z)
+    d = _act_backward(grad_xhat, hs[-1], layers[-1]["act"])
+    grads = [None] * len(layers)
+    gz = None
+    for i in range(len(layers) - 1, -1, -1):
+        L = layers[i]
+        if L["kind"] == "convT":
+            inp = hs[i - 1] if i > 0 else z.reshape(len(z), -1, 1, 1)
+            gi, gw, gb = torch.ops.aten.convolution_backward(
+                d, inp, L["W"], [L["W"].shape[1]], [L["stride"]] * 2, [L["pad"]] * 2, [1, 1], True, [0, 0], 1,
+                [True, True, L["b"] is not None])
+        else:
+            inp = hs[i - 1] if i > 0 else z
+            gw = d.t() @ inp
+            gb = d.sum(0) if L["b"] is not None else None
+            gi = d @ L["W"]
+        grads[i] = (gw, gb)
+        if i > 0:
+            d = _act_backward(gi, hs[i - 1], layers[i - 1]["act"])
+        else:
+            gz = gi.reshape(len(z), -1)
+    return grads, gz, hs[-1]
+
+
 def likelihood_grad(layers, z, x, sigma):
     """grad_z |G(z)-x|^2/(2 sigma^2) and the energy value (MCMC.py:55-56)."""
     hs = generator_forward(layers, z)

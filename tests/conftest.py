@@ -75,6 +75,36 @@ def build_g_case(name, device="cpu"):
                 prior_noise=prior_noise.to(device), rec=rec, meta=meta)
 
 
+def gtrain_inputs(name):
+    """G-update case (tests/golden/<name>_gtrain.npz): drop-in G with counter-hash weights, z0, x and
+    dL/dx_hat of g_loss = sum((x_hat - x)^2, [1,2,3]).mean() (workspace/train_gen_recon.py:227-228)."""
+    import torch
+
+    from damc import synth
+    from src import diffusion_net as dn
+
+    rec, meta = load_golden(name + "_gtrain")
+    G = getattr(dn, meta["ctor"])(nz=meta["nz"], ngf=meta["ngf"], nc=meta["nc"])
+    synth.load_into(G, SEED_G)
+    B, nz, nc, H = meta["B"], meta["nz"], meta["nc"], meta["H"]
+    x = torch.from_numpy(synth.uniform_f32(SEED_X, 0, (B, nc, H, H)))
+    z0 = torch.from_numpy(synth.normal_f32(SEED_Z0, 0, (B, nz)))
+    return G, z0, x, rec, meta
+
+
+def gtrain_check(grads, rec, meta, tol):
+    """Compare a list of per-parameter gradients (module order) with the golden subsamples/norms."""
+    worst = 0.0
+    for k, (pname, st, shape) in enumerate(meta["params"]):
+        g = np.asarray(grads[k], dtype=np.float64).reshape(-1)
+        assert list(np.asarray(grads[k]).shape) == shape, (pname, np.asarray(grads[k]).shape, shape)
+        e = rel_l2(g[::st], rec["grad%d_sub" % k])
+        n = abs(np.linalg.norm(g) - float(rec["grad%d_norm" % k])) / max(float(rec["grad%d_norm" % k]), 1e-30)
+        worst = max(worst, e, n)
+        assert e < tol and n < tol, (pname, e, n)
+    return worst
+
+
 def build_q_case(name, device="cpu"):
     import torch
 

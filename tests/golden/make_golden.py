@@ -182,6 +182,35 @@ def capture_generators(dn, mc, torch):
     return out
 
 
+def capture_gtrain(dn, torch):
+    """The G update (workspace/train_gen_recon.py:222-231) on the reference generator: x_hat = G(z0),
+    g_loss = sum((x_hat - x)^2, [1,2,3]).mean(), g_loss.backward().  Every parameter gradient is kept as
+    an evenly strided subsample (<= 2048 values) plus its full L2 norm, to keep the fixtures small."""
+    out = {}
+    for name, (ctor, nz, ngf, nc, H, B) in G_CONFIGS.items():
+        print("G train config", name, flush=True)
+        G = getattr(dn, ctor)(nz=nz, ngf=ngf, nc=nc)
+        synth.load_into(G, SEED_G)
+        G.train()
+        x = torch.from_numpy(synth.uniform_f32(SEED_X, 0, (B, nc, H, H)))
+        z0 = torch.from_numpy(synth.normal_f32(SEED_Z0, 0, (B, nz)))
+        G.zero_grad()
+        x_hat = G(z0)
+        g_loss = torch.sum((x_hat - x) ** 2, dim=[1, 2, 3]).mean()
+        g_loss.backward()
+        rec = {"g_loss": np.float32(g_loss.item())}
+        strides = []
+        for k, (pname, p) in enumerate(G.named_parameters()):
+            g = p.grad.detach().numpy().reshape(-1)
+            st = max(1, g.size // 2048)
+            rec["grad%d_sub" % k] = g[::st].copy()
+            rec["grad%d_norm" % k] = np.float64(np.linalg.norm(g.astype(np.float64)))
+            strides.append([pname, st, list(p.shape)])
+        meta = dict(kind="Gtrain", ctor=ctor, nz=nz, ngf=ngf, nc=nc, H=H, B=B, params=strides)
+        out[name + "_gtrain"] = (rec, meta)
+    return out
+
+
 def capture_q(dn, torch):
     out = {}
     for name, (ds, nc, nz, nif, nxemb, ntemb, H, B, var_type, n_int) in Q_CONFIGS.items():
@@ -277,6 +306,11 @@ def main():
 
     torch.set_num_threads(8)
     dn, mc = import_reference()
+    for name, (rec, meta) in capture_gtrain(dn, torch).items():
+        np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
+    if "--gtrain-only" in sys.argv:
+        print("done")
+        return
     for name, (rec, meta) in capture_generators(dn, mc, torch).items():
         np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
     for name, (rec, meta) in capture_q(dn, torch).items():

@@ -1,0 +1,99 @@
+"""GPU: the G update of a training iteration (workspace/train_gen_recon.py:222-231) on the HIP path.
+
+``_netG_*.forward`` on ROCm tensors runs damc.training (forward kernels + the HIP training backward:
+limb-engine weight gradients of the k4 s2 p1 / first layers, the direct output-layer weight gradient,
+bias column sums).  Checked against (a) the reference's own autograd gradients (golden subsamples and
+full norms, tests/golden/*_gtrain.npz) and (b) the oracle's explicit backward on the same inputs.
+
+Tolerance: rel-L2 <= 2e-5 per parameter tensor against the reference (fp32 results summed in a different
+order over up to B*H*W = 131K terms; the limb engine's products carry fp32's 24 significand bits,
+gemm.hip); at full width, accuracy-relative against fp64 (see the full-width test).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import G_NAMES, gtrain_check, gtrain_inputs, rel_l2
+from oracle import damc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+TOL = 2e-5
+
+
+def _hip_grads(G, z, x, want_z=False):
+    G.train()
+    for p in G.parameters():
+        p.grad = None
+    zz = z.clone().requires_grad_(want_z)
+    x_hat = G(zz)
+    loss = torch.sum((x_hat - x) ** 2, dim=[1, 2, 3]).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    return [p.grad.detach().cpu().numpy() for p in G.parameters()], float(loss.detach()), (zz.grad if want_z else None)
+
+
+@pytest.mark.parametrize("name", G_NAMES)
+def test_generator_train_grads_match_reference(gpu_device, name):
+    G, z0, x, rec, meta = gtrain_inputs(name)
+    G = G.to(gpu_device)
+    grads, loss, _ = _hip_grads(G, z0.to(gpu_device), x.to(gpu_device))
+    assert abs(loss - float(rec["g_loss"])) / float(rec["g_loss"]) < 1e-6
+    worst = gtrain_check(grads, rec, meta, TOL)
+    print("%s worst rel err vs reference %.2e" % (name, worst))
+
+
+@pytest.mark.parametrize("B", [40, 128])
+def test_generator_train_grads_full_width_vs_oracle(gpu_device, B):
+    """CIFAR-10 _netG_cifar10(ngf=128) at a ragged batch (B=40 -> padded to 64) and at the bench batch.
+
+    As in test_cifar_b128_step_vs_oracle, the full-width random-weight generator is ill-conditioned
+    (pre-activations within rounding of zero flip LReLU' between any two fp32 evaluations): the fp32
+    restatement of the reference's arithmetic itself sits up to ~1e-3 from fp64 on the first layers.
+    The criterion is accuracy-relative: per tensor, the HIP gradient's distance to an fp64 evaluation
+    stays within 3x the fp32 reference arithmetic's distance to it (+ a 1e-6 floor)."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=128, nc=3), 0)
+    z0 = torch.from_numpy(synth.normal_f32(2, 7, (B, 128)))
+    x = torch.from_numpy(synth.uniform_f32(1, 7, (B, 3, 32, 32)))
+    refs = []
+    for dt in (torch.float32, torch.float64):
+        L = orc.generator_layers(G, dt)
+        zz, xx = z0.to(dt), x.to(dt)
+        xh = orc.generator_sample(L, zz)
+        g, gz_ref, _ = orc.generator_train_grads(L, zz, 2.0 * (xh - xx) / B)
+        refs.append(([t for gw, gb in g for t in (gw, gb)] + [gz_ref]))
+    Gd = G.to(gpu_device)
+    grads, _, gz = _hip_grads(Gd, z0.to(gpu_device), x.to(gpu_device), want_z=True)
+    for k, (hip, r32, r64) in enumerate(zip(grads + [gz.cpu().numpy()], *refs)):
+        e_hip, e32 = rel_l2(hip, r64.numpy()), rel_l2(r32.numpy(), r64.numpy())
+        print("B=%d tensor %d: |hip - fp64| %.2e, |fp32 ref - fp64| %.2e" % (B, k, e_hip, e32))
+        assert e_hip <= 3 * e32 + 1e-6, (k, e_hip, e32)
+
+
+def test_generator_train_backward_is_deterministic(gpu_device):
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_svhn(nz=100, ngf=32, nc=3), 0).to(gpu_device)
+    z = torch.from_numpy(synth.normal_f32(2, 9, (48, 100))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(1, 9, (48, 3, 32, 32))).to(gpu_device)
+    a, _, _ = _hip_grads(G, z, x)
+    b, _, _ = _hip_grads(G, z, x)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
+
+
+def test_generator_forward_no_grad_is_hip(gpu_device):
+    """Under no_grad the drop-in forward is the plain HIP forward (gen_samples path) and matches the oracle."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_celeba64(nz=100, ngf=16, nc=3), 0)
+    z = torch.from_numpy(synth.normal_f32(2, 11, (5, 100)))
+    ref = orc.generator_sample(orc.generator_layers(G), z)
+    with torch.no_grad():
+        out = G.to(gpu_device)(z.to(gpu_device).reshape(5, 100, 1, 1))
+    assert not out.requires_grad
+    assert rel_l2(out.cpu().numpy(), ref.numpy()) < 1e-5

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import G_NAMES, Q_END_TOL, Q_NAMES, build_g_case, build_q_case, load_golden, rel_l2
+from conftest import (G_NAMES, Q_END_TOL, Q_NAMES, build_g_case, build_q_case, gtrain_check, gtrain_inputs,
+                      load_golden, rel_l2)
 from oracle import damc_oracle as orc
 
 torch.set_num_threads(8)
@@ -45,6 +46,20 @@ def test_generator_forward_and_grads(name):
     e, ge = orc.ebm_energy_grad(orc.ebm_params(c["E"]), c["z0"])
     assert rel_l2(e.numpy(), c["rec"]["ebm_e"]) < 1e-6
     assert rel_l2(ge.numpy(), c["rec"]["ebm_grad0"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", G_NAMES)
+def test_generator_train_grads(name):
+    """G update (train_gen_recon.py:222-231): the oracle's explicit backward vs the reference's autograd."""
+    G, z0, x, rec, meta = gtrain_inputs(name)
+    L = orc.generator_layers(G)
+    xh = orc.generator_sample(L, z0)
+    gx = 2.0 * (xh - x) / meta["B"]
+    loss = float(((xh - x) ** 2).sum(dim=(1, 2, 3)).mean())
+    assert abs(loss - float(rec["g_loss"])) / float(rec["g_loss"]) < 1e-6
+    grads, _, _ = orc.generator_train_grads(L, z0, gx)
+    flat = [t for gw, gb in grads for t in ((gw,) if gb is None else (gw, gb))]
+    gtrain_check([t.numpy() for t in flat], rec, meta, 1e-5)
 
 
 @pytest.mark.parametrize("name", FAST_G)
