@@ -1381,6 +1381,7 @@ size_t carve_train(const damc_generator_t* g, int B, char* base, TrainWs* t) {
       ctmp = std::max(ctmp, damc::colsum_tmp_floats((long)(Pd * nb), L.cout));
     } else if (L.kind == DAMC_LAYER_SMALLC) {
       part = std::max(part, damc::smallc_wgrad_part_floats(L, B));
+      ctmp = std::max(ctmp, damc::smallc_wgrad_tmp_floats(L, B));
       ctmp = std::max(ctmp, damc::colsum_tmp_floats((long)B * L.hout * L.wout, L.cout));
     } else {
       ctmp = std::max(ctmp, damc::colsum_tmp_floats(B, L.cout));
@@ -1427,7 +1428,7 @@ int train_backward(const damc_generator_t* g, int B, const float* z, const float
     const float* in32 = i ? ws.h[i - 1] : z;
     if (L.kind == DAMC_LAYER_SMALLC) {
       if (i == 0 || !h_f32(g, i - 1) || d_x3) return DAMC_ERR_UNSUPPORTED;
-      if (dW && (rc = damc::launch_smallc_wgrad(L, in32, d, B, tw.part, dW, s))) return rc;
+      if (dW && (rc = damc::launch_smallc_wgrad(L, in32, d, B, tw.part, tw.ctmp, dW, s))) return rc;
       if (db && (rc = damc::launch_colsum(d, (long)B * L.hout * L.wout, L.cout, L.cout, db, tw.ctmp, s))) return rc;
     } else if (L.kind == DAMC_LAYER_LINEAR) {
       if (d_x3 || (i > 0 && !h_f32(g, i - 1))) return DAMC_ERR_UNSUPPORTED;

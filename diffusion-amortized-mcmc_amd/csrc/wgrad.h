@@ -19,10 +19,12 @@ int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float*
 size_t colsum_tmp_floats(long R, int C);
 int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s);
 
-// Output-layer (Cout <= 4) weight gradient, direct: h NHWC fp32, delta NHWC [pix][Cout]; part is scratch
+// Output-layer (Cout <= 4) weight gradient, direct: h NHWC fp32, delta NHWC [pix][Cout]; part and tmp are
+// scratch (per-block partials in the PyTorch order, reduced by launch_colsum)
 size_t smallc_wgrad_part_floats(const damc_layer_t& L, int B);
-int launch_smallc_wgrad(const damc_layer_t& L, const float* h, const float* delta, int B, float* part, float* dW,
-                        hipStream_t s);
+size_t smallc_wgrad_tmp_floats(const damc_layer_t& L, int B);
+int launch_smallc_wgrad(const damc_layer_t& L, const float* h, const float* delta, int B, float* part, float* tmp,
+                        float* dW, hipStream_t s);
 
 // delta[(n * HW + p) * NC + o] = g[n][o][p] * act'(x_hat) (tanh: 1 - x_hat^2; none: 1) from NCHW tensors
 int launch_out_delta(const float* g, const float* xhat, int B, int NC, int HW, int act, float* delta, hipStream_t s);

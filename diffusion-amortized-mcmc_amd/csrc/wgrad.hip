@@ -137,40 +137,55 @@ int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float*
 }
 
 // --------------------------------------------------------------------------------------- column sums
-// grid (ceil(C/64), row blocks), 256 threads = 4 row lanes x 64 channels; fixed-order combine
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, long R, int C, long ld,
+// grid (ceil(C/CL), row blocks), 256 threads = RL row lanes x CL channel lanes (CL = min(64, pow2 >= C)),
+// each row lane summing every RL-th row of the block's range; the RL partials combine in a fixed tree
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, long R, int C, long ld, int CL,
                                                      long rows_per, float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[256];
+  const int RL = 256 / CL;
+  const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
+  const int c = blockIdx.x * CL + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min(R, r0 + rows_per);
   float sum = 0.f;
   if (c < C)
-    for (long r = r0 + rl; r < r1; r += 4) sum += X[r * ld + c];
-  red[rl][cl] = sum;
+    for (long r = r0 + rl; r < r1; r += RL) sum += X[r * ld + c];
+  red[threadIdx.x] = sum;
   __syncthreads();
-  if (rl == 0 && c < C) out[(long)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  for (int h = RL / 2; h > 0; h >>= 1) {
+    if (rl < h) red[threadIdx.x] += red[threadIdx.x + h * CL];
+    __syncthreads();
+  }
+  if (rl == 0 && c < C) out[(long)blockIdx.y * C + c] = red[cl];
 }
 
-static int colsum_blocks(long R) { return R <= 4096 ? 1 : (int)std::min<long>(256, (R + 1023) / 1024); }
+static int colsum_lanes(int C) {
+  int cl = 1;
+  while (cl < C && cl < 64) cl <<= 1;
+  return cl;
+}
+// row blocks of the first pass: <= 16 rows per thread, at most 1024 blocks (the second pass sums them)
+static long colsum_blocks(long R, int C) {
+  const long per = 16L * (256 / colsum_lanes(C));
+  return R <= per ? 1 : std::min<long>(1024, (R + per - 1) / per);
+}
 
-size_t colsum_tmp_floats(long R, int C) { return (size_t)colsum_blocks(R) * C; }
+size_t colsum_tmp_floats(long R, int C) { return (size_t)colsum_blocks(R, C) * C; }
 
 int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s) {
   if (!X || !out || R <= 0 || C <= 0 || ld < C) return DAMC_ERR_ARG;
   ProfScope ps("bias_grad", 0.0, s);
-  const int nrb = colsum_blocks(R);
-  const unsigned gx = (unsigned)((C + 63) / 64);
+  const int CL = colsum_lanes(C);
+  const long nrb = colsum_blocks(R, C);
+  const unsigned gx = (unsigned)((C + CL - 1) / CL);
   if (nrb == 1) {
-    hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, X, R, C, ld, R, out);
+    hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, X, R, C, ld, CL, R, out);
     return (int)hipGetLastError();
   }
   if (!tmp) return DAMC_ERR_ARG;
   const long per = (R + nrb - 1) / nrb;
-  hipLaunchKernelGGL(colsum_kernel, dim3(gx, (unsigned)nrb), dim3(256), 0, s, X, R, C, ld, per, tmp);
-  hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, (const float*)tmp, (long)nrb, C, (long)C,
-                     (long)nrb, out);
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, (unsigned)nrb), dim3(256), 0, s, X, R, C, ld, CL, per, tmp);
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, s, (const float*)tmp, nrb, C, (long)C, CL, nrb, out);
   return (int)hipGetLastError();
 }
 
@@ -204,7 +219,23 @@ __global__ __launch_bounds__(256) void smallc_wgrad_kernel(const float* __restri
     for (int yy = 0; yy < rows; ++yy) {
       const float* hr = h + ((long)n * Hin + iy0 + yy) * Win * Cin + ci;
       const float* wr = dw + (S * yy) * Wd * NC;
-      for (int ix = 0; ix < Win; ++ix) {
+      int ix = 0;
+      for (; ix + 4 <= Win; ix += 4) {  // four loads in flight, then their taps in order
+        float hv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) hv[u] = hr[(long)(ix + u) * Cin];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* w0 = wr + S * (ix + u) * NC;
+#pragma unroll
+          for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+              for (int o = 0; o < NC; ++o) acc[(ky * K + kx) * NC + o] += hv[u] * w0[(ky * Wd + kx) * NC + o];
+        }
+      }
+      for (; ix < Win; ++ix) {
         const float hv = hr[(long)ix * Cin];
         const float* w0 = wr + S * ix * NC;
 #pragma unroll
@@ -215,61 +246,63 @@ __global__ __launch_bounds__(256) void smallc_wgrad_kernel(const float* __restri
             for (int o = 0; o < NC; ++o) acc[(ky * K + kx) * NC + o] += hv * w0[(ky * Wd + kx) * NC + o];
       }
     }
-    float* pp = part + (long)(n * nrb + rb) * T * Cin + ci;
+    // this block's partial, in the PyTorch (Cin, Cout, k, k) order: a column sum over blocks is dW
+    float* pp = part + (long)(n * nrb + rb) * T * Cin + (long)ci * T;
 #pragma unroll
-    for (int j = 0; j < T; ++j) pp[(long)j * Cin] = acc[j];
+    for (int o = 0; o < NC; ++o)
+#pragma unroll
+      for (int t = 0; t < K * K; ++t) pp[o * K * K + t] = acc[t * NC + o];
   }
 }
 
-// dW[ci][o][ky][kx] = fixed-order sum over the partial blocks; one thread per (tap*NC + o, ci)
-template <int NC, int K>
-__global__ __launch_bounds__(256) void smallc_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int Cin,
-                                                                  float* __restrict__ dW) {
-  constexpr int T = K * K * NC;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)T * Cin) return;
-  const int j = (int)(i / Cin), ci = (int)(i - (long)j * Cin);
-  float sum = 0.f;
-  for (int b = 0; b < nblk; ++b) sum += part[(long)b * T * Cin + i];
-  const int o = j % NC, t = j / NC;
-  dW[((long)ci * NC + o) * (K * K) + t] = sum;
-}
-
-static int smallc_rows(const damc_layer_t& L) {
+// rows per block: >= 2048 blocks where the map allows (latency-bound loads), window within 40 KiB of LDS
+static int smallc_rows(const damc_layer_t& L, int B) {
   int R = 8;
   const int Wd = L.stride * (L.win - 1) + L.k;
-  while (R > 1 && (size_t)(L.stride * (R - 1) + L.k) * Wd * L.cout * sizeof(float) > 40960) R /= 2;
+  while (R > 1 && ((size_t)(L.stride * (R - 1) + L.k) * Wd * L.cout * sizeof(float) > 40960 ||
+                   (long)B * ((L.hin + R - 1) / R) < 2048))
+    R /= 2;
   return R;
 }
 
-size_t smallc_wgrad_part_floats(const damc_layer_t& L, int B) {
-  const int R = smallc_rows(L);
-  return (size_t)B * ((L.hin + R - 1) / R) * L.k * L.k * L.cout * L.cin;
+static long smallc_blocks(const damc_layer_t& L, int B) {
+  const int R = smallc_rows(L, B);
+  return (long)B * ((L.hin + R - 1) / R);
 }
 
-int launch_smallc_wgrad(const damc_layer_t& L, const float* h, const float* delta, int B, float* part, float* dW,
-                        hipStream_t s) {
+size_t smallc_wgrad_part_floats(const damc_layer_t& L, int B) {
+  return (size_t)smallc_blocks(L, B) * L.k * L.k * L.cout * L.cin;
+}
+
+size_t smallc_wgrad_tmp_floats(const damc_layer_t& L, int B) {
+  return colsum_tmp_floats(smallc_blocks(L, B), L.k * L.k * L.cout * L.cin);
+}
+
+int launch_smallc_wgrad(const damc_layer_t& L, const float* h, const float* delta, int B, float* part, float* tmp,
+                        float* dW, hipStream_t s) {
   if (!h || !delta || !part || !dW || B <= 0) return DAMC_ERR_ARG;
-  const int R = smallc_rows(L);
+  const int R = smallc_rows(L, B);
   const int Wd = L.stride * (L.win - 1) + L.k;
   const size_t sm = (size_t)(L.stride * (R - 1) + L.k) * Wd * L.cout * sizeof(float);
   if (sm > 65536) return DAMC_ERR_UNSUPPORTED;
   const int nrb = (L.hin + R - 1) / R;
   const dim3 grid((unsigned)nrb, (unsigned)B);
-  const long nout = (long)L.k * L.k * L.cout * L.cin;
-  const dim3 rgrid((unsigned)((nout + 255) / 256));
-  ProfScope ps("smallc_wgrad", 2.0 * B * L.hin * L.win * L.cin * L.k * L.k * L.cout, s);
-#define SW(NC_, K_)                                                                                                 \
-  if (L.cout == NC_ && L.k == K_) {                                                                                 \
-    hipLaunchKernelGGL((smallc_wgrad_kernel<NC_, K_>), grid, dim3(256), sm, s, h, delta, L.hin, L.win, L.cin,       \
-                       L.stride, L.pad, L.hout, L.wout, R, Wd, part);                                               \
-    hipLaunchKernelGGL((smallc_wgrad_reduce_kernel<NC_, K_>), rgrid, dim3(256), 0, s, (const float*)part, B * nrb, \
-                       L.cin, dW);                                                                                  \
-    return (int)hipGetLastError();                                                                                  \
+  const int T = L.k * L.k * L.cout;
+  bool launched = false;
+  {
+    ProfScope ps("smallc_wgrad", 2.0 * B * L.hin * L.win * L.cin * L.k * L.k * L.cout, s);
+#define SW(NC_, K_)                                                                                           \
+  if (!launched && L.cout == NC_ && L.k == K_) {                                                              \
+    hipLaunchKernelGGL((smallc_wgrad_kernel<NC_, K_>), grid, dim3(256), sm, s, h, delta, L.hin, L.win, L.cin, \
+                       L.stride, L.pad, L.hout, L.wout, R, Wd, part);                                         \
+    launched = true;                                                                                          \
   }
-  SW(3, 3) SW(3, 4) SW(1, 3) SW(1, 4) SW(2, 3) SW(2, 4) SW(4, 3) SW(4, 4)
+    SW(3, 3) SW(3, 4) SW(1, 3) SW(1, 4) SW(2, 3) SW(2, 4) SW(4, 3) SW(4, 4)
 #undef SW
-  return DAMC_ERR_UNSUPPORTED;
+  }
+  if (!launched) return DAMC_ERR_UNSUPPORTED;
+  DAMC_LAUNCH_CHECK();
+  return launch_colsum(part, (long)B * nrb, T * L.cin, (long)T * L.cin, dW, tmp, s);
 }
 
 // --------------------------------------------------------------------------------- output delta

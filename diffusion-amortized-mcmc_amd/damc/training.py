@@ -51,6 +51,7 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(L.damc_generator_train_forward(ctypes.byref(desc), ptr(zc), B, ptr(xh), ptr(ws), nbytes,
                                              _lib.stream_ptr(dev)), "damc_generator_train_forward")
         ctx.plan, ctx.ws, ctx.nbytes = plan, ws, nbytes
+        ctx.desc, ctx.keep = desc, (plan.buffers, getattr(plan, "_keep", None))
         ctx.save_for_backward(zc, xh, *params)
         return xh
 
@@ -59,9 +60,10 @@ class _GeneratorTrainFn(torch.autograd.Function):
         zc, xh = ctx.saved_tensors[:2]
         plan = ctx.plan
         dev = zc.device
-        # the saved parameters are the modules' own (autograd has checked they were not modified in place),
-        # so re-packing reproduces the forward's packed weights
-        desc = plan.refresh(dev)
+        # the saved parameters are the modules' own and autograd has checked they were not modified in place,
+        # so the packed buffers still hold the forward's weights (any re-pack in between wrote the same
+        # values); re-pack only if the plan re-allocated them (device change)
+        desc = ctx.desc if plan.desc is ctx.desc else plan.refresh(dev)
         gx = gx.to(torch.float32).contiguous()
         grads = _lib.GeneratorGrads()
         outs = []
@@ -74,7 +76,7 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(_lib.lib().damc_generator_train_backward(
             ctypes.byref(desc), ptr(zc), ptr(xh), ptr(gx), zc.shape[0], ctypes.byref(grads), ptr(gz), ptr(ctx.ws),
             ctx.nbytes, _lib.stream_ptr(dev)), "damc_generator_train_backward")
-        ctx.ws = None
+        ctx.ws = ctx.desc = ctx.keep = None
         return (gz, None, *outs)
 
 
