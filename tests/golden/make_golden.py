@@ -211,6 +211,46 @@ def capture_gtrain(dn, torch):
     return out
 
 
+def capture_checkpoint(dn, torch):
+    """A training checkpoint in the reference's format (workspace/train_gen_recon.py:284-294), written by the
+    reference's own modules and optimizers after one G / Q / E update at tiny widths, plus the reference G's
+    output on fixed inputs after loading it (tests/test_oracle_golden.py::test_reference_checkpoint_loads)."""
+    import torch.optim as optim
+
+    nz = 16
+    G = dn._netG_cifar10(nz=nz, ngf=4, nc=3)
+    E = dn._netE(nz=nz, ndf=8)
+    qargs = dict(nc=3, nz=nz, nxemb=16, ntemb=16, nf=1, nif=2, diffusion_residual=True, n_interval=4,
+                 logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                 dataset="cifar10")
+    Q, Q_dummy = dn._netQ_U(**qargs), dn._netQ_U(**qargs)
+    for i, m in enumerate((G, E, Q, Q_dummy)):
+        synth.load_into(m, 50 + i)
+    G_opt = optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    Q_opt = optim.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
+    E_opt = optim.Adam(E.parameters(), lr=1e-4, betas=(0.5, 0.999))
+    x = torch.from_numpy(synth.uniform_f32(60, 0, (4, 3, 32, 32)))
+    z = torch.from_numpy(synth.normal_f32(61, 0, (4, nz)))
+    torch.manual_seed(0)
+    G_opt.zero_grad()
+    torch.sum((G(z) - x) ** 2, dim=[1, 2, 3]).mean().backward()
+    G_opt.step()
+    Q_opt.zero_grad()
+    Q.calculate_loss(x=x, z=z, mask=torch.ones(4, 1)).mean().backward()
+    Q_opt.step()
+    E_opt.zero_grad()
+    (E(z).mean() - E(-z).mean()).backward()
+    E_opt.step()
+    save_dict = {"G_state_dict": G.state_dict(), "G_optimizer": G_opt.state_dict(), "Q_state_dict": Q.state_dict(),
+                 "Q_optimizer": Q_opt.state_dict(), "Q_dummy_state_dict": Q_dummy.state_dict(),
+                 "E_state_dict": E.state_dict(), "E_optimizer": E_opt.state_dict(), "iter": 1}
+    torch.save(save_dict, os.path.join(HERE, "ckpt_cifar10_tiny.pth.tar"))
+    with torch.no_grad():
+        rec = {"gen_x": G(z).numpy(), "ebm_e": E(z).numpy(), "xemb": Q.encoder(x).numpy()}
+    meta = dict(kind="ckpt", nz=nz, ngf=4, ndf=8, q=qargs)
+    np.savez(os.path.join(HERE, "ckpt_cifar10_tiny.npz"), meta=json.dumps(meta), **rec)
+
+
 def capture_q(dn, torch):
     out = {}
     for name, (ds, nc, nz, nif, nxemb, ntemb, H, B, var_type, n_int) in Q_CONFIGS.items():
@@ -306,6 +346,7 @@ def main():
 
     torch.set_num_threads(8)
     dn, mc = import_reference()
+    capture_checkpoint(dn, torch)
     for name, (rec, meta) in capture_gtrain(dn, torch).items():
         np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
     if "--gtrain-only" in sys.argv:

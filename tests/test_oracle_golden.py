@@ -128,3 +128,44 @@ def test_encoder_and_sweep(name):
                                         m["logsnr_max"], m["var_type"])
         assert rel_l2(eps_log[0].numpy(), rec["q_prior_eps3"][0]) < 1e-5
         assert rel_l2(zt.numpy(), rec["q_prior"]) < tol_end
+
+
+def test_reference_checkpoint_loads():
+    """a checkpoint written by the reference's training driver format
+    (train_gen_recon.py:284-294: G/Q/Q_dummy/E state dicts + Adam/AdamW optimizer states + iter) loads
+    unchanged into the drop-in modules and optimizers (train_gen_recon.py:163-170, eval_gen_recon.py:156-163),
+    and the loaded nets reproduce the reference's outputs.  Loaded with weights_only=True."""
+    import json
+    import os
+
+    import torch.optim as optim
+
+    from conftest import GOLDEN
+    from damc import synth
+    from src import diffusion_net as dn
+
+    sd = torch.load(os.path.join(GOLDEN, "ckpt_cifar10_tiny.pth.tar"), weights_only=True)
+    d = np.load(os.path.join(GOLDEN, "ckpt_cifar10_tiny.npz"))
+    meta = json.loads(str(d["meta"]))
+    nz = meta["nz"]
+    G = dn._netG_cifar10(nz=nz, ngf=meta["ngf"], nc=3)
+    E = dn._netE(nz=nz, ndf=meta["ndf"])
+    Q, Q_dummy = dn._netQ_U(**meta["q"]), dn._netQ_U(**meta["q"])
+    G.load_state_dict(sd["G_state_dict"])
+    Q.load_state_dict(sd["Q_state_dict"])
+    Q_dummy.load_state_dict(sd["Q_dummy_state_dict"])
+    E.load_state_dict(sd["E_state_dict"])
+    G_opt = optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    Q_opt = optim.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
+    E_opt = optim.Adam(E.parameters(), lr=1e-4, betas=(0.5, 0.999))
+    G_opt.load_state_dict(sd["G_optimizer"])
+    Q_opt.load_state_dict(sd["Q_optimizer"])
+    E_opt.load_state_dict(sd["E_optimizer"])
+    assert sd["iter"] + 1 == 2
+    assert len(G_opt.state) == len(list(G.parameters()))
+    x = torch.from_numpy(synth.uniform_f32(60, 0, (4, 3, 32, 32)))
+    z = torch.from_numpy(synth.normal_f32(61, 0, (4, nz)))
+    with torch.no_grad():
+        assert rel_l2(orc.generator_sample(orc.generator_layers(G), z).numpy(), d["gen_x"]) < 1e-6
+        assert rel_l2(E(z).numpy(), d["ebm_e"]) < 1e-6
+        assert rel_l2(orc.encoder_forward(Q.encoder, x).numpy(), d["xemb"]) < 1e-5
