@@ -49,7 +49,7 @@ class Ebm(ctypes.Structure):
     ]
 
 
-class CsqBlock(ctypes.Structure):
+class CsqBlock(ctypes.Structure):  # damc_csq_block_t
     _fields_ = [
         ("din", ctypes.c_int), ("dout", ctypes.c_int),
         ("wl", ctypes.c_void_p), ("bl", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("bs", ctypes.c_void_p),
@@ -65,6 +65,22 @@ class Denoiser(ctypes.Structure):
         ("wctx_t", ctypes.c_void_p), ("wctx_x", ctypes.c_void_p), ("bctx", ctypes.c_void_p),
         ("blocks", CsqBlock * 7),
     ]
+
+
+class DenoiserTrain(ctypes.Structure):
+    _fields_ = [
+        ("nz", ctypes.c_int), ("ntemb", ctypes.c_int), ("nxemb", ctypes.c_int), ("residual", ctypes.c_int),
+        ("bmat", ctypes.c_void_p),
+        ("tw1", ctypes.c_void_p), ("tb1", ctypes.c_void_p), ("tw2", ctypes.c_void_p), ("tb2", ctypes.c_void_p),
+        ("blocks", CsqBlock * 7),
+        ("wctx", ctypes.c_void_p * 7), ("bctx", ctypes.c_void_p * 7),
+    ]
+
+
+class DenoiserGrads(ctypes.Structure):
+    _fields_ = [("bmat", ctypes.c_void_p), ("tw1", ctypes.c_void_p), ("tb1", ctypes.c_void_p),
+                ("tw2", ctypes.c_void_p), ("tb2", ctypes.c_void_p)] + [
+        (k, ctypes.c_void_p * 7) for k in ("wl", "bl", "ws", "bs", "wg", "bg", "wb", "wctx", "bctx")]
 
 
 _P = ctypes.c_void_p
@@ -89,6 +105,10 @@ _SIGS = {
     "damc_generator_train_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
     "damc_generator_train_backward": (_I, [ctypes.POINTER(Generator), _P, _P, _P, _I, ctypes.POINTER(GeneratorGrads),
                                            _P, _P, _SZ, _P]),
+    "damc_denoiser_train_workspace_bytes": (_SZ, [ctypes.POINTER(DenoiserTrain), _I]),
+    "damc_denoiser_train_forward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _P, _P, _I, _P, _P, _SZ, _P]),
+    "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
+                                          _P, _P, _SZ, _P]),
     "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P, _P]),
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_z_update": (_I, [_P, _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P]),

@@ -95,3 +95,99 @@ def generator_apply(G, z):
     from .langevin import generator_forward
 
     return generator_forward(z.to(torch.float32).contiguous(), G)
+
+
+# ----------------------------------------------------------------------------------------- Q update
+# The denoiser of Q.calculate_loss (workspace/src/diffusion_net.py:624-645) on the HIP path
+# (SURVEY.md §8f row 2): damc_denoiser_train_forward / _backward over the live parameters in their
+# PyTorch layouts (the library stacks them per call).  The encoder / prior_emb / loss stay the caller's
+# autograd graph, fed with dL/dxemb.
+
+_BLOCK_KEYS = ("wl", "bl", "ws", "bs", "wg", "bg", "wb", "wctx", "bctx")
+
+
+def _blocks_of(p):
+    return list(p.in_layers) + list(p.mid_layers) + list(p.out_layers)
+
+
+def _denoiser_params(p):
+    """[(field, block index or None, parameter)] in a fixed order."""
+    t1, t2 = p.time_mlp[1], p.time_mlp[3]
+    out = [("bmat", None, p.B), ("tw1", None, t1.weight), ("tb1", None, t1.bias), ("tw2", None, t2.weight),
+           ("tb2", None, t2.bias)]
+    for b, blk in enumerate(_blocks_of(p)):
+        lc = blk._layer_ctx[1]
+        for key, t in zip(_BLOCK_KEYS, (blk._layer[0].weight, blk._layer[0].bias, blk._skip.weight, blk._skip.bias,
+                                        blk._hyper_gate.weight, blk._hyper_gate.bias, blk._hyper_bias.weight,
+                                        lc.weight, lc.bias)):
+            out.append((key, b, t))
+    return out
+
+
+def _denoiser_desc(p, params):
+    d = _lib.DenoiserTrain()
+    d.nz, d.ntemb, d.nxemb, d.residual = p.nz, p.ntemb, p.nxemb, int(bool(p.residual))
+    for (key, b, _), t in zip(_denoiser_params(p), params):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device.type != "cuda":
+            raise _lib.DamcError("denoiser parameter %s must be a contiguous float32 ROCm tensor" % key)
+        if b is None:
+            setattr(d, key, t.data_ptr())
+        elif key in ("wctx", "bctx"):
+            getattr(d, key)[b] = t.data_ptr()
+        else:
+            setattr(d.blocks[b], key, t.data_ptr())
+    for b, blk in enumerate(_blocks_of(p)):
+        d.blocks[b].din, d.blocks[b].dout = blk._layer[0].in_features, blk._layer[0].out_features
+    return d
+
+
+class _DenoiserTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, zt, se, xemb, p, *params):
+        dev = zt.device
+        zc = zt.detach().to(torch.float32).contiguous()
+        sc = se.detach().to(torch.float32).contiguous()
+        xc = xemb.detach().to(torch.float32).contiguous()
+        desc = _denoiser_desc(p, params)
+        B = zc.shape[0]
+        L = _lib.lib()
+        nbytes = int(L.damc_denoiser_train_workspace_bytes(ctypes.byref(desc), B))
+        if nbytes == 0:
+            raise _lib.DamcError("unsupported denoiser configuration for the HIP training path")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        eps = torch.empty(B, p.nz, dtype=torch.float32, device=dev)
+        check(L.damc_denoiser_train_forward(ctypes.byref(desc), ptr(zc), ptr(sc), ptr(xc), B, ptr(eps), ptr(ws),
+                                            nbytes, _lib.stream_ptr(dev)), "damc_denoiser_train_forward")
+        ctx.p, ctx.ws, ctx.nbytes, ctx.desc, ctx.B = p, ws, nbytes, desc, B
+        ctx.save_for_backward(*params)  # autograd's version check: no in-place update before the backward
+        return eps
+
+    @staticmethod
+    def backward(ctx, g):
+        params = ctx.saved_tensors
+        dev = g.device
+        g = g.to(torch.float32).contiguous()
+        grads = _lib.DenoiserGrads()
+        outs = []
+        for k, ((key, b, _), p) in enumerate(zip(_denoiser_params(ctx.p), params)):
+            t = torch.empty_like(p) if ctx.needs_input_grad[4 + k] else None
+            outs.append(t)
+            if t is not None:
+                if b is None:
+                    setattr(grads, key, t.data_ptr())
+                else:
+                    getattr(grads, key)[b] = t.data_ptr()
+        gz = torch.empty(ctx.B, ctx.p.nz, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        gx = torch.empty(ctx.B, ctx.p.nxemb, dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
+        check(_lib.lib().damc_denoiser_train_backward(
+            ctypes.byref(ctx.desc), ptr(g), ctx.B, ctypes.byref(grads), ptr(gz), ptr(gx), ptr(ctx.ws), ctx.nbytes,
+            _lib.stream_ptr(dev)), "damc_denoiser_train_backward")
+        ctx.ws = ctx.desc = None
+        return (gz, None, gx, None, *outs)
+
+
+def denoiser_apply(p, zt, se, xemb):
+    """eps_pred = p(zt, logsnr, xemb) given se = SinusoidalPosEmb(logsnr input), differentiable w.r.t. zt,
+    xemb and p's parameters (Diffusion_UnetA.forward, diffusion_net.py:477-533)."""
+    params = [t for _, _, t in _denoiser_params(p)]
+    return _DenoiserTrainFn.apply(zt, se, xemb, p, *params)

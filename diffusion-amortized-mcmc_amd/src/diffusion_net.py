@@ -224,6 +224,12 @@ class Diffusion_UnetA(nn.Module):
         assert z.shape == (b, self.nz) and logsnr.shape == (b,)
         assert (xemb is None and self.nxemb == 0) or xemb.shape == (b, self.nxemb)
         t_in = torch.arctan(torch.exp(-0.5 * torch.clamp(logsnr, min=-20.0, max=20.0))) / (0.5 * math.pi)
+        if z.is_cuda and xemb is not None:
+            # ROCm: forward + training backward on libdamc (damc.training.denoiser_apply); the sinusoidal
+            # time embedding of the per-sample logsnr stays these torch ops, as the reference evaluates it
+            from damc.training import denoiser_apply
+
+            return denoiser_apply(self, z, self.time_mlp[0](t_in), xemb)
         temb = self.time_mlp(t_in)
         ctx = temb if xemb is None else torch.cat([temb, xemb], dim=1)
         skips, out = [], self.input_emb(z)
@@ -269,7 +275,9 @@ class _netQ_U(nn.Module):
         return amortizer.q_forward(self, x=x, b=b, device=device, cond_w=cond_w)
 
     def calculate_loss(self, x=None, z=None, mask=None):
-        """Training loss of the denoiser (stock PyTorch; training is outside the hot path)."""
+        """Training loss of the denoiser (diffusion_net.py:624-645).  On ROCm tensors the denoiser's forward
+        and backward run on libdamc (Diffusion_UnetA.forward -> damc.training.denoiser_apply); the encoder,
+        prior_emb and the noising stay PyTorch."""
         assert z is not None
         if x is not None:
             xemb = self.encoder(x)

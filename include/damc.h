@@ -214,6 +214,36 @@ int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, i
                        uint64_t chain_base, float* eps_log, int eps_log_steps, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* ----------------------------------------------- Q training: denoiser loss step */
+/* The denoiser of Q.calculate_loss (workspace/src/diffusion_net.py:624-645, Diffusion_UnetA :463-533) as
+ * trained by the Q update of every iteration (workspace/train_gen_recon.py:211-220): eps_pred =
+ * p(zt, logsnr, xemb) with every intermediate kept, then the backward from dL/deps_pred to every parameter
+ * of p, to zt and to xemb (which the caller's autograd carries into the encoder / prior_emb).  All weights
+ * in PyTorch layouts.  temb_in (B, ntemb) is SinusoidalPosEmb of the per-sample logsnr input, evaluated by
+ * the caller with the reference's op sequence (diffusion_net.py:447-461, 490-491). */
+typedef struct {
+  int nz, ntemb, nxemb, residual;
+  const float* bmat;                  /* p.B (nz, nz/2)                                  */
+  const float *tw1, *tb1, *tw2, *tb2; /* time_mlp[1], time_mlp[3]: (out, in), (out)      */
+  damc_csq_block_t blocks[7];         /* in0 in1 in2 mid0 out0 out1 out2                 */
+  const float* wctx[7];               /* _layer_ctx[1].weight (dout, ntemb + nxemb)       */
+  const float* bctx[7];               /* _layer_ctx[1].bias (dout)                       */
+} damc_denoiser_train_t;
+typedef struct { /* gradients, same layouts (written, not accumulated; NULL entries are skipped) */
+  float* bmat;
+  float *tw1, *tb1, *tw2, *tb2;
+  float *wl[7], *bl[7], *ws[7], *bs[7], *wg[7], *bg[7], *wb[7], *wctx[7], *bctx[7];
+} damc_denoiser_grads_t;
+size_t damc_denoiser_train_workspace_bytes(const damc_denoiser_train_t* d, int batch);
+int damc_denoiser_train_forward(const damc_denoiser_train_t* d, const float* zt, const float* temb_in,
+                                const float* xemb, int batch, float* eps_pred, void* workspace, size_t workspace_bytes,
+                                void* stream);
+/* after damc_denoiser_train_forward on the same workspace: grad_eps (B, nz) -> grads, grad_zt (B, nz) and
+ * grad_xemb (B, nxemb) (either may be NULL) */
+int damc_denoiser_train_backward(const damc_denoiser_train_t* d, const float* grad_eps, int batch,
+                                 const damc_denoiser_grads_t* grads, float* grad_zt, float* grad_xemb,
+                                 void* workspace, size_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------------------- profiling */
 /* optional per-kernel HIP-event timing (bench.py roofline): records events around each
  * launch of the named kernel class on the launch stream; read back after a sync. */

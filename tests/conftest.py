@@ -105,6 +105,43 @@ def gtrain_check(grads, rec, meta, tol):
     return worst
 
 
+SEED_QT = 7  # tests/golden/make_golden.py qtrain_noise
+
+
+def qtrain_run(name, device):
+    """One Q.calculate_loss(x, z, mask).mean().backward() (train_gen_recon.py:211-217) of the drop-in Q with the
+    golden case's injected noise; returns (per-sample loss, [grads in named_parameters order, grad != None],
+    rec, meta)."""
+    import torch
+
+    from damc import synth
+    from src import diffusion_net as dn
+
+    rec, meta = load_golden(name + "_qtrain")
+    c = build_q_case(meta["q"], device)
+    Q, x, m = c["Q"], c["x"], c["meta"]
+    B, nz = m["B"], m["nz"]
+    Q.train()
+    z = torch.from_numpy(synth.normal_f32(SEED_Z0, 0, (B, nz))).to(device)
+    mask = torch.ones(B, 1, device=device)
+    mask[1::3] = 0.0
+    pe = synth.normal_f32(SEED_QT, 0, (B, nz))
+    u = synth.uniform_f32(SEED_QT, 1, (B,), 0.0, 1.0)
+    eps = synth.normal_f32(SEED_QT, 2, (B, nz))
+    orig = torch.randn, torch.rand, torch.randn_like
+    torch.randn = lambda *a, **k: torch.from_numpy(pe.copy()).to(k.get("device") or "cpu")
+    torch.rand = lambda *a, **k: torch.from_numpy(u.copy())
+    torch.randn_like = lambda t, **k: torch.from_numpy(eps.copy()).to(t.device)
+    try:
+        Q.zero_grad()
+        loss = Q.calculate_loss(x=x, z=z, mask=mask)
+        loss.mean().backward()
+    finally:
+        torch.randn, torch.rand, torch.randn_like = orig
+    grads = [p.grad.detach().cpu().numpy() for p in Q.parameters() if p.grad is not None]
+    return loss.detach().cpu().numpy(), grads, rec, meta
+
+
 def build_q_case(name, device="cpu"):
     import torch
 

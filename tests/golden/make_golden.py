@@ -251,6 +251,60 @@ def capture_checkpoint(dn, torch):
     np.savez(os.path.join(HERE, "ckpt_cifar10_tiny.npz"), meta=json.dumps(meta), **rec)
 
 
+QTRAIN_CONFIGS = ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"]
+SEED_QT = 7
+
+
+def qtrain_noise(B, nz):
+    """The random draws of one Q.calculate_loss call (diffusion_net.py:624-641), in call order:
+    prior_emb input randn(B, nz), u = rand(B), eps = randn_like(z)."""
+    return (synth.normal_f32(SEED_QT, 0, (B, nz)), synth.uniform_f32(SEED_QT, 1, (B,), 0.0, 1.0),
+            synth.normal_f32(SEED_QT, 2, (B, nz)))
+
+
+def capture_qtrain(dn, torch):
+    """The Q update's loss (workspace/train_gen_recon.py:211-217): Q.train(); Q.calculate_loss(x, z,
+    mask).mean().backward() on the reference Q with injected noise and a mixed mask; per-sample losses and
+    every parameter gradient (strided subsample <= 512 values + full L2 norm)."""
+    out = {}
+    for name in QTRAIN_CONFIGS:
+        ds, nc, nz, nif, nxemb, ntemb, H, B, var_type, n_int = Q_CONFIGS[name]
+        print("Q train config", name, flush=True)
+        Q = dn._netQ_U(nc=nc, nz=nz, nxemb=nxemb, ntemb=ntemb, nif=nif, diffusion_residual=True,
+                       n_interval=n_int, logsnr_min=-5.1, logsnr_max=9.8, var_type=var_type,
+                       with_noise=True, cond_w=0.0, net_arch="A", dataset=ds)
+        synth.load_into(Q, SEED_Q)
+        Q.train()
+        x = torch.from_numpy(synth.uniform_f32(SEED_X, 0, (B, nc, H, H)))
+        z = torch.from_numpy(synth.normal_f32(SEED_Z0, 0, (B, nz)))
+        mask = torch.ones(B, 1)
+        mask[1::3] = 0.0
+        pe, u, eps = qtrain_noise(B, nz)
+        orig = torch.randn, torch.rand, torch.randn_like
+        torch.randn = lambda *a, **k: torch.from_numpy(pe.copy())
+        torch.rand = lambda *a, **k: torch.from_numpy(u.copy())
+        torch.randn_like = lambda t, **k: torch.from_numpy(eps.copy())
+        try:
+            Q.zero_grad()
+            loss = Q.calculate_loss(x=x, z=z, mask=mask)
+            loss.mean().backward()
+        finally:
+            torch.randn, torch.rand, torch.randn_like = orig
+        rec = {"loss": loss.detach().numpy()}
+        params = []
+        for k, (pname, p) in enumerate(Q.named_parameters()):
+            if p.grad is None:
+                continue
+            g = p.grad.detach().numpy().reshape(-1)
+            st = max(1, g.size // 512)
+            rec["grad%d_sub" % len(params)] = g[::st].copy()
+            rec["grad%d_norm" % len(params)] = np.float64(np.linalg.norm(g.astype(np.float64)))
+            params.append([pname, st, list(p.shape)])
+        meta = dict(kind="Qtrain", q=name, params=params)
+        out[name + "_qtrain"] = (rec, meta)
+    return out
+
+
 def capture_q(dn, torch):
     out = {}
     for name, (ds, nc, nz, nif, nxemb, ntemb, H, B, var_type, n_int) in Q_CONFIGS.items():
@@ -347,6 +401,8 @@ def main():
     torch.set_num_threads(8)
     dn, mc = import_reference()
     capture_checkpoint(dn, torch)
+    for name, (rec, meta) in capture_qtrain(dn, torch).items():
+        np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
     for name, (rec, meta) in capture_gtrain(dn, torch).items():
         np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
     if "--gtrain-only" in sys.argv:

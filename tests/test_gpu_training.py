@@ -97,3 +97,67 @@ def test_generator_forward_no_grad_is_hip(gpu_device):
         out = G.to(gpu_device)(z.to(gpu_device).reshape(5, 100, 1, 1))
     assert not out.requires_grad
     assert rel_l2(out.cpu().numpy(), ref.numpy()) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------ Q update
+@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"])
+def test_q_update_matches_reference(gpu_device, name):
+    """The Q update's loss and gradients (train_gen_recon.py:211-217) with the denoiser forward/backward on
+    libdamc (damc_denoiser_train_*), the encoder / prior_emb / noising on PyTorch, vs the reference's autograd
+    on the same injected noise and a mixed mask.  Tolerance as for the G update."""
+    from conftest import qtrain_run
+
+    loss, grads, rec, meta = qtrain_run(name, gpu_device)
+    assert rel_l2(loss, rec["loss"]) < 1e-5
+    worst = gtrain_check(grads, rec, meta, TOL)
+    print("%s worst rel err vs reference %.2e" % (name, worst))
+
+
+def test_denoiser_train_vs_autograd_b128(gpu_device):
+    """Bench-size Q update (B=128, nz=128, nxemb=1024, ntemb=128, nf=4): HIP denoiser forward/backward vs
+    PyTorch autograd of the same module on the same device, all outputs and every parameter gradient."""
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    B = 128
+    p = synth.load_into(dn.Diffusion_UnetA(nz=128, nxemb=1024, ntemb=128, residual=True, nf=4), 3).to(gpu_device)
+    zt = torch.from_numpy(synth.normal_f32(5, 0, (B, 128))).to(gpu_device)
+    logsnr = torch.from_numpy(synth.uniform_f32(5, 1, (B,), -5.0, 9.0)).to(gpu_device)
+    xe = torch.from_numpy(synth.normal_f32(5, 2, (B, 1024))).to(gpu_device)
+    w = torch.from_numpy(synth.normal_f32(5, 3, (B, 128))).to(gpu_device)
+
+    def run(hip):
+        p.zero_grad()
+        x = xe.clone().requires_grad_(True)
+        if hip:
+            out = p(zt, logsnr.clone(), x)
+        else:
+            t_in = torch.arctan(torch.exp(-0.5 * torch.clamp(logsnr, -20.0, 20.0))) / (0.5 * np.pi)
+            out = _stock_denoiser(p, zt, t_in, x)
+        (out * w).sum().backward()
+        return out.detach(), x.grad.detach(), [q.grad.detach().clone() for q in p.parameters()]
+
+    o1, gx1, g1 = run(True)
+    o0, gx0, g0 = run(False)
+    assert rel_l2(o1.cpu().numpy(), o0.cpu().numpy()) < 1e-5
+    assert rel_l2(gx1.cpu().numpy(), gx0.cpu().numpy()) < 2e-5
+    for k, (a, b) in enumerate(zip(g1, g0)):
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) < 2e-5, k
+    assert training._DenoiserTrainFn is not None
+
+
+def _stock_denoiser(p, z, t_in, xemb):
+    """Diffusion_UnetA.forward's stock-PyTorch body (the drop-in's non-ROCm branch), for autograd."""
+    import torch.nn.functional as F
+
+    temb = p.time_mlp(t_in)
+    ctx = torch.cat([temb, xemb], dim=1)
+    skips, out = [], p.input_emb(z)
+    for layer in p.in_layers:
+        out = layer(ctx=ctx, x=out)
+        skips.append(out)
+        out = F.leaky_relu(out, negative_slope=0.01)
+    out = p.mid_layers[0](ctx=ctx, x=out)
+    for layer in p.out_layers:
+        out = layer(ctx=ctx, x=F.leaky_relu(torch.cat([out, skips.pop()], dim=1), negative_slope=0.01))
+    return z + out if p.residual else out

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from conftest import (G_NAMES, Q_END_TOL, Q_NAMES, build_g_case, build_q_case, gtrain_check, gtrain_inputs,
-                      load_golden, rel_l2)
+                      load_golden, qtrain_run, rel_l2)
 from oracle import damc_oracle as orc
 
 torch.set_num_threads(8)
@@ -169,3 +169,11 @@ def test_reference_checkpoint_loads():
         assert rel_l2(orc.generator_sample(orc.generator_layers(G), z).numpy(), d["gen_x"]) < 1e-6
         assert rel_l2(E(z).numpy(), d["ebm_e"]) < 1e-6
         assert rel_l2(orc.encoder_forward(Q.encoder, x).numpy(), d["xemb"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"])
+def test_q_update_loss_and_grads_cpu(name):
+    """Q update (train_gen_recon.py:211-217) of the drop-in Q on CPU (stock ops) vs the reference's autograd."""
+    loss, grads, rec, meta = qtrain_run(name, "cpu")
+    assert rel_l2(loss, rec["loss"]) < 1e-6
+    gtrain_check(grads, rec, meta, 1e-5)
