@@ -205,6 +205,40 @@ def g_update_bench(device, with_torch=True):
     return out
 
 
+def q_update_bench(device, with_torch=True):
+    """SURVEY.md §8(f) row 2, one Q update (train_gen_recon.py:211-220; 6 per iteration) at the bench config
+    (Q: nif 64, nxemb 1024, ntemb 128, B=128): Q.calculate_loss(x, z, mask).mean().backward() + clip + AdamW,
+    the denoiser's forward/backward on libdamc (drop-in), and the same on the stock PyTorch modules."""
+    import torch.optim as optim
+
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    Q = dn._netQ_U(nc=3, nz=NZ, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=100,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                   dataset="cifar10")
+    synth.load_into(Q, 20)
+    Q.to(device).train()
+    opt = optim.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
+    x = torch.from_numpy(synth.uniform_f32(51, 0, (B, 3, 32, 32))).to(device)
+    z = torch.from_numpy(synth.normal_f32(52, 0, (B, NZ))).to(device)
+    mask = (torch.from_numpy(synth.uniform_f32(53, 0, (B, 1), 0.0, 1.0)) >= 0.2).float().to(device)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
+        torch.nn.utils.clip_grad_norm_(Q.parameters(), max_norm=100)
+        opt.step()
+
+    out = {"config": "cifar10 Q update B=128 (nif 64, nxemb 1024, ntemb 128): loss fwd+bwd, clip, AdamW",
+           "hip_ms": round(event_ms(step), 3)}
+    if with_torch:
+        with training.stock_pytorch():
+            out["torch_ms"] = round(event_ms(step), 3)
+        out["speedup_vs_torch"] = round(out["torch_ms"] / out["hip_ms"], 2)
+    return out
+
+
 def traffic_from_profiles(kernel_class):
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
@@ -223,7 +257,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extras", action="store_true", help="skip the per-leg, amortizer and G-update timings")
-    ap.add_argument("--no-torch-g", action="store_true", help="skip the stock-PyTorch G-update comparison")
+    ap.add_argument("--no-torch-g", action="store_true", help="skip the stock-PyTorch G/Q-update comparisons")
     ap.add_argument("--no-live-prof", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--exact-fp32", action="store_true",
                     help="run the generator convolutions on the fp32-MFMA engine instead of the limb engine")
@@ -303,6 +337,7 @@ def main():
         extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
         extras["amortizer"] = amortizer_bench(device)
         extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
+        extras["q_update"] = q_update_bench(device, with_torch=not args.no_torch_g)
 
     t_max = elapsed
     if dist:
@@ -368,9 +403,10 @@ def main():
             "cpu_baseline": None,
         }
         if extras:
-            out["langevin_legs"] = {k: v for k, v in extras.items() if k not in ("amortizer", "g_update")}
+            out["langevin_legs"] = {k: v for k, v in extras.items() if k not in ("amortizer", "g_update", "q_update")}
             out["amortizer"] = extras["amortizer"]
             out["g_update"] = extras["g_update"]
+            out["q_update"] = extras["q_update"]
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_budget)
             out["cpu_baseline"] = cb

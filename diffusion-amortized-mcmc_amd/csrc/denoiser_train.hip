@@ -281,22 +281,55 @@ __global__ void dz_kernel(const float* __restrict__ g, const float* __restrict__
 
 inline dim3 grid1(long n) { return dim3((unsigned)((n + 255) / 256)); }
 
+// sum of S split-K slabs [S][M][N] (+ bias[n]) into C (row stride ldc), fixed order
+__global__ void slab_bias_sum_kernel(const float* __restrict__ slabs, int S, int M, int N,
+                                     const float* __restrict__ bias, float* __restrict__ C, long ldc) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (long)m * N);
+  float acc = 0.f;
+  for (int z = 0; z < S; ++z) acc += slabs[(long)z * M * N + i];
+  if (bias) acc += bias[n];
+  C[(long)m * ldc + n] = acc;
+}
+
+// C (M x N, row stride ldc) = A (M x K, lda) . B (K x N row-major, ldb) (+ bias).  A (B x din) activation
+// times a weight has M = B <= 256 rows: 1-4 output tiles of the engine, so those GEMMs split K over
+// workgroups (>= 2 K tiles each) into slab[S][M][N] and a fixed-order sum adds the slices and the bias.
+constexpr int kMaxSplit = 16;
 int gemm(const float* A, long lda, const float* Bm, long ldb, const float* bias, float* C, long ldc, int M, int N,
-         int K, const char* name, hipStream_t s) {
+         int K, const char* name, hipStream_t s, float* slab = nullptr) {
   GemmArgs a;
   a.A = A;
   a.lda = lda;
   a.B = Bm;
   a.ldb = ldb;
-  a.C = C;
-  a.ldc = ldc;
   a.M = M;
   a.N = N;
   a.K = K;
+  a.act = DAMC_ACT_NONE;
+  const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const int kt = (K + 31) / 32;
+  int S = 1;
+  if (slab && tiles < 64 && kt >= 4) S = std::min(kMaxSplit, std::max(1, std::min<int>(kt / 2, (int)(128 / tiles))));
+  if (S > 1) {
+    const int kper = (kt + S - 1) / S * 32;
+    S = (K + kper - 1) / kper;
+    a.C = slab;
+    a.ldc = N;
+    a.c_zstride = (long)M * N;
+    a.k_per_z = kper;
+    int rc = launch_gemm(a, A_DENSE, EPI_STORE, O_DENSE, S, name, 2.0 * M * N * K, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(slab_bias_sum_kernel, dim3((unsigned)(((long)M * N + 255) / 256)), dim3(256), 0, s,
+                       (const float*)slab, S, M, N, bias, C, ldc);
+    return (int)hipGetLastError();
+  }
+  a.C = C;
+  a.ldc = ldc;
   a.k_per_z = K;
   a.bias = bias;
   a.bias_mod = N;
-  a.act = DAMC_ACT_NONE;
   return launch_gemm(a, A_DENSE, EPI_BIAS_ACT, O_DENSE, 1, name, 2.0 * M * N * K, s);
 }
 
@@ -309,7 +342,7 @@ struct DW {
   float *se_in, *a1, *s1, *emb, *semb, *u, *c, *v, *zT, *X[7], *LS[7], *BG[7], *R[7];
   // backward
   float *D, *T, *dX, *dR[7], *dc, *du, *duT, *dsemb, *dtemb, *dtembT, *ds1, *da1, *da1T, *dv, *dzp;
-  float *gWLS[7], *gWBG[7], *gbD[7], *gWC, *gbC, *tmp;
+  float *gWLS[7], *gWBG[7], *gbD[7], *gWC, *gbC, *tmp, *slab;
   int off[8];
   int maxd, maxin;
 };
@@ -406,6 +439,10 @@ size_t carve(const damc_denoiser_train_t* d, int B, char* base, DW* w) {
   size_t tmpf = std::max(colsum_tmp_floats(B, 3 * t.maxd), colsum_tmp_floats(B, Dt));
   tmpf = std::max(tmpf, colsum_tmp_floats(B, T));
   t.tmp = take((long)tmpf);
+  {  // split-K slabs of the (B x N) GEMMs: N <= max(2 dout, din, sum dout, ntemb + nxemb)
+    const long nmax = std::max<long>(std::max(2L * t.maxd, (long)t.maxin), std::max<long>(Dt, E));
+    t.slab = take((long)kMaxSplit * B * nmax);
+  }
   if (w) *w = t;
   return off;
 }
@@ -459,25 +496,25 @@ int forward(const damc_denoiser_train_t* d, const float* zt, const float* se, co
   }
   // time MLP: temb = Lt2(silu(Lt1(se))) written into emb[:, :T] (se kept for dWt1)
   DAMC_CHECK(hipMemcpyAsync(w.se_in, se, sizeof(float) * B * T, hipMemcpyDeviceToDevice, s));
-  RC(gemm(w.se_in, T, w.T1_T, T, d->tb1, w.a1, T, B, T, T, "dn_gemm", s));
+  RC(gemm(w.se_in, T, w.T1_T, T, d->tb1, w.a1, T, B, T, T, "dn_gemm", s, w.slab));
   hipLaunchKernelGGL(silu_copy_kernel, grid1((long)B * T), dim3(256), 0, s, w.a1, (long)B * T, w.s1);
-  RC(gemm(w.s1, T, w.T2_T, T, d->tb2, w.emb, E, B, T, T, "dn_gemm", s));
+  RC(gemm(w.s1, T, w.T2_T, T, d->tb2, w.emb, E, B, T, T, "dn_gemm", s, w.slab));
   hipLaunchKernelGGL(emb_finish_kernel, grid1((long)B * E), dim3(256), 0, s, w.emb, xemb, B, T, X, w.semb);
   // the 7 ctx Linears in one GEMM, then c_b = silu
-  RC(gemm(w.semb, E, w.WC_T, Dt, w.bC, w.u, Dt, B, Dt, E, "dn_gemm", s));
+  RC(gemm(w.semb, E, w.WC_T, Dt, w.bC, w.u, Dt, B, Dt, E, "dn_gemm", s, w.slab));
   BlockOff bo;
   for (int b = 0; b < 8; ++b) bo.off[b] = w.off[b];
   hipLaunchKernelGGL(ctx_silu_kernel, grid1((long)B * Dt), dim3(256), 0, s, w.u, B, bo, w.c);
   // input embedding
-  RC(gemm(zt, nz, d->bmat, h, nullptr, w.v, h, B, h, nz, "dn_gemm", s));
+  RC(gemm(zt, nz, d->bmat, h, nullptr, w.v, h, B, h, nz, "dn_gemm", s, w.slab));
   hipLaunchKernelGGL(input_emb_kernel, grid1((long)B * (2 * h + nz)), dim3(256), 0, s, w.v, zt, B, nz, w.X[0], w.zT);
   // blocks; skip inputs: out0 <- in2, out1 <- in1, out2 <- in0
   const int hs_of[7] = {-1, -1, -1, 2, 1, 0, -1};
   for (int b = 0; b < 7; ++b) {
     const int di = d->blocks[b].din, dd = d->blocks[b].dout;
     const float* cb = w.c + (long)B * w.off[b];
-    RC(gemm(w.X[b], di, w.WLS_T[b], 2 * dd, w.bLS[b], w.LS[b], 2 * dd, B, 2 * dd, di, "dn_gemm", s));
-    RC(gemm(cb, dd, w.WBG_T[b], 2 * dd, w.bBG[b], w.BG[b], 2 * dd, B, 2 * dd, dd, "dn_gemm", s));
+    RC(gemm(w.X[b], di, w.WLS_T[b], 2 * dd, w.bLS[b], w.LS[b], 2 * dd, B, 2 * dd, di, "dn_gemm", s, w.slab));
+    RC(gemm(cb, dd, w.WBG_T[b], 2 * dd, w.bBG[b], w.BG[b], 2 * dd, B, 2 * dd, dd, "dn_gemm", s, w.slab));
     const bool last = b == 6;
     const float* hs = (!last && hs_of[b] >= 0) ? w.R[hs_of[b]] : nullptr;
     hipLaunchKernelGGL(csq_combine_kernel, grid1((long)B * dd), dim3(256), 0, s, w.LS[b], w.BG[b], B, dd, w.R[b],
@@ -498,8 +535,8 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
     const float* dR = b == 6 ? g : w.dR[b];
     const float* cb = w.c + (long)B * w.off[b];
     hipLaunchKernelGGL(csq_bwd_kernel, grid1((long)B * dd), dim3(256), 0, s, dR, w.LS[b], w.BG[b], B, dd, w.D, w.T);
-    RC(gemm(w.D, 3 * dd, w.WLS[b], di, nullptr, w.dX, di, B, di, 2 * dd, "dn_gemm", s));
-    RC(gemm(w.D + dd, 3 * dd, w.WBG[b], dd, nullptr, w.dc + w.off[b], Dt, B, dd, 2 * dd, "dn_gemm", s));
+    RC(gemm(w.D, 3 * dd, w.WLS[b], di, nullptr, w.dX, di, B, di, 2 * dd, "dn_gemm", s, w.slab));
+    RC(gemm(w.D + dd, 3 * dd, w.WBG[b], dd, nullptr, w.dc + w.off[b], Dt, B, dd, 2 * dd, "dn_gemm", s, w.slab));
     RC(gemm(w.T, B, w.X[b], di, nullptr, w.gWLS[b], di, 2 * dd, di, B, "dn_gemm", s));
     RC(gemm(w.T + (long)dd * B, B, cb, dd, nullptr, w.gWBG[b], dd, 2 * dd, dd, B, "dn_gemm", s));
     RC(launch_colsum(w.D, B, 3 * dd, 3 * dd, w.gbD[b], w.tmp, s));
@@ -517,13 +554,13 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
   hipLaunchKernelGGL(input_emb_bwd_kernel, grid1((long)B * h), dim3(256), 0, s, w.dX, w.v, B, nz, w.dv);
   if (gr->bmat) RC(gemm(w.zT, B, w.dv, h, nullptr, gr->bmat, h, nz, h, B, "dn_gemm", s));
   if (dzt) {
-    RC(gemm(w.dv, h, w.BmT, nz, nullptr, w.dzp, nz, B, nz, h, "dn_gemm", s));
+    RC(gemm(w.dv, h, w.BmT, nz, nullptr, w.dzp, nz, B, nz, h, "dn_gemm", s, w.slab));
     hipLaunchKernelGGL(dz_kernel, grid1((long)B * nz), dim3(256), 0, s, d->residual ? g : nullptr, w.dX, w.dzp, B,
                        nz, dzt);
   }
   // ctx: du = dc * silu'(u); dsemb = du Wc; dWc = du^T semb; dbc = colsum(du)
   hipLaunchKernelGGL(dsilu_t_kernel, grid1((long)B * Dt), dim3(256), 0, s, w.dc, w.u, B, Dt, w.du, w.duT);
-  RC(gemm(w.du, Dt, w.WC, E, nullptr, w.dsemb, E, B, E, Dt, "dn_gemm", s));
+  RC(gemm(w.du, Dt, w.WC, E, nullptr, w.dsemb, E, B, E, Dt, "dn_gemm", s, w.slab));
   RC(gemm(w.duT, B, w.semb, E, nullptr, w.gWC, E, Dt, E, B, "dn_gemm", s));
   RC(launch_colsum(w.du, B, Dt, Dt, w.gbC, w.tmp, s));
   hipLaunchKernelGGL(emb_bwd_kernel, grid1((long)B * E), dim3(256), 0, s, w.dsemb, w.emb, B, T, X, w.dtemb, w.dtembT,
@@ -532,7 +569,7 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
   if (gr->tw2) RC(gemm(w.dtembT, B, w.s1, T, nullptr, gr->tw2, T, T, T, B, "dn_gemm", s));
   if (gr->tb2) RC(launch_colsum(w.dtemb, B, T, T, gr->tb2, w.tmp, s));
   if (gr->tw1 || gr->tb1) {
-    RC(gemm(w.dtemb, T, d->tw2, T, nullptr, w.ds1, T, B, T, T, "dn_gemm", s));
+    RC(gemm(w.dtemb, T, d->tw2, T, nullptr, w.ds1, T, B, T, T, "dn_gemm", s, w.slab));
     hipLaunchKernelGGL(dsilu_t_kernel, grid1((long)B * T), dim3(256), 0, s, w.ds1, w.a1, B, T, w.da1, w.da1T);
     // dWt1 = da1^T se (se as kept by the forward)
     if (gr->tw1) RC(gemm(w.da1T, B, w.se_in, T, nullptr, gr->tw1, T, T, T, B, "dn_gemm", s));

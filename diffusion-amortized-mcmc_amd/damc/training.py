@@ -15,6 +15,7 @@ the k4 s2 p1 / first-layer weight gradients on the limb engine).  The loss, ``cl
 optimiser stay the caller's PyTorch code, unchanged.  Without grad (``torch.no_grad()``, or nothing
 requiring grad) it is the plain HIP forward.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -22,6 +23,20 @@ import torch
 from . import _lib
 from ._lib import check, ptr
 from .plans import generator_plan
+
+# The drop-in modules route their ROCm training forward/backward here while ENABLED; `stock_pytorch()`
+# turns that off explicitly (benchmark comparisons against the reference's own PyTorch path only).
+ENABLED = True
+
+
+@contextlib.contextmanager
+def stock_pytorch():
+    global ENABLED
+    prev, ENABLED = ENABLED, False
+    try:
+        yield
+    finally:
+        ENABLED = prev
 
 
 def _params_of(plan):

@@ -59,9 +59,10 @@ class _GeneratorBase(nn.Module):
         # (damc.training: dL/dW, dL/db, dL/dz for the G update, train_gen_recon.py:222-231).
         # Spectral-norm generators (use_spc_norm=True, default False) are outside the HIP path.
         if z.is_cuda and not self._spc:
-            from damc.training import generator_apply
+            from damc import training
 
-            return generator_apply(self, z)
+            if training.ENABLED:
+                return training.generator_apply(self, z)
         return self.gen(z.reshape(z.shape[0], self.nz, 1, 1))
 
 
@@ -227,9 +228,10 @@ class Diffusion_UnetA(nn.Module):
         if z.is_cuda and xemb is not None:
             # ROCm: forward + training backward on libdamc (damc.training.denoiser_apply); the sinusoidal
             # time embedding of the per-sample logsnr stays these torch ops, as the reference evaluates it
-            from damc.training import denoiser_apply
+            from damc import training
 
-            return denoiser_apply(self, z, self.time_mlp[0](t_in), xemb)
+            if training.ENABLED:
+                return training.denoiser_apply(self, z, self.time_mlp[0](t_in), xemb)
         temb = self.time_mlp(t_in)
         ctx = temb if xemb is None else torch.cat([temb, xemb], dim=1)
         skips, out = [], self.input_emb(z)

@@ -93,13 +93,21 @@ def gtrain_inputs(name):
 
 
 def gtrain_check(grads, rec, meta, tol):
-    """Compare a list of per-parameter gradients (module order) with the golden subsamples/norms."""
+    """Compare a list of per-parameter gradients (module order) with the golden subsamples/norms.
+
+    Errors are relative to the tensor's own norm, floored at 1e-3 x the largest gradient norm of the net:
+    a gradient that is analytically zero (e.g. the bias of a conv followed by InstanceNorm, whose mean the
+    norm removes) is rounding noise in every implementation and is checked against that floor."""
     worst = 0.0
+    norms = [float(rec["grad%d_norm" % k]) for k in range(len(meta["params"]))]
+    floor = 1e-3 * max(norms)
     for k, (pname, st, shape) in enumerate(meta["params"]):
         g = np.asarray(grads[k], dtype=np.float64).reshape(-1)
         assert list(np.asarray(grads[k]).shape) == shape, (pname, np.asarray(grads[k]).shape, shape)
-        e = rel_l2(g[::st], rec["grad%d_sub" % k])
-        n = abs(np.linalg.norm(g) - float(rec["grad%d_norm" % k])) / max(float(rec["grad%d_norm" % k]), 1e-30)
+        ref = np.asarray(rec["grad%d_sub" % k], dtype=np.float64)
+        den = max(np.linalg.norm(ref), floor * np.sqrt(ref.size / max(g.size, 1)), 1e-30)
+        e = float(np.linalg.norm(g[::st] - ref) / den)
+        n = abs(np.linalg.norm(g) - norms[k]) / max(norms[k], floor, 1e-30)
         worst = max(worst, e, n)
         assert e < tol and n < tol, (pname, e, n)
     return worst
