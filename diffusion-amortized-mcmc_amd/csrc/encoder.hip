@@ -3,6 +3,8 @@
 // Convolutions run on the fp32 MFMA implicit-GEMM engine (gemm.hip); InstanceNorm statistics are
 // per (sample, channel) Welford partials merged with Chan's formula (wave shuffles + LDS), then
 // one fused normalise + affine + LeakyReLU pass in place.
+#include <algorithm>
+
 #include "gemm.h"
 
 namespace {
@@ -116,9 +118,31 @@ __global__ __launch_bounds__(256) void in_apply_kernel(float* y, int B, int HW, 
   }
 }
 
+// pixel splits of the statistics pass: <= 64 pixels per split (the Welford chain of a thread is serial),
+// merged with Chan's formula
 int in_splits(int hw) {
-  int s = hw / 1024;
+  int s = hw / 64;
   return s < 1 ? 1 : (s > 64 ? 64 : s);
+}
+
+// split-K slices for a K-major conv whose output tiles would not fill the chip (the encoder's deeper
+// layers: 64 / 8 tiles at B=128), each slice >= 8 K tiles; 1 = no split
+int conv_split(long M, int N, int K) {
+  const long tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles >= 192 || K < 512) return 1;
+  const long s = std::min<long>((256 + tiles - 1) / tiles, K / 256);
+  return (int)std::max<long>(1, s);
+}
+
+// y[m][n] = sum of the S slabs [S][M][N] + bias[n], fixed order
+__global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restrict__ slabs, int S, long M, int N,
+                                                            const float* __restrict__ bias, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  float acc = 0.f;
+  for (int z = 0; z < S; ++z) acc += slabs[(long)z * M * N + i];
+  if (bias) acc += bias[i % N];
+  y[i] = acc;
 }
 
 }  // namespace
@@ -139,8 +163,19 @@ extern "C" int damc_nchw_to_nhwc(const float* x, int B, int C, int HW, float* y,
   return (int)hipGetLastError();
 }
 
+extern "C" size_t damc_conv2d_workspace_floats(int B, int hin, int win, int cin, int cout, int k, int stride,
+                                               int pad) {
+  if (B <= 0 || cin <= 0 || cout <= 0 || k <= 0 || stride <= 0) return 0;
+  const int hout = (hin + 2 * pad - k) / stride + 1, wout = (win + 2 * pad - k) / stride + 1;
+  if (hout <= 0 || wout <= 0 || !damc::conv_kmajor_ok(cin)) return 0;
+  const long M = (long)B * hout * wout;
+  const int S = conv_split(M, cout, k * k * cin);
+  return S > 1 ? (size_t)S * M * cout : 0;
+}
+
 extern "C" int damc_conv2d_nhwc(const float* x, int B, int hin, int win, int cin, const float* wp, const float* bias,
-                                int cout, int k, int stride, int pad, float* y, void* stream) {
+                                int cout, int k, int stride, int pad, float* y, float* workspace,
+                                size_t workspace_floats, void* stream) {
   if (!x || !wp || !y || B <= 0) return DAMC_ERR_ARG;
   const int hout = (hin + 2 * pad - k) / stride + 1, wout = (win + 2 * pad - k) / stride + 1;
   if (hout <= 0 || wout <= 0) return DAMC_ERR_ARG;
@@ -167,8 +202,24 @@ extern "C" int damc_conv2d_nhwc(const float* x, int B, int hin, int win, int cin
   a.bias = bias;
   a.bias_mod = cout;
   a.act = DAMC_ACT_NONE;
-  return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
-                           2.0 * a.M * (double)cout * a.K, as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  const double flops = 2.0 * a.M * (double)cout * a.K;
+  int S = a.b_kmajor ? conv_split(a.M, cout, a.K) : 1;
+  if (S > 1 && workspace && workspace_floats >= (size_t)S * a.M * cout) {
+    // split K over S slices (multiples of the engine's 32-deep K tile, so no tile straddles a tap)
+    a.k_per_z = (a.K / 32 + S - 1) / S * 32;
+    S = (a.K + a.k_per_z - 1) / a.k_per_z;
+    a.C = workspace;
+    a.c_zstride = (long)a.M * cout;
+    a.bias = nullptr;
+    int rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_STORE, damc::O_DENSE, S, "enc_conv", flops, s);
+    if (rc) return rc;
+    const long n = (long)a.M * cout;
+    hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       (const float*)workspace, S, (long)a.M, cout, bias, y);
+    return (int)hipGetLastError();
+  }
+  return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv", flops, s);
 }
 
 extern "C" size_t damc_instnorm_workspace_floats(int B, int hw, int c) {

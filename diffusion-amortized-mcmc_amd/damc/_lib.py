@@ -113,7 +113,8 @@ _SIGS = {
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_z_update": (_I, [_P, _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P]),
     "damc_philox_normal": (_I, [_P, _I, _I, _I, _U64, _U64, _U64, ctypes.c_uint32, _P]),
-    "damc_conv2d_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "damc_conv2d_workspace_floats": (_SZ, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "damc_conv2d_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "damc_pack_conv2d": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_instnorm_workspace_floats": (_SZ, [_I, _I, _I]),
     "damc_instnorm_lrelu_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P]),

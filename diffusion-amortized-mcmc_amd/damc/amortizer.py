@@ -124,9 +124,11 @@ class EncoderPlan:
             bias = _dev(conv.bias, dev) if conv.bias is not None else None
             Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
             y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
-            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(bias), cout, k, s, p, ptr(y), stream),
-                  "conv2d")
-            keep += [w, wp, bias]
+            nsl = int(L.damc_conv2d_workspace_floats(B, H, W, cin, cout, k, s, p))
+            sl = torch.empty(nsl, dtype=torch.float32, device=dev) if nsl else None
+            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(bias), cout, k, s, p, ptr(y), ptr(sl), nsl,
+                                     stream), "conv2d")
+            keep += [w, wp, bias, sl]
             if norm is not None:
                 nws = int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout))
                 ws = torch.empty(max(nws, 1), dtype=torch.float32, device=dev)

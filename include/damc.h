@@ -155,9 +155,13 @@ int damc_philox_normal(float* out, int n_steps, int batch, int nz, uint64_t seed
                        uint64_t chain_base, uint32_t stream_id, void* stream);
 
 /* ---------------------------------------------------------------- Q amortizer (a8-a11) */
-/* generic fp32 MFMA implicit-GEMM conv (NHWC) + bias: encoder building block */
+/* generic fp32 MFMA implicit-GEMM conv (NHWC) + bias: encoder building block.  workspace (floats, may be
+ * NULL / 0): split-K slabs for convolutions whose output tiles would not fill the chip, sized by
+ * damc_conv2d_workspace_floats (0 = no split for that shape) */
+size_t damc_conv2d_workspace_floats(int batch, int hin, int win, int cin, int cout, int k, int stride, int pad);
 int damc_conv2d_nhwc(const float* x, int batch, int hin, int win, int cin, const float* w_packed, const float* bias,
-                     int cout, int k, int stride, int pad, float* y, void* stream);
+                     int cout, int k, int stride, int pad, float* y, float* workspace, size_t workspace_floats,
+                     void* stream);
 /* pack Conv2d weight (Cout,Cin,k,k) into the engine's layout (same element count; opaque to callers):
  * (Cout, k,k,Cin) for the K-major engine when Cin % 32 == 0, else (k,k,Cin,Cout) */
 int damc_pack_conv2d(const float* w_torch, int cout, int cin, int k, float* w_packed, void* stream);
