@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "gemm.h"
+#include "wgrad.h"
 
 namespace {
 
@@ -237,4 +238,170 @@ extern "C" int damc_instnorm_lrelu_nhwc(float* y, int B, int hw, int c, const fl
   const int P = std::max(1, std::min(64, hw / 256));
   hipLaunchKernelGGL(in_apply_kernel, dim3(B * cg, P), dim3(256), 0, s, y, B, hw, c, S, ws, gamma, beta, eps, slope);
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ training (Q update)
+// InstanceNorm2d(affine) + LeakyReLU for the encoder's training forward/backward: the conv output y is kept,
+// h = lrelu(IN(y)) goes to its own buffer and (mean, rstd) per (sample, channel) are saved.  The backward
+// of a = gamma * (y - mean) * rstd + beta, h = lrelu(a) (biased variance, as InstanceNorm2d):
+//   dA = dh * lrelu'(a);  dy = rstd * gamma * (dA - mean_p(dA) - xhat * mean_p(dA * xhat))
+// with per-(sample, channel) sums over pixels taken in S splits and merged in fixed order.
+namespace {
+
+__global__ __launch_bounds__(256) void in_apply_train_kernel(const float* y, int B, int HW, int C, int S,
+                                                             const float* part, const float* gamma,
+                                                             const float* beta, float eps, float slope, float* h,
+                                                             float* stats) {
+  const int cg = (C + 63) / 64;
+  const int b = blockIdx.x / cg, c = (blockIdx.x % cg) * 64 + (threadIdx.x & 63);
+  const int prow = threadIdx.x >> 6;
+  __shared__ float sc[64], sh[64];
+  if (prow == 0) {
+    float scale = 0.f, shift = 0.f;
+    if (c < C) {
+      const float* pp = part + ((long)b * C + c) * S * 3;
+      Wf a{pp[0], pp[1], pp[2]};
+      for (int s = 1; s < S; ++s) a = wmerge(a, Wf{pp[3 * s], pp[3 * s + 1], pp[3 * s + 2]});
+      const float var = a.m2 / a.n;
+      const float rstd = 1.f / sqrtf(var + eps);
+      scale = rstd * gamma[c];
+      shift = beta[c] - a.mean * scale;
+      if (blockIdx.y == 0) {
+        stats[((long)b * C + c) * 2] = a.mean;
+        stats[((long)b * C + c) * 2 + 1] = rstd;
+      }
+    }
+    sc[threadIdx.x] = scale;
+    sh[threadIdx.x] = shift;
+  }
+  __syncthreads();
+  if (c >= C) return;
+  const float scl = sc[threadIdx.x & 63], shf = sh[threadIdx.x & 63];
+  const int P = gridDim.y;
+  const int p0 = (int)((long)HW * blockIdx.y / P), p1 = (int)((long)HW * (blockIdx.y + 1) / P);
+  for (int p = p0 + prow; p < p1; p += 4) {
+    const long o = ((long)b * HW + p) * C + c;
+    const float v = fmaf(y[o], scl, shf);
+    h[o] = v > 0.f ? v : v * slope;
+  }
+}
+
+// pass 1: per (b, c, split) partial sums {sum dA, sum dA * xhat}
+__global__ __launch_bounds__(256) void in_bwd_sums_kernel(const float* y, const float* stats, const float* dh, int B,
+                                                          int HW, int C, int S, const float* gamma, const float* beta,
+                                                          float slope, float* part) {
+  const int cg = (C + 63) / 64;
+  const int b = blockIdx.x / cg, c = (blockIdx.x % cg) * 64 + (threadIdx.x & 63);
+  const int prow = threadIdx.x >> 6;
+  const int s = blockIdx.y;
+  const int p0 = (int)((long)HW * s / S), p1 = (int)((long)HW * (s + 1) / S);
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    const float mean = stats[((long)b * C + c) * 2], rstd = stats[((long)b * C + c) * 2 + 1];
+    const float scl = rstd * gamma[c], shf = beta[c] - mean * scl;
+    for (int p = p0 + prow; p < p1; p += 4) {
+      const long o = ((long)b * HW + p) * C + c;
+      const float yv = y[o];
+      const float a = fmaf(yv, scl, shf);
+      const float dA = a > 0.f ? dh[o] : dh[o] * slope;
+      s1 += dA;
+      s2 += dA * ((yv - mean) * rstd);
+    }
+  }
+  __shared__ float r1[4][64], r2[4][64];
+  r1[prow][threadIdx.x & 63] = s1;
+  r2[prow][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (prow == 0 && c < C) {
+    const int l = threadIdx.x;
+    float* o = part + (((long)b * C + c) * S + s) * 2;
+    o[0] = ((r1[0][l] + r1[1][l]) + r1[2][l]) + r1[3][l];
+    o[1] = ((r2[0][l] + r2[1][l]) + r2[2][l]) + r2[3][l];
+  }
+}
+
+// pass 2: merge the S partials (fixed order), write dy; totals per (b, c) go to bc (B x C x 2) for dgamma/dbeta
+__global__ __launch_bounds__(256) void in_bwd_apply_kernel(const float* y, const float* stats, const float* dh, int B,
+                                                           int HW, int C, int S, const float* gamma,
+                                                           const float* beta, float slope, const float* part,
+                                                           float* dy, float* bc) {
+  const int cg = (C + 63) / 64;
+  const int b = blockIdx.x / cg, c = (blockIdx.x % cg) * 64 + (threadIdx.x & 63);
+  const int prow = threadIdx.x >> 6;
+  if (c >= C) return;
+  const float* pp = part + ((long)b * C + c) * S * 2;
+  float t1 = 0.f, t2 = 0.f;
+  for (int s = 0; s < S; ++s) {
+    t1 += pp[2 * s];
+    t2 += pp[2 * s + 1];
+  }
+  if (blockIdx.y == 0 && prow == 0) {  // bc [b][2][C]: dgamma rows (sum dA * xhat), then dbeta rows (sum dA)
+    bc[((long)b * 2) * C + c] = t2;
+    bc[((long)b * 2 + 1) * C + c] = t1;
+  }
+  const float mean = stats[((long)b * C + c) * 2], rstd = stats[((long)b * C + c) * 2 + 1];
+  const float g = gamma[c];
+  const float scl = rstd * g, shf = beta[c] - mean * scl;
+  const float m1 = t1 / (float)HW, m2 = t2 / (float)HW;
+  const int P = gridDim.y;
+  const int p0 = (int)((long)HW * blockIdx.y / P), p1 = (int)((long)HW * (blockIdx.y + 1) / P);
+  for (int p = p0 + prow; p < p1; p += 4) {
+    const long o = ((long)b * HW + p) * C + c;
+    const float yv = y[o];
+    const float a = fmaf(yv, scl, shf);
+    const float dA = a > 0.f ? dh[o] : dh[o] * slope;
+    const float xh = (yv - mean) * rstd;
+    dy[o] = scl * (dA - m1 - xh * m2);
+  }
+}
+
+}  // namespace
+
+extern "C" int damc_instnorm_lrelu_train_nhwc(const float* y, int B, int hw, int c, const float* gamma,
+                                              const float* beta, float eps, float slope, float* h, float* stats,
+                                              float* ws, void* stream) {
+  if (!y || !h || !stats || !gamma || !beta || !ws || B <= 0 || hw <= 0 || c <= 0) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  const int S = in_splits(hw);
+  const int cg = (c + 63) / 64;
+  ProfScope ps("instnorm", 0.0, s);
+  hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, y, B, hw, c, S, ws);
+  const int P = std::max(1, std::min(64, hw / 256));
+  hipLaunchKernelGGL(in_apply_train_kernel, dim3(B * cg, P), dim3(256), 0, s, y, B, hw, c, S, ws, gamma, beta, eps,
+                     slope, h, stats);
+  return (int)hipGetLastError();
+}
+
+extern "C" size_t damc_instnorm_bwd_workspace_floats(int B, int hw, int c) {
+  if (B <= 0 || hw <= 0 || c <= 0) return 0;
+  return (size_t)B * c * in_splits(hw) * 2 + (size_t)B * c * 2 + damc::colsum_tmp_floats(B, c);
+}
+
+extern "C" int damc_instnorm_lrelu_backward_nhwc(const float* y, const float* stats, const float* dh, int B, int hw,
+                                                 int c, const float* gamma, const float* beta, float slope, float* dy,
+                                                 float* dgamma, float* dbeta, float* ws, void* stream) {
+  if (!y || !stats || !dh || !dy || !gamma || !beta || !ws || B <= 0 || hw <= 0 || c <= 0) return DAMC_ERR_ARG;
+  hipStream_t s = as_stream(stream);
+  const int S = in_splits(hw);
+  const int cg = (c + 63) / 64;
+  float* part = ws;
+  float* bc = part + (size_t)B * c * S * 2;
+  float* tmp = bc + (size_t)B * c * 2;
+  ProfScope ps("instnorm_bwd", 0.0, s);
+  hipLaunchKernelGGL(in_bwd_sums_kernel, dim3(B * cg, S), dim3(256), 0, s, y, stats, dh, B, hw, c, S, gamma, beta,
+                     slope, part);
+  const int P = std::max(1, std::min(64, hw / 256));
+  hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(B * cg, P), dim3(256), 0, s, y, stats, dh, B, hw, c, S, gamma, beta,
+                     slope, (const float*)part, dy, bc);
+  DAMC_LAUNCH_CHECK();
+  // dgamma = sum_b bc[b][0][c], dbeta = sum_b bc[b][1][c]: fixed-order column sums over the B rows
+  if (dgamma) {
+    int rc = damc::launch_colsum(bc, B, c, 2L * c, dgamma, tmp, s);
+    if (rc) return rc;
+  }
+  if (dbeta) {
+    int rc = damc::launch_colsum(bc + c, B, c, 2L * c, dbeta, tmp, s);
+    if (rc) return rc;
+  }
+  return 0;
 }

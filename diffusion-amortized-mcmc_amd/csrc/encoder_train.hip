@@ -1,0 +1,293 @@
+// encoder_train.hip — Conv2d backward for the encoder of the Q update ("encoder bwd,
+// reusing the a10 kernels"; Encoder_* workspace/src/diffusion_net.py:227-413, trained by Q.calculate_loss
+// :624-645 six times per iteration, train_gen_recon.py:211-220).  Three shapes cover every encoder:
+//   (A) k4 s2 p1 with H = 2 Ho: the input gradient is a ConvTranspose2d k4 s2 p1 forward with the conv's own
+//       weight read as a transposed-conv weight (in = Cout, out = Cin), so it runs on the generator's
+//       phase-split UP2 path (limb engine when the gathered channel count allows); the weight gradient is
+//       the generator's O_WGRAD GEMM with the roles swapped (layer "input" = dy on the Ho x Wo grid, layer
+//       "output gradient" = x, phase-split) — its reduce writes the (Cout, Cin, 4, 4) layout directly;
+//   (B) the first conv, k3 s1 p1 with Cin <= 4: no input gradient (the image); the weight gradient is the
+//       output layer's direct kernel (wgrad.hip) with dy in the "activation" role and x in the "delta" role;
+//   (C) the last conv, covering its whole input (p0, output 1x1): a dense layer, two fp32 MFMA GEMMs.
+// Biases: fixed-order column sums of dy.
+#include <algorithm>
+
+#include "gemm.h"
+#include "wgrad.h"
+
+namespace {
+
+using namespace damc;
+
+enum { CASE_NONE = 0, CASE_UP = 1, CASE_FIRST = 2, CASE_DENSE = 3 };
+
+int conv_case(int hin, int win, int cin, int cout, int k, int stride, int pad, int* ho_, int* wo_) {
+  const int ho = (hin + 2 * pad - k) / stride + 1, wo = (win + 2 * pad - k) / stride + 1;
+  *ho_ = ho;
+  *wo_ = wo;
+  if (ho <= 0 || wo <= 0) return CASE_NONE;
+  if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho && win == 2 * wo && cin % 8 == 0) return CASE_UP;
+  if (k == 3 && stride == 1 && pad == 1 && cin <= 4) return CASE_FIRST;
+  if (pad == 0 && ho == 1 && wo == 1 && k == hin && k == win) return CASE_DENSE;
+  return CASE_NONE;
+}
+
+// the conv read as ConvTranspose2d k4 s2 p1 (input Cout on Ho x Wo -> output Cin on H x W)
+damc_layer_t up_view(int hin, int win, int cin, int cout, int ho, int wo) {
+  damc_layer_t L{};
+  L.kind = DAMC_LAYER_UP2;
+  L.cin = cout;
+  L.cout = cin;
+  L.k = 4;
+  L.stride = 2;
+  L.pad = 1;
+  L.hin = ho;
+  L.win = wo;
+  L.hout = hin;
+  L.wout = win;
+  L.act = DAMC_ACT_NONE;
+  return L;
+}
+
+// limb-engine capability of the transposed view's forward (gemm.hip launch_gemm_x3 constraints)
+bool up_x3(int cin, int cout) { return cout % KM_BK == 0 && cin % 8 == 0; }
+
+int up_split(int ho, int wo, int cin, int cout, int Bp, int* S, int* kper) {
+  const long M = 4L * cout, N = cin, K = (long)ho * wo * Bp;
+  const long base = ((M + 255) / 256) * ((N + 127) / 128) * 4;
+  const long nkt = K / 32;
+  const long sl = std::max(1L, std::min((512 + base - 1) / base, nkt));
+  const long kp = (nkt + sl - 1) / sl * 32;
+  *kper = (int)kp;
+  *S = (int)((K + kp - 1) / kp);
+  return 0;
+}
+
+// (co, (ky,kx,ci)) -> PyTorch (co, ci, ky, kx)
+__global__ void permute_dense_kernel(const float* __restrict__ g, int cout, int cin, int k, float* __restrict__ dw) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)cout * cin * k * k;
+  if (i >= n) return;
+  long t = i;
+  const int kx = (int)(t % k);
+  t /= k;
+  const int ky = (int)(t % k);
+  t /= k;
+  const int ci = (int)(t % cin);
+  const int co = (int)(t / cin);
+  dw[i] = g[(long)co * k * k * cin + ((long)ky * k + kx) * cin + ci];
+}
+
+// (n, c) -> (c, n)
+__global__ void transpose_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)R * C) return;
+  const int r = (int)(i / C), c = (int)(i - (long)r * C);
+  y[(long)c * R + r] = x[i];
+}
+
+struct Carve {
+  char* base;
+  size_t off = 0;
+  explicit Carve(char* b) : base(b) {}
+  template <class T>
+  T* take(size_t n) {
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += (n * sizeof(T) + 255) / 256 * 256;
+    return p;
+  }
+};
+
+struct Bufs {
+  float *wf = nullptr, *wb = nullptr, *tmp = nullptr, *slab = nullptr, *g = nullptr, *dyT = nullptr, *wk = nullptr;
+  unsigned short *dy3 = nullptr, *tin = nullptr, *tdl = nullptr;
+  float* part = nullptr;
+};
+
+size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int pad, char* base, Bufs* b, int* cs) {
+  int ho, wo;
+  const int c = conv_case(hin, win, cin, cout, k, stride, pad, &ho, &wo);
+  *cs = c;
+  Carve cv(base);
+  Bufs t;
+  const long M = (long)B * ho * wo;
+  t.tmp = cv.take<float>(std::max<size_t>(colsum_tmp_floats(M, cout), 1));
+  if (c == CASE_UP) {
+    const int Bp = (B + 31) / 32 * 32;
+    const long P = (long)ho * wo;
+    const size_t n = (size_t)cin * cout * 16;
+    t.wf = cv.take<float>(n + n * 3 / 2);  // fp32 packing + its x3 copy (damc_pack_generator_layer layout)
+    t.wb = cv.take<float>(n + n * 3 / 2);
+    t.dy3 = cv.take<unsigned short>((size_t)M * cout * 3);
+    t.tin = cv.take<unsigned short>((size_t)cout * P * Bp * 3);
+    t.tdl = cv.take<unsigned short>((size_t)4 * cin * P * Bp * 3);
+    int S, kp;
+    up_split(ho, wo, cin, cout, Bp, &S, &kp);
+    t.slab = cv.take<float>((size_t)4 * S * 4 * cout * cin);
+  } else if (c == CASE_FIRST) {
+    damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
+    L.kind = DAMC_LAYER_SMALLC;
+    L.cin = cout;
+    L.cout = cin;
+    L.k = 3;
+    L.stride = 1;
+    L.pad = 1;
+    t.part = cv.take<float>(smallc_wgrad_part_floats(L, B));
+    t.tmp = cv.take<float>(std::max(smallc_wgrad_tmp_floats(L, B), colsum_tmp_floats(M, cout)));
+  } else if (c == CASE_DENSE) {
+    const long KK = (long)k * k * cin;
+    t.dyT = cv.take<float>((size_t)cout * B);
+    t.g = cv.take<float>((size_t)cout * KK);
+    t.wk = cv.take<float>((size_t)cout * KK);
+  }
+  if (b) *b = t;
+  return c == CASE_NONE ? 0 : cv.off;
+}
+
+}  // namespace
+
+extern "C" size_t damc_conv2d_backward_workspace_bytes(int B, int hin, int win, int cin, int cout, int k, int stride,
+                                                       int pad) {
+  if (B <= 0 || hin <= 0 || win <= 0 || cin <= 0 || cout <= 0 || k <= 0 || stride <= 0) return 0;
+  int cs;
+  return carve(B, hin, win, cin, cout, k, stride, pad, nullptr, nullptr, &cs);
+}
+
+// x NHWC (B, hin, win, cin), dy NHWC (B, ho, wo, cout), w PyTorch (cout, cin, k, k) -> dx NHWC (optional),
+// dw (cout, cin, k, k), db (cout) (optional)
+extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const float* w, int B, int hin, int win,
+                                         int cin, int cout, int k, int stride, int pad, float* dx, float* dw,
+                                         float* db, void* wsp, size_t wsb, void* stream) {
+  if (!x || !dy || !w || !dw || B <= 0) return DAMC_ERR_ARG;
+  int cs;
+  const size_t need = carve(B, hin, win, cin, cout, k, stride, pad, nullptr, nullptr, &cs);
+  if (cs == CASE_NONE) return DAMC_ERR_UNSUPPORTED;
+  if (!wsp || wsb < need) return DAMC_ERR_WORKSPACE;
+  Bufs t;
+  carve(B, hin, win, cin, cout, k, stride, pad, reinterpret_cast<char*>(wsp), &t, &cs);
+  hipStream_t s = as_stream(stream);
+  const int ho = (hin + 2 * pad - k) / stride + 1, wo = (win + 2 * pad - k) / stride + 1;
+  const long M = (long)B * ho * wo;
+  int rc;
+  if (db && (rc = launch_colsum(dy, M, cout, cout, db, t.tmp, s))) return rc;
+  if (cs == CASE_FIRST) {
+    if (dx) return DAMC_ERR_UNSUPPORTED;  // the image needs no gradient
+    damc_layer_t L{};
+    L.kind = DAMC_LAYER_SMALLC;
+    L.cin = cout;  // dy plays the activation (channels across threads) ...
+    L.cout = cin;  // ... and x the small-channel "delta" window
+    L.k = 3;
+    L.stride = 1;
+    L.pad = 1;
+    L.hin = ho;
+    L.win = wo;
+    L.hout = hin;
+    L.wout = win;
+    return launch_smallc_wgrad(L, dy, x, B, t.part, t.tmp, dw, s);
+  }
+  if (cs == CASE_DENSE) {
+    const int KK = k * k * cin;
+    // dW = dy^T X (X = the NHWC input as (B, k*k*cin), (ky,kx,ci) order), then permuted to (co, ci, ky, kx)
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)(((long)B * cout + 255) / 256)), dim3(256), 0, s, dy, B, cout,
+                       t.dyT);
+    GemmArgs a;
+    a.A = t.dyT;
+    a.lda = B;
+    a.B = x;
+    a.ldb = KK;
+    a.C = t.g;
+    a.ldc = KK;
+    a.M = cout;
+    a.N = KK;
+    a.K = B;
+    a.k_per_z = B;
+    if ((rc = launch_gemm(a, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_wgrad", 2.0 * cout * KK * B, s))) return rc;
+    const long n = (long)cout * KK;
+    hipLaunchKernelGGL(permute_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)t.g,
+                       cout, cin, k, dw);
+    if (dx) {  // dX = dy W, W as (co, (ky,kx,ci)) = the K-major conv packing
+      if ((rc = damc_pack_conv2d(w, cout, cin, k, t.wk, stream))) return rc;
+      if (!conv_kmajor_ok(cin)) return DAMC_ERR_UNSUPPORTED;  // damc_pack_conv2d chose the other layout
+      GemmArgs d;
+      d.A = dy;
+      d.lda = cout;
+      d.B = t.wk;
+      d.ldb = KK;
+      d.C = dx;
+      d.ldc = KK;
+      d.M = B;
+      d.N = KK;
+      d.K = cout;
+      d.k_per_z = cout;
+      if ((rc = launch_gemm(d, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_dgrad", 2.0 * B * KK * cout, s))) return rc;
+    }
+    return (int)hipGetLastError();
+  }
+  // CASE_UP
+  const int Bp = (B + 31) / 32 * 32;
+  const long P = (long)ho * wo;
+  damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
+  // weight gradient: O_WGRAD with the transposed view's roles (input = dy, output gradient = x)
+  if ((rc = launch_transpose_x3(dy, nullptr, B, ho, wo, cout, ho, wo, 1, 1, 0, 0, Bp, t.tin, nullptr, s))) return rc;
+  for (int ph = 0; ph < 4; ++ph) {
+    rc = launch_transpose_x3(x, nullptr, B, hin, win, cin, ho, wo, 2, 2, ph >> 1, ph & 1, Bp,
+                             t.tdl + (size_t)ph * cin * P * Bp * 3, nullptr, s);
+    if (rc) return rc;
+  }
+  {
+    int S, kp;
+    up_split(ho, wo, cin, cout, Bp, &S, &kp);
+    GemmArgs a;
+    a.A3 = t.tin;
+    a.B3 = t.tdl;
+    a.Cg = cout;
+    a.Hin = ho;
+    a.Win = wo;
+    a.K = (int)(P * Bp);
+    a.wg_bp = Bp;
+    a.kw = 2;
+    a.wg_phases = 4;
+    a.M = 4 * cout;
+    a.N = cin;
+    a.ldc = cin;
+    a.c_zstride = (long)a.M * a.N;
+    a.b_zstride = (long)cin * a.K;
+    a.k_per_z = kp;
+    a.C = t.slab;
+    if ((rc = launch_wgrad_x3(a, S, "enc_wgrad", 2.0 * M * cout * cin * 16, s))) return rc;
+    if ((rc = launch_up2_wgrad_reduce(t.slab, S, cout, cin, dw, s))) return rc;
+  }
+  if (!dx) return 0;
+  // input gradient: the transposed view's forward (phase-split implicit GEMM) over dy
+  L.w_fwd = t.wf;
+  L.w_bwd = t.wb;
+  if ((rc = damc_pack_generator_layer(&L, w, t.wf, t.wb, stream))) return rc;
+  const size_t n = (size_t)cin * cout * 16;
+  GemmArgs a;
+  a.A = dy;
+  a.Hin = ho;
+  a.Win = wo;
+  a.Cg = cout;
+  a.Hq = ho;
+  a.Wq = wo;
+  a.kw = 2;
+  a.stride = 1;
+  a.B = t.wf;
+  a.b_kmajor = conv_kmajor_ok(cout);
+  a.ldb = a.b_kmajor ? 4L * cout : cin;
+  a.b_zstride = 4L * cout * cin;
+  a.C = dx;
+  a.ldc = cin;
+  a.M = (int)M;
+  a.N = cin;
+  a.K = 4 * cout;
+  a.Hout = hin;
+  a.Wout = win;
+  a.act = DAMC_ACT_NONE;
+  if (up_x3(cin, cout)) {
+    if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
+    a.A3 = t.dy3;
+    a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
+  }
+  return launch_gemm(a, A_CONV, EPI_BIAS_ACT, O_PHASE, 4, "enc_dgrad", 2.0 * M * cout * cin * 16, s);
+}

@@ -117,6 +117,11 @@ _SIGS = {
     "damc_conv2d_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "damc_pack_conv2d": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_instnorm_workspace_floats": (_SZ, [_I, _I, _I]),
+    "damc_instnorm_lrelu_train_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P]),
+    "damc_instnorm_bwd_workspace_floats": (_SZ, [_I, _I, _I]),
+    "damc_instnorm_lrelu_backward_nhwc": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P]),
+    "damc_conv2d_backward_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "damc_conv2d_backward_nhwc": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     "damc_instnorm_lrelu_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P]),
     "damc_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),

@@ -206,3 +206,138 @@ def denoiser_apply(p, zt, se, xemb):
     xemb and p's parameters (Diffusion_UnetA.forward, diffusion_net.py:477-533)."""
     params = [t for _, _, t in _denoiser_params(p)]
     return _DenoiserTrainFn.apply(zt, se, xemb, p, *params)
+
+
+# ------------------------------------------------------------------------------- Q update: encoder
+# Encoder_* (workspace/src/diffusion_net.py:227-413) as trained by Q.calculate_loss: forward on libdamc
+# keeping every conv output, InstanceNorm statistic and layer input; backward through
+# damc_instnorm_lrelu_backward_nhwc and damc_conv2d_backward_nhwc (the generator's limb-engine kernels with the
+# roles swapped for the k4 s2 p1 convs).  Shapes the C side does not cover keep the stock PyTorch path
+# (encoder_train_supported is False for them; the Q-update tests assert which path ran).
+
+_ENC_SUPPORT = {}
+
+
+def _enc_stages(enc):
+    from .amortizer import EncoderPlan
+
+    return EncoderPlan(enc).stages
+
+
+def _enc_params(stages):
+    out = []
+    for conv, norm, _ in stages:
+        out += [conv.weight, conv.bias]
+        if norm is not None:
+            out += [norm.weight, norm.bias]
+    return out
+
+
+def encoder_train_supported(enc, x):
+    key = (id(enc), tuple(x.shape))
+    hit = _ENC_SUPPORT.get(key)
+    if hit is not None:
+        return hit
+    ok = True
+    try:
+        stages = _enc_stages(enc)
+        B, _, H, W = x.shape
+        L = _lib.lib()
+        for i, (conv, norm, _) in enumerate(stages):
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            if conv.bias is None or (norm is None) != (i == len(stages) - 1):
+                ok = False
+                break
+            if int(L.damc_conv2d_backward_workspace_bytes(B, H, W, conv.in_channels, conv.out_channels, k, s, p)) == 0:
+                ok = False
+                break
+            H, W = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        ok = ok and H == 1 and W == 1
+    except NotImplementedError:
+        ok = False
+    _ENC_SUPPORT[key] = ok
+    return ok
+
+
+class _EncoderTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stages, *params):
+        L = _lib.lib()
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        B, C, H, W = x.shape
+        h = torch.empty(B, H, W, C, dtype=torch.float32, device=dev)
+        check(L.damc_nchw_to_nhwc(ptr(x.detach().float().contiguous()), B, C, H * W, ptr(h), stream), "nchw_to_nhwc")
+        saved = []
+        for conv, norm, slope in stages:
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            cout, cin = conv.out_channels, conv.in_channels
+            wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
+            check(L.damc_pack_conv2d(ptr(conv.weight), cout, cin, k, ptr(wp), stream), "pack conv2d")
+            Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+            y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
+            nsl = int(L.damc_conv2d_workspace_floats(B, H, W, cin, cout, k, s, p))
+            sl = torch.empty(nsl, dtype=torch.float32, device=dev) if nsl else None
+            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(conv.bias), cout, k, s, p, ptr(y), ptr(sl),
+                                     nsl, stream), "conv2d")
+            stats, out = None, y
+            if norm is not None:
+                out = torch.empty_like(y)
+                stats = torch.empty(B * cout * 2, dtype=torch.float32, device=dev)
+                ws = torch.empty(max(int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout)), 1), dtype=torch.float32,
+                                 device=dev)
+                check(L.damc_instnorm_lrelu_train_nhwc(ptr(y), B, Ho * Wo, cout, ptr(norm.weight), ptr(norm.bias),
+                                                       float(norm.eps), float(slope), ptr(out), ptr(stats), ptr(ws),
+                                                       stream), "instnorm train")
+            saved.append((h, y, stats, H, W, Ho, Wo))
+            h, H, W = out, Ho, Wo
+        ctx.stages, ctx.saved, ctx.B = stages, saved, B
+        ctx.save_for_backward(*params)
+        return h.reshape(B, -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        L = _lib.lib()
+        dev = g.device
+        stream = _lib.stream_ptr(dev)
+        B = ctx.B
+        params = ctx.saved_tensors
+        grads = [torch.empty_like(p) if ctx.needs_input_grad[2 + i] else None for i, p in enumerate(params)]
+        # parameter index of each stage's (conv.weight, conv.bias, norm.weight, norm.bias)
+        idx, pos = [], 0
+        for conv, norm, _ in ctx.stages:
+            idx.append(pos)
+            pos += 4 if norm is not None else 2
+        dh = g.to(torch.float32).contiguous()
+        for i in range(len(ctx.stages) - 1, -1, -1):
+            conv, norm, slope = ctx.stages[i]
+            h_in, y, stats, H, W, Ho, Wo = ctx.saved[i]
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            cout, cin = conv.out_channels, conv.in_channels
+            j = idx[i]
+            if norm is not None:
+                dy = torch.empty_like(y)
+                ws = torch.empty(max(int(L.damc_instnorm_bwd_workspace_floats(B, Ho * Wo, cout)), 1),
+                                 dtype=torch.float32, device=dev)
+                check(L.damc_instnorm_lrelu_backward_nhwc(ptr(y), ptr(stats), ptr(dh), B, Ho * Wo, cout,
+                                                          ptr(norm.weight), ptr(norm.bias), float(slope), ptr(dy),
+                                                          ptr(grads[j + 2]), ptr(grads[j + 3]), ptr(ws), stream),
+                      "instnorm backward")
+            else:
+                dy = dh
+            dx = torch.empty(B, H, W, cin, dtype=torch.float32, device=dev) if i > 0 else None
+            nbytes = int(L.damc_conv2d_backward_workspace_bytes(B, H, W, cin, cout, k, s, p))
+            ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+            dw = grads[j] if grads[j] is not None else torch.empty_like(conv.weight)
+            check(L.damc_conv2d_backward_nhwc(ptr(h_in), ptr(dy), ptr(conv.weight), B, H, W, cin, cout, k, s, p,
+                                              ptr(dx), ptr(dw), ptr(grads[j + 1]), ptr(ws), nbytes, stream),
+                  "conv2d backward")
+            dh = dx
+        ctx.saved = None
+        return (None, None, *grads)
+
+
+def encoder_apply(enc, x):
+    """xemb = Encoder_*(x) on the HIP path, differentiable w.r.t. the encoder's parameters (not x)."""
+    stages = _enc_stages(enc)
+    return _EncoderTrainFn.apply(x, stages, *_enc_params(stages))

@@ -144,6 +144,13 @@ class _EncoderBase(nn.Module):
         self.net = nn.Sequential(*mods)
 
     def forward(self, x):
+        # ROCm training forward (grad enabled, x itself not differentiated, as in Q.calculate_loss): libdamc
+        # forward + backward (damc.training.encoder_apply) for the shapes it covers
+        if x.is_cuda and torch.is_grad_enabled() and not x.requires_grad:
+            from damc import training
+
+            if training.ENABLED and training.encoder_train_supported(self, x):
+                return training.encoder_apply(self, x)
         return self.net(x).reshape(x.shape[0], self.nemb)
 
 

@@ -170,6 +170,25 @@ int damc_pack_conv2d(const float* w_torch, int cout, int cin, int k, float* w_pa
 size_t damc_instnorm_workspace_floats(int batch, int hw, int c);
 int damc_instnorm_lrelu_nhwc(float* y, int batch, int hw, int c, const float* gamma, const float* beta, float eps,
                              float slope, float* workspace, void* stream);
+/* Encoder training (the Q update's encoder backward; Encoder_* diffusion_net.py:227-413):
+ * InstanceNorm2d(affine) + LeakyReLU keeping the conv output y: h = lrelu(IN(y)) into its own buffer and
+ * stats (B, c, 2) = {mean, rstd}; workspace as damc_instnorm_workspace_floats */
+int damc_instnorm_lrelu_train_nhwc(const float* y, int batch, int hw, int c, const float* gamma, const float* beta,
+                                   float eps, float slope, float* h, float* stats, float* workspace, void* stream);
+size_t damc_instnorm_bwd_workspace_floats(int batch, int hw, int c);
+/* dh (grad of h) -> dy (grad of the conv output y), dgamma, dbeta (c) (either may be NULL) */
+int damc_instnorm_lrelu_backward_nhwc(const float* y, const float* stats, const float* dh, int batch, int hw, int c,
+                                      const float* gamma, const float* beta, float slope, float* dy, float* dgamma,
+                                      float* dbeta, float* workspace, void* stream);
+/* Conv2d backward on NHWC activations, weight in PyTorch (Cout, Cin, k, k): dx (NHWC, may be NULL), dw, db (may
+ * be NULL).  Supported: k4 s2 p1 with H = 2 Ho (limb engine), the first k3 s1 p1 conv with Cin <= 4 (no dx), and
+ * a last conv covering its whole input (p0, 1x1 output).  workspace bytes: 0 = shape not supported. */
+size_t damc_conv2d_backward_workspace_bytes(int batch, int hin, int win, int cin, int cout, int k, int stride,
+                                            int pad);
+int damc_conv2d_backward_nhwc(const float* x, const float* dy, const float* w, int batch, int hin, int win, int cin,
+                              int cout, int k, int stride, int pad, float* dx, float* dw, float* db, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
 /* NCHW -> NHWC transpose (encoder input) */
 int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* stream);
 

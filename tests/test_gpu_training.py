@@ -107,7 +107,18 @@ def test_q_update_matches_reference(gpu_device, name):
     on the same injected noise and a mixed mask.  Tolerance as for the G update."""
     from conftest import qtrain_run
 
-    loss, grads, rec, meta = qtrain_run(name, gpu_device)
+    from damc import training
+
+    calls = []
+    orig = training.encoder_apply
+    training.encoder_apply = lambda enc, x: calls.append(1) or orig(enc, x)
+    try:
+        loss, grads, rec, meta = qtrain_run(name, gpu_device)
+    finally:
+        training.encoder_apply = orig
+    # the encoder ran on libdamc for every topology whose convs the C side covers (mnist's 7 -> 3 stride-2
+    # conv is not a k4 s2 p1 with H = 2 Ho: stock PyTorch there)
+    assert bool(calls) == (name != "q_mnist_s")
     assert rel_l2(loss, rec["loss"]) < 1e-5
     # 1e-4: the time embedding sin/cos(1000 * f * t) (SinusoidalPosEmb, arguments up to ~1000 rad, whose own
     # fp32 rounding is ~3e-5 absolute) is torch's on each device, GPU vs the reference's CPU; with B = 3-4
@@ -164,3 +175,44 @@ def _stock_denoiser(p, z, t_in, xemb):
     for layer in p.out_layers:
         out = layer(ctx=ctx, x=F.leaky_relu(torch.cat([out, skips.pop()], dim=1), negative_slope=0.01))
     return z + out if p.residual else out
+
+
+def test_encoder_train_vs_autograd_b128(gpu_device):
+    """Bench-size encoder training (CIFAR-10 Encoder, nif 64, nemb 1024, B=128): libdamc forward/backward
+    (InstanceNorm backward, k4 s2 p1 convs through the limb engine with swapped roles, first and last conv)
+    against an fp64 evaluation of the same module, accuracy-relative: per tensor, the HIP result's distance to
+    fp64 stays within 3x the distance of PyTorch's own fp32 autograd (MIOpen) to fp64 (the four InstanceNorm
+    backwards subtract per-channel means, so the first layers' gradients carry cancellation in any fp32
+    evaluation).  Floor: 1e-3 x the largest gradient norm (conv biases feeding InstanceNorm have an
+    analytically zero gradient)."""
+    import copy
+
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    enc = synth.load_into(dn.Encoder_cifar10(nc=3, nemb=1024, nif=64), 4).to(gpu_device).train()
+    enc64 = copy.deepcopy(enc).double()
+    x = torch.from_numpy(synth.uniform_f32(6, 0, (128, 3, 32, 32))).to(gpu_device)
+    w = torch.from_numpy(synth.normal_f32(6, 1, (128, 1024))).to(gpu_device)
+    assert training.encoder_train_supported(enc, x)
+
+    def run(net, hip, xx, ww):
+        net.zero_grad()
+        if hip:
+            out = net(xx)
+        else:
+            with training.stock_pytorch():
+                out = net(xx)
+        (out * ww).sum().backward()
+        return out.detach().double(), [p.grad.detach().double().clone() for p in net.parameters()]
+
+    o1, g1 = run(enc, True, x, w)
+    o0, g0 = run(enc, False, x, w)
+    o64, g64 = run(enc64, False, x.double(), w.double())
+    assert float((o1 - o64).norm() / o64.norm()) <= 3 * float((o0 - o64).norm() / o64.norm()) + 1e-6
+    floor = 1e-3 * max(float(b.norm()) for b in g64)
+    for k, (a, b, r) in enumerate(zip(g1, g0, g64)):
+        den = max(float(r.norm()), floor)
+        e_hip, e32 = float((a - r).norm()) / den, float((b - r).norm()) / den
+        print("encoder tensor %d: |hip - fp64| %.2e, |torch fp32 - fp64| %.2e" % (k, e_hip, e32))
+        assert e_hip <= 3 * e32 + 1e-6, (k, e_hip, e32)
