@@ -264,8 +264,8 @@ __global__ __launch_bounds__(256) void in_apply_train_kernel(const float* y, int
       for (int s = 1; s < S; ++s) a = wmerge(a, Wf{pp[3 * s], pp[3 * s + 1], pp[3 * s + 2]});
       const float var = a.m2 / a.n;
       const float rstd = 1.f / sqrtf(var + eps);
-      scale = rstd * gamma[c];
-      shift = beta[c] - a.mean * scale;
+      scale = rstd;
+      shift = a.mean;
       if (blockIdx.y == 0) {
         stats[((long)b * C + c) * 2] = a.mean;
         stats[((long)b * C + c) * 2 + 1] = rstd;
@@ -276,12 +276,14 @@ __global__ __launch_bounds__(256) void in_apply_train_kernel(const float* y, int
   }
   __syncthreads();
   if (c >= C) return;
-  const float scl = sc[threadIdx.x & 63], shf = sh[threadIdx.x & 63];
+  // a = ((y - mean) * rstd) * gamma + beta, InstanceNorm's own order: the fused y * scale + shift form of
+  // the inference pass loses low bits when |mean| >> std, and the backward's LReLU' reads the sign of a
+  const float rstd = sc[threadIdx.x & 63], mean = sh[threadIdx.x & 63], g = gamma[c], bt = beta[c];
   const int P = gridDim.y;
   const int p0 = (int)((long)HW * blockIdx.y / P), p1 = (int)((long)HW * (blockIdx.y + 1) / P);
   for (int p = p0 + prow; p < p1; p += 4) {
     const long o = ((long)b * HW + p) * C + c;
-    const float v = fmaf(y[o], scl, shf);
+    const float v = __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(y[o], mean), rstd), g), bt);
     h[o] = v > 0.f ? v : v * slope;
   }
 }
@@ -298,14 +300,14 @@ __global__ __launch_bounds__(256) void in_bwd_sums_kernel(const float* y, const 
   float s1 = 0.f, s2 = 0.f;
   if (c < C) {
     const float mean = stats[((long)b * C + c) * 2], rstd = stats[((long)b * C + c) * 2 + 1];
-    const float scl = rstd * gamma[c], shf = beta[c] - mean * scl;
+    const float g = gamma[c], bt = beta[c];
     for (int p = p0 + prow; p < p1; p += 4) {
       const long o = ((long)b * HW + p) * C + c;
-      const float yv = y[o];
-      const float a = fmaf(yv, scl, shf);
+      const float xh = __fmul_rn(__fsub_rn(y[o], mean), rstd);
+      const float a = __fadd_rn(__fmul_rn(xh, g), bt);  // the forward's a, bit for bit
       const float dA = a > 0.f ? dh[o] : dh[o] * slope;
       s1 += dA;
-      s2 += dA * ((yv - mean) * rstd);
+      s2 += dA * xh;
     }
   }
   __shared__ float r1[4][64], r2[4][64];
@@ -340,17 +342,16 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(const float* y, const
     bc[((long)b * 2 + 1) * C + c] = t1;
   }
   const float mean = stats[((long)b * C + c) * 2], rstd = stats[((long)b * C + c) * 2 + 1];
-  const float g = gamma[c];
-  const float scl = rstd * g, shf = beta[c] - mean * scl;
+  const float g = gamma[c], bt = beta[c];
+  const float scl = rstd * g;
   const float m1 = t1 / (float)HW, m2 = t2 / (float)HW;
   const int P = gridDim.y;
   const int p0 = (int)((long)HW * blockIdx.y / P), p1 = (int)((long)HW * (blockIdx.y + 1) / P);
   for (int p = p0 + prow; p < p1; p += 4) {
     const long o = ((long)b * HW + p) * C + c;
-    const float yv = y[o];
-    const float a = fmaf(yv, scl, shf);
+    const float xh = __fmul_rn(__fsub_rn(y[o], mean), rstd);
+    const float a = __fadd_rn(__fmul_rn(xh, g), bt);
     const float dA = a > 0.f ? dh[o] : dh[o] * slope;
-    const float xh = (yv - mean) * rstd;
     dy[o] = scl * (dA - m1 - xh * m2);
   }
 }

@@ -177,42 +177,91 @@ def _stock_denoiser(p, z, t_in, xemb):
     return z + out if p.residual else out
 
 
-def test_encoder_train_vs_autograd_b128(gpu_device):
-    """Bench-size encoder training (CIFAR-10 Encoder, nif 64, nemb 1024, B=128): libdamc forward/backward
-    (InstanceNorm backward, k4 s2 p1 convs through the limb engine with swapped roles, first and last conv)
-    against an fp64 evaluation of the same module, accuracy-relative: per tensor, the HIP result's distance to
-    fp64 stays within 3x the distance of PyTorch's own fp32 autograd (MIOpen) to fp64 (the four InstanceNorm
-    backwards subtract per-channel means, so the first layers' gradients carry cancellation in any fp32
-    evaluation).  Floor: 1e-3 x the largest gradient norm (conv biases feeding InstanceNorm have an
-    analytically zero gradient)."""
-    import copy
+def test_encoder_train_stagewise_b128(gpu_device):
+    """Bench-size encoder training (CIFAR-10 Encoder, nif 64, nemb 1024, B=128): the libdamc backward replayed
+    stage by stage, each op (InstanceNorm+LReLU backward; Conv2d backward: dense last conv, k4 s2 p1 convs on
+    the limb engine with swapped roles, first conv via the direct kernel) fed the SAME inputs as an fp64 and an
+    fp32 PyTorch autograd evaluation.  Per output: |hip - fp64| <= 3 |torch fp32 - fp64| + 1e-6.
 
-    from damc import synth, training
+    End to end the two fp32 paths cannot be compared tightly at this size: one pre-activation of 2M sits within
+    1.3e-8 of zero at the third InstanceNorm, so LReLU' flips between any two fp32 evaluations and moves that
+    layer's gradient by ~1e-3 (the Q-update golden tests cover the end-to-end path at B <= 4)."""
+    import ctypes
+
+    import torch.nn.functional as F
+
+    from damc import _lib, synth, training
+    from damc._lib import ptr
     from src import diffusion_net as dn
 
+    B = 128
     enc = synth.load_into(dn.Encoder_cifar10(nc=3, nemb=1024, nif=64), 4).to(gpu_device).train()
-    enc64 = copy.deepcopy(enc).double()
-    x = torch.from_numpy(synth.uniform_f32(6, 0, (128, 3, 32, 32))).to(gpu_device)
-    w = torch.from_numpy(synth.normal_f32(6, 1, (128, 1024))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(6, 0, (B, 3, 32, 32))).to(gpu_device)
+    g = torch.from_numpy(synth.normal_f32(6, 1, (B, 1024))).to(gpu_device)
     assert training.encoder_train_supported(enc, x)
+    cap = {}
+    orig = training._EncoderTrainFn.forward
 
-    def run(net, hip, xx, ww):
-        net.zero_grad()
-        if hip:
-            out = net(xx)
+    def fwd(ctx, xx, stages, *params):
+        r = orig(ctx, xx, stages, *params)
+        cap["saved"], cap["stages"] = ctx.saved, ctx.stages
+        return r
+
+    training._EncoderTrainFn.forward = staticmethod(fwd)
+    try:
+        enc(x)
+    finally:
+        training._EncoderTrainFn.forward = staticmethod(orig)
+    L = _lib.lib()
+    st = _lib.stream_ptr(gpu_device)
+
+    def check3(name, ours, t32, t64):
+        e, e32 = rel_l2(ours.double().cpu().numpy(), t64.cpu().numpy()), rel_l2(t32.double().cpu().numpy(),
+                                                                             t64.cpu().numpy())
+        print("%s: |hip - fp64| %.2e  |torch32 - fp64| %.2e" % (name, e, e32))
+        assert e <= 3 * e32 + 1e-6, (name, e, e32)
+
+    dh = g.contiguous()
+    stages, saved = cap["stages"], cap["saved"]
+    for i in range(len(stages) - 1, -1, -1):
+        conv, norm, slope = stages[i]
+        h_in, y, stats, H, W, Ho, Wo = saved[i]
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        cout, cin = conv.out_channels, conv.in_channels
+        if norm is not None:
+            dy = torch.empty_like(y)
+            ws = torch.empty(int(L.damc_instnorm_bwd_workspace_floats(B, Ho * Wo, cout)), device=gpu_device)
+            dgm, dbt = torch.empty(cout, device=gpu_device), torch.empty(cout, device=gpu_device)
+            assert L.damc_instnorm_lrelu_backward_nhwc(ptr(y), ptr(stats), ptr(dh), B, Ho * Wo, cout, ptr(norm.weight),
+                                                       ptr(norm.bias), ctypes.c_float(slope), ptr(dy), ptr(dgm),
+                                                       ptr(dbt), ptr(ws), st) == 0
+            refs = []
+            for dt in (torch.float32, torch.float64):
+                yy = y.to(dt).permute(0, 3, 1, 2).clone().requires_grad_(True)
+                gm = norm.weight.detach().to(dt).clone().requires_grad_(True)
+                bt = norm.bias.detach().to(dt).clone().requires_grad_(True)
+                F.leaky_relu(F.instance_norm(yy, weight=gm, bias=bt, eps=norm.eps), slope).backward(
+                    dh.to(dt).reshape(B, Ho, Wo, cout).permute(0, 3, 1, 2))
+                refs.append((yy.grad.permute(0, 2, 3, 1), gm.grad, bt.grad))
+            for nm, ours, r32, r64 in zip(("dy", "dgamma", "dbeta"), (dy, dgm, dbt), refs[0], refs[1]):
+                check3("stage %d IN %s" % (i, nm), ours, r32, r64)
         else:
-            with training.stock_pytorch():
-                out = net(xx)
-        (out * ww).sum().backward()
-        return out.detach().double(), [p.grad.detach().double().clone() for p in net.parameters()]
-
-    o1, g1 = run(enc, True, x, w)
-    o0, g0 = run(enc, False, x, w)
-    o64, g64 = run(enc64, False, x.double(), w.double())
-    assert float((o1 - o64).norm() / o64.norm()) <= 3 * float((o0 - o64).norm() / o64.norm()) + 1e-6
-    floor = 1e-3 * max(float(b.norm()) for b in g64)
-    for k, (a, b, r) in enumerate(zip(g1, g0, g64)):
-        den = max(float(r.norm()), floor)
-        e_hip, e32 = float((a - r).norm()) / den, float((b - r).norm()) / den
-        print("encoder tensor %d: |hip - fp64| %.2e, |torch fp32 - fp64| %.2e" % (k, e_hip, e32))
-        assert e_hip <= 3 * e32 + 1e-6, (k, e_hip, e32)
+            dy = dh.reshape(B, Ho, Wo, cout)
+        dx = torch.empty(B, H, W, cin, device=gpu_device) if i > 0 else None
+        nb = int(L.damc_conv2d_backward_workspace_bytes(B, H, W, cin, cout, k, s, p))
+        ws = torch.empty(nb, dtype=torch.uint8, device=gpu_device)
+        dw, db = torch.empty_like(conv.weight), torch.empty_like(conv.bias)
+        assert L.damc_conv2d_backward_nhwc(ptr(h_in), ptr(dy.contiguous()), ptr(conv.weight), B, H, W, cin, cout, k,
+                                           s, p, ptr(dx), ptr(dw), ptr(db), ptr(ws), nb, st) == 0
+        refs = []
+        for dt in (torch.float32, torch.float64):
+            xx = h_in.to(dt).permute(0, 3, 1, 2).clone().requires_grad_(i > 0)
+            ww = conv.weight.detach().to(dt).clone().requires_grad_(True)
+            bb = conv.bias.detach().to(dt).clone().requires_grad_(True)
+            F.conv2d(xx, ww, bb, s, p).backward(dy.to(dt).permute(0, 3, 1, 2))
+            refs.append((ww.grad, bb.grad, xx.grad.permute(0, 2, 3, 1) if i > 0 else None))
+        check3("stage %d conv dw" % i, dw, refs[0][0], refs[1][0])
+        check3("stage %d conv db" % i, db, refs[0][1], refs[1][1])
+        if dx is not None:
+            check3("stage %d conv dx" % i, dx, refs[0][2], refs[1][2])
+        dh = dx
