@@ -56,7 +56,8 @@ int up_split(int ho, int wo, int cin, int cout, int Bp, int* S, int* kper) {
   const long M = 4L * cout, N = cin, K = (long)ho * wo * Bp;
   const long base = ((M + 255) / 256) * ((N + 127) / 128) * 4;
   const long nkt = K / 32;
-  const long sl = std::max(1L, std::min((512 + base - 1) / base, nkt));
+  // >= 512 workgroups, but at most 16 slices: the fixed-order reduce reads every slice once per output
+  const long sl = std::max(1L, std::min(std::min((512 + base - 1) / base, 16L), nkt));
   const long kp = (nkt + sl - 1) / sl * 32;
   *kper = (int)kp;
   *S = (int)((K + kp - 1) / kp);

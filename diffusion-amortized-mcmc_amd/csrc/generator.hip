@@ -1352,7 +1352,7 @@ void up2_wgrad_split(const damc_layer_t& L, int Bp, int* S, int* kper) {
   const long M = 4L * L.cin, N = L.cout, K = (long)L.hin * L.win * Bp;
   const long base = ((M + 255) / 256) * ((N + 127) / 128) * 4;
   const long nkt = K / 32;
-  long sl = std::max(1L, std::min((512 + base - 1) / base, nkt));
+  long sl = std::max(1L, std::min(std::min((512 + base - 1) / base, 16L), nkt));
   const long kp = (nkt + sl - 1) / sl * 32;
   *kper = (int)kp;
   *S = (int)((K + kp - 1) / kp);
