@@ -39,3 +39,35 @@ def test_host_only_calls():
     # descriptor validation runs on the host: an empty generator has no workspace
     g = _lib.Generator()
     assert L.damc_posterior_workspace_bytes(ctypes.byref(g), 8) == 0
+
+
+def test_training_shape_support_host_only():
+    """Host-side shape logic of the training entry points (no device work): which Conv2d backward shapes the
+    library covers (workspace 0 = unsupported), and descriptor validation of the denoiser training path."""
+    from damc import _lib
+
+    L = _lib.lib()
+    ws = L.damc_conv2d_backward_workspace_bytes
+    assert ws(128, 16, 16, 64, 128, 4, 2, 1) > 0       # k4 s2 p1, H = 2 Ho: limb-engine path
+    assert ws(128, 32, 32, 3, 64, 3, 1, 1) > 0         # first conv (Cin <= 4)
+    assert ws(128, 4, 4, 512, 1024, 4, 1, 0) > 0       # last conv covering its input
+    assert ws(128, 7, 7, 64, 128, 4, 2, 1) == 0        # mnist 7 -> 3: H != 2 Ho
+    assert ws(128, 32, 32, 64, 64, 3, 1, 1) == 0       # a k3 conv that is not the first
+    assert L.damc_conv2d_workspace_floats(128, 8, 8, 256, 512, 4, 2, 1) > 0  # under-filled: split-K slabs
+    d = _lib.DenoiserTrain()
+    assert L.damc_denoiser_train_workspace_bytes(ctypes.byref(d), 128) == 0  # empty descriptor rejected
+    g = _lib.Generator()
+    assert L.damc_generator_train_workspace_bytes(ctypes.byref(g), 128) == 0
+
+
+def test_encoder_training_dispatch_host_only():
+    """encoder_train_supported: CIFAR / CelebA topologies take the HIP path, mnist's does not (host logic)."""
+    import torch
+
+    from damc import training
+    from src import diffusion_net as dn
+
+    x32 = torch.empty(4, 3, 32, 32)
+    assert training.encoder_train_supported(dn.Encoder_cifar10(nc=3, nemb=64, nif=8), x32)
+    assert training.encoder_train_supported(dn.Encoder_celeba64(nc=3, nemb=64, nif=8), torch.empty(2, 3, 64, 64))
+    assert not training.encoder_train_supported(dn.Encoder_mnist(nc=1, nemb=64, nif=8), torch.empty(2, 1, 28, 28))
