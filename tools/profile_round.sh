@@ -13,3 +13,6 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-f
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/write.log" 2>&1
 python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "$OUT/pmc_traffic.json" > "$OUT/pmc_traffic.txt"
+timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE -d "$OUT/clock" -o run --output-format csv -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/clock.log" 2>&1
+(cd tools && python3 pmc_clock.py "../$OUT/clock" "../$OUT/trace") > "$OUT/clock.txt"
