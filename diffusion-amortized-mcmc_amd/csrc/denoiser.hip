@@ -11,7 +11,11 @@
 // applying eps = z + out, pred_x_from_eps and the reverse-step update with Philox noise in place.
 // Block kernel: 4 waves, wave w owns one of the four products (l, s, g, b) for a 16 x 32 output
 // tile on v_mfma_f32_16x16x4_f32; operands x / c are staged once per workgroup in LDS.
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
+
+#include <hip/hip_cooperative_groups.h>
 
 #include "gemm.h"
 
@@ -64,18 +68,24 @@ struct CsqArgs {
 // k = 16g + 4(lane>>4) + s), so each lane's operands for 4 steps are one 16-B LDS read (x / c) and one
 // 16-B global read of a weight row; a wave issues CSQ_CH groups of loads before their MFMAs.  The
 // eight partial tiles are added in a fixed order in the epilogue.
-__global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+// the step-dependent fields of a block's arguments (the cooperative sweep keeps CsqArgs in kernarg memory)
+struct TileDyn {
+  const float* qt;
+  float c0, c1, c2, c3, c4;
+  int last, with_noise;
+  const float* noise;
+  uint64_t step;
+  float* eps_log;
+};
+
+// one output tile (rows r0.., columns n0..) of one block; called uniformly by all CSQ_THREADS threads
+__device__ __forceinline__ void csq_tile(const CsqArgs& a, const TileDyn& dy, int r0, int n0, float* sm) {
   const int din = a.din, dout = a.dout;
   const int ldx = csq_ld(din), ldcs = csq_ld(dout);
   float* xs = sm;                 // [TM][ldx]
   float* cs = xs + TM * ldx;      // [TM][ldcs]
   float* red = cs + TM * ldcs;    // [8][TM][TN]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // grid (N tiles, M tiles): dispatch is round-robin over the 8 XCDs, so with N tiles a multiple of 8 each
-  // XCD owns the same output columns for every row tile and step — 1/8 of the sweep's 12.6 MB of weights,
-  // which then stays in that XCD's 4 MB L2 across all steps instead of streaming from the Infinity Cache
-  const int r0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
   const int kx16 = (din + 15) & ~15, kc16 = (dout + 15) & ~15;
 
   // ---- stage x (block input) for the 16 rows; columns [din, kx16) zero.  Staging is float4 and
@@ -138,7 +148,7 @@ __global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
       f32x4 v = zero4;
       if (row < a.B && n < dout) {
         const f32x4 u = *reinterpret_cast<const f32x4*>(a.px + (long)row * a.ldpx + n) +
-                        *reinterpret_cast<const f32x4*>(a.qt + n);
+                        *reinterpret_cast<const f32x4*>(dy.qt + n);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = u[e] / (1.f + expf(-u[e]));
       }
@@ -204,26 +214,86 @@ __global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
     const long zi = (long)row * a.nz + col;
     const float zv = a.zt[zi];
     const float eps = a.residual ? zv + o : o;
-    if (a.eps_log) a.eps_log[zi] = eps;
-    const float pred = mul_rn(a.c0, sub_rn(zv, mul_rn(eps, a.c1)));
+    if (dy.eps_log) dy.eps_log[zi] = eps;
+    const float pred = mul_rn(dy.c0, sub_rn(zv, mul_rn(eps, dy.c1)));
     float zn;
-    if (a.last) {
+    if (dy.last) {
       zn = pred;
     } else {
-      zn = add_rn(mul_rn(a.c2, zv), mul_rn(a.c3, pred));
-      if (a.with_noise) {
+      zn = add_rn(mul_rn(dy.c2, zv), mul_rn(dy.c3, pred));
+      if (dy.with_noise) {
         float xi;
-        if (a.noise) {
-          xi = a.noise[zi];
+        if (dy.noise) {
+          xi = dy.noise[zi];
         } else {
           float n4[4];
-          philox_normal4(a.seed, a.chain_base + row, a.step, (uint32_t)(col >> 2), DAMC_STREAM_SWEEP, n4);
+          philox_normal4(a.seed, a.chain_base + row, dy.step, (uint32_t)(col >> 2), DAMC_STREAM_SWEEP, n4);
           xi = n4[col & 3];
         }
-        zn = add_rn(zn, mul_rn(a.c4, xi));
+        zn = add_rn(zn, mul_rn(dy.c4, xi));
       }
     }
     a.zt[zi] = zn;
+  }
+}
+
+// grid (N tiles, M tiles): dispatch is round-robin over the 8 XCDs, so with N tiles a multiple of 8 each
+// XCD owns the same output columns for every row tile and step — 1/8 of the sweep's 12.6 MB of weights,
+// which then stays in that XCD's 4 MB L2 across all steps instead of streaming from the Infinity Cache
+__global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const TileDyn dy{a.qt, a.c0, a.c1, a.c2, a.c3, a.c4, a.last, a.with_noise, a.noise, a.step, a.eps_log};
+  csq_tile(a, dy, blockIdx.y * TM, blockIdx.x * TN, sm);
+}
+
+// Opt-in (DAMC_SWEEP_COOP=1, slower: see damc_reverse_sweep) — the whole sweep in ONE cooperative launch:
+// per step, the 7 blocks run back to back with a grid-wide barrier between them (block j+1 needs every
+// column of block j for its rows).  A workgroup takes tiles
+// t = blockIdx.x, blockIdx.x + grid, ... of each block, N tile fastest: with the grid a multiple of 8, tile t
+// stays on XCD t % 8 (same weight columns every step, L2-resident, as in the per-block launches).  Saves the
+// ~7 launch/drain gaps per step that dominate at B <= 128.
+struct SweepArgs {
+  CsqArgs blk[7];         // step-invariant fields of each block
+  const float* coef;      // (n, 6) device copy of the schedule scalars
+  const float* qt;        // (n, S) time part of the ctx pre-activation
+  const float* noise;     // injected (n-1, B, nz) or null
+  float* eps_log;         // (eps_log_steps, B, nz) or null
+  int coloff[7];
+  int S, n_steps, eps_log_steps, with_noise;
+};
+
+__global__ __launch_bounds__(CSQ_THREADS) void sweep_coop_kernel(SweepArgs sa) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+  int noisy_k = 0;
+  for (int k = 0; k < sa.n_steps; ++k) {
+    const float* c = sa.coef + 6 * k;
+    const bool last = c[5] != 0.f;
+    for (int j = 0; j < 7; ++j) {
+      const CsqArgs& a = sa.blk[j];
+      TileDyn dy{};
+      dy.qt = sa.qt + (size_t)k * sa.S + sa.coloff[j];
+      if (j == 6) {
+        dy.c0 = c[0];
+        dy.c1 = c[1];
+        dy.c2 = c[2];
+        dy.c3 = c[3];
+        dy.c4 = c[4];
+        dy.last = last;
+        dy.with_noise = sa.with_noise && !last;
+        dy.noise = (dy.with_noise && sa.noise) ? sa.noise + (size_t)noisy_k * a.B * a.nz : nullptr;
+        dy.step = (uint64_t)noisy_k;
+        dy.eps_log = (sa.eps_log && k < sa.eps_log_steps) ? sa.eps_log + (size_t)k * a.B * a.nz : nullptr;
+      }
+      const int ntn = (a.dout + TN - 1) / TN, ntm = (a.B + TM - 1) / TM;
+      for (int t = blockIdx.x; t < ntn * ntm; t += gridDim.x) {
+        const int tm = t / ntn, tn = t - tm * ntn;
+        __syncthreads();  // the previous tile's LDS images are no longer read
+        csq_tile(a, dy, tm * TM, tn * TN, sm);
+      }
+      grid.sync();
+    }
+    if (!last) ++noisy_k;
   }
 }
 
@@ -242,7 +312,7 @@ int sum_dout(const damc_denoiser_t* d) {
 }
 
 struct SweepWs {
-  float *px, *qt, *t1, *t2, *xs;
+  float *px, *qt, *t1, *t2, *xs, *coef;
   float* outs[7];
   size_t bytes;
 };
@@ -261,6 +331,7 @@ size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
   t.t1 = take((long)n * d->ntemb);
   t.t2 = take((long)n * d->ntemb);
   t.xs = take((long)B * d->nxemb);
+  t.coef = take((long)n * 6);
   for (int j = 0; j < 7; ++j) t.outs[j] = take((long)B * d->blocks[j].dout);
   t.bytes = off;
   if (w) *w = t;
@@ -387,6 +458,83 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
   for (int j = 0; j < 7; ++j) {
     const damc_csq_block_t& b = d->blocks[j];
     flops_step += 2.0 * B * (2.0 * b.din * b.dout + 2.0 * b.dout * b.dout);
+  }
+  // ---- opt-in (DAMC_SWEEP_COOP=1): the whole sweep as ONE cooperative launch with a grid-wide barrier
+  // between blocks.  Measured at CIFAR B=128: 151 us per denoise step against 64.5 us for the per-block
+  // launches below — the runtime's grid barrier costs ~18 us, more than a launch/drain gap; kept for A/B.
+  static const bool coop_env = [] {
+    const char* e = getenv("DAMC_SWEEP_COOP");
+    return e && e[0] == '1';
+  }();
+  if (coop_env) {
+    size_t sm_max = 0;
+    int max_tiles = 0;
+    for (int j = 0; j < 7; ++j) {
+      sm_max = std::max(sm_max, csq_smem_bytes(d->blocks[j].din, d->blocks[j].dout, j == 0 ? d->nz : 0));
+      max_tiles = std::max(max_tiles, ((d->blocks[j].dout + TN - 1) / TN) * ((B + TM - 1) / TM));
+    }
+    static const bool coop_ok = hipFuncSetAttribute((const void*)sweep_coop_kernel,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
+                                hipSuccess;
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (coop_ok && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_coop_kernel, CSQ_THREADS, sm_max) ==
+            hipSuccess &&
+        per_cu > 0) {
+      const int resident = per_cu * ncu;
+      int grid = (max_tiles + 7) / 8 * 8;
+      if (grid > resident) grid = resident / 8 * 8;
+      if (grid >= 8) {
+        SweepArgs sa{};
+        for (int j = 0; j < 7; ++j) {
+          const damc_csq_block_t& b = d->blocks[j];
+          CsqArgs& a = sa.blk[j];
+          a.srcA = srcA[j];
+          a.wa = wa[j];
+          a.srcB = srcB[j];
+          a.wb_ = wbw[j];
+          a.emb_mode = j == 0;
+          a.z = zt;
+          a.bmat = d->bmat;
+          a.nz = d->nz;
+          a.din = b.din;
+          a.dout = b.dout;
+          a.B = B;
+          a.wl = b.wl;
+          a.bl = b.bl;
+          a.ws = b.ws;
+          a.bs = b.bs;
+          a.wg = b.wg;
+          a.bg = b.bg;
+          a.wb = b.wb;
+          a.px = w.px + coloff[j];
+          a.ldpx = S;
+          a.out = O[j];
+          a.final_ = j == 6;
+          a.residual = d->residual;
+          a.seed = seed;
+          a.chain_base = chain_base;
+          a.zt = zt;
+          sa.coloff[j] = coloff[j];
+        }
+        DAMC_CHECK(hipMemcpyAsync(w.coef, coef, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice, s));
+        sa.coef = w.coef;
+        sa.qt = w.qt;
+        sa.noise = noise;
+        sa.eps_log = eps_log;
+        sa.eps_log_steps = eps_log ? eps_log_steps : 0;
+        sa.with_noise = with_noise;
+        sa.S = S;
+        sa.n_steps = n;
+        void* args[] = {&sa};
+        ProfScope ps("denoise_sweep", flops_step * n, s);
+        if (hipLaunchCooperativeKernel((const void*)sweep_coop_kernel, dim3(grid), dim3(CSQ_THREADS), args, sm_max,
+                                       s) == hipSuccess)
+          return (int)hipGetLastError();
+        (void)hipGetLastError();  // not launchable cooperatively here: per-block launches below
+      }
+    }
   }
   int noisy_k = 0;
   for (int k = 0; k < n; ++k) {
