@@ -197,6 +197,20 @@ def g_update_bench(device, with_torch=True):
     if n.value:
         out["wgrad_up2_avg_ms"] = round(tot.value / n.value, 4)
         out["wgrad_up2_tflops"] = round(fl.value / (tot.value / 1e3) / 1e12, 2)
+    # the update's clip_grad_norm_ + Adam (train_gen_recon.py:230-231) over G's 12.6 M parameters: damc.optim's
+    # fused norm + step against torch's foreach clip_grad_norm_ + Adam
+    from damc import optim as dopt
+
+    step_hip()
+    opt_t = torch.optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    opt_d = dopt.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+
+    def adam_torch():
+        torch.nn.utils.clip_grad_norm_(G.parameters(), max_norm=100)
+        opt_t.step()
+
+    out["clip_adam_hip_ms"] = round(event_ms(lambda: opt_d.clip_and_step(100)), 4)
+    out["clip_adam_torch_ms"] = round(event_ms(adam_torch), 4)
     if with_torch:
         print("bench: timing the stock PyTorch G update (MIOpen may tune on first use)", file=sys.stderr, flush=True)
         t_torch = event_ms(step_torch, reps=3)
@@ -219,19 +233,27 @@ def q_update_bench(device, with_torch=True):
                    dataset="cifar10")
     synth.load_into(Q, 20)
     Q.to(device).train()
+    from damc import optim as dopt
+
     opt = optim.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
+    opt_d = dopt.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
     x = torch.from_numpy(synth.uniform_f32(51, 0, (B, 3, 32, 32))).to(device)
     z = torch.from_numpy(synth.normal_f32(52, 0, (B, NZ))).to(device)
     mask = (torch.from_numpy(synth.uniform_f32(53, 0, (B, 1), 0.0, 1.0)) >= 0.2).float().to(device)
 
-    def step():
+    def step():  # the reference's sequence on stock PyTorch
         opt.zero_grad(set_to_none=True)
         Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
         torch.nn.utils.clip_grad_norm_(Q.parameters(), max_norm=100)
         opt.step()
 
+    def step_hip():  # drop-in modules + damc.optim's fused clip + AdamW
+        opt_d.zero_grad(set_to_none=True)
+        Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
+        opt_d.clip_and_step(100)
+
     out = {"config": "cifar10 Q update B=128 (nif 64, nxemb 1024, ntemb 128): loss fwd+bwd, clip, AdamW",
-           "hip_ms": round(event_ms(step), 3)}
+           "hip_ms": round(event_ms(step_hip), 3)}
     if with_torch:
         with training.stock_pytorch():
             out["torch_ms"] = round(event_ms(step), 3)

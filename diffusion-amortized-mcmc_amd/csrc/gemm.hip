@@ -1001,7 +1001,6 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int oct16 = (loct ^ sw) * 48;                                         // 16x16x32
   const int oct32[2] = {((loct) ^ sw) * 48, ((2 + loct) ^ sw) * 48};          // 32x32x16, k16 step s
 
-  constexpr bool DMA = (V & 4) != 0;
   {
   constexpr bool DMA = (V & 4) != 0;
   static_assert(OM != O_WGRAD || DMA, "O_WGRAD runs on the LDS-DMA staging path only");

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdamc.so")
+# DAMC_LIB_PATH: an alternative in-tree build for A/B timing (tools/); the default is the product library
+LIB_PATH = os.environ.get("DAMC_LIB_PATH") or os.path.join(_HERE, "libdamc.so")
 
 MAX_LAYERS = 10
 LAYER_PROJ, LAYER_UP2, LAYER_SMALLC, LAYER_LINEAR = 1, 2, 3, 4
@@ -83,6 +84,16 @@ class DenoiserGrads(ctypes.Structure):
         (k, ctypes.c_void_p * 7) for k in ("wl", "bl", "ws", "bs", "wg", "bg", "wb", "wctx", "bctx")]
 
 
+class AdamHparams(ctypes.Structure):
+    _fields_ = [("neg_step_size", ctypes.c_float), ("one_minus_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("one_minus_beta2", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("eps", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("decay_mul", ctypes.c_float), ("decoupled", ctypes.c_int)]
+
+
+ADAM_CHUNK = 8192
+ADAM_MAX_TENSORS = 96
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
@@ -128,6 +139,14 @@ _SIGS = {
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
     "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,
                                 _SZ, _P]),
+    "damc_adam_chunk_bytes": (_SZ, []),
+    "damc_adam_chunk_count": (_I, [ctypes.POINTER(ctypes.c_longlong), _I]),
+    "damc_adam_build_chunks": (_I, [ctypes.POINTER(ctypes.c_longlong), _I, _P, _I]),
+    "damc_grad_norm": (_I, [_P, _I, _P, _I, _F, _P, _P, _P]),
+    "damc_grad_sumsq": (_I, [_P, _I, _P, _I, _P, _P]),
+    "damc_grad_norm_finish": (_I, [_P, _I, _F, _P, _P]),
+    "damc_grad_scale": (_I, [_P, _I, _P, _I, _P, _P]),
+    "damc_adam_step": (_I, [_P, _I, _P, _P, _P, _P, _I, ctypes.POINTER(AdamHparams), _P, _P]),
     "damc_prof_enable": (_I, [_I]),
     "damc_prof_reset": (_I, []),
     "damc_prof_select": (_I, [ctypes.c_char_p]),

@@ -267,6 +267,51 @@ int damc_denoiser_train_backward(const damc_denoiser_train_t* d, const float* gr
                                  const damc_denoiser_grads_t* grads, float* grad_zt, float* grad_xemb,
                                  void* workspace, size_t workspace_bytes, void* stream);
 
+/* --------------------------------------------------------------------------- optimiser steps
+ * Replaces the G/E/Q updates' torch.nn.utils.clip_grad_norm_ + optim.Adam / optim.AdamW.step()
+ * (train_gen_recon.py:155-157, 219-231, 240-241) by multi-tensor kernels.  A launch covers up to
+ * DAMC_ADAM_MAX_TENSORS fp32 tensors whose device pointers travel in the kernel arguments (host arrays
+ * here), so nothing is rebuilt when autograd hands out new gradient buffers.  The chunk table depends
+ * only on the tensor sizes: entry = (tensor index, element offset, length <= DAMC_ADAM_CHUNK), built on
+ * the host by damc_adam_build_chunks and copied to device memory by the caller (plain bytes). */
+#define DAMC_ADAM_CHUNK 8192
+#define DAMC_ADAM_MAX_TENSORS 96
+typedef struct { /* per-step scalars, computed by the caller exactly as torch's _multi_tensor_adam does */
+  float neg_step_size;   /* -(lr / (1 - beta1^t))                                           */
+  float one_minus_beta1; /* lerp weight 1 - beta1                                            */
+  float beta2, one_minus_beta2;
+  float bc2_sqrt;        /* (1 - beta2^t) ** 0.5                                             */
+  float eps;
+  float weight_decay;    /* Adam (L2 into the gradient) when decoupled == 0                  */
+  float decay_mul;       /* AdamW: 1 - lr * weight_decay                                     */
+  int decoupled;
+} damc_adam_hparams_t;
+size_t damc_adam_chunk_bytes(void);
+/* host only: number of chunks for tensors of these sizes */
+int damc_adam_chunk_count(const long long* numel, int ntensors);
+/* host only: writes the chunk table into host_chunks (max_chunks entries); returns the count or < 0 */
+int damc_adam_build_chunks(const long long* numel, int ntensors, void* host_chunks, int max_chunks);
+/* clip_grad_norm_(max_norm, norm_type=2), first half: out[0] = total norm, out[1] = min(max_norm /
+ * (norm + 1e-6), 1).  grads: host array of ntensors (<= DAMC_ADAM_MAX_TENSORS) device pointers.
+ * workspace: nchunks floats.  Gradients are not scaled here (damc_grad_scale, or damc_adam_step's clip). */
+int damc_grad_norm(const void* dev_chunks, int nchunks, float* const* grads, int ntensors, float max_norm,
+                   float* workspace, float* out, void* stream);
+/* the two halves of damc_grad_norm, for gradient sets of more than DAMC_ADAM_MAX_TENSORS tensors: per-chunk
+ * sums of squares into partial[0, nchunks) (call once per <= 96-tensor slice, each into its own range),
+ * then the fixed-order total over all n partials */
+int damc_grad_sumsq(const void* dev_chunks, int nchunks, float* const* grads, int ntensors, float* partial,
+                    void* stream);
+int damc_grad_norm_finish(const float* partial, int n, float max_norm, float* out, void* stream);
+/* grads *= clip[1] (the second half of clip_grad_norm_) */
+int damc_grad_scale(const void* dev_chunks, int nchunks, float* const* grads, int ntensors, const float* clip,
+                    void* stream);
+/* one Adam/AdamW step over every chunk (params, grads, exp_avgs, exp_avg_sqs: host arrays of device
+ * pointers); clip (device, from damc_grad_norm) or NULL: when given, the gradient is scaled by clip[1]
+ * first and written back, as clip_grad_norm_ would have left it */
+int damc_adam_step(const void* dev_chunks, int nchunks, float* const* params, float* const* grads,
+                   float* const* exp_avgs, float* const* exp_avg_sqs, int ntensors, const damc_adam_hparams_t* hp,
+                   const float* clip, void* stream);
+
 /* --------------------------------------------------------------------------- profiling */
 /* optional per-kernel HIP-event timing (bench.py roofline): records events around each
  * launch of the named kernel class on the launch stream; read back after a sync. */

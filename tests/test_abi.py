@@ -71,3 +71,38 @@ def test_encoder_training_dispatch_host_only():
     assert training.encoder_train_supported(dn.Encoder_cifar10(nc=3, nemb=64, nif=8), x32)
     assert training.encoder_train_supported(dn.Encoder_celeba64(nc=3, nemb=64, nif=8), torch.empty(2, 3, 64, 64))
     assert not training.encoder_train_supported(dn.Encoder_mnist(nc=1, nemb=64, nif=8), torch.empty(2, 1, 28, 28))
+
+
+def test_adam_chunk_table_host_only():
+    """damc_adam_build_chunks (host-only, no GPU): 8192-element chunks per tensor, empty tensors skipped, at
+    most 96 tensors per table; damc.optim refuses CPU tensors (no fallback)."""
+    import ctypes as C
+
+    import pytest
+    import torch
+
+    from damc import _lib, optim
+
+    L = _lib.lib()
+    assert L.damc_adam_chunk_bytes() == 16
+    sizes = [20000, 0, 5, 8192]
+    arr = (C.c_longlong * len(sizes))(*sizes)
+    assert L.damc_adam_chunk_count(arr, len(sizes)) == 3 + 0 + 1 + 1
+    buf = (C.c_ubyte * (16 * 5))()
+    assert L.damc_adam_build_chunks(arr, len(sizes), buf, 4) < 0  # too small
+    assert L.damc_adam_build_chunks(arr, len(sizes), buf, 5) == 5
+    raw = bytes(buf)
+    rows = [(int.from_bytes(raw[16 * i:16 * i + 8], "little"), int.from_bytes(raw[16 * i + 8:16 * i + 12], "little"),
+             int.from_bytes(raw[16 * i + 12:16 * i + 16], "little")) for i in range(5)]
+    assert rows == [(0, 0, 8192), (8192, 0, 8192), (16384, 0, 20000 - 16384), (0, 2, 5), (0, 3, 8192)]
+    many = (C.c_longlong * 97)(*([1] * 97))
+    assert L.damc_adam_chunk_count(many, 97) < 0  # > DAMC_ADAM_MAX_TENSORS per table
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    with pytest.raises(_lib.DamcError):
+        optim.Adam([p]).step()
+    with pytest.raises(_lib.DamcError):
+        optim.clip_grad_norm_([p], 1.0)
+    with pytest.raises(NotImplementedError):
+        optim.Adam([p], amsgrad=True)
+    assert sorted(optim.AdamW([p]).defaults) == sorted(torch.optim.AdamW([p]).defaults)

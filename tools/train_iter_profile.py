@@ -1,6 +1,7 @@
 """Time the legs of one reference training iteration (workspace/train_gen_recon.py:179-241) at the bench
 config (CIFAR-10, B=128, nz=128, ngf=128, Q: nif 64, nxemb 1024, ntemb 128, 100 steps) on the drop-in
-package: Q(x) amortizer forwards, the Langevin block, 6 Q updates, the G update, the E update."""
+package: Q(x) amortizer forwards, the Langevin block, 6 Q updates, the G update, the E update.
+--damc-optim: the three optimisers and their clip_grad_norm_ on damc.optim (fused clip + Adam/AdamW)."""
 import os
 import sys
 import time
@@ -22,9 +23,20 @@ qa = dict(nc=3, nz=nz, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n
           logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A", dataset="cifar10")
 Q = synth.load_into(dn._netQ_U(**qa), 20).to(dev)
 Qd = synth.load_into(dn._netQ_U(**qa), 20).to(dev)
+DAMC_OPTIM = "--damc-optim" in sys.argv
+if DAMC_OPTIM:
+    from damc import optim  # noqa: E402,F811
 G_opt = optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
 Q_opt = optim.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
 E_opt = optim.Adam(E.parameters(), lr=1e-4, betas=(0.5, 0.999))
+
+
+def clip_step(opt, params, max_norm=100):
+    if DAMC_OPTIM:
+        opt.clip_and_step(max_norm)
+    else:
+        torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
+        opt.step()
 x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(dev)
 
 
@@ -54,21 +66,18 @@ def iteration(t):
         Q_opt.zero_grad()
         Q.train()
         Q.calculate_loss(x=x, z=zk_pos, mask=z_mask).mean().backward()
-        torch.nn.utils.clip_grad_norm_(Q.parameters(), max_norm=100)
-        Q_opt.step()
+        clip_step(Q_opt, Q.parameters())
     e3 = ev()
     G_opt.zero_grad()
     G.train()
     g_loss = torch.sum((G(zk_pos) - x) ** 2, dim=[1, 2, 3]).mean()
     g_loss.backward()
-    torch.nn.utils.clip_grad_norm_(G.parameters(), max_norm=100)
-    G_opt.step()
+    clip_step(G_opt, G.parameters())
     e4 = ev()
     E_opt.zero_grad()
     E.train()
     (E(zk_pos).mean() - E(zk_neg).mean()).backward()
-    torch.nn.utils.clip_grad_norm_(E.parameters(), max_norm=100)
-    E_opt.step()
+    clip_step(E_opt, E.parameters())
     e5 = ev()
     torch.cuda.synchronize()
     evs = [e0, e1, e2, e3, e4, e5]
