@@ -1016,6 +1016,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
     // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
     // barrier at the end of this tile (its vmcnt(0)) lands it
+    // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
     if (DMA && kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
     if (M16) {
       bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
