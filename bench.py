@@ -353,19 +353,19 @@ def main():
     L.damc_prof_enable(0)
     breakdown = query()
 
-    extras = None
-    if not args.no_extras:
-        # outside the timed region: does not enter `value`
-        extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
-        extras["amortizer"] = amortizer_bench(device)
-        extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
-        extras["q_update"] = q_update_bench(device, with_torch=not args.no_torch_g)
-
     t_max = elapsed
     if dist:
         t = torch.tensor([elapsed], device=device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         t_max = float(t.item())
+
+    extras = None
+    if not args.no_extras and rank == 0:
+        # outside the timed region (after the max-over-ranks reduction): does not enter `value`; rank 0 only
+        extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
+        extras["amortizer"] = amortizer_bench(device)
+        extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
+        extras["q_update"] = q_update_bench(device, with_torch=not args.no_torch_g)
 
     if rank == 0:
         zsteps = world * B * POST_STEPS * args.steps
