@@ -363,10 +363,11 @@ extern "C" size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int B, in
   return carve(d, B, n, nullptr, nullptr);
 }
 
-extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
-                                  const float* temb_in, const float* coef, int with_noise, const float* noise,
-                                  uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps,
-                                  void* wsp, size_t wsb, void* stream) {
+// step_offset: Philox step index of the first noisy step (a single-step call continues a sweep's noise stream)
+static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
+                              const float* temb_in, const float* coef, int with_noise, const float* noise,
+                              uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps, void* wsp,
+                              size_t wsb, void* stream, uint64_t step_offset) {
   int rc = validate(d);
   if (rc) return rc;
   if (!xemb || !zt || !temb_in || !coef || B <= 0 || n <= 0) return DAMC_ERR_ARG;
@@ -466,7 +467,7 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
     const char* e = getenv("DAMC_SWEEP_COOP");
     return e && e[0] == '1';
   }();
-  if (coop_env) {
+  if (coop_env && step_offset == 0) {
     size_t sm_max = 0;
     int max_tiles = 0;
     for (int j = 0; j < 7; ++j) {
@@ -579,7 +580,7 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
         a.noise = (a.with_noise && noise) ? noise + (size_t)noisy_k * B * d->nz : nullptr;
         a.seed = seed;
         a.chain_base = chain_base;
-        a.step = (uint64_t)noisy_k;
+        a.step = step_offset + (uint64_t)noisy_k;
         a.zt = zt;
         a.eps_log = (eps_log && k < eps_log_steps) ? eps_log + (size_t)k * B * d->nz : nullptr;
       }
@@ -592,4 +593,29 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
   }
   (void)temb_in;
   return 0;
+}
+
+extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
+                                  const float* temb_in, const float* coef, int with_noise, const float* noise,
+                                  uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps,
+                                  void* wsp, size_t wsb, void* stream) {
+  return reverse_sweep_impl(d, xemb, zt, B, n, temb_in, coef, with_noise, noise, seed, chain_base, eps_log,
+                            eps_log_steps, wsp, wsb, stream, 0);
+}
+
+// SURVEY.md §8b names
+extern "C" int damc_q_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
+                                    const float* temb_in, const float* coef, int with_noise, const float* noise,
+                                    uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps,
+                                    void* wsp, size_t wsb, void* stream) {
+  return reverse_sweep_impl(d, xemb, zt, B, n, temb_in, coef, with_noise, noise, seed, chain_base, eps_log,
+                            eps_log_steps, wsp, wsb, stream, 0);
+}
+
+extern "C" int damc_denoise_step(const damc_denoiser_t* d, const float* xemb, float* zt, int B, const float* temb_row,
+                                 const float* coef_row, int with_noise, const float* noise, uint64_t seed,
+                                 uint64_t noise_step, uint64_t chain_base, float* eps, void* wsp, size_t wsb,
+                                 void* stream) {
+  return reverse_sweep_impl(d, xemb, zt, B, 1, temb_row, coef_row, with_noise, noise, seed, chain_base, eps,
+                            eps ? 1 : 0, wsp, wsb, stream, noise_step);
 }

@@ -414,3 +414,8 @@ extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* 
   hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, e->w2, e->nh, e->nh, w2t);
   return (int)hipGetLastError();
 }
+
+// SURVEY.md §8b name of the EBM per-op hook
+extern "C" int damc_ebm_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad, void* stream) {
+  return damc_ebm_energy_grad(e, z, B, energy, grad, stream);
+}

@@ -406,3 +406,73 @@ extern "C" int damc_instnorm_lrelu_backward_nhwc(const float* y, const float* st
   }
   return 0;
 }
+
+// ---- the whole encoder forward in one call (damc_q_encoder_fwd): NCHW -> NHWC, then per layer the conv
+// (split-K slabs when its tiles would not fill the chip) and InstanceNorm + LeakyReLU in place; two
+// ping-pong activation buffers, the last conv writes xemb directly
+namespace {
+struct EncShapes {
+  int h[DAMC_MAX_ENC_LAYERS + 1], w[DAMC_MAX_ENC_LAYERS + 1];
+  size_t act_max = 0, slab_max = 0, in_max = 0;
+};
+bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
+  if (!e || B <= 0 || e->n_layers < 1 || e->n_layers > DAMC_MAX_ENC_LAYERS || e->nc <= 0 || e->h <= 0 || e->w <= 0)
+    return false;
+  sh->h[0] = e->h;
+  sh->w[0] = e->w;
+  int c = e->nc;
+  sh->act_max = (size_t)B * e->h * e->w * e->nc;
+  for (int i = 0; i < e->n_layers; ++i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    if (L.cin != c || L.cout <= 0 || L.k <= 0 || L.stride <= 0 || L.pad < 0 || !L.w_packed) return false;
+    if ((L.in_gamma == nullptr) != (L.in_beta == nullptr)) return false;
+    const int ho = (sh->h[i] + 2 * L.pad - L.k) / L.stride + 1, wo = (sh->w[i] + 2 * L.pad - L.k) / L.stride + 1;
+    if (ho <= 0 || wo <= 0) return false;
+    sh->h[i + 1] = ho;
+    sh->w[i + 1] = wo;
+    if (i + 1 < e->n_layers) sh->act_max = std::max(sh->act_max, (size_t)B * ho * wo * L.cout);
+    sh->slab_max = std::max(sh->slab_max,
+                            damc_conv2d_workspace_floats(B, sh->h[i], sh->w[i], L.cin, L.cout, L.k, L.stride, L.pad));
+    if (L.in_gamma) sh->in_max = std::max(sh->in_max, damc_instnorm_workspace_floats(B, ho * wo, L.cout));
+    c = L.cout;
+  }
+  return true;
+}
+size_t round256(size_t b) { return (b + 255) / 256 * 256; }
+}  // namespace
+
+extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B) {
+  EncShapes sh;
+  if (!enc_shapes(e, B, &sh)) return 0;
+  return 2 * round256(sh.act_max * 4) + round256(std::max<size_t>(sh.slab_max, 1) * 4) +
+         round256(std::max<size_t>(sh.in_max, 1) * 4);
+}
+
+extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B, float* xemb, void* wsp, size_t wsb,
+                                  void* stream) {
+  EncShapes sh;
+  if (!x || !xemb || !enc_shapes(e, B, &sh)) return DAMC_ERR_ARG;
+  const int n = e->n_layers;
+  if (sh.h[n] != 1 || sh.w[n] != 1) return DAMC_ERR_UNSUPPORTED;  // NHWC flatten == NCHW flatten only at 1 x 1
+  if (!wsp || wsb < damc_q_encoder_workspace_bytes(e, B)) return DAMC_ERR_WORKSPACE;
+  char* base = reinterpret_cast<char*>(wsp);
+  float* buf[2] = {reinterpret_cast<float*>(base), reinterpret_cast<float*>(base + round256(sh.act_max * 4))};
+  float* slabs = reinterpret_cast<float*>(base + 2 * round256(sh.act_max * 4));
+  float* inws = reinterpret_cast<float*>(base + 2 * round256(sh.act_max * 4) +
+                                         round256(std::max<size_t>(sh.slab_max, 1) * 4));
+  int rc;
+  if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) return rc;
+  for (int i = 0; i < n; ++i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
+    const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
+    if ((rc = damc_conv2d_nhwc(buf[i & 1], B, sh.h[i], sh.w[i], L.cin, L.w_packed, L.bias, L.cout, L.k, L.stride,
+                               L.pad, out, nsl ? slabs : nullptr, nsl, stream)))
+      return rc;
+    if (L.in_gamma &&
+        (rc = damc_instnorm_lrelu_nhwc(out, B, sh.h[i + 1] * sh.w[i + 1], L.cout, L.in_gamma, L.in_beta, L.in_eps,
+                                       L.slope, inws, stream)))
+      return rc;
+  }
+  return 0;
+}

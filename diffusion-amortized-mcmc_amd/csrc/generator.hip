@@ -1653,6 +1653,97 @@ extern "C" int damc_likelihood_grad(const damc_generator_t* g, const float* z, c
   return slab_sum(ws.slabs, ws.nslab, n, grad, s);
 }
 
+// ---- per-op hooks for ONE k4 s2 p1 ConvTranspose2d layer (damc_convT_fwd / damc_convT_dgrad),
+// NHWC activations, the same kernels and engine choice as inside the Langevin step
+static bool up2_hook_ok(const damc_layer_t* L, int B) {
+  return L && B > 0 && L->kind == DAMC_LAYER_UP2 && L->k == 4 && L->stride == 2 && L->pad == 1 && L->cin > 0 &&
+         L->cout > 0 && L->hout == 2 * L->hin && L->wout == 2 * L->win && L->w_fwd && L->w_bwd;
+}
+
+extern "C" size_t damc_convT_workspace_bytes(const damc_layer_t* L, int B) {
+  if (!up2_hook_ok(L, B)) return 0;
+  const size_t in = (size_t)B * L->hin * L->win * L->cin, out = (size_t)B * L->hout * L->wout * L->cout;
+  return (std::max(in, out) * 6 + 255) / 256 * 256;  // limb copy of the A operand
+}
+
+extern "C" int damc_convT_fwd(const damc_layer_t* L, const float* in, int B, float* out, void* wsp, size_t wsb,
+                              void* stream) {
+  if (!up2_hook_ok(L, B) || !in || !out) return DAMC_ERR_ARG;
+  if (!wsp || wsb < damc_convT_workspace_bytes(L, B)) return DAMC_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  GemmArgs a;
+  a.bias = L->bias;
+  a.bias_mod = L->cout;
+  a.act = L->act;
+  a.slope = L->slope;
+  a.C = out;
+  a.A = in;
+  a.Hin = L->hin;
+  a.Win = L->win;
+  a.Cg = L->cin;
+  a.Hq = L->hin;
+  a.Wq = L->win;
+  a.kw = 2;
+  a.stride = 1;
+  a.B = L->w_fwd;
+  a.b_kmajor = damc::conv_kmajor_ok(L->cin);
+  a.ldb = a.b_kmajor ? 4L * L->cin : L->cout;
+  a.b_zstride = 4L * L->cin * L->cout;
+  a.ldc = L->cout;
+  a.M = B * L->hin * L->win;
+  a.N = L->cout;
+  a.K = 4 * L->cin;
+  a.Hout = L->hout;
+  a.Wout = L->wout;
+  int rc;
+  if (x3_fwd(*L)) {
+    unsigned short* a3 = reinterpret_cast<unsigned short*>(wsp);
+    if ((rc = damc::launch_split_x3(in, (long)B * L->hin * L->win * L->cin, a3, s))) return rc;
+    a.A3 = a3;
+    a.B3 = x3_of(L->w_fwd, up2_floats(*L));
+  }
+  return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(*L, B), s);
+}
+
+extern "C" int damc_convT_dgrad(const damc_layer_t* L, const float* gout, int B, const float* mask_pre, int mask_act,
+                                float mask_slope, float* gin, void* wsp, size_t wsb, void* stream) {
+  if (!up2_hook_ok(L, B) || !gout || !gin) return DAMC_ERR_ARG;
+  if (!wsp || wsb < damc_convT_workspace_bytes(L, B)) return DAMC_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  GemmArgs a;
+  a.A = gout;
+  a.Hin = L->hout;
+  a.Win = L->wout;
+  a.Cg = L->cout;
+  a.Hq = L->hin;
+  a.Wq = L->win;
+  a.kw = 4;
+  a.stride = 2;
+  a.pad_y = 1;
+  a.pad_x = 1;
+  a.B = L->w_bwd;
+  a.b_kmajor = damc::conv_kmajor_ok(L->cout);
+  a.ldb = a.b_kmajor ? 16L * L->cout : L->cin;
+  a.C = gin;
+  a.ldc = L->cin;
+  a.M = B * L->hin * L->win;
+  a.N = L->cin;
+  a.K = 16 * L->cout;
+  a.k_per_z = a.K;
+  a.mask = mask_pre;
+  a.mask_act = mask_pre ? mask_act : DAMC_ACT_NONE;
+  a.mask_slope = mask_slope;
+  int rc;
+  if (x3_bwd(*L)) {
+    unsigned short* a3 = reinterpret_cast<unsigned short*>(wsp);
+    if ((rc = damc::launch_split_x3(gout, (long)B * L->hout * L->wout * L->cout, a3, s))) return rc;
+    a.A3 = a3;
+    a.B3 = x3_of(L->w_bwd, up2_floats(*L));
+  }
+  return damc::launch_gemm(a, damc::A_CONV, mask_pre ? damc::EPI_MASK : damc::EPI_STORE, damc::O_DENSE, 1,
+                           "upconv_dgrad", conv_flops(*L, B), s);
+}
+
 extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
                                        int B, int n_steps, float sigma, float step, int with_noise, const float* noise,
                                        uint64_t seed, uint64_t step_offset, uint64_t chain_base, float* diag,

@@ -84,6 +84,21 @@ class DenoiserGrads(ctypes.Structure):
         (k, ctypes.c_void_p * 7) for k in ("wl", "bl", "ws", "bs", "wg", "bg", "wb", "wctx", "bctx")]
 
 
+MAX_ENC_LAYERS = 8
+
+
+class EncLayer(ctypes.Structure):  # damc_enc_layer_t
+    _fields_ = [("cin", ctypes.c_int), ("cout", ctypes.c_int), ("k", ctypes.c_int), ("stride", ctypes.c_int),
+                ("pad", ctypes.c_int), ("w_packed", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+                ("in_gamma", ctypes.c_void_p), ("in_beta", ctypes.c_void_p), ("in_eps", ctypes.c_float),
+                ("slope", ctypes.c_float)]
+
+
+class Encoder(ctypes.Structure):  # damc_encoder_t
+    _fields_ = [("n_layers", ctypes.c_int), ("nc", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("layers", EncLayer * MAX_ENC_LAYERS)]
+
+
 class AdamHparams(ctypes.Structure):
     _fields_ = [("neg_step_size", ctypes.c_float), ("one_minus_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("one_minus_beta2", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("eps", ctypes.c_float),
@@ -112,6 +127,9 @@ _SIGS = {
                                      _U64, _U64, _U64, _P, _P, _SZ, _P]),
     "damc_likelihood_grad": (_I, [ctypes.POINTER(Generator), _P, _P, _I, _F, _P, _P, _SZ, _P]),
     "damc_generator_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
+    "damc_convT_workspace_bytes": (_SZ, [ctypes.POINTER(Layer), _I]),
+    "damc_convT_fwd": (_I, [ctypes.POINTER(Layer), _P, _I, _P, _P, _SZ, _P]),
+    "damc_convT_dgrad": (_I, [ctypes.POINTER(Layer), _P, _I, _P, _I, _F, _P, _P, _SZ, _P]),
     "damc_generator_train_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
     "damc_generator_train_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
     "damc_generator_train_backward": (_I, [ctypes.POINTER(Generator), _P, _P, _P, _I, ctypes.POINTER(GeneratorGrads),
@@ -135,10 +153,17 @@ _SIGS = {
     "damc_conv2d_backward_nhwc": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     "damc_instnorm_lrelu_nhwc": (_I, [_P, _I, _I, _I, _P, _P, _F, _F, _P, _P]),
     "damc_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _P, _P]),
+    "damc_q_encoder_workspace_bytes": (_SZ, [ctypes.POINTER(Encoder), _I]),
+    "damc_q_encoder_fwd": (_I, [ctypes.POINTER(Encoder), _P, _I, _P, _P, _SZ, _P]),
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
     "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,
                                 _SZ, _P]),
+    "damc_q_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,
+                                  _SZ, _P]),
+    "damc_denoise_step": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _P, _P, _I, _P, _U64, _U64, _U64, _P, _P, _SZ,
+                               _P]),
+    "damc_ebm_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_adam_chunk_bytes": (_SZ, []),
     "damc_adam_chunk_count": (_I, [ctypes.POINTER(ctypes.c_longlong), _I]),
     "damc_adam_build_chunks": (_I, [ctypes.POINTER(ctypes.c_longlong), _I, _P, _I]),

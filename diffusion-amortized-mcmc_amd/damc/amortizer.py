@@ -108,36 +108,39 @@ class EncoderPlan:
         self.nemb = enc.nemb
 
     def forward(self, x):
+        """The whole encoder in one damc_q_encoder_fwd call (weights packed from the live modules per call)."""
         L = _lib.lib()
         dev = x.device
         stream = _lib.stream_ptr(dev)
         B, C, H, W = x.shape
-        h = torch.empty(B, H, W, C, dtype=torch.float32, device=dev)
-        check(L.damc_nchw_to_nhwc(ptr(x), B, C, H * W, ptr(h), stream), "nchw_to_nhwc")
+        if len(self.stages) > _lib.MAX_ENC_LAYERS:
+            raise NotImplementedError("encoder with %d convolutions" % len(self.stages))
+        d = _lib.Encoder()
+        d.n_layers, d.nc, d.h, d.w = len(self.stages), C, H, W
         keep = []
-        for conv, norm, slope in self.stages:
+        for i, (conv, norm, slope) in enumerate(self.stages):
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             cout, cin = conv.out_channels, conv.in_channels
             w = _dev(conv.weight, dev)
             wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
             check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(wp), stream), "pack conv2d")
             bias = _dev(conv.bias, dev) if conv.bias is not None else None
-            Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-            y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
-            nsl = int(L.damc_conv2d_workspace_floats(B, H, W, cin, cout, k, s, p))
-            sl = torch.empty(nsl, dtype=torch.float32, device=dev) if nsl else None
-            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(bias), cout, k, s, p, ptr(y), ptr(sl), nsl,
-                                     stream), "conv2d")
-            keep += [w, wp, bias, sl]
+            e = d.layers[i]
+            e.cin, e.cout, e.k, e.stride, e.pad = cin, cout, k, s, p
+            e.w_packed, e.bias = ptr(wp), ptr(bias)
+            keep += [w, wp, bias]
             if norm is not None:
-                nws = int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout))
-                ws = torch.empty(max(nws, 1), dtype=torch.float32, device=dev)
                 g, b = _dev(norm.weight, dev), _dev(norm.bias, dev)
-                check(L.damc_instnorm_lrelu_nhwc(ptr(y), B, Ho * Wo, cout, ptr(g), ptr(b), float(norm.eps),
-                                                 slope, ptr(ws), stream), "instnorm")
-                keep += [ws, g, b]
-            h, H, W = y, Ho, Wo
-        return h.reshape(B, -1)
+                e.in_gamma, e.in_beta, e.in_eps, e.slope = ptr(g), ptr(b), float(norm.eps), slope
+                keep += [g, b]
+        nbytes = int(L.damc_q_encoder_workspace_bytes(ctypes.byref(d), B))
+        if nbytes == 0:
+            raise _lib.DamcError("unsupported encoder configuration for the HIP path")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        conv = self.stages[-1][0]
+        out = torch.empty(B, conv.out_channels, dtype=torch.float32, device=dev)
+        check(L.damc_q_encoder_fwd(ctypes.byref(d), ptr(x), B, ptr(out), ptr(ws), nbytes, stream), "damc_q_encoder_fwd")
+        return out.reshape(B, -1)
 
 
 # ----------------------------------------------------------------------------- denoiser

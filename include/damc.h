@@ -116,6 +116,18 @@ int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float*
 int damc_generator_forward(const damc_generator_t* g, const float* z, int batch, float* x_hat,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* per-op hooks for ONE k4 s2 p1 ConvTranspose2d (DAMC_LAYER_UP2) layer of a generator, NHWC
+ * activations, the same kernels and engine choice as inside damc_posterior_langevin:
+ *   damc_convT_fwd:   out (B, hout, wout, cout) = act(conv_transpose2d(in (B, hin, win, cin), W) + bias)
+ *   damc_convT_dgrad: gin (B, hin, win, cin) = conv_transpose2d^T(gout (B, hout, wout, cout), W), multiplied by
+ *                     act'(mask_pre) when mask_pre != NULL (the previous layer's activated output, act = mask_act)
+ * layer: packed by damc_pack_generator_layer; workspace: damc_convT_workspace_bytes (limb copy of the input). */
+size_t damc_convT_workspace_bytes(const damc_layer_t* layer, int batch);
+int damc_convT_fwd(const damc_layer_t* layer, const float* in, int batch, float* out, void* workspace,
+                   size_t workspace_bytes, void* stream);
+int damc_convT_dgrad(const damc_layer_t* layer, const float* gout, int batch, const float* mask_pre, int mask_act,
+                     float mask_slope, float* gin, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------- generator training step */
 /* The G update of a training iteration (workspace/train_gen_recon.py:222-231):
  *   x_hat = G(z); g_loss = sum((x_hat - x)^2, [1,2,3]).mean(); g_loss.backward()
@@ -147,6 +159,8 @@ int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps,
 /* per-op hook: energy (B) and grad_z sum E (B,nz) */
 int damc_ebm_energy_grad(const damc_ebm_t* ebm, const float* z, int batch, float* energy, float* grad,
                          void* stream);
+/* the same under SURVEY.md §8b's name */
+int damc_ebm_grad(const damc_ebm_t* ebm, const float* z, int batch, float* energy, float* grad, void* stream);
 /* per-op hook: z <- z - 0.5 step^2 (g + z) (+ step xi) ; g (B,nz) */
 int damc_z_update(float* z, const float* g, int batch, int nz, float step, int with_noise, const float* noise,
                   uint64_t seed, uint64_t step_index, uint64_t chain_base, void* stream);
@@ -192,6 +206,26 @@ int damc_conv2d_backward_nhwc(const float* x, const float* dy, const float* w, i
 /* NCHW -> NHWC transpose (encoder input) */
 int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* stream);
 
+/* The whole Encoder_* forward of _netQ_U (SURVEY.md §8b damc_q_encoder_fwd; diffusion_net.py:227-372, a10):
+ * [Conv2d -> InstanceNorm2d(affine) -> LeakyReLU]* -> Conv2d on the kernels above, x (B, nc, h, w) NCHW ->
+ * xemb (B, nemb) with nemb = cout * ho * wo of the last conv (1 x 1 in every Encoder_*, where the NHWC and
+ * the reference's NCHW flattening agree; other output sizes return DAMC_ERR_UNSUPPORTED). */
+#define DAMC_MAX_ENC_LAYERS 8
+typedef struct {
+  int cin, cout, k, stride, pad;
+  const float* w_packed;          /* damc_pack_conv2d layout                                          */
+  const float* bias;              /* (cout) or NULL                                                   */
+  const float *in_gamma, *in_beta; /* InstanceNorm2d affine (cout); NULL: no norm / activation after it */
+  float in_eps, slope;
+} damc_enc_layer_t;
+typedef struct {
+  int n_layers, nc, h, w;
+  damc_enc_layer_t layers[DAMC_MAX_ENC_LAYERS];
+} damc_encoder_t;
+size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* enc, int batch);
+int damc_q_encoder_fwd(const damc_encoder_t* enc, const float* x, int batch, float* xemb, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* Dense fp32 MFMA GEMM: C(M,N) = act(A(M,K) · B(K,N) + bias) with B row-major (K,N) */
 int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc, int m,
               int n, int k, int act, float slope, void* stream);
@@ -236,6 +270,18 @@ int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, i
                        const float* temb_in, const float* coef, int with_noise, const float* noise, uint64_t seed,
                        uint64_t chain_base, float* eps_log, int eps_log_steps, void* workspace,
                        size_t workspace_bytes, void* stream);
+/* the same under SURVEY.md §8b's name */
+int damc_q_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int batch, int n_steps,
+                         const float* temb_in, const float* coef, int with_noise, const float* noise, uint64_t seed,
+                         uint64_t chain_base, float* eps_log, int eps_log_steps, void* workspace,
+                         size_t workspace_bytes, void* stream);
+/* per-op hook (SURVEY.md §8b damc_denoise_step): ONE reverse step = damc_reverse_sweep with n_steps = 1 on the
+ * step's temb_row (ntemb) and coef_row (6, HOST); noise (B, nz) injected or NULL for Philox at step index
+ * noise_step (the k-th noisy step of a sweep uses k); eps (B, nz) receives the denoiser output or NULL.
+ * workspace: damc_sweep_workspace_bytes(d, batch, 1). */
+int damc_denoise_step(const damc_denoiser_t* d, const float* xemb, float* zt, int batch, const float* temb_row,
+                      const float* coef_row, int with_noise, const float* noise, uint64_t seed, uint64_t noise_step,
+                      uint64_t chain_base, float* eps, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ----------------------------------------------- Q training: denoiser loss step */
 /* The denoiser of Q.calculate_loss (workspace/src/diffusion_net.py:624-645, Diffusion_UnetA :463-533) as

@@ -9,7 +9,7 @@ from conftest import REPO
 def _declared():
     src = open(os.path.join(REPO, "include", "damc.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(damc_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(damc_[A-Za-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_the_boundary():

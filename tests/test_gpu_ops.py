@@ -1,0 +1,126 @@
+"""GPU: the per-op hooks SURVEY.md §8(b) names — damc_convT_fwd / damc_convT_dgrad (one k4 s2 p1
+ConvTranspose2d layer, diffusion_net.py:20-203), damc_denoise_step / damc_q_reverse_sweep (the reverse step,
+diffusion_net.py:585-622), damc_ebm_grad (_netE, :207-223), damc_q_encoder_fwd (Encoder_*, :227-372, covered
+through damc.amortizer.encoder_forward in test_gpu_amortizer.py) — against fp64 PyTorch references and
+against the whole-path entry points they are cut from.
+
+Tolerances: ConvT rel-L2 <= 1e-6 against fp64 (fp32-accurate limb engine, K <= 4096); the single-step
+calls reproduce the sweep to rel 1e-6 (same kernels; the per-sweep time-MLP GEMM runs with M = 1 instead
+of M = n); the EBM alias is bitwise.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import Q_NAMES, build_q_case, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("ngf,layer", [(32, 1), (32, 2), (128, 2)])
+def test_convT_hooks_match_fp64(gpu_device, ngf, layer):
+    from damc import _lib, plans, synth
+    from damc._lib import ptr
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=ngf, nc=3), 0).to(gpu_device).eval()
+    gd = plans.generator_plan(G).refresh(gpu_device)
+    Ld = gd.layers[layer]
+    conv = G.gen[2 * layer]
+    assert isinstance(conv, torch.nn.ConvTranspose2d) and Ld.kind == _lib.LAYER_UP2
+    B = 4
+    g = torch.Generator().manual_seed(5 + layer)
+    h = torch.randn(B, Ld.cin, Ld.hin, Ld.win, generator=g, dtype=torch.float64)
+    gout = torch.randn(B, Ld.cout, Ld.hout, Ld.wout, generator=g, dtype=torch.float64)
+    w = conv.weight.detach().cpu().double()
+    b = conv.bias.detach().cpu().double()
+    L = _lib.lib()
+    nbytes = int(L.damc_convT_workspace_bytes(ctypes.byref(Ld), B))
+    assert nbytes > 0
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=gpu_device)
+    stream = _lib.stream_ptr(gpu_device)
+    # forward: lrelu(conv_transpose2d(h) + b)
+    hin = _nhwc(h.float()).to(gpu_device)
+    out = torch.empty(B, Ld.hout, Ld.wout, Ld.cout, device=gpu_device)
+    _lib.check(L.damc_convT_fwd(ctypes.byref(Ld), ptr(hin), B, ptr(out), ptr(ws), nbytes, stream), "convT_fwd")
+    ref = F.leaky_relu(F.conv_transpose2d(h.float().double(), w, b, stride=2, padding=1), 0.2)
+    assert rel_l2(out.cpu().numpy(), _nhwc(ref).numpy()) < 1e-6
+    # input gradient, masked with lrelu' of the previous layer's (activated) output h
+    mask = _nhwc(h.float()).to(gpu_device)
+    gin = torch.empty(B, Ld.hin, Ld.win, Ld.cin, device=gpu_device)
+    gdev = _nhwc(gout.float()).to(gpu_device)
+    _lib.check(L.damc_convT_dgrad(ctypes.byref(Ld), ptr(gdev), B, ptr(mask), _lib.ACT_LRELU, 0.2, ptr(gin), ptr(ws),
+                                  nbytes, stream), "convT_dgrad")
+    gref = F.conv2d(gout.float().double(), w, stride=2, padding=1)
+    gref = gref * torch.where(h.float().double() > 0, 1.0, 0.2)
+    assert rel_l2(gin.cpu().numpy(), _nhwc(gref).numpy()) < 1e-6
+    # unmasked form
+    _lib.check(L.damc_convT_dgrad(ctypes.byref(Ld), ptr(gdev), B, None, 0, 0.0, ptr(gin), ptr(ws), nbytes, stream),
+               "convT_dgrad")
+    assert rel_l2(gin.cpu().numpy(), _nhwc(F.conv2d(gout.float().double(), w, stride=2, padding=1)).numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("name", Q_NAMES[:2])
+def test_denoise_steps_reproduce_the_sweep(gpu_device, name):
+    """n single damc_denoise_step calls (injected noise, step index k) == one damc_q_reverse_sweep."""
+    from damc import _lib, amortizer
+    from damc._lib import ptr
+
+    c = build_q_case(name, gpu_device)
+    Q = c["Q"]
+    xemb = amortizer.encoder_forward(Q.encoder, c["x"])
+    plan = amortizer.DenoiserPlan(Q.p)
+    d = plan.pack(gpu_device)
+    n, B = int(Q.n_interval), c["zt0"].shape[0]
+    coef_h, temb_d = amortizer.cached_step_tables(n, Q.logsnr_min, Q.logsnr_max, Q.var_type, plan.ntemb, gpu_device)
+    L = _lib.lib()
+    stream = _lib.stream_ptr(gpu_device)
+    noise = c["eps"].contiguous()
+    # whole sweep under the SURVEY name
+    nb = int(L.damc_sweep_workspace_bytes(ctypes.byref(d), B, n))
+    ws = torch.empty(nb, dtype=torch.uint8, device=gpu_device)
+    z_sweep = c["zt0"].clone()
+    _lib.check(L.damc_q_reverse_sweep(ctypes.byref(d), ptr(xemb), ptr(z_sweep), B, n, ptr(temb_d),
+                                      coef_h.numpy().ctypes.data_as(ctypes.c_void_p), 1, ptr(noise), 0, 0, None, 0,
+                                      ptr(ws), nb, stream), "q_reverse_sweep")
+    # the same, one step per call
+    nb1 = int(L.damc_sweep_workspace_bytes(ctypes.byref(d), B, 1))
+    ws1 = torch.empty(nb1, dtype=torch.uint8, device=gpu_device)
+    z = c["zt0"].clone()
+    eps = torch.empty_like(z)
+    coef_np = np.ascontiguousarray(coef_h.numpy())
+    for k in range(n):
+        row = coef_np[k:k + 1]
+        nk = noise[k] if k < n - 1 else None
+        _lib.check(L.damc_denoise_step(ctypes.byref(d), ptr(xemb), ptr(z), B, ptr(temb_d[k:k + 1].contiguous()),
+                                       row.ctypes.data_as(ctypes.c_void_p), 1, ptr(nk), 0, k, 0, ptr(eps), ptr(ws1),
+                                       nb1, stream), "denoise_step")
+        if k == 0:
+            assert rel_l2(eps.cpu().numpy(), c["rec"]["q_post_eps3"][0]) < 1e-5
+    torch.cuda.synchronize()
+    assert rel_l2(z.cpu().numpy(), z_sweep.cpu().numpy()) < 1e-6
+
+
+def test_ebm_grad_alias_is_bitwise(gpu_device):
+    from damc import _lib, plans, synth
+    from damc._lib import ptr
+    from src import diffusion_net as dn
+
+    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
+    ed = plans.ebm_plan(E).refresh(gpu_device)
+    z = torch.from_numpy(synth.normal_f32(3, 0, (64, 128))).to(gpu_device)
+    L = _lib.lib()
+    stream = _lib.stream_ptr(gpu_device)
+    e1, g1 = torch.empty(64, device=gpu_device), torch.empty(64, 128, device=gpu_device)
+    e2, g2 = torch.empty_like(e1), torch.empty_like(g1)
+    _lib.check(L.damc_ebm_energy_grad(ctypes.byref(ed), ptr(z), 64, ptr(e1), ptr(g1), stream), "ebm_energy_grad")
+    _lib.check(L.damc_ebm_grad(ctypes.byref(ed), ptr(z), 64, ptr(e2), ptr(g2), stream), "ebm_grad")
+    torch.cuda.synchronize()
+    assert torch.equal(e1, e2) and torch.equal(g1, g2)
