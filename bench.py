@@ -5,14 +5,16 @@ One bench "step" = the Langevin block of one reference training iteration
 (workspace/train_gen_recon.py:203-209): 30 posterior steps on B=128 chains
 (sample_langevin_post_z_with_prior, sigma=.1, s=.1, noise on) + 60 prior steps on 2B=256
 chains (sample_langevin_prior_z, s=.4, noise on).  `value` counts POSTERIOR z-steps only
-(B x 30 per step and rank) against the wall time of the whole block, i.e. the prior's time is
-charged but its (cheap) z-steps are not — conservative against the CPU-reference's 130
+(30 per posterior chain and step) against the wall time of the whole block, i.e. the prior's time
+is charged but its (cheap) z-steps are not — conservative against the CPU-reference's 130
 posterior z-steps/s.
 
-Multi-GPU: one process per GPU (torchrun), B=128 chains per rank with globally-indexed
-Philox noise (chain_base = rank * B): per-GPU work is fixed -> "scaling": "weak"; the chains
-never communicate, so there is no collective in the timed path (timing uses a barrier and a
-MAX all-reduce of the elapsed time only).
+Multi-GPU: one process per GPU (torchrun).  Chains never communicate, so there is no collective in
+the timed path (timing uses a barrier and a MAX all-reduce of the elapsed time only); noise is keyed
+by the GLOBAL chain index (damc.dist.block_plan):
+  --scaling weak   (default): B=128 chains per rank -> per-GPU work fixed, "scaling": "weak";
+  --scaling strong: the global B=128 (and 2B prior) chains split over the ranks (BASELINE.md's primary
+                    curve), "scaling": "strong"; the JSON records the per-rank batch.
 
 Data: synthetic (counter-hash weights / x ~ U[-1,1] / z0 ~ N(0,1); no datasets offline).
 """
@@ -25,6 +27,7 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "diffusion-amortized-mcmc_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 (= f32 MFMA rate), MI355X_MICROARCH.md
@@ -46,24 +49,53 @@ def build(device):
     return G, E
 
 
-def inputs(device, rank):
+def inputs(device, rank, plan, scaling):
+    """This rank's posterior inputs (x, z0) and prior initial state p0 (its rows of cat(z0, N(0, I)))."""
     from damc import synth
 
-    x = torch.from_numpy(synth.uniform_f32(1 + 1000 * rank, 0, (B, 3, 32, 32))).to(device)
-    z0 = torch.from_numpy(synth.normal_f32(2 + 1000 * rank, 0, (B, NZ))).to(device)
-    return x, z0
+    if scaling == "weak":  # a full batch per rank, seeded per rank
+        x = synth.uniform_f32(1 + 1000 * rank, 0, (B, 3, 32, 32))
+        z0 = synth.normal_f32(2 + 1000 * rank, 0, (B, NZ))
+        p0 = np.concatenate([z0, synth.normal_f32(3 + 1000 * rank, 0, (B, NZ))])
+    else:  # slices of the global batch
+        s, c = plan["post_start"], plan["post_count"]
+        qs, qc = plan["prior_start"], plan["prior_count"]
+        zg = synth.normal_f32(2, 0, (B, NZ))
+        x = synth.uniform_f32(1, 0, (B, 3, 32, 32))[s:s + c]
+        z0 = zg[s:s + c]
+        p0 = np.concatenate([zg, synth.normal_f32(3, 0, (B, NZ))])[qs:qs + qc]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return t(x), t(z0), t(p0)
 
 
-def one_block(lv, G, E, x, z0, zbuf, pbuf, seed, rank):
-    """30 posterior steps on B chains + 60 prior steps on 2B chains (train_gen_recon.py:203-209)."""
+def one_block(lv, G, E, x, z0, p0, zbuf, pbuf, seed, plan):
+    """30 posterior steps + 60 prior steps on this rank's chains (train_gen_recon.py:203-209)."""
     zbuf.copy_(z0)
-    lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=seed, chain_base=rank * B)
-    pbuf[:B].copy_(z0)
-    lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=seed + 1, chain_base=rank * 2 * B)
+    lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=seed, chain_base=plan["post_start"])
+    pbuf.copy_(p0)
+    lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=seed + 1, chain_base=plan["prior_start"])
 
 
-def cpu_baseline(budget_s=12.0):
-    """Oracle (CPU restatement, fp32, op for op the reference algorithm) on a bounded sample."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(budget_s=12.0, full=False):
+    """Oracle (CPU restatement, fp32, op for op the reference algorithm) on the same CIFAR-10 inputs.
+
+    Default (bounded, ~budget_s of CPU work): 1 warm-up call, then timed calls of 1 posterior step (B=128) +
+    2 prior steps (2B=256) — the block's 30:60 step ratio — until the budget is spent; value = B / median
+    per-call time.  full=True: BASELINE.md's protocol — 3 warm-up calls, then the median of 5 full-length
+    calls (30 posterior + 60 prior steps each; several minutes of CPU)."""
     from damc import synth
     from oracle import damc_oracle as orc
     from src import diffusion_net as dn
@@ -73,23 +105,33 @@ def cpu_baseline(budget_s=12.0):
     E = synth.load_into(dn._netE(nz=NZ), 10).eval()
     L, P = orc.generator_layers(G), orc.ebm_params(E)
     x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32)))
-    z = torch.from_numpy(synth.normal_f32(2, 0, (B, NZ)))
-    zp = torch.cat([z, torch.randn_like(z)])
-    # warm-up (allocator / oneDNN primitive creation)
-    orc.posterior_langevin(L, P, z, x, 1, SIGMA, S_POST)
-    n = 0
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, NZ)))
+    zp0 = torch.cat([z0, torch.from_numpy(synth.normal_f32(3, 0, (B, NZ)))])
+    npost, nprior = (POST_STEPS, PRIOR_STEPS) if full else (1, 2)
+
+    def call():
+        orc.posterior_langevin(L, P, z0, x, npost, SIGMA, S_POST, noise=torch.randn(npost, B, NZ))
+        orc.prior_langevin(P, zp0, nprior, S_PRIOR, noise=torch.randn(nprior, 2 * B, NZ))
+
+    for _ in range(3 if full else 1):
+        call()
+    ts = []
     t0 = time.perf_counter()
     while True:
-        # per posterior step, 2 prior steps on 2B chains (the 30:60 ratio of the block)
-        z = orc.posterior_langevin(L, P, z, x, 1, SIGMA, S_POST, noise=torch.randn(1, B, NZ))
-        zp = orc.prior_langevin(P, zp, 2, S_PRIOR, noise=torch.randn(2, 2 * B, NZ))
-        n += 1
+        t1 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t1)
         el = time.perf_counter() - t0
-        if (el > budget_s and n >= 2) or n >= 200:
+        if (full and len(ts) >= 5) or (not full and ((el > budget_s and len(ts) >= 5) or len(ts) >= 200)):
             break
-    return dict(value=B * n / el, unit="z-steps/s", cores=threads, kind="port",
-                sample="%d posterior steps (B=128, CIFAR-10 G ngf=128) + %d prior steps (2B=256) of the "
-                       "fp32 oracle restatement, %.1f s" % (n, 2 * n, el))
+    med = sorted(ts)[len(ts) // 2]
+    what = ("%d full-length calls (30 posterior steps on B=128 + 60 prior steps on 2B=256) after 3 warm-ups"
+            % len(ts)) if full else ("%d timed calls of 1 posterior step (B=128) + 2 prior steps (2B=256) after 1 "
+                                      "warm-up, %.1f s" % (len(ts), el))
+    return dict(value=round(B * npost / med, 2), unit="z-steps/s", cores=threads, kind="port",
+                cpu_model=cpu_model(), statistic="median per call",
+                sample="%s of the fp32 oracle restatement (CIFAR-10 _netG_cifar10 ngf=128 + _netE), torch %d threads"
+                       % (what, threads))
 
 
 def event_ms(fn, reps=5):
@@ -106,20 +148,62 @@ def event_ms(fn, reps=5):
     return sorted(ts)[len(ts) // 2]
 
 
-def langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank):
+def langevin_breakdown(lv, G, E, x, z0, p0, zbuf, pbuf, plan):
     """the posterior (a1) and prior (a2) legs of the block timed separately."""
     def post():
         zbuf.copy_(z0)
-        lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=7, chain_base=rank * B)
+        lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=7, chain_base=plan["post_start"])
 
     def prior():
-        lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=8, chain_base=rank * 2 * B)
+        pbuf.copy_(p0)
+        lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=8, chain_base=plan["prior_start"])
 
     tp, tq = event_ms(post), event_ms(prior)
+    nb, nq = zbuf.shape[0], pbuf.shape[0]
     return {"posterior_ms_per_langevin_step": round(tp / POST_STEPS, 4),
-            "posterior_z_steps_per_s": round(B * POST_STEPS / (tp / 1e3), 1),
+            "posterior_z_steps_per_s": round(nb * POST_STEPS / (tp / 1e3), 1),
             "prior_ms_per_langevin_step": round(tq / PRIOR_STEPS, 4),
-            "prior_z_steps_per_s": round(2 * B * PRIOR_STEPS / (tq / 1e3), 1)}
+            "prior_z_steps_per_s": round(nq * PRIOR_STEPS / (tq / 1e3), 1)}
+
+
+# SURVEY.md §8(d) per-config posterior work (4 B MAC_G FLOP per batch-step) and BASELINE configs 2/4/5 at
+# their per-rank sizes on one GPU: (name, generator ctor, nz, ngf, image, B, steps, sigma)
+CONFIG_LEGS = (
+    ("svhn B=64 (config 2)", "_netG_svhn", 100, 64, 32, 64, 30, 0.1, 69.5e6),
+    ("celeba64 B=32 (config 4, per rank of 8)", "_netG_celeba64", 100, 128, 64, 32, 10, 0.1, 410.6e6),
+    ("celeba64 B=256 (config 4, one GPU)", "_netG_celeba64", 100, 128, 64, 256, 5, 0.1, 410.6e6),
+    ("celebaHQ B=8 (config 5, per rank of 8)", "_netG_celebaHQ", 128, 128, 256, 8, 5, 1.0, 6547.3e6),
+    ("celebaHQ B=64 (config 5, one GPU)", "_netG_celebaHQ", 128, 128, 256, 64, 3, 1.0, 6547.3e6),
+)
+
+
+def config_legs(lv, device, peak):
+    """ms per posterior Langevin step (G fwd + dgrad + E + update) and the fraction of the GEMM engine's
+    peak for the other BASELINE configs' generators at full width (17.8 / 420.4 / 1,676
+    GFLOP per batch-step at SVHN B=64 / CelebA-64 B=256 / CelebA-HQ B=64)."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    out = {}
+    for name, ctor, nz, ngf, hw, bsz, steps, sigma, mac in CONFIG_LEGS:
+        G = synth.load_into(getattr(dn, ctor)(nz=nz, ngf=ngf, nc=3), 0).to(device).eval()
+        E = synth.load_into(dn._netE(nz=nz), 10).to(device).eval()
+        x = torch.from_numpy(synth.uniform_f32(61, 0, (bsz, 3, hw, hw))).to(device)
+        z0 = torch.from_numpy(synth.normal_f32(62, 0, (bsz, nz))).to(device)
+        z = torch.empty_like(z0)
+
+        def run():
+            z.copy_(z0)
+            lv.posterior_langevin(z, x, G, E, steps, sigma, 0.1, True, seed=9)
+
+        ms = event_ms(run, reps=3) / steps
+        flop = 4.0 * bsz * (mac + 65.8e3)
+        out[name] = {"ms_per_step": round(ms, 3), "z_steps_per_s": round(bsz / (ms / 1e3), 1),
+                     "gflop_per_step": round(flop / 1e9, 1), "tflops": round(flop / (ms / 1e3) / 1e12, 1),
+                     "frac_of_peak": round(flop / (ms / 1e3) / 1e12 / peak, 3)}
+        del G, E, x, z0, z
+        torch.cuda.empty_cache()
+    return out
 
 
 def amortizer_bench(device):
@@ -276,8 +360,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: B=128 chains per rank (default); strong: the global B=128 split over the ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="CPU baseline by BASELINE.md's full protocol (median of 5 full-length calls; minutes)")
+    ap.add_argument("--no-config-legs", action="store_true", help="skip the SVHN / CelebA-64 / CelebA-HQ legs")
     ap.add_argument("--no-extras", action="store_true", help="skip the per-leg, amortizer and G-update timings")
     ap.add_argument("--no-torch-g", action="store_true", help="skip the stock-PyTorch G/Q-update comparisons")
     ap.add_argument("--no-live-prof", action="store_true", help="no per-launch HIP events in the timed region")
@@ -300,12 +389,14 @@ def main():
     device = torch.device("cuda", local)
 
     from damc import _lib
+    from damc import dist as ddist
     from damc import langevin as lv
 
+    plan = ddist.block_plan(B, rank, world, args.scaling)
     G, E = build(device)
-    x, z0 = inputs(device, rank)
+    x, z0, p0 = inputs(device, rank, plan, args.scaling)
     zbuf = torch.empty_like(z0)
-    pbuf = torch.randn(2 * B, NZ, device=device)
+    pbuf = torch.empty_like(p0)
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -314,7 +405,7 @@ def main():
         torch.cuda.synchronize(device)
 
     for i in range(args.warmup):
-        one_block(lv, G, E, x, z0, zbuf, pbuf, 1000 + i, rank)
+        one_block(lv, G, E, x, z0, p0, zbuf, pbuf, 1000 + i, plan)
     L = _lib.lib()
     L.damc_prof_reset()
     # live HIP events only around the dominant kernel classes (every event pair costs the stream a gap)
@@ -323,7 +414,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_block(lv, G, E, x, z0, zbuf, pbuf, 2000 + i, rank)
+        one_block(lv, G, E, x, z0, p0, zbuf, pbuf, 2000 + i, plan)
     barrier()
     elapsed = time.perf_counter() - t0
     L.damc_prof_enable(0)
@@ -348,7 +439,7 @@ def main():
     L.damc_prof_reset()
     L.damc_prof_select(None)
     L.damc_prof_enable(1)
-    one_block(lv, G, E, x, z0, zbuf, pbuf, 3000, rank)
+    one_block(lv, G, E, x, z0, p0, zbuf, pbuf, 3000, plan)
     torch.cuda.synchronize(device)
     L.damc_prof_enable(0)
     breakdown = query()
@@ -362,20 +453,26 @@ def main():
     extras = None
     if not args.no_extras and rank == 0:
         # outside the timed region (after the max-over-ranks reduction): does not enter `value`; rank 0 only
-        extras = langevin_breakdown(lv, G, E, x, z0, zbuf, pbuf, rank)
+        extras = langevin_breakdown(lv, G, E, x, z0, p0, zbuf, pbuf, plan)
         extras["amortizer"] = amortizer_bench(device)
         extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
         extras["q_update"] = q_update_bench(device, with_torch=not args.no_torch_g)
 
+    limb_peak = PEAK_BF16_TFLOPS / LIMB_PRODUCTS if limb else PEAK_FP32_TFLOPS
+    legs = None
+    if not args.no_extras and not args.no_config_legs and rank == 0:
+        legs = config_legs(lv, device, limb_peak)
+
     if rank == 0:
-        zsteps = world * B * POST_STEPS * args.steps
+        chains = world * B if args.scaling == "weak" else B
+        zsteps = chains * POST_STEPS * args.steps
         value = zsteps / t_max
         dom = max(("upconv_fwd", "upconv_dgrad"), key=lambda k: classes.get(k, {}).get("total_ms", 0.0))
         c = classes.get(dom, dict(total_ms=float("nan"), launches=1, flops=float("nan")))
         avg_s = c["total_ms"] / c["launches"] / 1e3
         flops_per_launch = c["flops"] / c["launches"]
         achieved = flops_per_launch / avg_s / 1e12
-        peak = PEAK_BF16_TFLOPS / LIMB_PRODUCTS if limb else PEAK_FP32_TFLOPS
+        peak = limb_peak
         traffic = traffic_from_profiles(dom)
         gemm_ms = sum(breakdown[k]["total_ms"] for k in breakdown if k.startswith(("upconv", "proj"))) or None
         gemm_fl = sum(breakdown[k]["flops"] for k in breakdown if k.startswith(("upconv", "proj")))
@@ -389,14 +486,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * t_max / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (counter-hash weights, x~U[-1,1], z0~N(0,1); CIFAR-10 _netG_cifar10 ngf=128 + _netE)",
             "config": {
                 "workload": "cifar10 train-iteration Langevin block: 30 posterior steps on B=128 + 60 prior "
-                            "steps on 2B=256 per rank (value counts posterior z-steps only)",
-                "global_batch": world * B, "z_dim": NZ, "ngf": NGF, "posterior_steps": POST_STEPS,
+                            "steps on 2B=256 %s (value counts posterior z-steps only)"
+                            % ("per rank" if args.scaling == "weak" else "split over the ranks"),
+                "global_batch": chains, "per_rank_batch": plan["post_count"],
+                "per_rank_prior_chains": plan["prior_count"], "z_dim": NZ, "ngf": NGF, "posterior_steps": POST_STEPS,
                 "prior_steps": PRIOR_STEPS, "sigma": SIGMA, "step_size": S_POST, "prior_step_size": S_PRIOR,
                 "parallelism": "dp%d (chains sharded, no collective)" % world,
             },
@@ -429,8 +528,10 @@ def main():
             out["amortizer"] = extras["amortizer"]
             out["g_update"] = extras["g_update"]
             out["q_update"] = extras["q_update"]
+        if legs:
+            out["config_legs"] = legs
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args.cpu_budget)
+            cb = cpu_baseline(args.cpu_budget, full=args.cpu_full)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(out))

@@ -9,6 +9,8 @@
 //         -> PROJ dgrad (split-K GEMM into slabs)  ->  fused EBM grad + slab sum + z update
 // dgrad outputs overwrite the activation they are masked with (same thread reads h, writes dh).
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "gemm.h"
@@ -953,9 +955,11 @@ int validate(const damc_generator_t* g) {
       default:
         return DAMC_ERR_ARG;
     }
+    if (L.engine != DAMC_ENGINE_LIMB && L.engine != DAMC_ENGINE_FP32) return DAMC_ERR_ARG;
     if (i > 0) {
       const damc_layer_t& P = g->layers[i - 1];
       if (P.cout != L.cin || P.hout != L.hin || P.wout != L.win) return DAMC_ERR_ARG;
+      if (P.engine != L.engine) return DAMC_ERR_ARG;  // one engine per generator
     }
     if (!last && L.act == DAMC_ACT_TANH) return DAMC_ERR_UNSUPPORTED;
   }
@@ -978,25 +982,23 @@ int proj_k_per(long K, int S) { return (int)(((K + S - 1) / S + 31) / 32 * 32); 
 
 // Limb engine (gemm.hip, fp32-accurate bf16 MFMA) for the UP2 convolutions whose gathered channel
 // count is a multiple of 32.  Packed weights and workspaces always carry the x3 copies such a layer
-// can use; damc_set_exact_fp32(1) (or DAMC_EXACT_FP32=1 at load) routes the launches to the fp32-MFMA
-// K-major engine instead.
-int g_exact_fp32 = [] {
-  const char* e = getenv("DAMC_EXACT_FP32");
-  return (e && e[0] == '1') ? 1 : 0;
-}();
+// can use; a descriptor whose layers say engine = DAMC_ENGINE_FP32 routes the launches to the fp32-MFMA
+// K-major engine instead.  The choice travels in the descriptor (no process-global state), so two
+// streams or threads may use different engines at once.
+bool limb(const damc_layer_t& L) { return L.engine == DAMC_ENGINE_LIMB; }
 bool x3_fwd_cap(const damc_layer_t& L) {
   return L.kind == DAMC_LAYER_UP2 && L.cin % damc::KM_BK == 0 && L.cout % 8 == 0;
 }
 bool x3_bwd_cap(const damc_layer_t& L) {
   return L.kind == DAMC_LAYER_UP2 && L.cout % damc::KM_BK == 0 && L.cin % 8 == 0;
 }
-bool x3_fwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_fwd_cap(L); }
+bool x3_fwd(const damc_layer_t& L) { return limb(L) && x3_fwd_cap(L); }
 // first layer z.W as a 1x1 convolution on the limb engine (z split into limbs per call)
 bool x3_proj_cap(const damc_layer_t& L) {
   return L.kind == DAMC_LAYER_PROJ && L.cin % damc::KM_BK == 0 && L.cout % 8 == 0;
 }
-bool x3_proj(const damc_layer_t& L) { return !g_exact_fp32 && x3_proj_cap(L); }
-bool x3_bwd(const damc_layer_t& L) { return !g_exact_fp32 && x3_bwd_cap(L); }
+bool x3_proj(const damc_layer_t& L) { return limb(L) && x3_proj_cap(L); }
+bool x3_bwd(const damc_layer_t& L) { return limb(L) && x3_bwd_cap(L); }
 size_t up2_floats(const damc_layer_t& L) { return (size_t)L.cin * L.cout * 16; }
 // x3 copy of a packed weight matrix, stored behind its fp32 packing (n floats, 16-B aligned)
 const unsigned short* x3_of(const float* w, size_t n) { return reinterpret_cast<const unsigned short*>(w + n); }
@@ -1015,7 +1017,7 @@ bool hbits_cap(const damc_generator_t* g, int j) {
   const bool prod = (j == 0) ? x3_proj_cap(L) : x3_fwd_cap(L);
   return prod && L.act == DAMC_ACT_LRELU && (x3_bwd_cap(N) || smallc_k3(N));
 }
-bool hbits(const damc_generator_t* g, int j) { return !g_exact_fp32 && hbits_cap(g, j); }
+bool hbits(const damc_generator_t* g, int j) { return limb(g->layers[0]) && hbits_cap(g, j); }
 // the fp32 activation j is stored unless sign bits carry the mask and the next layer's forward gathers
 // limbs (the output layer's forward reads fp32)
 bool h_f32(const damc_generator_t* g, int j) {
@@ -1601,12 +1603,6 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
   return (int)hipGetLastError();
 }
 
-extern "C" int damc_set_exact_fp32(int on) {
-  const int prev = g_exact_fp32;
-  g_exact_fp32 = on ? 1 : 0;
-  return prev;
-}
-
 extern "C" size_t damc_posterior_workspace_bytes(const damc_generator_t* g, int B) {
   if (validate(g) || B <= 0) return 0;
   return carve(g, B, nullptr, nullptr);
@@ -1789,6 +1785,15 @@ static int setup_train(const damc_generator_t* g, int B, void* wsp, size_t wsb, 
   return 0;
 }
 
+// The engine a G-update forward ran on decides which buffers it filled (limbs + sign bits, or fp32
+// activations), so the backward must run on the same one: train_forward records (batch, engine) per
+// workspace and train_backward refuses a descriptor that disagrees (DAMC_ERR_ARG) instead of reading
+// buffers the forward never wrote.  Keyed by the caller's workspace, so concurrent streams / threads with
+// their own workspaces do not interfere.
+static std::mutex g_train_mu;
+static std::unordered_map<const void*, long> g_train_rec;
+static long train_key(const damc_generator_t* g, int B) { return (long)B * 4 + g->layers[0].engine; }
+
 extern "C" int damc_generator_train_forward(const damc_generator_t* g, const float* z, int B, float* xhat, void* wsp,
                                             size_t wsb, void* stream) {
   Workspace ws;
@@ -1798,7 +1803,10 @@ extern "C" int damc_generator_train_forward(const damc_generator_t* g, const flo
   if (!z || !xhat) return DAMC_ERR_ARG;
   hipStream_t s = as_stream(stream);
   if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
-  return forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s);
+  if ((rc = forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s))) return rc;
+  std::lock_guard<std::mutex> lk(g_train_mu);
+  g_train_rec[wsp] = train_key(g, B);
+  return 0;
 }
 
 extern "C" int damc_generator_train_backward(const damc_generator_t* g, const float* z, const float* xhat,
@@ -1809,5 +1817,11 @@ extern "C" int damc_generator_train_backward(const damc_generator_t* g, const fl
   int rc = setup_train(g, B, wsp, wsb, &ws, &tw);
   if (rc) return rc;
   if (!z || !xhat || !grad_xhat || !grads) return DAMC_ERR_ARG;
+  {
+    std::lock_guard<std::mutex> lk(g_train_mu);
+    auto it = g_train_rec.find(wsp);
+    if (it == g_train_rec.end() || it->second != train_key(g, B)) return DAMC_ERR_ARG;
+    g_train_rec.erase(it);
+  }
   return train_backward(g, B, z, xhat, grad_xhat, grads, grad_z, ws, tw, as_stream(stream));
 }

@@ -160,7 +160,8 @@ __global__ __launch_bounds__(kThreads) void grad_norm_finish_kernel(const float*
     const float norm = (float)sqrt(red[0]);
     const float coef = max_norm / (norm + 1e-6f);  // clip_grad.py: max_norm / (total_norm + 1e-6), fp32
     out[0] = norm;
-    out[1] = fminf(coef, 1.0f);
+    // torch.clamp(coef, max=1.0) propagates a NaN (non-finite total norm); fminf would return 1 instead
+    out[1] = (coef != coef) ? coef : fminf(coef, 1.0f);
   }
 }
 

@@ -6,12 +6,15 @@ this directory.  There is deliberately NO fallback: if the .so is missing or a c
 """
 import ctypes
 import os
+import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DAMC_LIB_PATH: an alternative in-tree build for A/B timing (tools/); the default is the product library
 LIB_PATH = os.environ.get("DAMC_LIB_PATH") or os.path.join(_HERE, "libdamc.so")
 
+ABI_VERSION = 2
 MAX_LAYERS = 10
+ENGINE_LIMB, ENGINE_FP32 = 0, 1
 LAYER_PROJ, LAYER_UP2, LAYER_SMALLC, LAYER_LINEAR = 1, 2, 3, 4
 ACT_NONE, ACT_LRELU, ACT_TANH = 0, 1, 2
 
@@ -26,6 +29,7 @@ class Layer(ctypes.Structure):
         ("hin", ctypes.c_int), ("win", ctypes.c_int), ("hout", ctypes.c_int), ("wout", ctypes.c_int),
         ("act", ctypes.c_int), ("slope", ctypes.c_float),
         ("w_fwd", ctypes.c_void_p), ("w_bwd", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("engine", ctypes.c_int),
     ]
 
 
@@ -121,7 +125,6 @@ _SIGS = {
     "damc_generator_layer_packed_sizes": (_I, [ctypes.POINTER(Layer), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "damc_pack_generator_layer": (_I, [ctypes.POINTER(Layer), _P, _P, _P, _P]),
     "damc_pack_ebm": (_I, [ctypes.POINTER(Ebm), _P, _P, _P]),
-    "damc_set_exact_fp32": (_I, [_I]),
     "damc_posterior_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
     "damc_posterior_langevin": (_I, [ctypes.POINTER(Generator), ctypes.POINTER(Ebm), _P, _P, _I, _I, _F, _F, _I, _P,
                                      _U64, _U64, _U64, _P, _P, _SZ, _P]),
@@ -172,6 +175,8 @@ _SIGS = {
     "damc_grad_norm_finish": (_I, [_P, _I, _F, _P, _P]),
     "damc_grad_scale": (_I, [_P, _I, _P, _I, _P, _P]),
     "damc_adam_step": (_I, [_P, _I, _P, _P, _P, _P, _I, ctypes.POINTER(AdamHparams), _P, _P]),
+    "damc_fid_accumulate": (_I, [_P, _I, _I, _P, _P, _P]),
+    "damc_fid_mean_cov": (_I, [_P, _P, ctypes.c_double, _I, _P, _P, _P]),
     "damc_prof_enable": (_I, [_I]),
     "damc_prof_reset": (_I, []),
     "damc_prof_select": (_I, [ctypes.c_char_p]),
@@ -201,24 +206,38 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.damc_abi_version() != 1:
+        if handle.damc_abi_version() != ABI_VERSION:
             raise DamcError("libdamc ABI mismatch")
         _lib = handle
     return _lib
 
 
+_engine_state = threading.local()
+
+
+def current_engine():
+    """The generator convolution engine descriptors get when they are (re)packed on this thread:
+    ENGINE_LIMB unless inside ``exact_fp32()`` (or DAMC_EXACT_FP32=1 in the environment)."""
+    e = getattr(_engine_state, "engine", None)
+    if e is None:
+        e = ENGINE_FP32 if os.environ.get("DAMC_EXACT_FP32", "0") == "1" else ENGINE_LIMB
+    return e
+
+
 class exact_fp32:
-    """Context manager: run the generator convolutions on the fp32-MFMA engine instead of the limb engine."""
+    """Context manager: generator convolutions packed inside it run on the fp32-MFMA engine instead of the
+    limb engine.  The choice is per thread and travels in each call's descriptor (no library-global state)."""
 
     def __init__(self, on=True):
         self.on = on
 
     def __enter__(self):
-        self.prev = lib().damc_set_exact_fp32(1 if self.on else 0)
+        self.prev = getattr(_engine_state, "engine", None)
+        _engine_state.engine = ENGINE_FP32 if self.on else ENGINE_LIMB
         return self
 
     def __exit__(self, *exc):
-        lib().damc_set_exact_fp32(self.prev)
+        _engine_state.engine = self.prev
         return False
 
 

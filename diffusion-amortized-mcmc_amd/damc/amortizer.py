@@ -244,8 +244,13 @@ def reverse_sweep(Q, xemb, zt, noise=None, seed=None, chain_base=0, eps_log_step
     return eps_log
 
 
-def q_forward(Q, x=None, b=None, device=None, cond_w=-1):
-    """_netQ_U.forward on the HIP path (diffusion_net.py:585-622)."""
+def q_forward(Q, x=None, b=None, device=None, cond_w=-1, zt=None, seed=None, chain_base=0):
+    """_netQ_U.forward on the HIP path (diffusion_net.py:585-622).
+
+    zt / seed / chain_base (not in the reference's signature; sharded callers only): the initial latent
+    (default: torch.randn(b, nz) on the host generator, as the reference), the sweep's Philox key and the
+    global index of row 0 — a shard that passes its slice of the global zt, the global seed and its slice
+    start reproduces its rows of the 1-GPU sweep bit for bit."""
     if cond_w is not None and cond_w > 0 and x is not None:
         raise NotImplementedError("classifier-free guidance (cond_w > 0) is dead code in the reference drivers")
     if x is not None:
@@ -256,8 +261,10 @@ def q_forward(Q, x=None, b=None, device=None, cond_w=-1):
     else:
         device = torch.device(device) if device is not None else torch.device("cuda")
         xemb = prior_embedding(Q, torch.randn(b, Q.nz, device=device))
-    zt = torch.randn(b, Q.nz).to(device)
+    zt = torch.randn(b, Q.nz).to(device) if zt is None else zt.to(device=device, dtype=torch.float32).clone()
     if zt.device.type != "cuda":
         raise _lib.DamcError("the HIP sweep needs a ROCm device (got %s)" % zt.device)
-    reverse_sweep(Q, xemb, zt)
+    if zt.shape != (b, Q.nz):
+        raise _lib.DamcError("zt must be (%d, %d)" % (b, Q.nz))
+    reverse_sweep(Q, xemb, zt, seed=seed, chain_base=chain_base)
     return zt

@@ -21,6 +21,26 @@ def shard(global_batch, rank, world):
     return start, base + (1 if rank < rem else 0)
 
 
+def block_plan(global_batch, rank, world, scaling="weak"):
+    """Which chains one rank runs in a Langevin block (bench.py; train_gen_recon.py:203-209: posterior on B
+    chains, prior on 2B = cat(z0, N(0, I)) chains), and the global index of its first chain of each kind.
+
+    weak:   every rank runs a full batch of its own (B posterior + 2B prior chains); rank r's chains are
+            global chains [r B, (r+1) B) and [2 r B, 2 (r+1) B) -> noise streams never collide.
+    strong: the global batch is split: posterior rows shard(B) and prior rows shard(2B) of the global
+            arrays; chain_base = the slice start, so the union over ranks is the 1-GPU block bit for bit.
+    Returns dict(post_start, post_count, prior_start, prior_count) — *_start are the chain_base values (and,
+    for strong, the slice offsets into the global inputs)."""
+    B = int(global_batch)
+    if scaling == "weak":
+        return dict(post_start=rank * B, post_count=B, prior_start=rank * 2 * B, prior_count=2 * B)
+    if scaling == "strong":
+        ps, pc = shard(B, rank, world)
+        qs, qc = shard(2 * B, rank, world)
+        return dict(post_start=ps, post_count=pc, prior_start=qs, prior_count=qc)
+    raise ValueError("scaling must be 'weak' or 'strong', got %r" % (scaling,))
+
+
 def _dist():
     import torch.distributed as d
 
@@ -82,20 +102,25 @@ def sharded_recon_mse(Q, G, E, batches, g_l_steps=10, g_llhd_sigma=0.1, g_l_step
     """Eval reconstruction MSE over global batches, each split across ranks (eval_gen_recon.py:177-212).
 
     batches: iterable of global x batches (identical on every rank); rank r processes its slice.
+    Every rank draws the same global initial latents and sweep key from its (identically seeded) torch
+    generator and runs its slice with chain_base = the slice start, so the Q sweep and the posterior
+    chains of the union of the shards are bitwise the 1-GPU run's.
     """
-    from . import langevin
+    from . import amortizer, langevin
 
     d = _dist()
     rank, world = (d.get_rank(), d.get_world_size()) if d is not None else (0, 1)
     meter = None
     for x in batches:
         s, c = shard(x.shape[0], rank, world)
+        zt = torch.randn(x.shape[0], Q.nz)  # global draws, identical on every rank (host generator)
+        seed = langevin.new_seed()
         if c == 0:
             continue
         xs = x[s:s + c].contiguous()
         meter = meter or ReconMSE(xs.device)
         with torch.no_grad():
-            z = Q(xs)
+            z = amortizer.q_forward(Q, x=xs, zt=zt[s:s + c], seed=seed, chain_base=s)
         langevin.posterior_langevin(z, xs, G, E, g_l_steps, g_llhd_sigma, g_l_step_size, False, chain_base=s)
         meter.update(langevin.generator_forward(z, G), xs)
     if meter is None:

@@ -103,6 +103,8 @@ def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, st
     B = z.shape[0]
     if noise is not None:
         noise = _f32c(noise.to(dev), "noise")
+        if noise.numel() < n_steps * B * ep.nz:
+            raise _lib.DamcError("noise must hold (n_steps, B, nz) values")
     if seed is None:
         seed = new_seed() if (with_noise and noise is None) else 0
     dg = torch.zeros(max(n_steps, 1), 2, dtype=torch.float32, device=dev) if diag else None
@@ -131,8 +133,15 @@ def philox_normal(n_steps, batch, nz, seed, device, step_offset=0, chain_base=0,
 
 
 def z_update(z, g, step, with_noise, noise=None, seed=0, step_index=0, chain_base=0):
+    """Per-op hook: z <- z - 0.5 step^2 (g + z) (+ step xi), in place (MCMC.py:36-38,62-64)."""
     _f32c(z, "z")
     _f32c(g, "g")
+    if g.shape != z.shape:
+        raise _lib.DamcError("g must have z's shape")
+    if noise is not None:
+        noise = _f32c(noise, "noise")
+        if noise.numel() < z.numel():
+            raise _lib.DamcError("noise must hold (B, nz) values")
     check(_lib.lib().damc_z_update(ptr(z), ptr(g), z.shape[0], z.shape[1], float(step), int(bool(with_noise)),
                                    ptr(noise), seed, step_index, chain_base, _lib.stream_ptr(z.device)),
           "damc_z_update")

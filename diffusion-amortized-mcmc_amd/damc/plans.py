@@ -115,9 +115,11 @@ class GeneratorPlan:
             d.w_bwd = wb.data_ptr() if bwd.value else None
         self.desc = desc
 
-    def refresh(self, device):
-        """(Re)pack the live parameters; returns the ctypes descriptor."""
+    def refresh(self, device, engine=None):
+        """(Re)pack the live parameters; returns the ctypes descriptor.  engine: _lib.ENGINE_* for every layer
+        (default: _lib.current_engine() of the calling thread)."""
         device = torch.device(device)
+        engine = _lib.current_engine() if engine is None else int(engine)
         if device.type != "cuda":
             raise _lib.DamcError("the HIP generator path needs CUDA (ROCm) tensors, got %s" % device)
         if self.device != device or self.desc is None:
@@ -132,6 +134,7 @@ class GeneratorPlan:
                 self._keep.append(w)
             wf, wb = self.buffers[i]
             d = self.desc.layers[i]
+            d.engine = engine
             check(L.damc_pack_generator_layer(ctypes.byref(d), ptr(w), ptr(wf),
                                               ptr(wb) if d.w_bwd else None, stream), "pack generator layer")
             if m.bias is not None:

@@ -17,6 +17,7 @@ requiring grad) it is the plain HIP forward.
 """
 import contextlib
 import ctypes
+import weakref
 
 import torch
 
@@ -66,7 +67,11 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(L.damc_generator_train_forward(ctypes.byref(desc), ptr(zc), B, ptr(xh), ptr(ws), nbytes,
                                              _lib.stream_ptr(dev)), "damc_generator_train_forward")
         ctx.plan, ctx.ws, ctx.nbytes = plan, ws, nbytes
-        ctx.desc, ctx.keep = desc, (plan.buffers, getattr(plan, "_keep", None))
+        # a private copy: a later refresh of the plan (other engine, other thread) must not change what the
+        # backward runs on — it has to be the engine that filled this workspace
+        ctx.desc = type(desc).from_buffer_copy(desc)
+        ctx.keep = (plan.buffers, getattr(plan, "_keep", None))
+        ctx.plan_desc = desc
         ctx.save_for_backward(zc, xh, *params)
         return xh
 
@@ -78,7 +83,10 @@ class _GeneratorTrainFn(torch.autograd.Function):
         # the saved parameters are the modules' own and autograd has checked they were not modified in place,
         # so the packed buffers still hold the forward's weights (any re-pack in between wrote the same
         # values); re-pack only if the plan re-allocated them (device change)
-        desc = ctx.desc if plan.desc is ctx.desc else plan.refresh(dev)
+        desc = ctx.desc
+        if plan.desc is not ctx.plan_desc:  # buffers re-allocated (device change): re-pack, same engine
+            fresh = plan.refresh(dev, engine=desc.layers[0].engine)
+            desc = type(fresh).from_buffer_copy(fresh)
         gx = gx.to(torch.float32).contiguous()
         grads = _lib.GeneratorGrads()
         outs = []
@@ -91,7 +99,7 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(_lib.lib().damc_generator_train_backward(
             ctypes.byref(desc), ptr(zc), ptr(xh), ptr(gx), zc.shape[0], ctypes.byref(grads), ptr(gz), ptr(ctx.ws),
             ctx.nbytes, _lib.stream_ptr(dev)), "damc_generator_train_backward")
-        ctx.ws = ctx.desc = ctx.keep = None
+        ctx.ws = ctx.desc = ctx.keep = ctx.plan_desc = None
         return (gz, None, *outs)
 
 
@@ -215,7 +223,7 @@ def denoiser_apply(p, zt, se, xemb):
 # roles swapped for the k4 s2 p1 convs).  Shapes the C side does not cover keep the stock PyTorch path
 # (encoder_train_supported is False for them; the Q-update tests assert which path ran).
 
-_ENC_SUPPORT = {}
+_ENC_SUPPORT = weakref.WeakKeyDictionary()  # encoder -> {input shape: verdict}; dies with the encoder
 
 
 def _enc_stages(enc):
@@ -234,8 +242,9 @@ def _enc_params(stages):
 
 
 def encoder_train_supported(enc, x):
-    key = (id(enc), tuple(x.shape))
-    hit = _ENC_SUPPORT.get(key)
+    per_enc = _ENC_SUPPORT.setdefault(enc, {})
+    key = tuple(x.shape)
+    hit = per_enc.get(key)
     if hit is not None:
         return hit
     ok = True
@@ -255,7 +264,7 @@ def encoder_train_supported(enc, x):
         ok = ok and H == 1 and W == 1
     except NotImplementedError:
         ok = False
-    _ENC_SUPPORT[key] = ok
+    per_enc[key] = ok
     return ok
 
 

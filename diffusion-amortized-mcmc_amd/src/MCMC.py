@@ -97,11 +97,14 @@ def gen_samples_with_diffusion_prior(b, device, netQ, netG):
 
 
 def _fid(fid_samples, real_m, real_s, save_name):
-    import pytorch_fid_wrapper as pfw  # third-party, not vendored (FID parity unpinned)
+    """pfw.fid(samples, real_m, real_s) (MCMC.py:136-139) with the statistics on the HIP path: Inception pool
+    features (pytorch-fid, third-party: SURVEY.md §8c, FID parity unpinned) -> damc_fid_accumulate (fp64
+    sum f / sum f f^T on the device) -> mu, sigma -> pytorch-fid's Frechet distance (damc.fid)."""
+    from damc import fid as _dfid
 
     fid_samples = torch.cat(fid_samples, dim=0)
     fid_samples = (1.0 + torch.clamp(fid_samples, min=-1.0, max=1.0)) / 2.0
-    fid = pfw.fid(fid_samples, real_m=real_m, real_s=real_s, device="cuda:0")
+    fid = _dfid.fid_of_samples(fid_samples.to("cuda:0"), real_m, real_s)
     if save_name is not None:
         import torchvision
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DAMC_ABI_VERSION 1
+#define DAMC_ABI_VERSION 2
 #define DAMC_MAX_LAYERS 10
 
 enum {
@@ -50,6 +50,13 @@ enum {
   DAMC_LAYER_LINEAR = 4  /* nn.Linear (toy MLP generator)                                  */
 };
 enum { DAMC_ACT_NONE = 0, DAMC_ACT_LRELU = 1, DAMC_ACT_TANH = 2, DAMC_ACT_SILU = 3 };
+/* Convolution engine of a generator layer (every layer of one generator must name the same one):
+ *   DAMC_ENGINE_LIMB: layers whose gathered channel count is a multiple of 32 run on the limb engine —
+ *     fp32 operands split into 3 bf16 limbs, 6 limb products per fp32 product on bf16 MFMA, fp32
+ *     accumulation (error vs fp64 equal to fp32 MFMA's); the other layers on the fp32 MFMA engine;
+ *   DAMC_ENGINE_FP32: every convolution on the fp32 MFMA engine (v_mfma_f32_32x32x2_f32).
+ * Packed weights and workspaces are sized for either engine. */
+enum { DAMC_ENGINE_LIMB = 0, DAMC_ENGINE_FP32 = 1 };
 
 typedef struct {
   int kind;
@@ -60,6 +67,7 @@ typedef struct {
   const float* w_fwd;        /* packed forward weights  (damc_pack_generator_layer)       */
   const float* w_bwd;        /* packed dgrad weights                                      */
   const float* bias;         /* (cout) or NULL                                            */
+  int engine;                /* DAMC_ENGINE_* (0 = limb engine, the default)              */
 } damc_layer_t;
 
 typedef struct {
@@ -86,12 +94,6 @@ int damc_generator_layer_packed_sizes(const damc_layer_t* layer, size_t* fwd_flo
 /* re-lay PyTorch weight (ConvT: (Cin,Cout,k,k); Linear: (out,in)) into layer->w_fwd / w_bwd */
 int damc_pack_generator_layer(const damc_layer_t* layer, const float* w_torch, float* w_fwd, float* w_bwd,
                               void* stream);
-/* Generator convolutions whose gathered channel count is a multiple of 32 run on the limb engine by
- * default: fp32 operands split into 3 bf16 limbs, 6 limb products per fp32 product on bf16 MFMA, fp32
- * accumulation (error vs fp64 equal to fp32 MFMA's).  on != 0 selects the fp32-MFMA engine
- * (v_mfma_f32_32x32x2_f32) for later launches; returns the previous setting.  Initial value: env
- * DAMC_EXACT_FP32=1.  Packed weights / workspaces are sized for either engine. */
-int damc_set_exact_fp32(int on);
 /* w1t (nz,nh) and w2t (nh,nh) from the PyTorch w1/w2 */
 int damc_pack_ebm(const damc_ebm_t* ebm, float* w1t, float* w2t, void* stream);
 
@@ -136,9 +138,10 @@ int damc_convT_dgrad(const damc_layer_t* layer, const float* gout, int batch, co
  * weight and bias gradients of every layer (PyTorch layouts: ConvTranspose2d (Cin, Cout, k, k), Linear
  * (out, in); WRITTEN, not accumulated; NULL entries are skipped) and, if grad_z != NULL, dL/dz (B, nz).
  * The two calls must use the same descriptor, batch and workspace, with no other call on that workspace in
- * between.  ConvT weight gradients run on the limb engine (fp32-accurate bf16 MFMA) whatever
- * damc_set_exact_fp32 says; layer inputs and gradients with a batch that is not a multiple of 32 are
- * zero-padded to one. */
+ * between: train_forward records (workspace, batch, engine) and train_backward returns DAMC_ERR_ARG for a
+ * descriptor or batch that disagrees.  ConvT weight gradients run on the limb engine (fp32-accurate bf16
+ * MFMA) whatever the layers' engine; layer inputs and gradients with a batch that is not a multiple of 32
+ * are zero-padded to one. */
 typedef struct {
   float* w[DAMC_MAX_LAYERS];
   float* b[DAMC_MAX_LAYERS];
@@ -357,6 +360,15 @@ int damc_grad_scale(const void* dev_chunks, int nchunks, float* const* grads, in
 int damc_adam_step(const void* dev_chunks, int nchunks, float* const* params, float* const* grads,
                    float* const* exp_avgs, float* const* exp_avg_sqs, int ntensors, const damc_adam_hparams_t* hp,
                    const float* clip, void* stream);
+
+/* ------------------------------------------------------------ FID statistics */
+/* calculate_fid* (workspace/src/MCMC.py:130-176) reduce Inception pool features to (mu, sigma) before the
+ * Frechet distance (pytorch-fid's calculate_frechet_distance, via pfw.fid).  Here the statistics accumulate on
+ * the device in fp64: s1 (d) += sum over the n rows of feats (n, d) fp32, s2 (d, d) += feats^T feats; across
+ * GPUs the caller all-reduces (s1, s2, n) once (damc.fid over RCCL).  Deterministic (fixed summation order). */
+int damc_fid_accumulate(const float* feats, int n, int d, double* s1, double* s2, void* stream);
+/* mu = s1 / n, sigma = (s2 - n mu mu^T) / (n - 1) (np.cov's unbiased estimate); n > 1 */
+int damc_fid_mean_cov(const double* s1, const double* s2, double n, int d, double* mu, double* sigma, void* stream);
 
 /* --------------------------------------------------------------------------- profiling */
 /* optional per-kernel HIP-event timing (bench.py roofline): records events around each

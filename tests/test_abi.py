@@ -34,11 +34,51 @@ def test_host_only_calls():
     from damc import _lib
 
     L = _lib.lib()
-    assert L.damc_abi_version() == 1
+    assert L.damc_abi_version() == _lib.ABI_VERSION == 2
     assert b"invalid" in L.damc_error_string(1001)
     # descriptor validation runs on the host: an empty generator has no workspace
     g = _lib.Generator()
     assert L.damc_posterior_workspace_bytes(ctypes.byref(g), 8) == 0
+
+
+def _cifar_desc(ngf=16):
+    """_netG_cifar10 topology (diffusion_net.py:20-51) as a host-side descriptor (no device pointers)."""
+    from damc import _lib
+
+    g = _lib.Generator()
+    g.n_layers, g.nz, g.nc, g.h, g.w = 4, 128, 3, 32, 32
+    spec = [(_lib.LAYER_PROJ, 128, ngf * 8, 8, 1, 0, 1, 8), (_lib.LAYER_UP2, ngf * 8, ngf * 4, 4, 2, 1, 8, 16),
+            (_lib.LAYER_UP2, ngf * 4, ngf * 2, 4, 2, 1, 16, 32), (_lib.LAYER_SMALLC, ngf * 2, 3, 3, 1, 1, 32, 32)]
+    for i, (kind, cin, cout, k, s, p, hin, hout) in enumerate(spec):
+        d = g.layers[i]
+        d.kind, d.cin, d.cout, d.k, d.stride, d.pad = kind, cin, cout, k, s, p
+        d.hin = d.win = hin
+        d.hout = d.wout = hout
+        d.act, d.slope = (_lib.ACT_TANH, 0.0) if i == 3 else (_lib.ACT_LRELU, 0.2)
+    return g
+
+
+def test_engine_field_is_validated_host_only():
+    """The convolution engine is a per-descriptor field (ABI 2): limb (default) and fp32 descriptors are
+    valid and size the same workspace; a generator mixing engines, or naming an unknown one, is refused."""
+    from damc import _lib
+
+    L = _lib.lib()
+    g = _cifar_desc()
+    n_limb = L.damc_posterior_workspace_bytes(ctypes.byref(g), 8)
+    assert n_limb > 0
+    for i in range(4):
+        g.layers[i].engine = _lib.ENGINE_FP32
+    assert L.damc_posterior_workspace_bytes(ctypes.byref(g), 8) == n_limb
+    g.layers[2].engine = _lib.ENGINE_LIMB
+    assert L.damc_posterior_workspace_bytes(ctypes.byref(g), 8) == 0
+    g.layers[2].engine = 7
+    assert L.damc_posterior_workspace_bytes(ctypes.byref(g), 8) == 0
+    # the Python default engine is per thread
+    assert _lib.current_engine() == _lib.ENGINE_LIMB
+    with _lib.exact_fp32():
+        assert _lib.current_engine() == _lib.ENGINE_FP32
+    assert _lib.current_engine() == _lib.ENGINE_LIMB
 
 
 def test_training_shape_support_host_only():

@@ -74,3 +74,71 @@ def test_reductions_match_single_process():
         assert abs(mse - want_mse) < 1e-12
         assert torch.allclose(mu, want_mu, atol=1e-12)
         assert torch.allclose(sigma, want_sigma, atol=1e-10)
+
+
+def _plan_worker(rank, world, port, q):
+    """One rank of a strong-scaling bench block: its plan and its slices of the global inputs."""
+    import sys
+
+    import torch.distributed as d
+
+    from conftest import REPO
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    d.init_process_group("gloo", rank=rank, world_size=world)
+    plan = ddist.block_plan(bench.B, rank, world, "strong")
+    x, z0, p0 = bench.inputs(torch.device("cpu"), rank, plan, "strong")
+    # reassemble on every rank: gather the per-rank row counts, then the padded slices
+    counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    d.all_gather(counts, torch.tensor([plan["post_count"], plan["prior_count"]]))
+    pad = lambda t, n: torch.cat([t, t.new_zeros((n - t.shape[0],) + tuple(t.shape[1:]))])  # noqa: E731
+    mx, mq = max(int(c[0]) for c in counts), max(int(c[1]) for c in counts)
+    gx = [torch.empty((mx,) + tuple(x.shape[1:])) for _ in range(world)]
+    gz = [torch.empty(mx, z0.shape[1]) for _ in range(world)]
+    gp = [torch.empty(mq, p0.shape[1]) for _ in range(world)]
+    d.all_gather(gx, pad(x, mx))
+    d.all_gather(gz, pad(z0, mx))
+    d.all_gather(gp, pad(p0, mq))
+    bases = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    d.all_gather(bases, torch.tensor([plan["post_start"], plan["prior_start"]]))
+    if rank == 0:
+        n = [(int(c[0]), int(c[1])) for c in counts]
+        q.put((torch.cat([g[:c] for g, (c, _) in zip(gx, n)]), torch.cat([g[:c] for g, (c, _) in zip(gz, n)]),
+               torch.cat([g[:c] for g, (_, c) in zip(gp, n)]), [tuple(int(v) for v in b) for b in bases], n))
+    d.destroy_process_group()
+
+
+def test_strong_scaling_plan_reassembles_the_global_block():
+    """bench.py --scaling strong over gloo, world 2: the ranks' slices of x / z0 / the prior chains
+    concatenate to the global B=128 block (2B = 256 prior chains = cat(z0, N(0, I))), and each rank's Philox
+    chain_base is the global index of its first chain, so noise streams are those of the 1-GPU block."""
+    import sys
+
+    from conftest import REPO
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    x, z0, p0, bases, counts = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    plan1 = ddist.block_plan(bench.B, 0, 1, "strong")
+    gx, gz, gp = bench.inputs(torch.device("cpu"), 0, plan1, "strong")
+    assert torch.equal(x, gx) and torch.equal(z0, gz) and torch.equal(p0, gp)
+    assert gp.shape[0] == 2 * bench.B and torch.equal(gp[:bench.B], gz)
+    assert bases == [(0, 0), (counts[0][0], counts[0][1])]
+    assert sum(c for c, _ in counts) == bench.B and sum(c for _, c in counts) == 2 * bench.B
+    weak = [ddist.block_plan(bench.B, r, 4, "weak") for r in range(4)]
+    assert [w["post_start"] for w in weak] == [0, 128, 256, 384]
+    assert [w["prior_start"] for w in weak] == [0, 256, 512, 768]

@@ -246,7 +246,63 @@ def test_limb_engine_as_accurate_as_fp32_mfma(lv, gpu_device):
     limb = run()
     with _lib.exact_fp32():
         exact = run()
-    assert _lib.lib().damc_set_exact_fp32(0) == 0  # the context restored the default engine
+    assert _lib.current_engine() == _lib.ENGINE_LIMB  # the context restored the default engine
     for got, ex, ref in zip(limb, exact, (g64, x64, z64)):
         e_limb, e_exact = rel_l2(got, ref), rel_l2(ex, ref)
         assert e_limb <= 1.5 * e_exact + 1e-7, (e_limb, e_exact)
+
+
+def test_engine_is_per_call_not_global(lv, gpu_device):
+    """The engine travels in each call's descriptor: a thread inside exact_fp32() and the main thread on the
+    limb engine run at the same time without affecting each other, and each reproduces its own serial result."""
+    import threading
+
+    from damc import _lib
+
+    G, E, x, z0 = _cifar_full(gpu_device, 8)
+    limb = lv.likelihood_grad(z0, x, G, 0.1).cpu()
+    with _lib.exact_fp32():
+        exact = lv.likelihood_grad(z0, x, G, 0.1).cpu()
+    assert not torch.equal(limb, exact)  # the two engines round differently
+    out = {}
+
+    def worker():
+        with _lib.exact_fp32():
+            for _ in range(4):
+                out["exact"] = lv.likelihood_grad(z0, x, G, 0.1).cpu()
+
+    t = threading.Thread(target=worker)
+    t.start()
+    for _ in range(4):
+        out["limb"] = lv.likelihood_grad(z0, x, G, 0.1).cpu()
+    t.join()
+    assert torch.equal(out["limb"], limb) and torch.equal(out["exact"], exact)
+
+
+def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
+    """x_hat = G(z) inside exact_fp32() with loss.backward() outside must give the exact engine's
+    gradients (the backward uses the forward's recorded engine), not read buffers the forward never wrote."""
+    from damc import _lib
+
+    G, E, x, z0 = _cifar_full(gpu_device, 8)
+    G.train()
+    for p in G.parameters():
+        p.requires_grad_(True)
+
+    def grads(inside):
+        G.zero_grad(set_to_none=True)
+        if inside:
+            with _lib.exact_fp32():
+                xh = G(z0)
+            loss = torch.sum((xh - x) ** 2, dim=[1, 2, 3]).mean()
+        else:
+            with _lib.exact_fp32():
+                xh = G(z0)
+                loss = torch.sum((xh - x) ** 2, dim=[1, 2, 3]).mean()
+        loss.backward()  # outside the context when inside=True
+        return [p.grad.detach().clone() for p in G.parameters()]
+
+    split = grads(True)
+    whole = grads(False)
+    for a, b in zip(split, whole):
+        assert torch.equal(a, b)

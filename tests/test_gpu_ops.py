@@ -124,3 +124,29 @@ def test_ebm_grad_alias_is_bitwise(gpu_device):
     _lib.check(L.damc_ebm_grad(ctypes.byref(ed), ptr(z), 64, ptr(e2), ptr(g2), stream), "ebm_grad")
     torch.cuda.synchronize()
     assert torch.equal(e1, e2) and torch.equal(g1, g2)
+
+
+def test_z_update_hook_vs_oracle(gpu_device):
+    """damc_z_update (include/damc.h): z <- z - 0.5 s^2 (g + z) (+ s xi), separately rounded as the reference's
+    z.data - 0.5*s*s*z_grad and + s*randn (MCMC.py:36-38,62-64) — bitwise against the same fp32 ops on the CPU,
+    with injected noise and with the in-kernel Philox draw (= damc_philox_normal's stream)."""
+    from damc import langevin as lv
+
+    g0 = torch.Generator().manual_seed(3)
+    z0 = torch.randn(37, 128, generator=g0)
+    g = torch.randn(37, 128, generator=g0)
+    xi = torch.randn(37, 128, generator=g0)
+    s = 0.1
+    c1 = np.float32(0.5 * s * s)
+    want = (z0 - torch.tensor(c1) * (g + z0)) + torch.tensor(np.float32(s)) * xi
+    z = z0.to(gpu_device)
+    lv.z_update(z, g.to(gpu_device), s, True, noise=xi.to(gpu_device))
+    assert torch.equal(z.cpu(), want)
+    z = z0.to(gpu_device)
+    lv.z_update(z, g.to(gpu_device), s, False)
+    assert torch.equal(z.cpu(), z0 - torch.tensor(c1) * (g + z0))
+    # in-kernel Philox: the posterior stream of damc_philox_normal at the same (seed, step, chain)
+    z = z0.to(gpu_device)
+    lv.z_update(z, g.to(gpu_device), s, True, seed=11, step_index=4, chain_base=100)
+    xi_k = lv.philox_normal(1, 37, 128, seed=11, device=gpu_device, step_offset=4, chain_base=100)[0].cpu()
+    assert torch.equal(z.cpu(), (z0 - torch.tensor(c1) * (g + z0)) + torch.tensor(np.float32(s)) * xi_k)
