@@ -332,7 +332,7 @@ bool ebm_shape_ok(int R, int nz, int nh) {
 
 // host helpers used by generator.hip
 int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
-                                 int nz, float step, int with_noise, const float* noise, uint64_t seed,
+                                 int nz, double step, int with_noise, const float* noise, uint64_t seed,
                                  uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s) {
   damc_ebm_t ev{};
   int use_ebm = 0;
@@ -342,17 +342,17 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
     if (ev.nz != nz) return DAMC_ERR_ARG;
   }
   if (!ebm_shape_ok(RU, nz, use_ebm ? ev.nh : 0)) return DAMC_ERR_UNSUPPORTED;
-  const float c1 = (float)(0.5 * (double)step * (double)step);
+  const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
   const size_t sm = ebm_smem_floats(RU, nz, use_ebm ? ev.nh : 0) * sizeof(float);
   ProfScope ps("posterior_update", 0.0, s);
   hipLaunchKernelGGL((posterior_update_kernel<RU>), dim3((B + RU - 1) / RU), dim3(EBM_THREADS), sm, s, ev, use_ebm, z, slabs,
-                     nslab, slab_stride, B, nz, c1, step, with_noise, noise, seed, step_idx, chain_base, diag);
+                     nslab, slab_stride, B, nz, c1, (float)step, with_noise, noise, seed, step_idx, chain_base, diag);
   return (int)hipGetLastError();
 }
 
 extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* stream);
 
-extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_steps, float step, int with_noise,
+extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_steps, double step, int with_noise,
                                    const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
                                    float* diag, void* stream) {
   if (!e || !z || B <= 0 || n_steps < 0) return DAMC_ERR_ARG;
@@ -361,10 +361,10 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
   if (n_steps == 0) return 0;
-  const float c1 = (float)(0.5 * (double)step * (double)step);
+  const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
   const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
   ProfScope ps("prior_chain", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
-  hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, s, *e, z, B, n_steps, c1, step,
+  hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, s, *e, z, B, n_steps, c1, (float)step,
                      with_noise, noise, seed, step_offset, chain_base, diag);
   return (int)hipGetLastError();
 }
@@ -379,13 +379,13 @@ extern "C" int damc_ebm_energy_grad(const damc_ebm_t* e, const float* z, int B, 
   return (int)hipGetLastError();
 }
 
-extern "C" int damc_z_update(float* z, const float* g, int B, int nz, float step, int with_noise, const float* noise,
+extern "C" int damc_z_update(float* z, const float* g, int B, int nz, double step, int with_noise, const float* noise,
                              uint64_t seed, uint64_t step_index, uint64_t chain_base, void* stream) {
   if (!z || !g || B <= 0 || nz <= 0) return DAMC_ERR_ARG;
   const long n = (long)B * nz;
-  const float c1 = (float)(0.5 * (double)step * (double)step);
+  const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
   hipLaunchKernelGGL(z_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), z, g, n, nz, c1,
-                     step, with_noise, noise, seed, step_index, chain_base);
+                     (float)step, with_noise, noise, seed, step_index, chain_base);
   return (int)hipGetLastError();
 }
 

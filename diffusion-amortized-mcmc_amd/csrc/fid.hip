@@ -83,9 +83,10 @@ __global__ void fid_mean_cov_kernel(const double* __restrict__ s1, const double*
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)d * d) return;
   const int i = (int)(idx / d), j = (int)(idx - (long)i * d);
-  const double mi = s1[i] / n, mj = s1[j] / n;
-  sigma[idx] = (s2[idx] - n * mi * mj) / (n - 1.0);
-  if (j == 0) mu[i] = mi;
+  // the product in (min, max) index order, so sigma is exactly symmetric like s2
+  const double a = s1[min(i, j)] / n, b = s1[max(i, j)] / n;
+  sigma[idx] = (s2[idx] - n * a * b) / (n - 1.0);
+  if (j == 0) mu[i] = s1[i] / n;
 }
 
 }  // namespace

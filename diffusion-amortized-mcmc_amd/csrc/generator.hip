@@ -19,7 +19,7 @@
 using damc::GemmArgs;
 
 int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
-                                 int nz, float step, int with_noise, const float* noise, uint64_t seed,
+                                 int nz, double step, int with_noise, const float* noise, uint64_t seed,
                                  uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s);
 
 namespace {
@@ -1630,14 +1630,14 @@ extern "C" int damc_generator_forward(const damc_generator_t* g, const float* z,
   return forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s);
 }
 
-extern "C" int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int B, float sigma,
+extern "C" int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int B, double sigma,
                                     float* grad, void* wsp, size_t wsb, void* stream) {
   Workspace ws;
   int rc = setup_ws(g, B, wsp, wsb, &ws);
   if (rc) return rc;
   if (!z || !x || !grad) return DAMC_ERR_ARG;
   hipStream_t s = as_stream(stream);
-  const float inv_s2 = (float)(1.0 / ((double)sigma * sigma));
+  const float inv_s2 = (float)(1.0 / (sigma * sigma));
   if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
   if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, nullptr, true, s))) return rc;
   if (g->n_layers == 1) {
@@ -1741,7 +1741,7 @@ extern "C" int damc_convT_dgrad(const damc_layer_t* L, const float* gout, int B,
 }
 
 extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
-                                       int B, int n_steps, float sigma, float step, int with_noise, const float* noise,
+                                       int B, int n_steps, double sigma, double step, int with_noise, const float* noise,
                                        uint64_t seed, uint64_t step_offset, uint64_t chain_base, float* diag,
                                        void* wsp, size_t wsb, void* stream) {
   Workspace ws;
@@ -1752,7 +1752,7 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   if (ebm && (ebm->nz != g->nz || !ebm->w1t || !ebm->w2t)) return DAMC_ERR_ARG;
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 4 * (size_t)n_steps, s));
-  const float inv_s2 = (float)(1.0 / ((double)sigma * sigma));
+  const float inv_s2 = (float)(1.0 / (sigma * sigma));
   for (int i = 0; i < n_steps; ++i) {
     float* dg = diag ? diag + 4 * i : nullptr;
     if ((rc = forward_hidden(g, z, B, ws, s))) return rc;

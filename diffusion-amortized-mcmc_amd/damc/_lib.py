@@ -116,6 +116,7 @@ ADAM_MAX_TENSORS = 96
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
+_D = ctypes.c_double
 _U64 = ctypes.c_uint64
 _SZ = ctypes.c_size_t
 
@@ -126,9 +127,9 @@ _SIGS = {
     "damc_pack_generator_layer": (_I, [ctypes.POINTER(Layer), _P, _P, _P, _P]),
     "damc_pack_ebm": (_I, [ctypes.POINTER(Ebm), _P, _P, _P]),
     "damc_posterior_workspace_bytes": (_SZ, [ctypes.POINTER(Generator), _I]),
-    "damc_posterior_langevin": (_I, [ctypes.POINTER(Generator), ctypes.POINTER(Ebm), _P, _P, _I, _I, _F, _F, _I, _P,
+    "damc_posterior_langevin": (_I, [ctypes.POINTER(Generator), ctypes.POINTER(Ebm), _P, _P, _I, _I, _D, _D, _I, _P,
                                      _U64, _U64, _U64, _P, _P, _SZ, _P]),
-    "damc_likelihood_grad": (_I, [ctypes.POINTER(Generator), _P, _P, _I, _F, _P, _P, _SZ, _P]),
+    "damc_likelihood_grad": (_I, [ctypes.POINTER(Generator), _P, _P, _I, _D, _P, _P, _SZ, _P]),
     "damc_generator_forward": (_I, [ctypes.POINTER(Generator), _P, _I, _P, _P, _SZ, _P]),
     "damc_convT_workspace_bytes": (_SZ, [ctypes.POINTER(Layer), _I]),
     "damc_convT_fwd": (_I, [ctypes.POINTER(Layer), _P, _I, _P, _P, _SZ, _P]),
@@ -141,9 +142,9 @@ _SIGS = {
     "damc_denoiser_train_forward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _P, _P, _I, _P, _P, _SZ, _P]),
     "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
                                           _P, _P, _SZ, _P]),
-    "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P, _P]),
+    "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _P]),
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
-    "damc_z_update": (_I, [_P, _P, _I, _I, _F, _I, _P, _U64, _U64, _U64, _P]),
+    "damc_z_update": (_I, [_P, _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P]),
     "damc_philox_normal": (_I, [_P, _I, _I, _I, _U64, _U64, _U64, ctypes.c_uint32, _P]),
     "damc_conv2d_workspace_floats": (_SZ, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "damc_conv2d_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P, _SZ, _P]),

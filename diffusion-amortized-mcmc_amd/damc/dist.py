@@ -113,8 +113,9 @@ def sharded_recon_mse(Q, G, E, batches, g_l_steps=10, g_llhd_sigma=0.1, g_l_step
     meter = None
     for x in batches:
         s, c = shard(x.shape[0], rank, world)
-        zt = torch.randn(x.shape[0], Q.nz)  # global draws, identical on every rank (host generator)
-        seed = langevin.new_seed()
+        # global draws, identical on every rank (host generator), in q_forward's order: zt, then the sweep key
+        zt = torch.randn(x.shape[0], Q.nz)
+        seed = langevin.new_seed() if Q.with_noise else 0
         if c == 0:
             continue
         xs = x[s:s + c].contiguous()

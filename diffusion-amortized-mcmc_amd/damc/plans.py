@@ -116,8 +116,9 @@ class GeneratorPlan:
         self.desc = desc
 
     def refresh(self, device, engine=None):
-        """(Re)pack the live parameters; returns the ctypes descriptor.  engine: _lib.ENGINE_* for every layer
-        (default: _lib.current_engine() of the calling thread)."""
+        """(Re)pack the live parameters; returns a per-call copy of the ctypes descriptor (so threads asking for
+        different engines never share one).  engine: _lib.ENGINE_* for every layer (default:
+        _lib.current_engine() of the calling thread)."""
         device = torch.device(device)
         engine = _lib.current_engine() if engine is None else int(engine)
         if device.type != "cuda":
@@ -134,7 +135,6 @@ class GeneratorPlan:
                 self._keep.append(w)
             wf, wb = self.buffers[i]
             d = self.desc.layers[i]
-            d.engine = engine
             check(L.damc_pack_generator_layer(ctypes.byref(d), ptr(w), ptr(wf),
                                               ptr(wb) if d.w_bwd else None, stream), "pack generator layer")
             if m.bias is not None:
@@ -145,7 +145,10 @@ class GeneratorPlan:
                 d.bias = b.data_ptr()
             else:
                 d.bias = None
-        return self.desc
+        out = _lib.Generator.from_buffer_copy(self.desc)
+        for i in range(out.n_layers):
+            out.layers[i].engine = engine
+        return out
 
     def workspace(self, batch):
         L = _lib.lib()

@@ -67,11 +67,10 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(L.damc_generator_train_forward(ctypes.byref(desc), ptr(zc), B, ptr(xh), ptr(ws), nbytes,
                                              _lib.stream_ptr(dev)), "damc_generator_train_forward")
         ctx.plan, ctx.ws, ctx.nbytes = plan, ws, nbytes
-        # a private copy: a later refresh of the plan (other engine, other thread) must not change what the
-        # backward runs on — it has to be the engine that filled this workspace
-        ctx.desc = type(desc).from_buffer_copy(desc)
+        # refresh returned a private descriptor: a later refresh (other engine, other thread) cannot change what
+        # the backward runs on — it has to be the engine that filled this workspace
+        ctx.desc = desc
         ctx.keep = (plan.buffers, getattr(plan, "_keep", None))
-        ctx.plan_desc = desc
         ctx.save_for_backward(zc, xh, *params)
         return xh
 
@@ -84,9 +83,8 @@ class _GeneratorTrainFn(torch.autograd.Function):
         # so the packed buffers still hold the forward's weights (any re-pack in between wrote the same
         # values); re-pack only if the plan re-allocated them (device change)
         desc = ctx.desc
-        if plan.desc is not ctx.plan_desc:  # buffers re-allocated (device change): re-pack, same engine
-            fresh = plan.refresh(dev, engine=desc.layers[0].engine)
-            desc = type(fresh).from_buffer_copy(fresh)
+        if plan.buffers is not ctx.keep[0]:  # buffers re-allocated (device change): re-pack, same engine
+            desc = plan.refresh(dev, engine=desc.layers[0].engine)
         gx = gx.to(torch.float32).contiguous()
         grads = _lib.GeneratorGrads()
         outs = []
@@ -99,7 +97,7 @@ class _GeneratorTrainFn(torch.autograd.Function):
         check(_lib.lib().damc_generator_train_backward(
             ctypes.byref(desc), ptr(zc), ptr(xh), ptr(gx), zc.shape[0], ctypes.byref(grads), ptr(gz), ptr(ctx.ws),
             ctx.nbytes, _lib.stream_ptr(dev)), "damc_generator_train_backward")
-        ctx.ws = ctx.desc = ctx.keep = ctx.plan_desc = None
+        ctx.ws = ctx.desc = ctx.keep = None
         return (gz, None, *outs)
 
 

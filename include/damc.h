@@ -16,6 +16,8 @@
  *     any call (everything is stream-ordered and graph-capturable);
  *   - return 0 on success, otherwise a hipError_t value or one of DAMC_ERR_* (the Python
  *     side raises RuntimeError with damc_error_string()).
+ *   - step sizes / sigma are the reference's Python floats (double): the updates use float32(0.5 step^2) and
+ *     float32(step) (and float32(1 / sigma^2)), the values PyTorch's fp32 scalar ops round them to;
  *   - noise: with_noise != 0 and noise == NULL draws xi ~ N(0,1) in-kernel from
  *     Philox4x32-10 keyed by (seed) with counter (dim/4, step + step_offset,
  *     chain_base + chain, stream_id): a chain's noise depends on its GLOBAL index only, so
@@ -107,12 +109,12 @@ size_t damc_posterior_workspace_bytes(const damc_generator_t* g, int batch);
  * z (B,nz) updated in place; x (B,nc,h,w) NCHW; diag (optional, n_steps*4 floats, zeroed by
  * the call): per step {sum E, |G(z)-x|^2/(2sigma^2), |z|^2/2, mean(grad)} before the update. */
 int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm_t* ebm, float* z, const float* x,
-                            int batch, int n_steps, float sigma, float step, int with_noise,
+                            int batch, int n_steps, double sigma, double step, int with_noise,
                             const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
                             float* diag, void* workspace, size_t workspace_bytes, void* stream);
 
 /* per-op hooks (parity tests): grad_z |G(z)-x|^2/(2 sigma^2) -> grad (B,nz) */
-int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int batch, float sigma,
+int damc_likelihood_grad(const damc_generator_t* g, const float* z, const float* x, int batch, double sigma,
                          float* grad, void* workspace, size_t workspace_bytes, void* stream);
 /* x_hat = G(z) (B,nc,h,w) NCHW — gen_samples / gen_samples_with_diffusion_prior (MCMC.py:119-150) */
 int damc_generator_forward(const damc_generator_t* g, const float* z, int batch, float* x_hat,
@@ -156,7 +158,7 @@ int damc_generator_train_backward(const damc_generator_t* g, const float* z, con
 /* ----------------------------------------------------------------- prior Langevin (a2) */
 /* sample_langevin_prior_z (MCMC.py:27-46): all n_steps in ONE persistent launch.
  * diag (optional, n_steps*2 floats): {sum E, |z|^2/2} per step before the update. */
-int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps, float step, int with_noise,
+int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps, double step, int with_noise,
                         const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
                         float* diag, void* stream);
 /* per-op hook: energy (B) and grad_z sum E (B,nz) */
@@ -165,7 +167,7 @@ int damc_ebm_energy_grad(const damc_ebm_t* ebm, const float* z, int batch, float
 /* the same under SURVEY.md §8b's name */
 int damc_ebm_grad(const damc_ebm_t* ebm, const float* z, int batch, float* energy, float* grad, void* stream);
 /* per-op hook: z <- z - 0.5 step^2 (g + z) (+ step xi) ; g (B,nz) */
-int damc_z_update(float* z, const float* g, int batch, int nz, float step, int with_noise, const float* noise,
+int damc_z_update(float* z, const float* g, int batch, int nz, double step, int with_noise, const float* noise,
                   uint64_t seed, uint64_t step_index, uint64_t chain_base, void* stream);
 /* Philox N(0,1) draw used by every Langevin kernel (statistical tests) -> out (n_steps,B,nz) */
 int damc_philox_normal(float* out, int n_steps, int batch, int nz, uint64_t seed, uint64_t step_offset,
