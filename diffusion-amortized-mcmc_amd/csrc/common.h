@@ -81,11 +81,22 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint64_t chain, ui
 
 enum { DAMC_STREAM_POSTERIOR = 0x51, DAMC_STREAM_PRIOR = 0x52, DAMC_STREAM_SWEEP = 0x53 };
 
-// fp32 ops that must not be contracted into FMA (bit-level match with the reference's
-// separately rounded PyTorch elementwise ops: z - (c*g), then + s*xi)
-__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+// fp32 ops that must not be contracted into FMA (bit-level match with the reference's separately rounded
+// PyTorch elementwise ops: z - (c*g), then + s*xi).  HIP's __fmul_rn & co. are plain operators, which
+// -ffp-contract=fast fuses after inlining; the pragma (honoured under the Makefile's
+// -ffp-contract=fast-honor-pragmas) leaves these operations without the contract flag.
+__device__ __forceinline__ float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float sub_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
 
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == DAMC_ACT_LRELU) return v > 0.f ? v : v * slope;

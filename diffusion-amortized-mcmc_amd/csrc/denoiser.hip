@@ -1,308 +1,322 @@
 // denoiser.hip — Diffusion_UnetA eps-prediction and the amortizer's latent reverse sweep
 // (_netQ_U.forward, workspace/src/diffusion_net.py:585-622) on gfx950.
 //
-// Per sweep (once):  SiLU(xemb) -> px = SiLU(xemb) . Wctx_x           (B, sum dout)   [step-invariant]
-//                    time-MLP on the n sinusoidal embeddings -> qt = SiLU(temb) . Wctx_t + bctx
-//                                                                      (n, sum dout)   [batch-invariant]
-// Per step (7 launches): one fused ConcatSquash block kernel per block:
-//     out = (x Wl + bl) * sigmoid(c Wg + bg) + c Wb + (x Ws + bs),   c = SiLU(px[b] + qt[k])
-// with the block input x = lrelu(cat(prev, skip), 0.01) formed while staging (in0: the Fourier input
-// embedding [sin 2pi zB, cos 2pi zB, z] is computed in the prologue), and the last block's epilogue
-// applying eps = z + out, pred_x_from_eps and the reverse-step update with Philox noise in place.
-// Block kernel: 4 waves, wave w owns one of the four products (l, s, g, b) for a 16 x 32 output
-// tile on v_mfma_f32_16x16x4_f32; operands x / c are staged once per workgroup in LDS.
+// A ConcatSquash block (diffusion_net.py:417-445) is
+//     out = (x Wl^T + bl) * sigmoid(c Wg^T + bg) + c Wb^T + (x Ws^T + bs),   c = SiLU(Lc(SiLU(cat(temb, xemb))))
+// and its ctx c depends on (step, row) only — never on zt.  So per call (not per step):
+//   1. pack   : every weight from the caller's PyTorch layouts into the workspace (the nets train between calls);
+//   2. ctx    : time MLP on the n sinusoidal embeddings (batch-invariant) and SiLU(xemb) . Wctx_x (step-invariant),
+//               c[k][b] = SiLU(px[b] + qt[k]) for all n*B (step, row) pairs;
+//   3. hyper  : per block one fp32-MFMA GEMM over the n*B rows, [gate | hyper bias] = [sigmoid(c Wg^T + bg) | c Wb^T]
+//               (EPI_GATE).  51 % + 20 % of the reference's per-step MACs (ctx Linear, hyper Linears) leave the
+//               dependent chain this way.
+// What stays in the chain is x Wl^T and x Ws^T of the 7 blocks plus the reverse-step update: 7 dependent launches
+// per step (block j+1 needs every column of block j for its rows).  They are kept short:
+//   * one workgroup = 16 rows x 8 output columns of BOTH products (one 16 x 16 v_mfma_f32_16x16x4_f32 tile: 8 Wl
+//     rows + 8 Ws rows of the packed weight), 4 waves splitting K in quarters; each lane's x and weight fragments
+//     are f32x4 global loads issued together up front through the k-permutation of the MFMA steps (step s of
+//     k-group g reads k = 16 g + 4 (lane >> 4) + s on both operands), so a launch costs one memory round trip;
+//   * the epilogue operands (gate, hyper bias, biases, zt, the Philox draw) are fetched before the main loop;
+//   * N tiles are the fastest grid index: with dout / 8 a multiple of 8 an N tile stays on one XCD for every step,
+//     so each XCD keeps 1/8 of the chain's weights in its L2;
+//   * the 7n launches are captured once into a HIP graph (cached per workspace / shape / schedule) and replayed:
+//     eager launches cost the host ~3.5 us each, more than these kernels take on the GPU.
+// The last block's epilogue applies eps = z + out, pred_x_from_eps and the reverse step with Philox noise in place.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <vector>
-
-#include <hip/hip_cooperative_groups.h>
 
 #include "gemm.h"
 
 namespace {
 
-constexpr int TM = 16, TN = 16;     // output tile of one workgroup
-constexpr int CSQ_THREADS = 512;    // 8 waves: two per product (l, s, g, b), each over half of K
-constexpr int CSQ_CH = 8;           // k-groups (16 k each) whose loads one wave keeps in flight
+constexpr int CH_THREADS = 256;  // 4 waves, K split in quarters
+constexpr int TM = 16;           // rows per workgroup
+constexpr int TC = 8;            // output columns per workgroup (x 2 products)
+constexpr int KG = 64;           // K padding granule: 4 waves x one 16-deep k-group
+constexpr int CH_CHUNK = 8;      // k-groups whose loads a lane keeps in flight at once
 
-// LDS row stride of a [TM][K] operand image: a multiple of 64 plus 8 floats, which makes the
-// ds_read_b128 fragment reads (rows m = lane&15, k-quads lane>>4) conflict-free
-__host__ __device__ inline int csq_ld(int k) { return (k + 63) / 64 * 64 + 8; }
+// per-call values read by the last block (device memory in the workspace, written before each sweep so a cached
+// graph needs no new kernel arguments)
+struct SweepCall {
+  const float* noise;  // injected (n-1, B, nz) or null (Philox)
+  float* eps_log;      // (eps_log_steps, B, nz) or null
+  uint64_t seed, chain_base, step_offset;
+  int with_noise, eps_log_steps;
+};
 
-// emb_nz > 0 (block in0): room for the Fourier matrix B (nz, nz/2) as well
-__host__ __device__ inline size_t csq_smem_bytes(int din, int dout, int emb_nz = 0) {
-  return sizeof(float) * ((size_t)TM * (csq_ld(din) + csq_ld(dout)) + 8 * TM * TN + (size_t)emb_nz * (emb_nz / 2));
-}
-
-struct CsqArgs {
-  const float* srcA;  // block input source 1 (B, wa)
-  int wa;
-  const float* srcB;  // concat source 2 (B, wb) or null
-  int wb_;
-  int emb_mode;       // 1: input = Fourier embedding of z (in0)
-  const float* z;     // (B, nz) current zt
-  const float* bmat;  // (nz, nz/2)
+struct ChainArgs {
+  const float* srcA;  // block input = lrelu(cat(srcA, srcB), 0.01) (not in0)
+  const float* srcB;
+  int wa, wb;
+  int emb;            // in0: input = [sin 2pi zB, cos 2pi zB, z]
+  const float* z;     // (B, nz) current zt (the workspace copy)
+  const float* bmat;  // (nz, nz/2) packed copy
   int nz;
-  int din, dout, B;
-  const float *wl, *bl, *ws, *bs, *wg, *bg, *wb;  // PyTorch Linear layout (out, in): k contiguous
-  const float* px;    // (B, ldpx) at this block's column offset
-  int ldpx;
-  const float* qt;    // (ldpx) row of this step at this block's column offset
+  int din, kp, dout, B;
+  const float* w;     // [ntn][16][kp]: rows 0-7 Wl, 8-15 Ws of the tile's columns (zero-padded)
+  const float* bls;   // [ntn][16]: bl, bs
+  const float* gh;    // this step's rows: gate at gh[b * ldgh + n], hyper bias at gh[b * ldgh + dout + n]
+  long ldgh;
   float* out;         // (B, dout)
-  // final block (reverse step) epilogue
-  int final_;
-  int residual;
+  // last block
+  int final_, residual, last, k, noisy_k;
   float c0, c1, c2, c3, c4;
-  int last;
-  int with_noise;
-  const float* noise;  // (B, nz) for this step or null
-  uint64_t seed, chain_base, step;
-  float* zt;           // updated in place (== z)
-  float* eps_log;      // (B, nz) or null
+  float* zt;          // == z
+  const SweepCall* call;
+  int dbg;  // timing experiments only (DAMC_CHAIN_DBG, wrong results): 1 no x loads, 2 no weight loads, 4 no MFMA,
+            // 8 no epilogue prefetch, 16 no output stores
 };
 
-// One ConcatSquashLinear block (diffusion_net.py:417-460) for a 16 x 16 output tile:
-//   out = (x Wl^T + bl) * sigmoid(c Wg^T + bg) + c Wb^T + (x Ws^T + bs),   c = SiLU(px + qt)
-// x (16 x din) and c (16 x dout) are staged in LDS.  Wave w computes product w>>1 over half w&1 of
-// its K on v_mfma_f32_16x16x4_f32 through a k-permutation (MFMA step s of k-group g uses
-// k = 16g + 4(lane>>4) + s), so each lane's operands for 4 steps are one 16-B LDS read (x / c) and one
-// 16-B global read of a weight row; a wave issues CSQ_CH groups of loads before their MFMAs.  The
-// eight partial tiles are added in a fixed order in the epilogue.
-// the step-dependent fields of a block's arguments (the cooperative sweep keeps CsqArgs in kernarg memory)
-struct TileDyn {
-  const float* qt;
-  float c0, c1, c2, c3, c4;
-  int last, with_noise;
-  const float* noise;
-  uint64_t step;
-  float* eps_log;
-};
+__host__ __device__ inline int kpad(int din) { return (din + KG - 1) / KG * KG; }
+__host__ __device__ inline int emb_ld(int kp) { return kp + 8; }  // in0 LDS image row stride (floats)
 
-// one output tile (rows r0.., columns n0..) of one block; called uniformly by all CSQ_THREADS threads
-__device__ __forceinline__ void csq_tile(const CsqArgs& a, const TileDyn& dy, int r0, int n0, float* sm) {
-  const int din = a.din, dout = a.dout;
-  const int ldx = csq_ld(din), ldcs = csq_ld(dout);
-  float* xs = sm;                 // [TM][ldx]
-  float* cs = xs + TM * ldx;      // [TM][ldcs]
-  float* red = cs + TM * ldcs;    // [8][TM][TN]
+__global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[4][TM][16];
+  extern __shared__ __attribute__((aligned(16))) float embs[];  // in0: [TM][emb_ld(kp)]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kx16 = (din + 15) & ~15, kc16 = (dout + 15) & ~15;
-
-  // ---- stage x (block input) for the 16 rows; columns [din, kx16) zero.  Staging is float4 and
-  // unrolled so that a thread's global loads are in flight together (this kernel is latency-bound)
-  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  if (a.emb_mode) {
-    const int half = a.nz >> 1, nzq = a.nz >> 2;
-    float* bm = red + 8 * TM * TN;  // [nz][half]
-    const int nbq = (a.nz * half) >> 2;
-#pragma unroll 4
-    for (int i = tid; i < nbq; i += CSQ_THREADS)
-      *reinterpret_cast<f32x4*>(bm + 4 * i) = *reinterpret_cast<const f32x4*>(a.bmat + 4 * (long)i);
-    // z rows -> xs[:, 2*half : 2*half + nz] (also the embedding's operand, read back from LDS)
-#pragma unroll 4
-    for (int i = tid; i < TM * nzq; i += CSQ_THREADS) {
-      const int r = i / nzq, k = 4 * (i - r * nzq);
-      const int row = r0 + r;
-      const f32x4 v = row < a.B ? *reinterpret_cast<const f32x4*>(a.z + (long)row * a.nz + k) : zero4;
-      *reinterpret_cast<f32x4*>(xs + r * ldx + 2 * half + k) = v;
-    }
-    for (int i = tid; i < TM * (kx16 - din); i += CSQ_THREADS) {
-      const int r = i / (kx16 - din);
-      xs[r * ldx + din + (i - r * (kx16 - din))] = 0.f;
-    }
-    __syncthreads();
-    const float two_pi = 6.28318548f;  // fp32(2*pi), as the reference's 2*np.pi*tensor
-    for (int i = tid; i < TM * half; i += CSQ_THREADS) {
-      const int r = i / half, j = i - r * half;
-      const float* zr = xs + r * ldx + 2 * half;
-      float sdot = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < a.nz; ++k) sdot = fmaf(zr[k], bm[k * half + j], sdot);
-      const float ph = two_pi * sdot;
-      const bool ok = r0 + r < a.B;
-      xs[r * ldx + j] = ok ? sinf(ph) : 0.f;
-      xs[r * ldx + half + j] = ok ? cosf(ph) : 0.f;
-    }
-  } else {
-    const int q16 = kx16 >> 2;
-#pragma unroll 4
-    for (int i = tid; i < TM * q16; i += CSQ_THREADS) {
-      const int r = i / q16, k = 4 * (i - r * q16);
-      const int row = r0 + r;
-      f32x4 v = zero4;
-      if (row < a.B && k < din)
-        v = k < a.wa ? *reinterpret_cast<const f32x4*>(a.srcA + (long)row * a.wa + k)
-                     : *reinterpret_cast<const f32x4*>(a.srcB + (long)row * a.wb_ + (k - a.wa));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.01f * v[e];
-      *reinterpret_cast<f32x4*>(xs + r * ldx + k) = v;
-    }
-  }
-  // ---- stage c = SiLU(px + qt); columns [dout, kc16) zero
-  {
-    const int q16 = kc16 >> 2;
-#pragma unroll 4
-    for (int i = tid; i < TM * q16; i += CSQ_THREADS) {
-      const int r = i / q16, n = 4 * (i - r * q16);
-      const int row = r0 + r;
-      f32x4 v = zero4;
-      if (row < a.B && n < dout) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(a.px + (long)row * a.ldpx + n) +
-                        *reinterpret_cast<const f32x4*>(dy.qt + n);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = u[e] / (1.f + expf(-u[e]));
-      }
-      *reinterpret_cast<f32x4*>(cs + r * ldcs + n) = v;
-    }
-  }
-  __syncthreads();
-
-  // ---- wave w: product w>>1 over k-groups [g_lo, g_hi) (half w&1)
-  const int prod = wave >> 1, hf = wave & 1;
-  const float* As = (prod < 2) ? xs : cs;
-  const int lda_s = (prod < 2) ? ldx : ldcs;
-  const int K = (prod < 2) ? din : dout;
-  const float* W = prod == 0 ? a.wl : prod == 1 ? a.ws : prod == 2 ? a.wg : a.wb;
-  const int ng = (K + 15) >> 4, gh = (ng + 1) >> 1;
-  const int g_lo = hf * gh, g_hi = min(ng, g_lo + gh);
+  const int ntn = (a.dout + TC - 1) / TC;
+  const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
+  const int r0 = tm * TM, n0 = tn * TC;
   const int m = lane & 15, q = lane >> 4;
-  const int n = n0 + m;
-  const bool nok = n < dout;
-  const float* Wn = W + (long)(nok ? n : 0) * K;
-  const float* Am = As + m * lda_s + 4 * q;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int g0 = g_lo; g0 < g_hi; g0 += CSQ_CH) {
-    f32x4 bw[CSQ_CH], av[CSQ_CH];
-#pragma unroll
-    for (int c = 0; c < CSQ_CH; ++c) {
-      const int g = g0 + c;
-      const int k = 16 * g + 4 * q;
-      const bool ok = g < g_hi;
-      bw[c] = (ok && nok && k < K) ? *reinterpret_cast<const f32x4*>(Wn + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-      av[c] = ok ? *reinterpret_cast<const f32x4*>(Am + 16 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int c = 0; c < CSQ_CH; ++c) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][0], bw[c][0], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][1], bw[c][1], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][2], bw[c][2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][3], bw[c][3], acc1, 0, 0, 0);
-    }
-  }
-  // C layout 16x16x4: col = lane & 15, row = (lane >> 4) * 4 + reg
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[(wave * TM + q * 4 + r) * TN + m] = acc0[r] + acc1[r];
-  __syncthreads();
 
-  // ---- combine: out = (l + bl) * sigmoid(g + bg) + b + (s + bs)
-  for (int i = tid; i < TM * TN; i += CSQ_THREADS) {
-    const int r = i / TN, c = i - r * TN;
-    const int row = r0 + r, col = n0 + c;
-    if (row >= a.B || col >= dout) continue;
-    auto P = [&](int p) { return red[((2 * p) * TM + r) * TN + c] + red[((2 * p + 1) * TM + r) * TN + c]; };
-    const float l = P(0) + a.bl[col];
-    const float sk = P(1) + a.bs[col];
-    const float g = P(2) + a.bg[col];
-    const float bb = P(3);
-    const float gate = 1.f / (1.f + expf(-g));
-    const float o = l * gate + bb + sk;
-    if (!a.final_) {
-      a.out[(long)row * dout + col] = o;
-      continue;
-    }
-    // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 * (z - eps * c1)
-    const long zi = (long)row * a.nz + col;
-    const float zv = a.zt[zi];
-    const float eps = a.residual ? zv + o : o;
-    if (dy.eps_log) dy.eps_log[zi] = eps;
-    const float pred = mul_rn(dy.c0, sub_rn(zv, mul_rn(eps, dy.c1)));
-    float zn;
-    if (dy.last) {
-      zn = pred;
-    } else {
-      zn = add_rn(mul_rn(dy.c2, zv), mul_rn(dy.c3, pred));
-      if (dy.with_noise) {
-        float xi;
-        if (dy.noise) {
-          xi = dy.noise[zi];
+  // ---- epilogue operands first (independent of the main loop): thread (row er, column ec)
+  const int er = tid >> 3, ec = tid & 7;
+  const int erow = r0 + er, ecol = n0 + ec;
+  const bool eok = tid < TM * TC && erow < a.B && ecol < a.dout;
+  float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, zv = 0.f, xi = 0.f;
+  const SweepCall* call = a.call;
+  if (eok && !(a.dbg & 8)) {
+    gate = a.gh[(long)erow * a.ldgh + ecol];
+    hb = a.gh[(long)erow * a.ldgh + a.dout + ecol];
+    bl = a.bls[tn * 16 + ec];
+    bs = a.bls[tn * 16 + 8 + ec];
+    if (a.final_) {
+      zv = a.zt[(long)erow * a.nz + ecol];
+      if (!a.last && call->with_noise) {
+        if (call->noise) {
+          xi = call->noise[((long)a.noisy_k * a.B + erow) * a.nz + ecol];
         } else {
           float n4[4];
-          philox_normal4(a.seed, a.chain_base + row, dy.step, (uint32_t)(col >> 2), DAMC_STREAM_SWEEP, n4);
-          xi = n4[col & 3];
+          philox_normal4(call->seed, call->chain_base + erow, call->step_offset + a.noisy_k, (uint32_t)(ecol >> 2),
+                         DAMC_STREAM_SWEEP, n4);
+          xi = n4[ecol & 3];
         }
-        zn = add_rn(zn, mul_rn(dy.c4, xi));
       }
     }
-    a.zt[zi] = zn;
   }
-}
 
-// grid (N tiles, M tiles): dispatch is round-robin over the 8 XCDs, so with N tiles a multiple of 8 each
-// XCD owns the same output columns for every row tile and step — 1/8 of the sweep's 12.6 MB of weights,
-// which then stays in that XCD's 4 MB L2 across all steps instead of streaming from the Infinity Cache
-__global__ __launch_bounds__(CSQ_THREADS) void csq_block_kernel(CsqArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const TileDyn dy{a.qt, a.c0, a.c1, a.c2, a.c3, a.c4, a.last, a.with_noise, a.noise, a.step, a.eps_log};
-  csq_tile(a, dy, blockIdx.y * TM, blockIdx.x * TN, sm);
-}
-
-// Opt-in (DAMC_SWEEP_COOP=1, slower: see damc_reverse_sweep) — the whole sweep in ONE cooperative launch:
-// per step, the 7 blocks run back to back with a grid-wide barrier between them (block j+1 needs every
-// column of block j for its rows).  A workgroup takes tiles
-// t = blockIdx.x, blockIdx.x + grid, ... of each block, N tile fastest: with the grid a multiple of 8, tile t
-// stays on XCD t % 8 (same weight columns every step, L2-resident, as in the per-block launches).  Saves the
-// ~7 launch/drain gaps per step that dominate at B <= 128.
-struct SweepArgs {
-  CsqArgs blk[7];         // step-invariant fields of each block
-  const float* coef;      // (n, 6) device copy of the schedule scalars
-  const float* qt;        // (n, S) time part of the ctx pre-activation
-  const float* noise;     // injected (n-1, B, nz) or null
-  float* eps_log;         // (eps_log_steps, B, nz) or null
-  int coloff[7];
-  int S, n_steps, eps_log_steps, with_noise;
-};
-
-__global__ __launch_bounds__(CSQ_THREADS) void sweep_coop_kernel(SweepArgs sa) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-  int noisy_k = 0;
-  for (int k = 0; k < sa.n_steps; ++k) {
-    const float* c = sa.coef + 6 * k;
-    const bool last = c[5] != 0.f;
-    for (int j = 0; j < 7; ++j) {
-      const CsqArgs& a = sa.blk[j];
-      TileDyn dy{};
-      dy.qt = sa.qt + (size_t)k * sa.S + sa.coloff[j];
-      if (j == 6) {
-        dy.c0 = c[0];
-        dy.c1 = c[1];
-        dy.c2 = c[2];
-        dy.c3 = c[3];
-        dy.c4 = c[4];
-        dy.last = last;
-        dy.with_noise = sa.with_noise && !last;
-        dy.noise = (dy.with_noise && sa.noise) ? sa.noise + (size_t)noisy_k * a.B * a.nz : nullptr;
-        dy.step = (uint64_t)noisy_k;
-        dy.eps_log = (sa.eps_log && k < sa.eps_log_steps) ? sa.eps_log + (size_t)k * a.B * a.nz : nullptr;
+  // ---- in0: the Fourier input embedding of the 16 rows into LDS (zB on MFMA, wave w -> 16-column tiles w, w+4..)
+  const int ld = emb_ld(a.kp);
+  if (a.emb) {
+    const int nz = a.nz, half = nz >> 1;
+    const int row = r0 + m;
+    const bool rok = row < a.B;
+    const int nzg = (nz + 15) >> 4;
+    for (int t = wave; t * 16 < half; t += 4) {
+      const int col = t * 16 + m;
+      const bool cok = col < half;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int g = 0; g < nzg; ++g) {
+        const int k = 16 * g + 4 * q;
+        const f32x4 zv4 = (rok && k < nz) ? *reinterpret_cast<const f32x4*>(a.z + (long)row * nz + k)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        float bv[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[s] = (cok && k + s < nz) ? a.bmat[(long)(k + s) * half + col] : 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[s], bv[s], acc, 0, 0, 0);
       }
-      const int ntn = (a.dout + TN - 1) / TN, ntm = (a.B + TM - 1) / TM;
-      for (int t = blockIdx.x; t < ntn * ntm; t += gridDim.x) {
-        const int tm = t / ntn, tn = t - tm * ntn;
-        __syncthreads();  // the previous tile's LDS images are no longer read
-        csq_tile(a, dy, tm * TM, tn * TN, sm);
+      const float two_pi = 6.28318548f;  // fp32(2*pi), as the reference's 2*np.pi*tensor
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 4 * q + r;
+        if (cok) {
+          const float ph = two_pi * acc[r];
+          const bool ok = r0 + rr < a.B;
+          embs[rr * ld + col] = ok ? sinf(ph) : 0.f;
+          embs[rr * ld + half + col] = ok ? cosf(ph) : 0.f;
+        }
       }
-      grid.sync();
     }
-    if (!last) ++noisy_k;
+    // z itself, then zeros up to kp
+    for (int i = tid; i < TM * (a.kp - 2 * half); i += CH_THREADS) {
+      const int rr = i / (a.kp - 2 * half), c = i - rr * (a.kp - 2 * half);
+      const int row2 = r0 + rr;
+      embs[rr * ld + 2 * half + c] = (row2 < a.B && c < nz) ? a.z[(long)row2 * nz + c] : 0.f;
+    }
+    __syncthreads();
   }
+
+  // ---- main loop: wave w covers k in [w kq, (w+1) kq) of the padded K
+  const int kq = a.kp >> 2;
+  const int ng = kq >> 4;
+  const int kbase = wave * kq;
+  const int xrow = r0 + m;
+  const bool xok = xrow < a.B;
+  const float* wrow = a.w + ((long)tn * 16 + m) * a.kp + kbase + 4 * q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < ng; g0 += CH_CHUNK) {
+    f32x4 xa[CH_CHUNK], wb[CH_CHUNK];
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      const int g = g0 + c;
+      const int k = kbase + 16 * g + 4 * q;
+      f32x4 wv = {0.f, 0.f, 0.f, 0.f}, xv = {0.f, 0.f, 0.f, 0.f};
+      if (g < ng) {
+        if (!(a.dbg & 2)) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * g);
+        if (a.emb) {
+          xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
+        } else if (xok && k < a.din && !(a.dbg & 1)) {
+          xv = k < a.wa ? *reinterpret_cast<const f32x4*>(a.srcA + (long)xrow * a.wa + k)
+                        : *reinterpret_cast<const f32x4*>(a.srcB + (long)xrow * a.wb + (k - a.wa));
+        }
+      }
+      wb[c] = wv;
+      xa[c] = xv;
+    }
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      f32x4 x = xa[c];
+      if (!a.emb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.01f * x[e];
+      }
+      if (a.dbg & 4) {
+        acc[0] += x[0] * wb[c][0] + x[1] * wb[c][1] + x[2] * wb[c][2] + x[3] * wb[c][3];
+        continue;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], wb[c][s], acc, 0, 0, 0);
+    }
+  }
+  // C layout 16x16x4: column = lane & 15 (0-7 Wl, 8-15 Ws), rows 4 (lane >> 4) + r
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
+  __syncthreads();
+
+  if (!eok) return;
+  float l = 0.f, sk = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {  // fixed order: deterministic
+    l += red[w][er][ec];
+    sk += red[w][er][8 + ec];
+  }
+  // ConcatSquashLinearSkipCtx.forward: ret = layer(x) * gate + bias; ret + skip(x)
+  const float o = ((l + bl) * gate + hb) + (sk + bs);
+  if (!a.final_) {
+    if (!(a.dbg & 16)) a.out[(long)erow * a.dout + ecol] = o;
+    return;
+  }
+  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
+  const long zi = (long)erow * a.nz + ecol;
+  const float eps = a.residual ? zv + o : o;
+  if (call->eps_log && a.k < call->eps_log_steps) call->eps_log[(long)a.k * a.B * a.nz + zi] = eps;
+  const float pred = mul_rn(a.c0, sub_rn(zv, mul_rn(eps, a.c1)));
+  float zn;
+  if (a.last) {
+    zn = pred;
+  } else {
+    zn = add_rn(mul_rn(a.c2, zv), mul_rn(a.c3, pred));
+    if (call->with_noise) zn = add_rn(zn, mul_rn(a.c4, xi));
+  }
+  a.zt[zi] = zn;
 }
 
+// ------------------------------------------------------------------------------------- per-call helpers
 __global__ void silu_kernel(const float* x, long n, float* y) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const float v = x[i];
     y[i] = v / (1.f + expf(-v));
   }
+}
+
+// c[k][b][s] = SiLU(px[b][s] + qt[k][s])
+__global__ void ctx_kernel(const float* __restrict__ px, const float* __restrict__ qt, int B, int S, long total,
+                           float* __restrict__ c) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long per = (long)B * S;
+  const long k = i / per;
+  const long r = i - k * per;
+  const int s = (int)(r % S);
+  const float u = px[r] + qt[k * S + s];
+  c[i] = u / (1.f + expf(-u));
+}
+
+struct PackBlock {
+  const float *wl, *bl, *ws, *bs, *wg, *bg, *wb, *wctx, *bctx;
+  int din, dout, kp, coloff;
+  float *w, *bls, *wgb, *bg2;
+};
+struct PackArgs {
+  PackBlock b[7];
+  int ntemb, nxemb, S;
+  float *wctx_t, *wctx_x, *bctx;
+};
+
+// grid.y = block, grid.z = part: 0 chain weights [tile][16][kp] + biases, 1 [Wg^T | Wb^T] (dout, 2 dout) + [bg | 0],
+// 2 the block's columns of Wctx_t (ntemb, S), Wctx_x (nxemb, S) and bctx (S)
+__global__ void pack_denoiser_kernel(PackArgs pa) {
+  const PackBlock& b = pa.b[blockIdx.y];
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.z == 0) {
+    const int ntn = (b.dout + TC - 1) / TC;
+    const long n = (long)ntn * 16 * b.kp;
+    if (i < n) {
+      const int k = (int)(i % b.kp);
+      const long rr = i / b.kp;
+      const int r = (int)(rr % 16), t = (int)(rr / 16);
+      const int col = t * TC + (r & 7);
+      float v = 0.f;
+      if (col < b.dout && k < b.din) v = (r < 8 ? b.wl : b.ws)[(long)col * b.din + k];
+      b.w[i] = v;
+    }
+    if (i < (long)ntn * 16) {
+      const int r = (int)(i % 16), t = (int)(i / 16);
+      const int col = t * TC + (r & 7);
+      b.bls[i] = col < b.dout ? (r < 8 ? b.bl : b.bs)[col] : 0.f;
+    }
+  } else if (blockIdx.z == 1) {
+    const long n = (long)b.dout * 2 * b.dout;
+    if (i < n) {
+      const int k = (int)(i / (2 * b.dout)), c = (int)(i % (2 * b.dout));
+      b.wgb[i] = c < b.dout ? b.wg[(long)c * b.dout + k] : b.wb[(long)(c - b.dout) * b.dout + k];
+    }
+    if (i < 2 * b.dout) b.bg2[i] = i < b.dout ? b.bg[i] : 0.f;
+  } else {
+    const int kc = pa.ntemb + pa.nxemb;
+    const long n = (long)kc * b.dout;
+    if (i < n) {
+      const int k = (int)(i / b.dout), c = (int)(i % b.dout);
+      const float v = b.wctx[(long)c * kc + k];
+      if (k < pa.ntemb) pa.wctx_t[(long)k * pa.S + b.coloff + c] = v;
+      else pa.wctx_x[(long)(k - pa.ntemb) * pa.S + b.coloff + c] = v;
+    }
+    if (i < b.dout) pa.bctx[b.coloff + i] = b.bctx[i];
+  }
+}
+
+// (rows, cols) -> (cols, rows)
+__global__ void transpose_kernel(const float* in, int rows, int cols, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const long r = i / cols, c = i - r * cols;
+  out[c * rows + r] = in[i];
+}
+
+__global__ void sweep_setup_kernel(SweepCall c, SweepCall* dst, const float* zt, float* zw, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *dst = c;
+  if (i < n) zw[i] = zt[i];
+}
+
+__global__ void copy_kernel(const float* src, float* dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
 }
 
 int sum_dout(const damc_denoiser_t* d) {
@@ -312,8 +326,11 @@ int sum_dout(const damc_denoiser_t* d) {
 }
 
 struct SweepWs {
-  float *px, *qt, *t1, *t2, *xs, *coef;
+  float *w[7], *bls[7], *wgb[7], *bg2[7];
+  float *wctx_t, *wctx_x, *bctx, *tw1t, *tw2t, *bmat;
+  float *px, *qt, *t1, *t2, *xs, *cx, *gh, *z;
   float* outs[7];
+  SweepCall* call;
   size_t bytes;
 };
 
@@ -325,14 +342,32 @@ size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
     return p;
   };
   const int S = sum_dout(d);
+  const int nt = d->ntemb, nx = d->nxemb;
   SweepWs t;
+  for (int j = 0; j < 7; ++j) {
+    const damc_csq_block_t& b = d->blocks[j];
+    const int ntn = (b.dout + TC - 1) / TC;
+    t.w[j] = take((long)ntn * 16 * kpad(b.din));
+    t.bls[j] = take((long)ntn * 16);
+    t.wgb[j] = take((long)b.dout * 2 * b.dout);
+    t.bg2[j] = take(2L * b.dout);
+  }
+  t.wctx_t = take((long)nt * S);
+  t.wctx_x = take((long)nx * S);
+  t.bctx = take(S);
+  t.tw1t = take((long)nt * nt);
+  t.tw2t = take((long)nt * nt);
+  t.bmat = take((long)d->nz * (d->nz / 2));
   t.px = take((long)B * S);
   t.qt = take((long)n * S);
-  t.t1 = take((long)n * d->ntemb);
-  t.t2 = take((long)n * d->ntemb);
-  t.xs = take((long)B * d->nxemb);
-  t.coef = take((long)n * 6);
+  t.t1 = take((long)n * nt);
+  t.t2 = take((long)n * nt);
+  t.xs = take((long)B * nx);
+  t.cx = take((long)n * B * S);
+  t.gh = take((long)n * B * 2 * S);
+  t.z = take((long)B * d->nz);
   for (int j = 0; j < 7; ++j) t.outs[j] = take((long)B * d->blocks[j].dout);
+  t.call = reinterpret_cast<SweepCall*>(take(64));
   t.bytes = off;
   if (w) *w = t;
   return off;
@@ -345,15 +380,171 @@ int validate(const damc_denoiser_t* d) {
   // in0 in1 in2 mid out0 out1 out2 widths (Diffusion_UnetA with w = 32 * nf)
   const int din[7] = {2 * nz, w, 2 * w, 2 * w, 4 * w, 4 * w, 2 * w};
   const int dout[7] = {w, 2 * w, 2 * w, 2 * w, 2 * w, w, nz};
+  if (!d->bmat || !d->tw1 || !d->tb1 || !d->tw2 || !d->tb2) return DAMC_ERR_ARG;
   for (int j = 0; j < 7; ++j) {
     const damc_csq_block_t& b = d->blocks[j];
     if (b.din != din[j] || b.dout != dout[j]) return DAMC_ERR_ARG;
-    if (!b.wl || !b.bl || !b.ws || !b.bs || !b.wg || !b.bg || !b.wb) return DAMC_ERR_ARG;
-    // float4 weight rows / LDS images / staging need every width % 4 == 0; the operand images must fit
+    if (!b.wl || !b.bl || !b.ws || !b.bs || !b.wg || !b.bg || !b.wb || !d->wctx[j] || !d->bctx[j]) return DAMC_ERR_ARG;
+    // float4 fragments / staging need every width % 4 == 0; the in0 LDS image must fit
     if ((b.din & 3) || (b.dout & 3) || (nz & 3)) return DAMC_ERR_UNSUPPORTED;
-    if (csq_smem_bytes(b.din, b.dout, j == 0 ? nz : 0) > 160 * 1024) return DAMC_ERR_UNSUPPORTED;
   }
+  if ((size_t)TM * emb_ld(kpad(2 * nz)) * sizeof(float) > 64 * 1024) return DAMC_ERR_UNSUPPORTED;
   return 0;
+}
+
+struct Launch {
+  ChainArgs a;
+  unsigned grid;
+  size_t smem;
+};
+
+// the chain launches of one sweep (n steps from step index k0), in order
+void chain_launches(const damc_denoiser_t* d, const SweepWs& w, int B, int n, const float* coef,
+                    std::vector<Launch>& out) {
+  const int S = sum_dout(d);
+  int coloff[7];
+  for (int j = 0, o = 0; j < 7; ++j) {
+    coloff[j] = o;
+    o += d->blocks[j].dout;
+  }
+  float* const* O = w.outs;
+  const float* srcA[7] = {nullptr, O[0], O[1], O[2], O[3], O[4], O[5]};
+  const float* srcB[7] = {nullptr, nullptr, nullptr, nullptr, O[2], O[1], O[0]};
+  const int wa[7] = {0, d->blocks[0].dout, d->blocks[1].dout, d->blocks[2].dout, d->blocks[3].dout,
+                     d->blocks[4].dout, d->blocks[5].dout};
+  const int wbw[7] = {0, 0, 0, 0, d->blocks[2].dout, d->blocks[1].dout, d->blocks[0].dout};
+  out.clear();
+  static const int dbg = [] {
+    const char* e = getenv("DAMC_CHAIN_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  int noisy_k = 0;
+  for (int k = 0; k < n; ++k) {
+    const float* c = coef + 6 * (size_t)k;
+    const bool last = c[5] != 0.f;
+    for (int j = 0; j < 7; ++j) {
+      const damc_csq_block_t& b = d->blocks[j];
+      Launch L;
+      ChainArgs& a = L.a;
+      memset(&a, 0, sizeof(a));
+      a.srcA = srcA[j];
+      a.srcB = srcB[j];
+      a.wa = wa[j];
+      a.wb = wbw[j];
+      a.emb = j == 0;
+      a.z = w.z;
+      a.bmat = w.bmat;
+      a.nz = d->nz;
+      a.din = b.din;
+      a.kp = kpad(b.din);
+      a.dout = b.dout;
+      a.B = B;
+      a.w = w.w[j];
+      a.bls = w.bls[j];
+      a.gh = w.gh + (size_t)k * B * 2 * S + 2 * coloff[j];
+      a.ldgh = 2L * S;
+      a.out = O[j];
+      a.final_ = j == 6;
+      a.zt = w.z;
+      a.call = w.call;
+      a.dbg = dbg;
+      if (a.final_) {
+        a.residual = d->residual;
+        a.last = last;
+        a.k = k;
+        a.noisy_k = noisy_k;
+        a.c0 = c[0];
+        a.c1 = c[1];
+        a.c2 = c[2];
+        a.c3 = c[3];
+        a.c4 = c[4];
+      }
+      L.grid = (unsigned)(((b.dout + TC - 1) / TC) * ((B + TM - 1) / TM));
+      L.smem = a.emb ? (size_t)TM * emb_ld(a.kp) * sizeof(float) : 0;
+      out.push_back(L);
+    }
+    if (!last) ++noisy_k;
+  }
+}
+
+int launch_chain(const std::vector<Launch>& ls, hipStream_t s) {
+  for (const Launch& L : ls) hipLaunchKernelGGL(chain_kernel, dim3(L.grid), dim3(CH_THREADS), L.smem, s, L.a);
+  return (int)hipGetLastError();
+}
+
+// ---- graph cache: the chain of one sweep depends only on workspace addresses, shapes and the schedule scalars
+struct GraphEntry {
+  int dev;
+  const void* wsp;
+  size_t wsb;
+  int B, n;
+  std::vector<char> key;  // shapes + schedule bytes
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+  unsigned long stamp;
+};
+std::mutex g_mu;
+std::vector<GraphEntry> g_cache;
+unsigned long g_clock = 0;
+constexpr size_t kMaxGraphs = 16;
+
+bool graphs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DAMC_SWEEP_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+std::vector<char> graph_key(const damc_denoiser_t* d, int n, const float* coef) {
+  std::vector<char> k;
+  auto put = [&](const void* p, size_t nb) { k.insert(k.end(), (const char*)p, (const char*)p + nb); };
+  int dims[4] = {d->nz, d->ntemb, d->nxemb, d->residual};
+  put(dims, sizeof(dims));
+  for (int j = 0; j < 7; ++j) put(&d->blocks[j].din, 2 * sizeof(int));
+  put(coef, sizeof(float) * 6 * (size_t)n);
+  return k;
+}
+
+// replay (capturing on first use) the chain of a sweep; returns 0 or a hip error
+int run_chain_graph(const damc_denoiser_t* d, const SweepWs& w, void* wsp, size_t wsb, int B, int n, const float* coef,
+                    hipStream_t s) {
+  int dev = 0;
+  DAMC_CHECK(hipGetDevice(&dev));
+  std::vector<char> key = graph_key(d, n, coef);
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (GraphEntry& e : g_cache) {
+    if (e.dev == dev && e.wsp == wsp && e.wsb == wsb && e.B == B && e.n == n && e.key == key) {
+      e.stamp = ++g_clock;
+      return (int)hipGraphLaunch(e.exec, s);
+    }
+  }
+  std::vector<Launch> ls;
+  chain_launches(d, w, B, n, coef, ls);
+  hipStream_t cs;
+  DAMC_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipError_t err = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
+  if (err == hipSuccess) {
+    for (const Launch& L : ls) hipLaunchKernelGGL(chain_kernel, dim3(L.grid), dim3(CH_THREADS), L.smem, cs, L.a);
+    err = hipStreamEndCapture(cs, &graph);
+  }
+  if (err == hipSuccess) err = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipStreamDestroy(cs);
+  if (err != hipSuccess) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return (int)err;
+  }
+  if (g_cache.size() >= kMaxGraphs) {
+    auto old = std::min_element(g_cache.begin(), g_cache.end(),
+                                [](const GraphEntry& x, const GraphEntry& y) { return x.stamp < y.stamp; });
+    (void)hipGraphExecDestroy(old->exec);
+    (void)hipGraphDestroy(old->graph);
+    g_cache.erase(old);
+  }
+  g_cache.push_back(GraphEntry{dev, wsp, wsb, B, n, std::move(key), graph, exec, ++g_clock});
+  return (int)hipGraphLaunch(exec, s);
 }
 
 }  // namespace
@@ -367,7 +558,7 @@ extern "C" size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int B, in
 static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
                               const float* temb_in, const float* coef, int with_noise, const float* noise,
                               uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps, void* wsp,
-                              size_t wsb, void* stream, uint64_t step_offset) {
+                              size_t wsb, void* stream, uint64_t step_offset, bool allow_graph) {
   int rc = validate(d);
   if (rc) return rc;
   if (!xemb || !zt || !temb_in || !coef || B <= 0 || n <= 0) return DAMC_ERR_ARG;
@@ -378,8 +569,54 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   hipStream_t s = as_stream(stream);
   const int S = sum_dout(d);
   const int nt = d->ntemb, nx = d->nxemb;
+  int coloff[7];
+  for (int j = 0, o = 0; j < 7; ++j) {
+    coloff[j] = o;
+    o += d->blocks[j].dout;
+  }
 
-  // ---- per-sweep precompute: time-MLP (batch-invariant) and the ctx Linear split
+  // ---- 1. pack the live weights
+  {
+    PackArgs pa;
+    long maxn = 0;
+    for (int j = 0; j < 7; ++j) {
+      const damc_csq_block_t& b = d->blocks[j];
+      PackBlock& p = pa.b[j];
+      p.wl = b.wl;
+      p.bl = b.bl;
+      p.ws = b.ws;
+      p.bs = b.bs;
+      p.wg = b.wg;
+      p.bg = b.bg;
+      p.wb = b.wb;
+      p.wctx = d->wctx[j];
+      p.bctx = d->bctx[j];
+      p.din = b.din;
+      p.dout = b.dout;
+      p.kp = kpad(b.din);
+      p.coloff = coloff[j];
+      p.w = w.w[j];
+      p.bls = w.bls[j];
+      p.wgb = w.wgb[j];
+      p.bg2 = w.bg2[j];
+      const long ntn = (b.dout + TC - 1) / TC;
+      maxn = std::max({maxn, ntn * 16 * p.kp, 2L * b.dout * b.dout, (long)(nt + nx) * b.dout});
+    }
+    pa.ntemb = nt;
+    pa.nxemb = nx;
+    pa.S = S;
+    pa.wctx_t = w.wctx_t;
+    pa.wctx_x = w.wctx_x;
+    pa.bctx = w.bctx;
+    hipLaunchKernelGGL(pack_denoiser_kernel, dim3((unsigned)((maxn + 255) / 256), 7, 3), dim3(256), 0, s, pa);
+    const long ntt = (long)nt * nt;
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw1, nt, nt, w.tw1t);
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw2, nt, nt, w.tw2t);
+    DAMC_CHECK(hipMemcpyAsync(w.bmat, d->bmat, sizeof(float) * d->nz * (d->nz / 2), hipMemcpyDeviceToDevice, s));
+    DAMC_LAUNCH_CHECK();
+  }
+
+  // ---- 2. ctx: time MLP (n rows), xemb part (B rows), c for every (step, row)
   {
     damc::GemmArgs g;
     g.M = n;
@@ -388,7 +625,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     g.k_per_z = nt;
     g.A = temb_in;
     g.lda = nt;
-    g.B = d->tw1;
+    g.B = w.tw1t;
     g.ldb = nt;
     g.C = w.t1;
     g.ldc = nt;
@@ -398,19 +635,19 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     if ((rc = damc::launch_gemm(g, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "sweep_pre", 2.0 * n * nt * nt, s)))
       return rc;
     g.A = w.t1;
-    g.B = d->tw2;
+    g.B = w.tw2t;
     g.C = w.t2;
     g.bias = d->tb2;
     g.act = DAMC_ACT_SILU;  // the ctx Linear consumes SiLU(temb)
     if ((rc = damc::launch_gemm(g, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "sweep_pre", 2.0 * n * nt * nt, s)))
       return rc;
     g.A = w.t2;
-    g.B = d->wctx_t;
+    g.B = w.wctx_t;
     g.ldb = S;
     g.N = S;
     g.C = w.qt;
     g.ldc = S;
-    g.bias = d->bctx;
+    g.bias = w.bctx;
     g.bias_mod = S;
     g.act = DAMC_ACT_NONE;
     if ((rc = damc::launch_gemm(g, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "sweep_pre", 2.0 * n * nt * S, s)))
@@ -424,175 +661,66 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     h.k_per_z = nx;
     h.A = w.xs;
     h.lda = nx;
-    h.B = d->wctx_x;
+    h.B = w.wctx_x;
     h.ldb = S;
     h.C = w.px;
     h.ldc = S;
     if ((rc = damc::launch_gemm(h, damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, 1, "sweep_pre", 2.0 * B * nx * S, s)))
       return rc;
-  }
-
-  // the widest blocks (din 4w) need more than the default 64 KB of dynamic LDS
-  static const bool lds_ok = hipFuncSetAttribute((const void*)csq_block_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  if (!lds_ok) return DAMC_ERR_UNSUPPORTED;
-
-  // ---- the sweep: 7 fused block launches per step
-  int coloff[7];
-  {
-    int o = 0;
-    for (int j = 0; j < 7; ++j) {
-      coloff[j] = o;
-      o += d->blocks[j].dout;
-    }
-  }
-  // coef is a HOST table: the per-step scalars travel by value in the kernel arguments
-  const float* cf = coef;
-  // block inputs: source pointers per block (in0: emb of z)
-  float* const* O = w.outs;
-  const float* srcA[7] = {nullptr, O[0], O[1], O[2], O[3], O[4], O[5]};
-  const float* srcB[7] = {nullptr, nullptr, nullptr, nullptr, O[2], O[1], O[0]};
-  const int wa[7] = {0, d->blocks[0].dout, d->blocks[1].dout, d->blocks[2].dout, d->blocks[3].dout,
-                     d->blocks[4].dout, d->blocks[5].dout};
-  const int wbw[7] = {0, 0, 0, 0, d->blocks[2].dout, d->blocks[1].dout, d->blocks[0].dout};
-  double flops_step = 0;
-  for (int j = 0; j < 7; ++j) {
-    const damc_csq_block_t& b = d->blocks[j];
-    flops_step += 2.0 * B * (2.0 * b.din * b.dout + 2.0 * b.dout * b.dout);
-  }
-  // ---- opt-in (DAMC_SWEEP_COOP=1): the whole sweep as ONE cooperative launch with a grid-wide barrier
-  // between blocks.  Measured at CIFAR B=128: 151 us per denoise step against 64.5 us for the per-block
-  // launches below — the runtime's grid barrier costs ~18 us, more than a launch/drain gap; kept for A/B.
-  static const bool coop_env = [] {
-    const char* e = getenv("DAMC_SWEEP_COOP");
-    return e && e[0] == '1';
-  }();
-  if (coop_env && step_offset == 0) {
-    size_t sm_max = 0;
-    int max_tiles = 0;
-    for (int j = 0; j < 7; ++j) {
-      sm_max = std::max(sm_max, csq_smem_bytes(d->blocks[j].din, d->blocks[j].dout, j == 0 ? d->nz : 0));
-      max_tiles = std::max(max_tiles, ((d->blocks[j].dout + TN - 1) / TN) * ((B + TM - 1) / TM));
-    }
-    static const bool coop_ok = hipFuncSetAttribute((const void*)sweep_coop_kernel,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
-                                hipSuccess;
-    int per_cu = 0, dev = 0, ncu = 0;
-    if (coop_ok && hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_coop_kernel, CSQ_THREADS, sm_max) ==
-            hipSuccess &&
-        per_cu > 0) {
-      const int resident = per_cu * ncu;
-      int grid = (max_tiles + 7) / 8 * 8;
-      if (grid > resident) grid = resident / 8 * 8;
-      if (grid >= 8) {
-        SweepArgs sa{};
-        for (int j = 0; j < 7; ++j) {
-          const damc_csq_block_t& b = d->blocks[j];
-          CsqArgs& a = sa.blk[j];
-          a.srcA = srcA[j];
-          a.wa = wa[j];
-          a.srcB = srcB[j];
-          a.wb_ = wbw[j];
-          a.emb_mode = j == 0;
-          a.z = zt;
-          a.bmat = d->bmat;
-          a.nz = d->nz;
-          a.din = b.din;
-          a.dout = b.dout;
-          a.B = B;
-          a.wl = b.wl;
-          a.bl = b.bl;
-          a.ws = b.ws;
-          a.bs = b.bs;
-          a.wg = b.wg;
-          a.bg = b.bg;
-          a.wb = b.wb;
-          a.px = w.px + coloff[j];
-          a.ldpx = S;
-          a.out = O[j];
-          a.final_ = j == 6;
-          a.residual = d->residual;
-          a.seed = seed;
-          a.chain_base = chain_base;
-          a.zt = zt;
-          sa.coloff[j] = coloff[j];
-        }
-        DAMC_CHECK(hipMemcpyAsync(w.coef, coef, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice, s));
-        sa.coef = w.coef;
-        sa.qt = w.qt;
-        sa.noise = noise;
-        sa.eps_log = eps_log;
-        sa.eps_log_steps = eps_log ? eps_log_steps : 0;
-        sa.with_noise = with_noise;
-        sa.S = S;
-        sa.n_steps = n;
-        void* args[] = {&sa};
-        ProfScope ps("denoise_sweep", flops_step * n, s);
-        if (hipLaunchCooperativeKernel((const void*)sweep_coop_kernel, dim3(grid), dim3(CSQ_THREADS), args, sm_max,
-                                       s) == hipSuccess)
-          return (int)hipGetLastError();
-        (void)hipGetLastError();  // not launchable cooperatively here: per-block launches below
-      }
-    }
-  }
-  int noisy_k = 0;
-  for (int k = 0; k < n; ++k) {
-    const float* c = cf + 6 * (size_t)k;
-    const bool last = c[5] != 0.f;
-    ProfScope ps("denoise_step", flops_step, s);
-    for (int j = 0; j < 7; ++j) {
-      const damc_csq_block_t& b = d->blocks[j];
-      CsqArgs a{};
-      a.srcA = srcA[j];
-      a.wa = wa[j];
-      a.srcB = srcB[j];
-      a.wb_ = wbw[j];
-      a.emb_mode = j == 0;
-      a.z = zt;
-      a.bmat = d->bmat;
-      a.nz = d->nz;
-      a.din = b.din;
-      a.dout = b.dout;
-      a.B = B;
-      a.wl = b.wl;
-      a.bl = b.bl;
-      a.ws = b.ws;
-      a.bs = b.bs;
-      a.wg = b.wg;
-      a.bg = b.bg;
-      a.wb = b.wb;
-      a.px = w.px + coloff[j];
-      a.ldpx = S;
-      a.qt = w.qt + (size_t)k * S + coloff[j];
-      a.out = O[j];
-      a.final_ = j == 6;
-      if (a.final_) {
-        a.residual = d->residual;
-        a.c0 = c[0];
-        a.c1 = c[1];
-        a.c2 = c[2];
-        a.c3 = c[3];
-        a.c4 = c[4];
-        a.last = last;
-        a.with_noise = with_noise && !last;
-        a.noise = (a.with_noise && noise) ? noise + (size_t)noisy_k * B * d->nz : nullptr;
-        a.seed = seed;
-        a.chain_base = chain_base;
-        a.step = step_offset + (uint64_t)noisy_k;
-        a.zt = zt;
-        a.eps_log = (eps_log && k < eps_log_steps) ? eps_log + (size_t)k * B * d->nz : nullptr;
-      }
-      const size_t sm = csq_smem_bytes(b.din, b.dout, j == 0 ? d->nz : 0);
-      dim3 grid((b.dout + TN - 1) / TN, (B + TM - 1) / TM);
-      hipLaunchKernelGGL(csq_block_kernel, grid, dim3(CSQ_THREADS), sm, s, a);
-    }
-    if (!last) ++noisy_k;
+    const long tot = (long)n * B * S;
+    hipLaunchKernelGGL(ctx_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, w.px, w.qt, B, S, tot, w.cx);
     DAMC_LAUNCH_CHECK();
   }
-  (void)temb_in;
-  return 0;
+
+  // ---- 3. every block's gate and hyper bias for every (step, row): [sigmoid(c Wg^T + bg) | c Wb^T]
+  for (int j = 0; j < 7; ++j) {
+    const int dout = d->blocks[j].dout;
+    damc::GemmArgs g;
+    g.M = n * B;
+    g.N = 2 * dout;
+    g.K = dout;
+    g.k_per_z = dout;
+    g.A = w.cx + coloff[j];
+    g.lda = S;
+    g.B = w.wgb[j];
+    g.ldb = 2 * dout;
+    g.C = w.gh + 2 * coloff[j];
+    g.ldc = 2L * S;
+    g.bias = w.bg2[j];
+    g.bias_mod = 2 * dout;
+    g.gate_cols = dout;
+    if ((rc = damc::launch_gemm(g, damc::A_DENSE, damc::EPI_GATE, damc::O_DENSE, 1, "sweep_hyper",
+                                2.0 * n * B * dout * 2.0 * dout, s)))
+      return rc;
+  }
+
+  // ---- 4. the dependent chain
+  SweepCall call;
+  call.noise = (with_noise && noise) ? noise : nullptr;
+  call.eps_log = eps_log;
+  call.eps_log_steps = eps_log ? eps_log_steps : 0;
+  call.seed = seed;
+  call.chain_base = chain_base;
+  call.step_offset = step_offset;
+  call.with_noise = with_noise ? 1 : 0;
+  const long nzb = (long)B * d->nz;
+  hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, call, w.call, zt, w.z,
+                     nzb);
+  DAMC_LAUNCH_CHECK();
+  double flops_step = 0;
+  for (int j = 0; j < 7; ++j) flops_step += 2.0 * B * 2.0 * d->blocks[j].din * d->blocks[j].dout;
+  {
+    ProfScope ps("denoise_chain", flops_step * n, s);
+    if (allow_graph && graphs_enabled()) {
+      if ((rc = run_chain_graph(d, w, wsp, wsb, B, n, coef, s))) return rc;
+    } else {
+      std::vector<Launch> ls;
+      chain_launches(d, w, B, n, coef, ls);
+      if ((rc = launch_chain(ls, s))) return rc;
+    }
+  }
+  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, w.z, zt, nzb);
+  return (int)hipGetLastError();
 }
 
 extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt, int B, int n,
@@ -600,7 +728,7 @@ extern "C" int damc_reverse_sweep(const damc_denoiser_t* d, const float* xemb, f
                                   uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps,
                                   void* wsp, size_t wsb, void* stream) {
   return reverse_sweep_impl(d, xemb, zt, B, n, temb_in, coef, with_noise, noise, seed, chain_base, eps_log,
-                            eps_log_steps, wsp, wsb, stream, 0);
+                            eps_log_steps, wsp, wsb, stream, 0, true);
 }
 
 // SURVEY.md §8b names
@@ -609,7 +737,7 @@ extern "C" int damc_q_reverse_sweep(const damc_denoiser_t* d, const float* xemb,
                                     uint64_t seed, uint64_t chain_base, float* eps_log, int eps_log_steps,
                                     void* wsp, size_t wsb, void* stream) {
   return reverse_sweep_impl(d, xemb, zt, B, n, temb_in, coef, with_noise, noise, seed, chain_base, eps_log,
-                            eps_log_steps, wsp, wsb, stream, 0);
+                            eps_log_steps, wsp, wsb, stream, 0, true);
 }
 
 extern "C" int damc_denoise_step(const damc_denoiser_t* d, const float* xemb, float* zt, int B, const float* temb_row,
@@ -617,5 +745,5 @@ extern "C" int damc_denoise_step(const damc_denoiser_t* d, const float* xemb, fl
                                  uint64_t noise_step, uint64_t chain_base, float* eps, void* wsp, size_t wsb,
                                  void* stream) {
   return reverse_sweep_impl(d, xemb, zt, B, 1, temb_row, coef_row, with_noise, noise, seed, chain_base, eps,
-                            eps ? 1 : 0, wsp, wsb, stream, noise_step);
+                            eps ? 1 : 0, wsp, wsb, stream, noise_step, false);
 }

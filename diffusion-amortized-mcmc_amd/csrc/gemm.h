@@ -5,7 +5,7 @@
 namespace damc {
 
 enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_SCALAR = 2 };
-enum Epi { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_MASK = 2, EPI_RESID = 3 };
+enum Epi { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_MASK = 2, EPI_RESID = 3, EPI_GATE = 4 };
 enum OMode { O_DENSE = 0, O_PHASE = 1, O_WGRAD = 2 };
 
 // C[M,N] (+)= A[M,K] · B[K,N], K reduced in fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fmaf chains).
@@ -61,6 +61,9 @@ struct GemmArgs {
   const unsigned char* mask_sgn = nullptr;
   // O_WGRAD geometry (see above)
   int wg_phases = 1, wg_bp = 0;
+  // EPI_GATE: v + bias[n], then sigmoid on the columns n < gate_cols (a ConcatSquash block's hyper gate and
+  // hyper bias computed by one GEMM, diffusion_net.py:441-443)
+  int gate_cols = 0;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered

@@ -56,6 +56,9 @@ __device__ __forceinline__ void epi_element(const GemmArgs& p, float* Cz, long i
     v = act_apply(v, p.act, p.slope);
   } else if (EPI == EPI_MASK) {
     v *= act_grad_from_out(p.mask[idx], p.mask_act, p.mask_slope);
+  } else if (EPI == EPI_GATE) {
+    if (p.bias) v += p.bias[n];
+    if (n < p.gate_cols) v = 1.f / (1.f + expf(-v));
   } else if (EPI == EPI_RESID) {
     if (p.bias) v += p.bias[n % p.bias_mod];
     const float t = act_apply(v, p.act, p.slope);
@@ -1322,6 +1325,7 @@ int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const 
   DAMC_G(A_DENSE, EPI_BIAS_ACT, O_DENSE)
   DAMC_G(A_DENSE, EPI_MASK, O_DENSE)
   DAMC_G(A_DENSE, EPI_RESID, O_DENSE)
+  DAMC_G(A_DENSE, EPI_GATE, O_DENSE)
   DAMC_G(A_CONV, EPI_BIAS_ACT, O_PHASE)
   DAMC_G(A_CONV, EPI_MASK, O_DENSE)
   DAMC_G(A_CONV, EPI_BIAS_ACT, O_DENSE)

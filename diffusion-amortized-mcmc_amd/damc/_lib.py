@@ -62,17 +62,7 @@ class CsqBlock(ctypes.Structure):  # damc_csq_block_t
     ]
 
 
-class Denoiser(ctypes.Structure):
-    _fields_ = [
-        ("nz", ctypes.c_int), ("ntemb", ctypes.c_int), ("nxemb", ctypes.c_int), ("residual", ctypes.c_int),
-        ("bmat", ctypes.c_void_p),
-        ("tw1", ctypes.c_void_p), ("tb1", ctypes.c_void_p), ("tw2", ctypes.c_void_p), ("tb2", ctypes.c_void_p),
-        ("wctx_t", ctypes.c_void_p), ("wctx_x", ctypes.c_void_p), ("bctx", ctypes.c_void_p),
-        ("blocks", CsqBlock * 7),
-    ]
-
-
-class DenoiserTrain(ctypes.Structure):
+class Denoiser(ctypes.Structure):  # damc_denoiser_t (= damc_denoiser_train_t): PyTorch layouts throughout
     _fields_ = [
         ("nz", ctypes.c_int), ("ntemb", ctypes.c_int), ("nxemb", ctypes.c_int), ("residual", ctypes.c_int),
         ("bmat", ctypes.c_void_p),
@@ -80,6 +70,9 @@ class DenoiserTrain(ctypes.Structure):
         ("blocks", CsqBlock * 7),
         ("wctx", ctypes.c_void_p * 7), ("bctx", ctypes.c_void_p * 7),
     ]
+
+
+DenoiserTrain = Denoiser
 
 
 class DenoiserGrads(ctypes.Structure):

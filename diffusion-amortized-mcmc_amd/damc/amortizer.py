@@ -145,7 +145,9 @@ class EncoderPlan:
 
 # ----------------------------------------------------------------------------- denoiser
 class DenoiserPlan:
-    """Packed Diffusion_UnetA (diffusion_net.py:463-533)."""
+    """Diffusion_UnetA (diffusion_net.py:463-533) as a damc_denoiser_t: pointers to the live parameters in their
+    PyTorch layouts (the library re-lays them out into its workspace per call), plus a workspace cached per
+    (batch, steps, device) so the library's cached HIP graph of the reverse sweep is reused across calls."""
 
     def __init__(self, p):
         self.p = p
@@ -153,34 +155,23 @@ class DenoiserPlan:
         if len(self.blocks) != 7:
             raise NotImplementedError("Diffusion_UnetA with %d blocks" % len(self.blocks))
         self.nz, self.ntemb, self.nxemb = p.nz, p.ntemb, p.nxemb
+        self._ws = None
 
     def pack(self, device):
-        t = lambda w: _dev(w, device).t().contiguous()  # noqa: E731  W (out,in) -> W^T (in,out)
-        d = _lib.Denoiser()
-        d.nz, d.ntemb, d.nxemb, d.residual = self.nz, self.ntemb, self.nxemb, int(bool(self.p.residual))
-        keep = []
-        bmat = _dev(self.p.B, device)
-        tw1, tb1 = t(self.p.time_mlp[1].weight), _dev(self.p.time_mlp[1].bias, device)
-        tw2, tb2 = t(self.p.time_mlp[3].weight), _dev(self.p.time_mlp[3].bias, device)
-        ctx_w = [_dev(blk._layer_ctx[1].weight, device) for blk in self.blocks]
-        wctx_t = torch.cat([w[:, :self.ntemb] for w in ctx_w], dim=0).t().contiguous()
-        wctx_x = torch.cat([w[:, self.ntemb:] for w in ctx_w], dim=0).t().contiguous()
-        bctx = torch.cat([_dev(blk._layer_ctx[1].bias, device) for blk in self.blocks]).contiguous()
-        keep += [bmat, tw1, tb1, tw2, tb2, wctx_t, wctx_x, bctx]
-        d.bmat, d.tw1, d.tb1, d.tw2, d.tb2 = [x.data_ptr() for x in (bmat, tw1, tb1, tw2, tb2)]
-        d.wctx_t, d.wctx_x, d.bctx = wctx_t.data_ptr(), wctx_x.data_ptr(), bctx.data_ptr()
-        for j, blk in enumerate(self.blocks):
-            lin, skip = blk._layer[0], blk._skip
-            # block weights stay in the PyTorch (out, in) layout: the block kernel reads k-contiguous rows
-            c = lambda w: _dev(w, device).contiguous()  # noqa: E731
-            arrs = [c(lin.weight), _dev(lin.bias, device), c(skip.weight), _dev(skip.bias, device),
-                    c(blk._hyper_gate.weight), _dev(blk._hyper_gate.bias, device), c(blk._hyper_bias.weight)]
-            keep += arrs
-            b = d.blocks[j]
-            b.din, b.dout = lin.in_features, lin.out_features
-            b.wl, b.bl, b.ws, b.bs, b.wg, b.bg, b.wb = [x.data_ptr() for x in arrs]
-        self._keep = keep
-        return d
+        from .training import _denoiser_desc, _denoiser_params
+
+        params = [_dev(t, device) for _, _, t in _denoiser_params(self.p)]
+        self._keep = params  # copies (only if a parameter lives elsewhere) stay alive for the call
+        return _denoiser_desc(self.p, params)
+
+    def workspace(self, desc, B, n, device):
+        nbytes = int(_lib.lib().damc_sweep_workspace_bytes(ctypes.byref(desc), B, n))
+        if nbytes == 0:
+            raise _lib.DamcError("unsupported denoiser configuration for the HIP path")
+        key = (int(B), int(n), str(device))
+        if self._ws is None or self._ws[0] != key or self._ws[1].numel() < nbytes:
+            self._ws = (key, torch.empty(nbytes, dtype=torch.uint8, device=device))
+        return self._ws[1], nbytes
 
 
 _ENC = weakref.WeakKeyDictionary()
@@ -226,10 +217,7 @@ def reverse_sweep(Q, xemb, zt, noise=None, seed=None, chain_base=0, eps_log_step
     B = zt.shape[0]
     coef_h, temb_d = cached_step_tables(n, Q.logsnr_min, Q.logsnr_max, Q.var_type, plan.ntemb, dev)
     L = _lib.lib()
-    nbytes = int(L.damc_sweep_workspace_bytes(ctypes.byref(d), B, n))
-    if nbytes == 0:
-        raise _lib.DamcError("unsupported denoiser configuration for the HIP path")
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ws, nbytes = plan.workspace(d, B, n, dev)
     with_noise = bool(Q.with_noise) if with_noise is None else bool(with_noise)
     if noise is not None:
         noise = noise.to(device=dev, dtype=torch.float32).contiguous()

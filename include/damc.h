@@ -236,11 +236,9 @@ int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bia
               int n, int k, int act, float slope, void* stream);
 
 /* Denoiser Diffusion_UnetA (diffusion_net.py:417-533) and its reverse sweep (diffusion_net.py:595-622).
- * Seven ConcatSquashLinearSkipCtx blocks (in0 in1 in2 mid0 out0 out1 out2); every Linear weight is
- * packed as W^T (in, out).  The ctx Linear of each block, Lc(SiLU(cat(temb, xemb))), is split into its
- * step-invariant xemb part (computed once per sweep, (B, sum dout)) and its batch-invariant temb part
- * (computed once per step for the whole batch, (n_steps, sum dout)); blocks are concatenated along
- * the output axis in block order. */
+ * Seven ConcatSquashLinearSkipCtx blocks (in0 in1 in2 mid0 out0 out1 out2).  Every weight is the caller's
+ * PyTorch tensor in its own layout (nn.Linear (out, in)); the library re-lays them out into its workspace per
+ * call (the nets train between calls), so the caller does no per-call packing. */
 typedef struct {
   int din, dout;
   /* PyTorch nn.Linear layout (out, in), k contiguous */
@@ -252,18 +250,22 @@ typedef struct {
 
 typedef struct {
   int nz, ntemb, nxemb, residual;
-  const float* bmat;               /* p.B (nz, nz/2)                                         */
-  const float *tw1, *tb1;          /* time_mlp[1]: (ntemb, ntemb) W^T, (ntemb)               */
-  const float *tw2, *tb2;          /* time_mlp[3]                                            */
-  const float* wctx_t;             /* (ntemb, sum dout): temb columns of every ctx Linear    */
-  const float* wctx_x;             /* (nxemb, sum dout): xemb columns of every ctx Linear    */
-  const float* bctx;               /* (sum dout)                                             */
-  damc_csq_block_t blocks[7];
+  const float* bmat;                  /* p.B (nz, nz/2)                                  */
+  const float *tw1, *tb1, *tw2, *tb2; /* time_mlp[1], time_mlp[3]: (out, in), (out)      */
+  damc_csq_block_t blocks[7];         /* in0 in1 in2 mid0 out0 out1 out2                 */
+  const float* wctx[7];               /* _layer_ctx[1].weight (dout, ntemb + nxemb)       */
+  const float* bctx[7];               /* _layer_ctx[1].bias (dout)                       */
 } damc_denoiser_t;
 
 /* workspace bytes for damc_reverse_sweep */
 size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch, int n_steps);
-/* The reverse sweep (n_steps = n_interval denoiser evaluations, i = n_steps-1 .. 0, k = n_steps-1-i):
+/* The reverse sweep (n_steps = n_interval denoiser evaluations, i = n_steps-1 .. 0, k = n_steps-1-i).
+ * Per call the library packs the weights, then evaluates everything that does not depend on zt for all
+ * steps at once: the time MLP (batch-invariant), the ctx Linear's xemb part (step-invariant), and for every
+ * (step, row) a block's ctx c = SiLU(Lc(SiLU(cat(temb, xemb)))), its gate sigmoid(c Wg^T + bg) and hyper
+ * bias c Wb^T (fp32 MFMA GEMMs over n*B rows).  The dependent chain — per step the 7 blocks'
+ * x Wl^T / x Ws^T products plus the reverse-step update — then runs as 7 launches per step, replayed from a
+ * HIP graph cached per (workspace, shapes, schedule) so the host does not bound the ~2 us kernels.
  *   eps = p(zt, l_t, xemb); pred = c0 * (zt - eps * c1); zt <- last ? pred : c2*zt + c3*pred (+ c4*xi)
  * temb_in (n_steps, ntemb): SinusoidalPosEmb of the step's logsnr input (host, fp32, as the reference);
  * coef (n_steps, 6), a HOST pointer: {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std,
@@ -293,16 +295,10 @@ int damc_denoise_step(const damc_denoiser_t* d, const float* xemb, float* zt, in
  * trained by the Q update of every iteration (workspace/train_gen_recon.py:211-220): eps_pred =
  * p(zt, logsnr, xemb) with every intermediate kept, then the backward from dL/deps_pred to every parameter
  * of p, to zt and to xemb (which the caller's autograd carries into the encoder / prior_emb).  All weights
- * in PyTorch layouts.  temb_in (B, ntemb) is SinusoidalPosEmb of the per-sample logsnr input, evaluated by
- * the caller with the reference's op sequence (diffusion_net.py:447-461, 490-491). */
-typedef struct {
-  int nz, ntemb, nxemb, residual;
-  const float* bmat;                  /* p.B (nz, nz/2)                                  */
-  const float *tw1, *tb1, *tw2, *tb2; /* time_mlp[1], time_mlp[3]: (out, in), (out)      */
-  damc_csq_block_t blocks[7];         /* in0 in1 in2 mid0 out0 out1 out2                 */
-  const float* wctx[7];               /* _layer_ctx[1].weight (dout, ntemb + nxemb)       */
-  const float* bctx[7];               /* _layer_ctx[1].bias (dout)                       */
-} damc_denoiser_train_t;
+ * in PyTorch layouts (the damc_denoiser_t of the sweep).  temb_in (B, ntemb) is SinusoidalPosEmb of the
+ * per-sample logsnr input, evaluated by the caller with the reference's op sequence (diffusion_net.py:447-461,
+ * 490-491). */
+typedef damc_denoiser_t damc_denoiser_train_t;
 typedef struct { /* gradients, same layouts (written, not accumulated; NULL entries are skipped) */
   float* bmat;
   float *tw1, *tb1, *tw2, *tb2;

@@ -1,9 +1,12 @@
 """GPU parity: the amortizer Q on the HIP path (encoder + prior embedding + reverse sweep) vs the
-reference's golden vectors (workspace/src/diffusion_net.py:227-622).
+reference's golden vectors and the fp64 oracle (workspace/src/diffusion_net.py:227-622).
 
-Tolerances: encoder xemb rel-L2 <= 1e-5; eps of the first reverse step <= 1e-5, of steps 2-3 <= 1e-4
-(inherited rounding, amplified by sqrt(1+e^-l) per step); end-point of the sweep <= conftest.Q_END_TOL
-(2x the reference's own fp32-vs-fp64 spread on that case).
+Tolerances: encoder xemb rel-L2 <= 1e-5 and eps of the first reverse step <= 1e-5 against the golden.  Later
+steps amplify rounding by sqrt(1+e^-l) per step, and the reference's own fp32 result is already up to 2.4e-4
+(step 3) / 8e-2 (end of a 10-step sweep) / 1e-2 (100 steps) away from an fp64 evaluation of the same sweep
+(printed by these tests), so eps of steps 2-3 and the sweep end-point are judged accuracy-relative: the HIP
+result's distance to the fp64 oracle must stay within 3x the reference golden's distance to it (+ a 1e-5 /
+1e-6 floor).  The golden itself is still bounded by conftest.Q_END_TOL.
 """
 import pytest
 import torch
@@ -11,6 +14,27 @@ import torch
 from conftest import Q_END_TOL, Q_NAMES, build_q_case, rel_l2
 
 pytestmark = pytest.mark.gpu
+
+_FP64 = {}
+
+
+def fp64_sweeps(name):
+    """fp64 oracle: eps of steps 1-3 and the end-point of the posterior sweep (Q(x)) and the prior sweep
+    (Q(x=None) on the case's prior-embedding noise), cached per case."""
+    if name not in _FP64:
+        from oracle import damc_oracle as orc
+
+        c = build_q_case(name)
+        Q, m = c["Q"].double(), c["meta"]
+        args = (m["n_interval"], m["logsnr_min"], m["logsnr_max"], m["var_type"])
+        with torch.no_grad():
+            xemb = orc.encoder_forward(Q.encoder, c["x"].double())
+            zp, ep = orc.reverse_sweep(Q, xemb, c["zt0"].double(), c["eps"].double(), *args)
+            pe = orc.prior_embedding(Q, c["pe_noise"].double())
+            zq, eq = orc.reverse_sweep(Q, pe, c["zt0"].double(), c["eps"].double(), *args)
+        _FP64[name] = dict(post=zp.numpy(), post_eps=[e.numpy() for e in ep[:3]], prior=zq.numpy(),
+                           prior_eps=[e.numpy() for e in eq[:3]])
+    return _FP64[name]
 
 
 @pytest.fixture(scope="module")
@@ -27,27 +51,39 @@ def test_encoder_matches_reference(am, gpu_device, name):
     assert rel_l2(xemb.cpu().numpy(), c["rec"]["xemb"]) < 1e-5
 
 
+def _check_sweep(name, eps, zt, rec_eps, rec_end, ref_eps, ref_end, nsteps):
+    assert rel_l2(eps[0], rec_eps[0]) < 1e-5
+    for k in range(1, nsteps):
+        e_hip, e_ref = rel_l2(eps[k], ref_eps[k]), rel_l2(rec_eps[k], ref_eps[k])
+        print("%s eps step %d: |hip-fp64| %.2e  |reference-fp64| %.2e" % (name, k + 1, e_hip, e_ref))
+        assert e_hip <= 3 * e_ref + 1e-5, k
+    e_hip, e_ref = rel_l2(zt, ref_end), rel_l2(rec_end, ref_end)
+    print("%s sweep end: |hip-fp64| %.2e  |reference-fp64| %.2e  |hip-reference| %.2e"
+          % (name, e_hip, e_ref, rel_l2(zt, rec_end)))
+    assert e_hip <= 3 * e_ref + 1e-6
+    assert rel_l2(zt, rec_end) < Q_END_TOL[name]
+
+
 @pytest.mark.parametrize("name", Q_NAMES)
 def test_posterior_sweep_matches_reference(am, gpu_device, name):
     c = build_q_case(name, gpu_device)
     Q, rec = c["Q"], c["rec"]
+    ref = fp64_sweeps(name)
     xemb = am.encoder_forward(Q.encoder, c["x"])
     zt = c["zt0"].clone()
     eps = am.reverse_sweep(Q, xemb, zt, noise=c["eps"], eps_log_steps=3).cpu().numpy()
-    for k in range(3):
-        assert rel_l2(eps[k], rec["q_post_eps3"][k]) < (1e-5 if k == 0 else 1e-4), k
-    assert rel_l2(zt.cpu().numpy(), rec["q_post"]) < Q_END_TOL[name]
+    _check_sweep(name, eps, zt.cpu().numpy(), rec["q_post_eps3"], rec["q_post"], ref["post_eps"], ref["post"], 3)
 
 
 @pytest.mark.parametrize("name", Q_NAMES)
 def test_prior_sweep_matches_reference(am, gpu_device, name):
     c = build_q_case(name, gpu_device)
     Q, rec = c["Q"], c["rec"]
+    ref = fp64_sweeps(name)
     xemb = am.prior_embedding(Q, c["pe_noise"])
     zt = c["zt0"].clone()
     eps = am.reverse_sweep(Q, xemb, zt, noise=c["eps"], eps_log_steps=1).cpu().numpy()
-    assert rel_l2(eps[0], rec["q_prior_eps3"][0]) < 1e-5
-    assert rel_l2(zt.cpu().numpy(), rec["q_prior"]) < Q_END_TOL[name]
+    _check_sweep(name, eps, zt.cpu().numpy(), rec["q_prior_eps3"], rec["q_prior"], ref["prior_eps"], ref["prior"], 1)
 
 
 def test_denoise_step_vs_oracle_at_baseline_width(am, gpu_device):
