@@ -66,20 +66,28 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint64_t chain, ui
                                                uint32_t stream_id, float out[4]) {
   Philox4 r = philox4x32_10(quad, (uint32_t)step, (uint32_t)chain, stream_id ^ (uint32_t)(chain >> 32) * 0x9E3779B9u,
                             (uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(step >> 32));
-  const float two_pi = 6.28318530717958647692f;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     float u1 = u01_open(r.v[2 * p]);
     float u2 = u01_open(r.v[2 * p + 1]);
     float rad = sqrtf(-2.0f * logf(u1));
-    float s, c;
-    sincosf(two_pi * u2, &s, &c);
+    // Box-Muller angle 2 pi u2 by the hardware sin / cos, whose argument is in revolutions (u2 in (0, 1]):
+    // no argument reduction, hence no large-argument path whose private array would give every kernel that
+    // draws noise a scratch segment
+    const float s = __builtin_amdgcn_sinf(u2), c = __builtin_amdgcn_cosf(u2);
     out[2 * p] = rad * c;
     out[2 * p + 1] = rad * s;
   }
 }
 
 enum { DAMC_STREAM_POSTERIOR = 0x51, DAMC_STREAM_PRIOR = 0x52, DAMC_STREAM_SWEEP = 0x53 };
+
+// element i & 3 of a 4-value draw without a runtime-indexed private array (which the compiler would place in
+// scratch memory: a per-dispatch scratch setup and slow private loads for every kernel that draws noise)
+__device__ __forceinline__ float pick4(const float (&v)[4], int i) {
+  const int j = i & 3;
+  return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+}
 
 // fp32 ops that must not be contracted into FMA (bit-level match with the reference's separately rounded
 // PyTorch elementwise ops: z - (c*g), then + s*xi).  HIP's __fmul_rn & co. are plain operators, which

@@ -37,6 +37,7 @@ constexpr int TM = 16;           // rows per workgroup
 constexpr int TC = 8;            // output columns per workgroup (x 2 products)
 constexpr int KG = 64;           // K padding granule: 4 waves x one 16-deep k-group
 constexpr int CH_CHUNK = 8;      // k-groups whose loads a lane keeps in flight at once
+constexpr int EMB_G = 8;         // in0: 16-deep k-groups of z (nz <= 128)
 
 // per-call values read by the last block (device memory in the workspace, written before each sweep so a cached
 // graph needs no new kernel arguments)
@@ -53,7 +54,7 @@ struct ChainArgs {
   int wa, wb;
   int emb;            // in0: input = [sin 2pi zB, cos 2pi zB, z]
   const float* z;     // (B, nz) current zt (the workspace copy)
-  const float* bmat;  // (nz, nz/2) packed copy
+  const float* bmat;  // B^T (nz/2, nz), packed per call
   int nz;
   int din, kp, dout, B;
   const float* w;     // [ntn][16][kp]: rows 0-7 Wl, 8-15 Ws of the tile's columns (zero-padded)
@@ -67,15 +68,19 @@ struct ChainArgs {
   float* zt;          // == z
   const SweepCall* call;
   int dbg;  // timing experiments only (DAMC_CHAIN_DBG, wrong results): 1 no x loads, 2 no weight loads, 4 no MFMA,
-            // 8 no epilogue prefetch, 16 no output stores
+            // 8 no epilogue prefetch, 16 no output stores; in0: 32 no sin/cos, 64 no B loads, 128 no zB MFMA
 };
 
 __host__ __device__ inline int kpad(int din) { return (din + KG - 1) / KG * KG; }
 __host__ __device__ inline int emb_ld(int kp) { return kp + 8; }  // in0 LDS image row stride (floats)
 
+// EMB: the in0 block (Fourier embedding, sin / cos with their large-argument path) is its own instantiation, so
+// the six other blocks' kernels carry no scratch segment
+template <bool EMB>
 __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   extern __shared__ __attribute__((aligned(16))) float embs[];  // in0: [TM][emb_ld(kp)]
+  if (a.dbg & 512) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (a.dout + TC - 1) / TC;
   const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
           float n4[4];
           philox_normal4(call->seed, call->chain_base + erow, call->step_offset + a.noisy_k, (uint32_t)(ecol >> 2),
                          DAMC_STREAM_SWEEP, n4);
-          xi = n4[ecol & 3];
+          xi = pick4(n4, ecol);
         }
       }
     }
@@ -110,43 +115,62 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 
   // ---- in0: the Fourier input embedding of the 16 rows into LDS (zB on MFMA, wave w -> 16-column tiles w, w+4..)
   const int ld = emb_ld(a.kp);
-  if (a.emb) {
+  if (EMB) {
     const int nz = a.nz, half = nz >> 1;
     const int row = r0 + m;
     const bool rok = row < a.B;
-    const int nzg = (nz + 15) >> 4;
+    // all of a lane's z and B operands are loaded before the first MFMA (one memory round trip; nz <= 128)
+    f32x4 zv4[EMB_G];
+#pragma unroll
+    for (int g = 0; g < EMB_G; ++g) {
+      const int k = 16 * g + 4 * q;
+      zv4[g] = (rok && k < nz) ? *reinterpret_cast<const f32x4*>(a.z + (long)row * nz + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     for (int t = wave; t * 16 < half; t += 4) {
       const int col = t * 16 + m;
       const bool cok = col < half;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int g = 0; g < nzg; ++g) {
+      f32x4 bv[EMB_G];  // a.bmat is B^T (half, nz): lane (m, q) reads B[16 g + 4 q + s][col] as one f32x4
+#pragma unroll
+      for (int g = 0; g < EMB_G; ++g) {
         const int k = 16 * g + 4 * q;
-        const f32x4 zv4 = (rok && k < nz) ? *reinterpret_cast<const f32x4*>(a.z + (long)row * nz + k)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
-        float bv[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) bv[s] = (cok && k + s < nz) ? a.bmat[(long)(k + s) * half + col] : 0.f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[s], bv[s], acc, 0, 0, 0);
+        bv[g] = (cok && k < nz && !(a.dbg & 64)) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * nz + k)
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      const float two_pi = 6.28318548f;  // fp32(2*pi), as the reference's 2*np.pi*tensor
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (!(a.dbg & 128)) {
+#pragma unroll
+        for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][s], bv[g][s], acc, 0, 0, 0);
+      }
+      // sin / cos (2 pi zB) on the hardware units, whose argument is in revolutions: t = zB - rint(zB) is exact,
+      // so the only rounding is the unit's (the reference rounds 2 pi zB to fp32 first, ~4e-6 rad at |zB| ~ 10;
+      // both are below the spread of zB itself between summation orders)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = 4 * q + r;
         if (cok) {
-          const float ph = two_pi * acc[r];
+          const float t = acc[r] - rintf(acc[r]);
           const bool ok = r0 + rr < a.B;
-          embs[rr * ld + col] = ok ? sinf(ph) : 0.f;
-          embs[rr * ld + half + col] = ok ? cosf(ph) : 0.f;
+          embs[rr * ld + col] = ok ? ((a.dbg & 32) ? t : __builtin_amdgcn_sinf(t)) : 0.f;
+          embs[rr * ld + half + col] = ok ? ((a.dbg & 32) ? t : __builtin_amdgcn_cosf(t)) : 0.f;
         }
       }
     }
-    // z itself, then zeros up to kp
-    for (int i = tid; i < TM * (a.kp - 2 * half); i += CH_THREADS) {
-      const int rr = i / (a.kp - 2 * half), c = i - rr * (a.kp - 2 * half);
-      const int row2 = r0 + rr;
-      embs[rr * ld + 2 * half + c] = (row2 < a.B && c < nz) ? a.z[(long)row2 * nz + c] : 0.f;
+    // z itself from the registers that already hold it (wave 0: lane (m, q) has z[row m][16 g + 4 q + s]),
+    // then zeros up to kp (no global loads here: a strided load loop would serialise its memory latencies)
+    if (wave == 0) {
+#pragma unroll
+      for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 16 * g + 4 * q + s;
+          if (k < nz) embs[m * ld + 2 * half + k] = zv4[g][s];
+        }
     }
+    for (int c = 2 * half + nz + tid; c < a.kp; c += CH_THREADS)
+#pragma unroll
+      for (int rr = 0; rr < TM; ++rr) embs[rr * ld + c] = 0.f;
     __syncthreads();
   }
 
@@ -167,7 +191,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       f32x4 wv = {0.f, 0.f, 0.f, 0.f}, xv = {0.f, 0.f, 0.f, 0.f};
       if (g < ng) {
         if (!(a.dbg & 2)) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * g);
-        if (a.emb) {
+        if (EMB) {
           xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
         } else if (xok && k < a.din && !(a.dbg & 1)) {
           xv = k < a.wa ? *reinterpret_cast<const f32x4*>(a.srcA + (long)xrow * a.wa + k)
@@ -180,7 +204,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 #pragma unroll
     for (int c = 0; c < CH_CHUNK; ++c) {
       f32x4 x = xa[c];
-      if (!a.emb) {
+      if (!EMB) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.01f * x[e];
       }
@@ -191,6 +215,10 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], wb[c][s], acc, 0, 0, 0);
     }
+  }
+  if (a.dbg & 256) {
+    if (acc[0] == 12345.f) a.out[0] = acc[1];
+    return;
   }
   // C layout 16x16x4: column = lane & 15 (0-7 Wl, 8-15 Ws), rows 4 (lane >> 4) + r
 #pragma unroll
@@ -388,7 +416,7 @@ int validate(const damc_denoiser_t* d) {
     // float4 fragments / staging need every width % 4 == 0; the in0 LDS image must fit
     if ((b.din & 3) || (b.dout & 3) || (nz & 3)) return DAMC_ERR_UNSUPPORTED;
   }
-  if ((size_t)TM * emb_ld(kpad(2 * nz)) * sizeof(float) > 64 * 1024) return DAMC_ERR_UNSUPPORTED;
+  if (nz > 16 * EMB_G) return DAMC_ERR_UNSUPPORTED;
   return 0;
 }
 
@@ -467,8 +495,13 @@ void chain_launches(const damc_denoiser_t* d, const SweepWs& w, int B, int n, co
   }
 }
 
+void launch_one(const Launch& L, hipStream_t s) {
+  if (L.a.emb) hipLaunchKernelGGL(chain_kernel<true>, dim3(L.grid), dim3(CH_THREADS), L.smem, s, L.a);
+  else hipLaunchKernelGGL(chain_kernel<false>, dim3(L.grid), dim3(CH_THREADS), L.smem, s, L.a);
+}
+
 int launch_chain(const std::vector<Launch>& ls, hipStream_t s) {
-  for (const Launch& L : ls) hipLaunchKernelGGL(chain_kernel, dim3(L.grid), dim3(CH_THREADS), L.smem, s, L.a);
+  for (const Launch& L : ls) launch_one(L, s);
   return (int)hipGetLastError();
 }
 
@@ -527,7 +560,7 @@ int run_chain_graph(const damc_denoiser_t* d, const SweepWs& w, void* wsp, size_
   hipGraphExec_t exec = nullptr;
   hipError_t err = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
   if (err == hipSuccess) {
-    for (const Launch& L : ls) hipLaunchKernelGGL(chain_kernel, dim3(L.grid), dim3(CH_THREADS), L.smem, cs, L.a);
+    for (const Launch& L : ls) launch_one(L, cs);
     err = hipStreamEndCapture(cs, &graph);
   }
   if (err == hipSuccess) err = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
@@ -612,7 +645,9 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     const long ntt = (long)nt * nt;
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw1, nt, nt, w.tw1t);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw2, nt, nt, w.tw2t);
-    DAMC_CHECK(hipMemcpyAsync(w.bmat, d->bmat, sizeof(float) * d->nz * (d->nz / 2), hipMemcpyDeviceToDevice, s));
+    const long nb = (long)d->nz * (d->nz / 2);
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, d->bmat, d->nz, d->nz / 2,
+                       w.bmat);
     DAMC_LAUNCH_CHECK();
   }
 

@@ -147,7 +147,7 @@ __device__ __forceinline__ float noise_at(const float* noise, long noise_idx, in
   if (noise) return noise[noise_idx];
   float n4[4];
   philox_normal4(seed, chain, step, (uint32_t)(c >> 2), stream_id, n4);
-  return n4[c & 3];
+  return pick4(n4, c);
 }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -313,7 +313,255 @@ __global__ void philox_normal_kernel(float* out, int n_steps, int B, int nz, uin
   const int c = (int)(rem - r * nz);
   float n4[4];
   philox_normal4(seed, chain_base + r, step_offset + st, (uint32_t)(c >> 2), stream_id, n4);
-  out[i] = n4[c & 3];
+  out[i] = pick4(n4, c);
+}
+
+// ================================================================================================
+// Register-resident EBM (the default for nh <= 208, nz <= 128: _netE at every BASELINE config).
+//
+// The prior chain (and one posterior update) of ONE chain per 1024-thread workgroup, with both weight matrices
+// held in VGPRs for the whole launch: W1 (nh x nz) and W2 (nh x nh) are read from HBM/L2 once per launch instead
+// of once per step (the streaming version re-read ~0.5 MB per workgroup per step, ~3.5 us at one CU's L2
+// bandwidth).  Wave w owns rows j = 13 w + r (r < 13) of both matrices; lane l owns the columns k = l + 64 i:
+//   w2[r][i] = W2[13 w + r][l + 64 i] (i < 4),  w1[r][i] = W1[13 w + r][l + 64 i] (i < 2)   -> 78 VGPRs.
+// Forward products (W z, W2 h1) are per-lane partial sums over the lane's columns for the wave's 13 rows, summed
+// over the 64 lanes by a halving exchange (17 shuffles for 16 rows instead of 13 x 6); the lane ends up holding
+// row (lane >> 2) & 15.  Backward products (W2^T g2, W1^T g1) are per-lane partial sums over the wave's rows for
+// the lane's columns (the row factors g2 / g1 broadcast by readlane), summed over the 16 waves through LDS.
+// At one chain per workgroup the FC layers are matrix-vector products: MFMA would run them at 1/16 of its
+// width (16x16x4: 16 columns of which one is live), the same f32 rate as the VALU FMAs used here
+// (MI355X_MICROARCH.md: f32 MFMA = the f32 vector rate), so the VALU is the right unit.
+constexpr int EB_THREADS = 1024, EB_WAVES = 16, EB_RW = 13, EB_K2 = 4, EB_K1 = 2;
+bool ebm_reg_ok(int nz, int nh) { return nz > 0 && nz <= 64 * EB_K1 && nh > 0 && nh <= EB_WAVES * EB_RW; }
+
+// v[16]: per-lane partial sums of 16 rows -> the sum over the 64 lanes of row (lane >> 2) & 15, in every lane
+__device__ __forceinline__ float reduce16_rows(float (&v)[16], int lane) {
+  {
+    const bool up = lane & 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float keep = up ? v[i + 8] : v[i], send = up ? v[i] : v[i + 8];
+      v[i] = keep + __shfl_xor(send, 32, 64);
+    }
+  }
+  {
+    const bool up = lane & 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float keep = up ? v[i + 4] : v[i], send = up ? v[i] : v[i + 4];
+      v[i] = keep + __shfl_xor(send, 16, 64);
+    }
+  }
+  {
+    const bool up = lane & 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float keep = up ? v[i + 2] : v[i], send = up ? v[i] : v[i + 2];
+      v[i] = keep + __shfl_xor(send, 8, 64);
+    }
+  }
+  {
+    const bool up = lane & 4;
+    const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
+    v[0] = keep + __shfl_xor(send, 4, 64);
+  }
+  float t = v[0];
+  t += __shfl_xor(t, 2, 64);
+  t += __shfl_xor(t, 1, 64);
+  return t;
+}
+
+enum { EB_PRIOR = 0, EB_POSTERIOR = 1, EB_GRAD = 2 };
+
+struct EbArgs {
+  damc_ebm_t e;
+  float* z;            // (B, nz): updated in place (PRIOR, POSTERIOR); read (GRAD)
+  const float* glik;   // POSTERIOR: likelihood gradient (B, nz)
+  float* energy;       // GRAD: (B) or null
+  float* grad;         // GRAD: (B, nz)
+  int B, n_steps;
+  float c1, step;
+  int with_noise;
+  const float* noise;  // injected: PRIOR (n_steps, B, nz), POSTERIOR (B, nz)
+  uint64_t seed, step_offset, chain_base;
+  float* diag;         // PRIOR: (n_steps, 2) {sum E, |z|^2/2};  POSTERIOR: (4) {sum E, -, |z|^2/2, mean grad}
+};
+
+__device__ __forceinline__ float block_sum1024(float v, float* red) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < EB_WAVES; ++w) t += red[w];
+  return t;  // valid in thread 0
+}
+
+template <int MODE>
+__global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
+  const damc_ebm_t& e = a.e;
+  const int nz = e.nz, nh = e.nh;
+  const float sl = e.slope;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chain = blockIdx.x;
+  __shared__ float zs[64 * EB_K1];
+  __shared__ float h1s[EB_WAVES * EB_RW];
+  __shared__ float part2[EB_WAVES][64 * EB_K2];
+  __shared__ float part1[EB_WAVES][64 * EB_K1];
+  __shared__ float red[EB_WAVES];
+
+  // ---- weights -> registers (once per launch); column-coalesced rows
+  float w2[EB_RW][EB_K2], w1[EB_RW][EB_K1];
+#pragma unroll
+  for (int r = 0; r < EB_RW; ++r) {
+    const int j = EB_RW * wave + r;
+#pragma unroll
+    for (int i = 0; i < EB_K2; ++i) {
+      const int k = lane + 64 * i;
+      w2[r][i] = (j < nh && k < nh) ? e.w2[(long)j * nh + k] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < EB_K1; ++i) {
+      const int c = lane + 64 * i;
+      w1[r][i] = (j < nh && c < nz) ? e.w1[(long)j * nz + c] : 0.f;
+    }
+  }
+  // this lane's reduced row and its per-row constants
+  const int rr = (lane >> 2) & 15;
+  const int jr = EB_RW * wave + rr;
+  const bool rok = rr < EB_RW && jr < nh;
+  const float b1r = rok ? e.b1[jr] : 0.f, b2r = rok ? e.b2[jr] : 0.f, w3r = rok ? e.w3[jr] : 0.f;
+  // z of this chain -> LDS
+  if (tid < 64 * EB_K1) zs[tid] = tid < nz ? a.z[(long)chain * nz + tid] : 0.f;
+  __syncthreads();
+
+  const int nsteps = MODE == EB_PRIOR ? a.n_steps : 1;
+  for (int it = 0; it < nsteps; ++it) {
+    // ---- layer 1 forward: a1 = W1 z + b1, h1 = lrelu(a1)
+    float zl[EB_K1];
+#pragma unroll
+    for (int i = 0; i < EB_K1; ++i) zl[i] = zs[lane + 64 * i];
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = 0.f;
+      if (r < EB_RW) {
+#pragma unroll
+        for (int i = 0; i < EB_K1; ++i) p = fmaf(w1[r][i], zl[i], p);
+      }
+      v[r] = p;
+    }
+    const float a1 = reduce16_rows(v, lane) + b1r;
+    const float m1 = a1 > 0.f ? 1.f : sl;  // lrelu'(a1) of row jr
+    if (rok && (lane & 3) == 0) h1s[jr] = a1 > 0.f ? a1 : a1 * sl;
+    __syncthreads();
+    // ---- layer 2 forward: a2 = W2 h1 + b2; g2 = w3 lrelu'(a2)
+    float hl[EB_K2];
+#pragma unroll
+    for (int i = 0; i < EB_K2; ++i) {
+      const int k = lane + 64 * i;
+      hl[i] = k < nh ? h1s[k] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = 0.f;
+      if (r < EB_RW) {
+#pragma unroll
+        for (int i = 0; i < EB_K2; ++i) p = fmaf(w2[r][i], hl[i], p);
+      }
+      v[r] = p;
+    }
+    const float a2 = reduce16_rows(v, lane) + b2r;
+    const float g2 = rok ? (a2 > 0.f ? w3r : w3r * sl) : 0.f;
+    const bool want_e = (MODE == EB_PRIOR || MODE == EB_POSTERIOR) ? a.diag != nullptr : a.energy != nullptr;
+    float en = 0.f;
+    if (want_e && rok && (lane & 3) == 0) en = w3r * (a2 > 0.f ? a2 : a2 * sl);
+    // ---- layer 2 backward: partial (W2^T g2)[k] over this wave's rows
+    float q2[EB_K2] = {};
+#pragma unroll
+    for (int r = 0; r < EB_RW; ++r) {
+      const float gr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g2), 4 * r));
+#pragma unroll
+      for (int i = 0; i < EB_K2; ++i) q2[i] = fmaf(w2[r][i], gr, q2[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < EB_K2; ++i) part2[wave][lane + 64 * i] = q2[i];
+    __syncthreads();
+    // ---- g1 = (W2^T g2) * lrelu'(a1) for this wave's rows: lane (row l >> 2, quarter l & 3) sums 4 waves
+    float g1 = 0.f;
+    if (lane < 4 * EB_RW) {
+      const int j = EB_RW * wave + (lane >> 2), w0 = 4 * (lane & 3);
+      if (j < nh) g1 = part2[w0][j] + part2[w0 + 1][j] + part2[w0 + 2][j] + part2[w0 + 3][j];
+    }
+    g1 += __shfl_xor(g1, 1, 64);
+    g1 += __shfl_xor(g1, 2, 64);
+    g1 *= m1;  // lane l < 52 holds row l >> 2 = rr: its own a1
+    // ---- layer 1 backward: partial (W1^T g1)[c] over this wave's rows
+    float q1[EB_K1] = {};
+#pragma unroll
+    for (int r = 0; r < EB_RW; ++r) {
+      const float gr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g1), 4 * r));
+#pragma unroll
+      for (int i = 0; i < EB_K1; ++i) q1[i] = fmaf(w1[r][i], gr, q1[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < EB_K1; ++i) part1[wave][lane + 64 * i] = q1[i];
+    __syncthreads();
+    // ---- gz = sum over waves; the update (fixed summation orders: deterministic, batch-independent)
+    float zsq = 0.f, gsum = 0.f;
+    if (tid < nz) {
+      float gz = 0.f;
+#pragma unroll
+      for (int w = 0; w < EB_WAVES; ++w) gz += part1[w][tid];
+      const long gi = (long)chain * nz + tid;
+      const float zv = zs[tid];
+      if (MODE == EB_GRAD) {
+        a.grad[gi] = gz;
+      } else {
+        float g = (MODE == EB_POSTERIOR) ? a.glik[gi] + gz : gz;
+        g += zv;
+        zsq = zv * zv;
+        gsum = g;
+        float zn = sub_rn(zv, mul_rn(a.c1, g));
+        if (a.with_noise) {
+          float xi;
+          if (MODE == EB_PRIOR) {
+            xi = noise_at(a.noise, ((long)it * a.B + chain) * nz + tid, 1, a.seed, a.chain_base + chain,
+                          a.step_offset + it, tid, DAMC_STREAM_PRIOR);
+          } else {
+            xi = noise_at(a.noise, gi, 1, a.seed, a.chain_base + chain, a.step_offset, tid, DAMC_STREAM_POSTERIOR);
+          }
+          zn = add_rn(zn, mul_rn(a.step, xi));
+        }
+        zs[tid] = zn;
+      }
+    }
+    if (want_e) {  // uniform branch
+      const float et = block_sum1024(en, red);
+      if (MODE == EB_GRAD) {
+        if (tid == 0) a.energy[chain] = et + e.b3[0];
+      } else {
+        const float zt = block_sum1024(zsq, red);
+        if (MODE == EB_PRIOR) {
+          if (tid == 0) {
+            atomicAdd(&a.diag[2 * it + 0], et + e.b3[0]);
+            atomicAdd(&a.diag[2 * it + 1], 0.5f * zt);
+          }
+        } else {
+          const float gt = block_sum1024(gsum, red);
+          if (tid == 0) {
+            atomicAdd(&a.diag[0], et + e.b3[0]);
+            atomicAdd(&a.diag[2], 0.5f * zt);
+            atomicAdd(&a.diag[3], gt / (float)((long)a.B * nz));
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (MODE != EB_GRAD && tid < nz) a.z[(long)chain * nz + tid] = zs[tid];
 }
 
 // rows per workgroup: per step a workgroup streams all four weight panels (~0.5 MB, L2-resident) once,
@@ -341,8 +589,26 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
     use_ebm = 1;
     if (ev.nz != nz) return DAMC_ERR_ARG;
   }
-  if (!ebm_shape_ok(RU, nz, use_ebm ? ev.nh : 0)) return DAMC_ERR_UNSUPPORTED;
   const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
+  if (use_ebm && nslab == 1 && ebm_reg_ok(nz, ev.nh)) {
+    EbArgs a{};
+    a.e = ev;
+    a.z = z;
+    a.glik = slabs;
+    a.B = B;
+    a.c1 = c1;
+    a.step = (float)step;
+    a.with_noise = with_noise;
+    a.noise = noise;
+    a.seed = seed;
+    a.step_offset = step_idx;
+    a.chain_base = chain_base;
+    a.diag = diag;
+    ProfScope ps("posterior_update", 4.0 * B * ((double)nz * ev.nh + (double)ev.nh * ev.nh), s);
+    hipLaunchKernelGGL(ebm_reg_kernel<EB_POSTERIOR>, dim3(B), dim3(EB_THREADS), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  if (!ebm_shape_ok(RU, nz, use_ebm ? ev.nh : 0)) return DAMC_ERR_UNSUPPORTED;
   const size_t sm = ebm_smem_floats(RU, nz, use_ebm ? ev.nh : 0) * sizeof(float);
   ProfScope ps("posterior_update", 0.0, s);
   hipLaunchKernelGGL((posterior_update_kernel<RU>), dim3((B + RU - 1) / RU), dim3(EBM_THREADS), sm, s, ev, use_ebm, z, slabs,
@@ -357,11 +623,29 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
                                    float* diag, void* stream) {
   if (!e || !z || B <= 0 || n_steps < 0) return DAMC_ERR_ARG;
   if (!e->w1t || !e->w2t) return DAMC_ERR_ARG;
-  if (!ebm_shape_ok(RP, e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
   if (n_steps == 0) return 0;
   const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
+  if (ebm_reg_ok(e->nz, e->nh)) {
+    EbArgs a{};
+    a.e = *e;
+    a.z = z;
+    a.B = B;
+    a.n_steps = n_steps;
+    a.c1 = c1;
+    a.step = (float)step;
+    a.with_noise = with_noise;
+    a.noise = noise;
+    a.seed = seed;
+    a.step_offset = step_offset;
+    a.chain_base = chain_base;
+    a.diag = diag;
+    ProfScope ps("prior_chain", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
+    hipLaunchKernelGGL(ebm_reg_kernel<EB_PRIOR>, dim3(B), dim3(EB_THREADS), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  if (!ebm_shape_ok(RP, e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
   ProfScope ps("prior_chain", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
   hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, s, *e, z, B, n_steps, c1, (float)step,
@@ -372,6 +656,16 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
 extern "C" int damc_ebm_energy_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad,
                                     void* stream) {
   if (!e || !z || !grad || B <= 0) return DAMC_ERR_ARG;
+  if (ebm_reg_ok(e->nz, e->nh)) {
+    EbArgs a{};
+    a.e = *e;
+    a.z = const_cast<float*>(z);
+    a.energy = energy;
+    a.grad = grad;
+    a.B = B;
+    hipLaunchKernelGGL(ebm_reg_kernel<EB_GRAD>, dim3(B), dim3(EB_THREADS), 0, as_stream(stream), a);
+    return (int)hipGetLastError();
+  }
   if (!ebm_shape_ok(RP, e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   const size_t sm = ebm_smem_floats(RP, e->nz, e->nh) * sizeof(float);
   hipLaunchKernelGGL((ebm_energy_grad_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, as_stream(stream), *e, z, B,
