@@ -1,0 +1,160 @@
+"""GPU: the BASELINE configs beyond CIFAR-10 at their full widths and per-rank sizes on the HIP path
+(BASELINE.json configs 2, 4, 5; workspace/src/diffusion_net.py:53-170 generators, :268-372 encoders,
+workspace/train_gen_recon.py:64-92 their nz / ngf / nif):
+  * SVHN _netG_svhn(nz=100, ngf=64), B=64: one step, and 30 steps with injected noise;
+  * CelebA-64 _netG_celeba64(nz=100, ngf=128): B=32 (per rank of 256 over 8 GPUs) one step and 10 no-noise steps
+    (the eval path) with the reconstruction MSE; B=256 (the whole batch on one GPU) one step;
+  * CelebA-HQ _netG_celebaHQ(nz=128, ngf=128), sigma=1.0: B=8 (per rank of 64) one step; B=64 the likelihood
+    gradient of the whole batch in one call;
+  * Encoder_celeba64 / Encoder_celebaHQ at nif=64 (nemb 1024), and CelebA-HQ's Q(x): encoder + the 100-step
+    reverse sweep (nxemb 1024, ntemb 128, injected noise) at B=8.
+The criterion is accuracy-relative against an fp64 evaluation of the same algorithm (oracle/damc_oracle.py):
+the HIP result's distance to fp64 must stay within 3x the fp32 oracle's (the reference's own arithmetic), plus
+a small floor — per sample (median and 90th percentile) for latents and gradients, whose batches can hold a
+sample sitting on a LeakyReLU kink; each test prints both distances."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+GEN = {  # name: (constructor, nz, ngf, image size)
+    "svhn": ("_netG_svhn", 100, 64, 32),
+    "celeba64": ("_netG_celeba64", 100, 128, 64),
+    "celebaHQ": ("_netG_celebaHQ", 128, 128, 256),
+}
+
+
+def _case(name, B, device):
+    from damc import synth
+    from src import diffusion_net as dn
+
+    ctor, nz, ngf, hw = GEN[name]
+    G = synth.load_into(getattr(dn, ctor)(nz=nz, ngf=ngf, nc=3), 0).to(device).eval()
+    E = synth.load_into(dn._netE(nz=nz), 10).to(device).eval()
+    x = torch.from_numpy(synth.uniform_f32(11, 0, (B, 3, hw, hw))).to(device)
+    z0 = torch.from_numpy(synth.normal_f32(12, 0, (B, nz))).to(device)
+    return G, E, x, z0
+
+
+def _oracles(G, E):
+    from oracle import damc_oracle as orc
+
+    return ((orc.generator_layers(G), orc.ebm_params(E)),
+            (orc.generator_layers(G, torch.float64), orc.ebm_params(E, torch.float64)))
+
+
+def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0):
+    """Distance to fp64 against the fp32 reference arithmetic's.  per_row: per-sample relative errors, judged by
+    their median and 90th percentile: a sample with a hidden pre-activation within fp32 rounding of the LeakyReLU
+    kink can take the other derivative (1 vs 0.2) under any summation order (the SVHN B=64 batch's sample 54 has
+    a first-layer unit at 1.2e-8), an ill-conditioned row that is only bounded (max row error < 5e-2)."""
+    if not per_row:
+        e_hip, e_32 = rel_l2(got, ref64), rel_l2(ref32, ref64)
+        print("%s: |hip-fp64| %.2e  |fp32 reference arithmetic-fp64| %.2e" % (what, e_hip, e_32))
+        assert e_hip <= factor * e_32 + floor, (what, e_hip, e_32)
+        return
+    rows = lambda a: np.array([rel_l2(a[i], ref64[i]) for i in range(ref64.shape[0])])  # noqa: E731
+    eh, e3 = rows(got), rows(ref32)
+    q = lambda e, p: float(np.quantile(e, p))  # noqa: E731
+    print("%s: per-row |hip-fp64| median %.2e p90 %.2e max %.2e (row %d);  fp32 reference median %.2e p90 %.2e max %.2e"
+          % (what, q(eh, .5), q(eh, .9), eh.max(), eh.argmax(), q(e3, .5), q(e3, .9), e3.max()))
+    assert q(eh, .5) <= factor * q(e3, .5) + floor, what
+    assert q(eh, .9) <= factor * q(e3, .9) + floor, what
+    assert eh.max() < 5e-2, what
+
+
+@pytest.mark.parametrize("name,B,steps,noise,sigma", [
+    ("svhn", 64, 1, False, 0.1), ("svhn", 64, 30, True, 0.1),
+    ("celeba64", 32, 1, False, 0.1), ("celeba64", 32, 10, False, 0.1), ("celeba64", 256, 1, False, 0.1),
+    ("celebaHQ", 8, 1, False, 1.0)])
+def test_full_width_posterior_vs_fp64(gpu_device, name, B, steps, noise, sigma):
+    from damc import langevin as lv
+    from oracle import damc_oracle as orc
+
+    G, E, x, z0 = _case(name, B, gpu_device)
+    (L32, P32), (L64, P64) = _oracles(G, E)
+    nz = z0.shape[1]
+    xi = torch.from_numpy(np.random.default_rng(B + steps).standard_normal((steps, B, nz)).astype(np.float32)) \
+        if noise else None
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, E, steps, sigma, 0.1, noise, noise=None if xi is None else xi.to(gpu_device))
+    zc, xc = z0.cpu(), x.cpu()
+    r32 = orc.posterior_langevin(L32, P32, zc, xc, steps, sigma, 0.1, noise=xi).numpy()
+    r64 = orc.posterior_langevin(L64, P64, zc.double(), xc.double(), steps, sigma, 0.1,
+                                 noise=None if xi is None else xi.double()).numpy()
+    # one step: per sample (a kink sample is bounded, not compared); several steps: the whole batch, whose rel-L2
+    # both implementations grow chaotically
+    _check("%s B=%d %d step(s) z" % (name, B, steps), z.cpu().numpy(), r32, r64, 1e-7 if steps == 1 else 1e-6,
+           per_row=steps == 1)
+    if steps == 10:  # eval path: reconstruction MSE of the 10-step no-noise posterior (eval_gen_recon.py:184-194)
+        mse = ((lv.generator_forward(z, G) - x) ** 2).mean(dim=(1, 2, 3)).cpu().numpy()
+        m32 = ((orc.generator_sample(L32, torch.from_numpy(r32)) - xc) ** 2).mean(dim=(1, 2, 3)).numpy()
+        m64 = ((orc.generator_sample(L64, torch.from_numpy(r64)) - xc.double()) ** 2).mean(dim=(1, 2, 3)).numpy()
+        _check("%s B=%d recon MSE" % (name, B), mse, m32, m64, 1e-7)
+
+
+def test_celebaHQ_b64_likelihood_gradient_vs_fp64(gpu_device):
+    """CelebA-HQ's whole B=64 batch (BASELINE config 5 on one GPU) in one call: forward + input gradient."""
+    from damc import langevin as lv
+    from oracle import damc_oracle as orc
+
+    G, E, x, z0 = _case("celebaHQ", 64, gpu_device)
+    (L32, _), (L64, _) = _oracles(G, E)
+    g = lv.likelihood_grad(z0, x, G, 1.0).cpu().numpy()
+    g32 = orc.likelihood_grad(L32, z0.cpu(), x.cpu(), 1.0)[0].numpy()
+    g64 = orc.likelihood_grad(L64, z0.cpu().double(), x.cpu().double(), 1.0)[0].numpy()
+    # 7 layers, 5 of them k4 s2 p1 with K = 16 Cout up to 32768: the GEMM engines accumulate each output's K
+    # products in one fp32 chain (MFMA), oneDNN's CPU kernels in blocked partial sums, ~1.5-2x less rounding
+    # per layer (tools/diag_smallc.py: 1.7x after one k4 s2 layer, 3.7x after two at Cout 256); hence 8x here
+    _check("celebaHQ B=64 likelihood gradient", g, g32, g64, 1e-7, per_row=True, factor=8.0)
+    xh = lv.generator_forward(z0, G).cpu().numpy()
+    _check("celebaHQ B=64 G(z)", xh, orc.generator_sample(L32, z0.cpu()).numpy(),
+           orc.generator_sample(L64, z0.cpu().double()).numpy(), 1e-7)
+
+
+@pytest.mark.parametrize("name,B", [("celeba64", 32), ("celebaHQ", 8)])
+def test_full_width_encoder_vs_fp64(gpu_device, name, B):
+    from damc import amortizer, synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    hw = GEN[name][3]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 0, (B, 3, hw, hw))).to(gpu_device)
+    got = amortizer.encoder_forward(enc, x).cpu().numpy()
+    with torch.no_grad():
+        e32 = orc.encoder_forward(enc.cpu(), x.cpu()).numpy()
+        e64 = orc.encoder_forward(enc.double(), x.cpu().double()).numpy()
+    _check("Encoder_%s nif=64 B=%d xemb" % (name, B), got, e32, e64, 1e-7)
+
+
+def test_celebaHQ_q_sweep_vs_fp64(gpu_device):
+    """CelebA-HQ Q(x) at its per-rank size (B=8 of 64): Encoder_celebaHQ(nif=64) + the 100-step 'large' reverse sweep
+    (nxemb 1024, ntemb 128; train_gen_recon.py:360-380 defaults) with injected noise, vs the fp64 oracle."""
+    from damc import amortizer, synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    B, n = 8, 100
+    Q = dn._netQ_U(nc=3, nz=128, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=n,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                   dataset="celebaHQ")
+    synth.load_into(Q, 20)
+    Q.to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(14, 0, (B, 3, 256, 256))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(15, 0, (B, 128)))
+    eps = torch.from_numpy(np.random.default_rng(16).standard_normal((n - 1, B, 128)).astype(np.float32))
+    xemb = amortizer.encoder_forward(Q.encoder, x)
+    zt = zt0.to(gpu_device)
+    amortizer.reverse_sweep(Q, xemb, zt, noise=eps.to(gpu_device))
+    args = (n, -5.1, 9.8, "large")
+    Qc = Q.cpu()
+    with torch.no_grad():
+        z32, _ = orc.reverse_sweep(Qc, orc.encoder_forward(Qc.encoder, x.cpu()), zt0, eps, *args)
+        Qd = Qc.double()
+        z64, _ = orc.reverse_sweep(Qd, orc.encoder_forward(Qd.encoder, x.cpu().double()), zt0.double(), eps.double(),
+                                   *args)
+    _check("celebaHQ Q(x) 100-step sweep B=8", zt.cpu().numpy(), z32.numpy(), z64.numpy(), 1e-6)
