@@ -128,6 +128,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
+// supertile raster: linear id l in [0, T * P) -> (M tile tm, pair p), blocks of SM x SP ids (SP = min(4, P) pairs
+// fastest, then SM = 32 / SP M tiles), blocks ordered M-major; edge blocks are smaller.  Bijective.
+__device__ __forceinline__ void supertile(int l, int T, int P, int& tm, int& p) {
+  const int SP = P < 4 ? P : 4;
+  const int SMf = 32 / SP;
+  const int SM = T < SMf ? T : SMf;
+  const int rowsz = SM * P;              // ids of one full block row (SM M tiles, all pairs)
+  const int tmb = l / rowsz;
+  const int sm = min(SM, T - tmb * SM);  // M tiles in this block row (smaller on the last)
+  int rem = l - tmb * rowsz;
+  const int pb = rem / (sm * SP);        // full pair blocks come first; the last may be narrower
+  const int sp = min(SP, P - pb * SP);
+  rem -= pb * sm * SP;
+  tm = tmb * SM + rem / sp;
+  p = pb * SP + rem % sp;
+}
+
 template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT, int SCHED>
 __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
   typedef TileCfg<BK, MT> C;
@@ -795,7 +812,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // V: variant bits (tools/gemm_bench.hip A/B): 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
 // wave, 2 = s_setprio(1) around the MFMA cluster, 4 = LDS-DMA staging (buffer_load ... lds straight into
-// the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write)
+// the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write), 8 = channel-major K
+// walk (all taps of a 32-channel slice back to back, so the tap-shifted re-reads of the same input pixels hit
+// L2 instead of coming back from the Infinity Cache / HBM after a whole tap's worth of channels), 16 = supertile
+// raster (a 1-D grid; each XCD's 32 concurrent workgroups form a block of <= 8 M tiles x 4 (N tile, phase) pairs
+// with the 4 phases of an N tile adjacent, so the phases' overlapping input windows and the weight panels are
+// shared in L2 instead of every XCD streaming all phases' panels; DMA and non-WGRAD only)
 #ifndef DAMC_X3_VARIANT
 #define DAMC_X3_VARIANT 5  // measured best (profiles/r01/gemm_bench.txt)
 #endif
@@ -821,11 +843,23 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  constexpr bool RASTER = (V & 16) != 0 && OM != O_WGRAD;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntn = (p.N + X3_BN - 1) / X3_BN;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn, z;
+  if constexpr (RASTER) {
+    const int nph = OM == O_PHASE ? 4 : 1;
+    const int ntm = (p.M + X3_BM - 1) / X3_BM;
+    int pr;
+    supertile(wgid, ntm, ntn * nph, tm, pr);
+    tn = pr / nph;
+    z = pr - tn * nph;
+  } else {
+    tm = wgid / ntn;
+    tn = wgid - tm * ntn;
+    z = blockIdx.z;
+  }
   const int m0 = tm * X3_BM, n0 = tn * X3_BN;
-  const int z = blockIdx.z;
 
   int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
   const unsigned short* Bg = p.B3;
@@ -944,6 +978,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // LDS-DMA form: chunk id -> LDS byte 16 id, so each wave-instruction fills 1 KiB at a wave-uniform base
   typedef __attribute__((address_space(3))) void* lds_t;
   const int wbase = (tid & ~63) * 16;
+  constexpr bool CMAJ = (V & 8) != 0 && OM != O_WGRAD;
+  const int taps = kh * kw;
   auto dma_ab = [&](int k0, int buf) {
     unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
     if constexpr (OM == O_WGRAD) {
@@ -959,6 +995,18 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16,
                                                  live ? (int)(abase[j] + k0 * 6) : (int)KM_OOB, 0, 0, 0);
       }
+    } else if constexpr (CMAJ) {
+      // K tile kt = (channel slice kt / taps, tap kt % taps): B column k0 = tap * Cg + 32 * slice
+      const int kt = k0 / X3_BK, sl = kt / taps, tp = kt - sl * taps;
+      tap = tp;
+      tky = tp / kw;
+      tkx = tp - tky * kw;
+      set_tap();
+      ci0 = sl * X3_BK;
+      k0 = tp * Cg + ci0;
+#pragma unroll
+      for (int j = 0; j < X3_AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < X3_AJ; ++j)
@@ -968,7 +1016,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     for (int j = 0; j < X3_BJ; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
                                                k0 * 6, 0, 0);
-    if constexpr (OM != O_WGRAD) {
+    if constexpr (OM != O_WGRAD && !CMAJ) {
       ci0 += X3_BK;
       if (ci0 == Cg) {
         ci0 = 0;
@@ -1169,7 +1217,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 static void launch_x3_t(const GemmArgs& a, int zdim, hipStream_t s) {
   const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
-  hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
+  if ((V & 16) && OM != O_WGRAD)  // supertile raster: phases folded into a 1-D grid
+    hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
 }
 
 // fp32 [rows][C] -> x3 [rows][C/8][3][8]; one thread per channel octet

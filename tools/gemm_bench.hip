@@ -234,7 +234,7 @@ int main(int argc, char** argv) {
     sh.a3 = split_dev(a.A, na);
     sh.b3 = split_dev(sh.bt, (size_t)(sh.phase ? 4 : 1) * a.N * a.K);
   }
-  V vars[] = {{"KM/p3", run_km<3>}, {"X3/v3", run_x3<3>}, {"X3/v5", run_x3<5>}};
+  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v13", run_x3<13>}, {"X3/v21", run_x3<21>}, {"X3/v29", run_x3<29>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
