@@ -289,6 +289,7 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
     a.A3 = t.dy3;
     a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
+    a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy
   }
   return launch_gemm(a, A_CONV, EPI_BIAS_ACT, O_PHASE, 4, "enc_dgrad", 2.0 * M * cout * cin * 16, s);
 }

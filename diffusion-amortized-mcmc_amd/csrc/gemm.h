@@ -64,6 +64,9 @@ struct GemmArgs {
   // EPI_GATE: v + bias[n], then sigmoid on the columns n < gate_cols (a ConcatSquash block's hyper gate and
   // hyper bias computed by one GEMM, diffusion_net.py:441-443)
   int gate_cols = 0;
+  // limb engine: B3 holds -B on the odd blocks of X3_NEGK consecutive k of every row (launch_split_x3_negblk),
+  // and the kernel subtracts those blocks' sums (the MFMA's truncation bias then alternates sign; gemm.hip)
+  int b_negblk = 0;
 };
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
@@ -73,6 +76,10 @@ inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
 
 // fp32 [n/C rows][C] -> x3 limb layout [rows][C/8][3][8] bf16 (n % 8 == 0, 16-B aligned)
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
+// the same for a weight operand whose rows are K long, with the values of the odd X3_NEGK-blocks of each row
+// negated (exact); the GEMM launches that read it set GemmArgs::b_negblk
+constexpr int X3_NEGK = 256;
+int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s);
 
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);

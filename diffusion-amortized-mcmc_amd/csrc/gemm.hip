@@ -805,6 +805,8 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
 // write groups are contiguous.  Double-buffered: 2 x 384 rows x 192 B = 147,456 B, one workgroup per CU.
 constexpr int X3_BM = 256, X3_BN = 128, X3_BK = 32, X3_ROWB = 192;
 __device__ __forceinline__ int x3_swz(int row) { return (row >> 1) & 3; }
+constexpr int X3_FLUSH = 8;  // K tiles per MFMA accumulation block (power of two)
+static_assert(X3_FLUSH * 32 == X3_NEGK, "sign blocks are accumulation blocks");
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
 constexpr int X3_AJ = X3_BM * X3_CHUNKS / 512, X3_BJ = X3_BN * X3_CHUNKS / 512;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -812,9 +814,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // V: variant bits (tools/gemm_bench.hip A/B): 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
 // wave, 2 = s_setprio(1) around the MFMA cluster, 4 = LDS-DMA staging (buffer_load ... lds straight into
-// the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write), 8 = channel-major K
-// walk (all taps of a 32-channel slice back to back, so the tap-shifted re-reads of the same input pixels hit
-// L2 instead of coming back from the Infinity Cache / HBM after a whole tap's worth of channels), 16 = supertile
+// the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write), 16 = supertile
 // raster (a 1-D grid; each XCD's 32 concurrent workgroups form a block of <= 8 M tiles x 4 (N tile, phase) pairs
 // with the 4 phases of an N tile adjacent, so the phases' overlapping input windows and the weight panels are
 // shared in L2 instead of every XCD streaming all phases' panels; DMA and non-WGRAD only)
@@ -978,8 +978,6 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // LDS-DMA form: chunk id -> LDS byte 16 id, so each wave-instruction fills 1 KiB at a wave-uniform base
   typedef __attribute__((address_space(3))) void* lds_t;
   const int wbase = (tid & ~63) * 16;
-  constexpr bool CMAJ = (V & 8) != 0 && OM != O_WGRAD;
-  const int taps = kh * kw;
   auto dma_ab = [&](int k0, int buf) {
     unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
     if constexpr (OM == O_WGRAD) {
@@ -995,18 +993,6 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16,
                                                  live ? (int)(abase[j] + k0 * 6) : (int)KM_OOB, 0, 0, 0);
       }
-    } else if constexpr (CMAJ) {
-      // K tile kt = (channel slice kt / taps, tap kt % taps): B column k0 = tap * Cg + 32 * slice
-      const int kt = k0 / X3_BK, sl = kt / taps, tp = kt - sl * taps;
-      tap = tp;
-      tky = tp / kw;
-      tkx = tp - tky * kw;
-      set_tap();
-      ci0 = sl * X3_BK;
-      k0 = tp * Cg + ci0;
-#pragma unroll
-      for (int j = 0; j < X3_AJ; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < X3_AJ; ++j)
@@ -1016,7 +1002,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     for (int j = 0; j < X3_BJ; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
                                                k0 * 6, 0, 0);
-    if constexpr (OM != O_WGRAD && !CMAJ) {
+    if constexpr (OM != O_WGRAD) {
       ci0 += X3_BK;
       if (ci0 == Cg) {
         ci0 = 0;
@@ -1030,18 +1016,28 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     }
   };
 
-  f32x16 acc[2][2];
-  f32x4 acc16[4][4];
+  // Blocked accumulation: the MFMA chain runs over X3_FLUSH K tiles, then adds into tot (a second fp32 sum
+  // over the blocks, round-to-nearest VALU adds) and restarts from zero.  Rounding error of one output then
+  // grows with sqrt(K/32 * X3_FLUSH) + K/32/sqrt(X3_FLUSH) instead of K/32: ~3x less at K = 16384
+  // (tools/diag_hq.py), for 64 VGPRs and 64 v_add_f32 per X3_FLUSH tiles.
+  // Sign alternation (b_negblk): v_mfma_f32_16x16x32_bf16 aligns its 32 products and the accumulator before
+  // one rounding and drops the low bits toward -inf, a bias of -0.19 x 2^-24 max|term| per instruction on
+  // random operands that flips sign when the operands are negated (tools/mfma_bias.hip).  A bias that keeps
+  // its sign survives every later layer and the first layer's 32768-term sum where rounding noise cancels
+  // (tools/diag_chain.py: 3x the CPU's error on CelebA-HQ's z gradient); with -B stored on odd blocks and
+  // those blocks subtracted, consecutive blocks' biases cancel.
+  f32x16 acc[2][2], tot[2][2];
+  f32x4 acc16[4][4], tot16[4][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc16[i][j] = tot16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // 32x32x16: fragment of k16 step s, lane half h = octet 2s + h of the row, limb l at +16 l
   // 16x16x32: lane quarter q = octet q of the row (the whole 32-deep K tile in one MFMA)
@@ -1096,6 +1092,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
           acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
         }
       if (V & 2) __builtin_amdgcn_s_setprio(0);
+      if (((kt + 1) & (X3_FLUSH - 1)) == 0) {
+        const bool neg = p.b_negblk && ((kt / X3_FLUSH) & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            tot16[i][j] = neg ? tot16[i][j] - acc16[i][j] : tot16[i][j] + acc16[i][j];
+            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
     } else {
       bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
 #pragma unroll
@@ -1127,9 +1133,35 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
           }
       if (V & 2) __builtin_amdgcn_s_setprio(0);
+      if (((kt + 1) & (X3_FLUSH - 1)) == 0) {
+        const bool neg = p.b_negblk && ((kt / X3_FLUSH) & 1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            tot[i][j] = neg ? tot[i][j] - acc[i][j] : tot[i][j] + acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+          }
+      }
     }
     __syncthreads();
   }
+  }
+  // the last partial block
+  {
+    const bool neg = p.b_negblk && ((nk / X3_FLUSH) & 1);
+    if (M16) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc16[i][j] = neg ? tot16[i][j] - acc16[i][j] : tot16[i][j] + acc16[i][j];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = neg ? tot[i][j] - acc[i][j] : tot[i][j] + acc[i][j];
+    }
   }
   // ---- epilogue through LDS: the block's 256 x 128 fp32 tile, then one thread per (row, channel octet):
   // 2 x 16-B fp32 stores and (C3) 3 x 16-B limb stores per octet, each row's 128 channels contiguous
@@ -1236,6 +1268,31 @@ __global__ void split_x3_kernel(const float* __restrict__ x, long n8, unsigned s
   o[0] = h;
   o[1] = m;
   o[2] = l;
+}
+
+// rows of K values; octets in odd X3_NEGK-blocks of a row negated
+__global__ void split_x3_negblk_kernel(const float* __restrict__ x, long n8, int K8, unsigned short* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const long k8 = i % K8;
+  const float sg = ((k8 * 8 / X3_NEGK) & 1) ? -1.f : 1.f;
+  const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
+  const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
+  const float v[8] = {sg * v0.x, sg * v0.y, sg * v0.z, sg * v0.w, sg * v1.x, sg * v1.y, sg * v1.z, sg * v1.w};
+  bf16x8 h, m, l;
+  split3_octet(v, h, m, l);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * i;
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
+int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s) {
+  if (K <= 0 || K % 8 != 0 || n % K != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0) return DAMC_ERR_ARG;
+  const long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(split_x3_negblk_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, y);
+  return (int)hipGetLastError();
 }
 
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {

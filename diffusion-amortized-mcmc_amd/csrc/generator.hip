@@ -1114,6 +1114,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.A = z;
       a.A3 = ws.z3;
       a.B3 = x3_of(L.w_bwd, (size_t)L.cin * N);
+      a.b_negblk = 1;
       a.Cg = L.cin;
       a.ldc = N;
       a.M = B;
@@ -1179,6 +1180,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       if (x3_fwd(L)) {
         a.A3 = ws.h3[i - 1];
         a.B3 = x3_of(L.w_fwd, up2_floats(L));
+        a.b_negblk = 1;
         if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {  // the next layer's operand
           a.C3 = ws.h3[i];
           wrote_x3 = true;
@@ -1279,6 +1281,7 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
       if (x3) {
         a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
+        a.b_negblk = 1;
         if (hbits(g, i - 1)) {
           a.mask_sgn = ws.hb[i - 1];
           a.mask = nullptr;
@@ -1580,14 +1583,19 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
     case DAMC_LAYER_PROJ:
       if (!wb) return DAMC_ERR_ARG;
       hipLaunchKernelGGL(pack_proj_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf, wb);
-      if (x3_proj_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wb, n, reinterpret_cast<unsigned short*>(wb + n), s));
+      if (x3_proj_cap(*L))
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wb, n, L->cin, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_UP2:
       if (!wb || L->k != 4) return DAMC_ERR_ARG;
       hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, (int)damc::conv_kmajor_ok(L->cin),
                          (int)damc::conv_kmajor_ok(L->cout), wf, wb);
-      if (x3_fwd_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wf, n, reinterpret_cast<unsigned short*>(wf + n), s));
-      if (x3_bwd_cap(*L)) DAMC_CHECK((hipError_t)damc::launch_split_x3(wb, n, reinterpret_cast<unsigned short*>(wb + n), s));
+      // x3 copies with sign-alternating K blocks (gemm.h GemmArgs::b_negblk): rows of 4 Cin (forward, per phase
+      // and output channel) and 16 Cout (input gradient, per input channel)
+      if (x3_fwd_cap(*L))
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wf, n, 4 * L->cin, reinterpret_cast<unsigned short*>(wf + n), s));
+      if (x3_bwd_cap(*L))
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wb, n, 16 * L->cout, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_SMALLC:
       if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));
@@ -1697,6 +1705,7 @@ extern "C" int damc_convT_fwd(const damc_layer_t* L, const float* in, int B, flo
     if ((rc = damc::launch_split_x3(in, (long)B * L->hin * L->win * L->cin, a3, s))) return rc;
     a.A3 = a3;
     a.B3 = x3_of(L->w_fwd, up2_floats(*L));
+    a.b_negblk = 1;
   }
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(*L, B), s);
 }
@@ -1735,6 +1744,7 @@ extern "C" int damc_convT_dgrad(const damc_layer_t* L, const float* gout, int B,
     if ((rc = damc::launch_split_x3(gout, (long)B * L->hout * L->wout * L->cout, a3, s))) return rc;
     a.A3 = a3;
     a.B3 = x3_of(L->w_bwd, up2_floats(*L));
+    a.b_negblk = 1;
   }
   return damc::launch_gemm(a, damc::A_CONV, mask_pre ? damc::EPI_MASK : damc::EPI_STORE, damc::O_DENSE, 1,
                            "upconv_dgrad", conv_flops(*L, B), s);

@@ -106,10 +106,10 @@ def test_celebaHQ_b64_likelihood_gradient_vs_fp64(gpu_device):
     g = lv.likelihood_grad(z0, x, G, 1.0).cpu().numpy()
     g32 = orc.likelihood_grad(L32, z0.cpu(), x.cpu(), 1.0)[0].numpy()
     g64 = orc.likelihood_grad(L64, z0.cpu().double(), x.cpu().double(), 1.0)[0].numpy()
-    # 7 layers, 5 of them k4 s2 p1 with K = 16 Cout up to 32768: the GEMM engines accumulate each output's K
-    # products in one fp32 chain (MFMA), oneDNN's CPU kernels in blocked partial sums, ~1.5-2x less rounding
-    # per layer (tools/diag_smallc.py: 1.7x after one k4 s2 layer, 3.7x after two at Cout 256); hence 8x here
-    _check("celebaHQ B=64 likelihood gradient", g, g32, g64, 1e-7, per_row=True, factor=8.0)
+    # 7 layers, 5 of them k4 s2 p1 with K = 16 Cout up to 16384, then the first layer's 32768-term sum: a bias in
+    # the GEMM's rounding survives that sum where noise cancels, so this is the test of the limb engine's blocked,
+    # sign-alternating accumulation (gemm.hip; without it the HIP median was 13x the fp32 reference's)
+    _check("celebaHQ B=64 likelihood gradient", g, g32, g64, 1e-7, per_row=True)
     xh = lv.generator_forward(z0, G).cpu().numpy()
     _check("celebaHQ B=64 G(z)", xh, orc.generator_sample(L32, z0.cpu()).numpy(),
            orc.generator_sample(L64, z0.cpu().double()).numpy(), 1e-7)

@@ -57,6 +57,7 @@ struct Shape {
   float* bt;  // weights transposed per phase to [n][k] for the K-major engine
   unsigned short* a3 = nullptr;  // limb-engine operands (x3 layout)
   unsigned short* b3 = nullptr;
+  unsigned short* b3n = nullptr;  // the same with odd X3_NEGK-blocks negated (GemmArgs::b_negblk)
 };
 
 static unsigned short* split_dev(const float* d, size_t n) {
@@ -70,11 +71,12 @@ static unsigned short* split_dev(const float* d, size_t n) {
   return y;
 }
 
-template <int V>
+template <int V, int NEG = 0>
 static void run_x3(const Shape& sh, hipStream_t s) {
   GemmArgs a = sh.a;
   a.A3 = sh.a3;
-  a.B3 = sh.b3;
+  a.B3 = NEG ? sh.b3n : sh.b3;
+  a.b_negblk = NEG;
   a.b_zstride = (long)a.N * a.K;
   if (sh.phase)
     launch_x3_t<EPI_BIAS_ACT, O_PHASE, V>(a, 4, s);
@@ -91,11 +93,11 @@ static std::vector<float> to_host(const float* d, size_t n) {
 // fp64 reference of sampled outputs; returns {max, mean} of |c - ref| / (sum_k |a b| + |bias|)
 static void ref_check(const Shape& sh, int B, const std::vector<float>& hA, const std::vector<float>& hB,
                       const std::vector<float>& hbias, const std::vector<float>& hmask, const std::vector<float>& hc,
-                      double* emax, double* emean) {
+                      double* emax, double* emean, double* ebias) {
   const GemmArgs& a = sh.a;
   const int hwq = a.Hq * a.Wq;
   unsigned st = 12345;
-  double mx = 0, sm = 0;
+  double mx = 0, sm = 0, sb = 0;
   const int NS = 384;
   for (int t = 0; t < NS; ++t) {
     st = st * 1664525u + 1013904223u;
@@ -131,10 +133,12 @@ static void ref_check(const Shape& sh, int B, const std::vector<float>& hA, cons
     const double e = std::fabs(hc[idx] - v) / asum;
     mx = std::max(mx, e);
     sm += e;
+    sb += (hc[idx] - v) / asum;
   }
   (void)B;
   *emax = mx;
   *emean = sm / NS;
+  *ebias = sb / NS;
 }
 
 // per-phase transpose of B[K][N] (ldb = N) into Bt[N][K]
@@ -233,8 +237,15 @@ int main(int argc, char** argv) {
     const size_t na = (size_t)(a.M / (a.Hq * a.Wq)) * a.Hin * a.Win * a.Cg;
     sh.a3 = split_dev(a.A, na);
     sh.b3 = split_dev(sh.bt, (size_t)(sh.phase ? 4 : 1) * a.N * a.K);
+    const size_t nb = (size_t)(sh.phase ? 4 : 1) * a.N * a.K;
+    CK(hipMalloc(&sh.b3n, nb * 6));
+    if (launch_split_x3_negblk(sh.bt, (long)nb, a.K, sh.b3n, 0) != 0) {
+      printf("split failed\n");
+      exit(1);
+    }
+    CK(hipDeviceSynchronize());
   }
-  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v13", run_x3<13>}, {"X3/v21", run_x3<21>}, {"X3/v29", run_x3<29>}};
+  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v5neg", run_x3<5, 1>}, {"X3/v21", run_x3<21>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
@@ -257,9 +268,9 @@ int main(int argc, char** argv) {
         vars[v].fn(s2, s);
         CK(hipStreamSynchronize(s));
         std::vector<float> hc = to_host(c, nout);
-        double emax, emean;
-        ref_check(sh, B, hA, hB, hbias, hmask, hc, &emax, &emean);
-        printf("  %s max %.2e mean %.2e", vars[v].name, emax, emean);
+        double emax, emean, ebias;
+        ref_check(sh, B, hA, hB, hbias, hmask, hc, &emax, &emean, &ebias);
+        printf("  %s max %.2e mean %.2e bias %+.1e", vars[v].name, emax, emean, ebias);
       }
       printf("   (|c - fp64| / sum|ab|)\n");
       CK(hipFree(c));
