@@ -815,7 +815,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // V: variant bits (tools/gemm_bench.hip A/B): 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
 // wave, 2 = s_setprio(1) around the MFMA cluster, 4 = LDS-DMA staging (buffer_load ... lds straight into
 // the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write), 16 = supertile
-// raster (a 1-D grid; each XCD's 32 concurrent workgroups form a block of <= 8 M tiles x 4 (N tile, phase) pairs
+// raster (32 = one MFMA accumulation chain over all of K: no blocking, no sign alternation; A/B only) (a 1-D grid; each XCD's 32 concurrent workgroups form a block of <= 8 M tiles x 4 (N tile, phase) pairs
 // with the 4 phases of an N tile adjacent, so the phases' overlapping input windows and the weight panels are
 // shared in L2 instead of every XCD streaming all phases' panels; DMA and non-WGRAD only)
 #ifndef DAMC_X3_VARIANT
@@ -838,6 +838,7 @@ __device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf1
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool M16 = (V & 1) != 0;
+  constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (X3_BM + X3_BN) * X3_ROWB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1092,16 +1093,6 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
           acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
         }
       if (V & 2) __builtin_amdgcn_s_setprio(0);
-      if (((kt + 1) & (X3_FLUSH - 1)) == 0) {
-        const bool neg = p.b_negblk && ((kt / X3_FLUSH) & 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            tot16[i][j] = neg ? tot16[i][j] - acc16[i][j] : tot16[i][j] + acc16[i][j];
-            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-      }
     } else {
       bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
 #pragma unroll
@@ -1133,34 +1124,52 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
           }
       if (V & 2) __builtin_amdgcn_s_setprio(0);
-      if (((kt + 1) & (X3_FLUSH - 1)) == 0) {
-        const bool neg = p.b_negblk && ((kt / X3_FLUSH) & 1);
+    }
+    __syncthreads();
+    // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
+    // (a flush between them and the barrier measured 6-8 % slower)
+    if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
+      const float sg = (p.b_negblk && ((kt / FLUSH) & 1)) ? -1.f : 1.f;
+      if (M16) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
+            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            tot[i][j] = neg ? tot[i][j] - acc[i][j] : tot[i][j] + acc[i][j];
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-          }
+            for (int r = 0; r < 16; ++r) {
+              tot[i][j][r] = __builtin_fmaf(sg, acc[i][j][r], tot[i][j][r]);
+              acc[i][j][r] = 0.f;
+            }
       }
     }
-    __syncthreads();
   }
   }
   // the last partial block
   {
-    const bool neg = p.b_negblk && ((nk / X3_FLUSH) & 1);
+    const float sg = (p.b_negblk && nk > 0 && (((nk - 1) / FLUSH) & 1)) ? -1.f : 1.f;
     if (M16) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc16[i][j] = neg ? tot16[i][j] - acc16[i][j] : tot16[i][j] + acc16[i][j];
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
     } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = neg ? tot[i][j] - acc[i][j] : tot[i][j] + acc[i][j];
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_fmaf(sg, acc[i][j][r], tot[i][j][r]);
     }
   }
   // ---- epilogue through LDS: the block's 256 x 128 fp32 tile, then one thread per (row, channel octet):

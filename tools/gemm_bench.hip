@@ -245,7 +245,7 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
   }
-  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v5neg", run_x3<5, 1>}, {"X3/v21", run_x3<21>}};
+  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v5neg", run_x3<5, 1>}, {"X3/v37(chain)", run_x3<37>}, {"X3/v69(flush32)", run_x3<69>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
