@@ -8,7 +8,10 @@
 //       "output gradient" = x, phase-split) — its reduce writes the (Cout, Cin, 4, 4) layout directly;
 //   (B) the first conv, k3 s1 p1 with Cin <= 4: no input gradient (the image); the weight gradient is the
 //       output layer's direct kernel (wgrad.hip) with dy in the "activation" role and x in the "delta" role;
-//   (C) the last conv, covering its whole input (p0, output 1x1): a dense layer, two fp32 MFMA GEMMs.
+//   (C) the last conv, covering its whole input (p0, output 1x1): a dense layer, two fp32 MFMA GEMMs;
+//   (A') k4 s2 p1 with H = 2 Ho + 1 (Encoder_mnist's 7 -> 3): x zero-padded by one row and column and dy by one
+//       output row and column turn it into (A) exactly — output rows < Ho read input rows < H only, the extra
+//       output row reads the zero row and gets dy = 0, so dW and dx[:H, :W] are unchanged — then dx is cropped.
 // Biases: fixed-order column sums of dy.
 #include <algorithm>
 
@@ -19,7 +22,7 @@ namespace {
 
 using namespace damc;
 
-enum { CASE_NONE = 0, CASE_UP = 1, CASE_FIRST = 2, CASE_DENSE = 3 };
+enum { CASE_NONE = 0, CASE_UP = 1, CASE_FIRST = 2, CASE_DENSE = 3, CASE_UP_ODD = 4 };
 
 int conv_case(int hin, int win, int cin, int cout, int k, int stride, int pad, int* ho_, int* wo_) {
   const int ho = (hin + 2 * pad - k) / stride + 1, wo = (win + 2 * pad - k) / stride + 1;
@@ -27,6 +30,7 @@ int conv_case(int hin, int win, int cin, int cout, int k, int stride, int pad, i
   *wo_ = wo;
   if (ho <= 0 || wo <= 0) return CASE_NONE;
   if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho && win == 2 * wo && cin % 8 == 0) return CASE_UP;
+  if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho + 1 && win == 2 * wo + 1 && cin % 8 == 0) return CASE_UP_ODD;
   if (k == 3 && stride == 1 && pad == 1 && cin <= 4) return CASE_FIRST;
   if (pad == 0 && ho == 1 && wo == 1 && k == hin && k == win) return CASE_DENSE;
   return CASE_NONE;
@@ -79,6 +83,27 @@ __global__ void permute_dense_kernel(const float* __restrict__ g, int cout, int 
   dw[i] = g[(long)co * k * k * cin + ((long)ky * k + kx) * cin + ci];
 }
 
+// NHWC (B, H, W, C) -> (B, H2, W2, C) with zeros beyond H x W (H2 >= H, W2 >= W), or the crop back (H2 <= H)
+__global__ void pad_crop_kernel(const float* __restrict__ x, int B, int H, int W, int C, float* __restrict__ y, int H2,
+                                int W2) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * H2 * W2 * C) return;
+  long t = i;
+  const int c = (int)(t % C);
+  t /= C;
+  const int xx = (int)(t % W2);
+  t /= W2;
+  const int yy = (int)(t % H2);
+  const int b = (int)(t / H2);
+  y[i] = (yy < H && xx < W) ? x[(((long)b * H + yy) * W + xx) * C + c] : 0.f;
+}
+
+int pad_crop(const float* x, int B, int H, int W, int C, float* y, int H2, int W2, hipStream_t s) {
+  const long n = (long)B * H2 * W2 * C;
+  hipLaunchKernelGGL(pad_crop_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, B, H, W, C, y, H2, W2);
+  return (int)hipGetLastError();
+}
+
 // (n, c) -> (c, n)
 __global__ void transpose_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ y) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -103,7 +128,23 @@ struct Bufs {
   float *wf = nullptr, *wb = nullptr, *tmp = nullptr, *slab = nullptr, *g = nullptr, *dyT = nullptr, *wk = nullptr;
   unsigned short *dy3 = nullptr, *tin = nullptr, *tdl = nullptr;
   float* part = nullptr;
+  float *xp = nullptr, *dyp = nullptr, *dxp = nullptr;  // CASE_UP_ODD: padded x, dy and dx
 };
+
+void carve_up(Carve& cv, int B, int ho, int wo, int cin, int cout, Bufs& t) {
+  const long M = (long)B * ho * wo;
+  const int Bp = (B + 31) / 32 * 32;
+  const long P = (long)ho * wo;
+  const size_t n = (size_t)cin * cout * 16;
+  t.wf = cv.take<float>(n + n * 3 / 2);  // fp32 packing + its x3 copy (damc_pack_generator_layer layout)
+  t.wb = cv.take<float>(n + n * 3 / 2);
+  t.dy3 = cv.take<unsigned short>((size_t)M * cout * 3);
+  t.tin = cv.take<unsigned short>((size_t)cout * P * Bp * 3);
+  t.tdl = cv.take<unsigned short>((size_t)4 * cin * P * Bp * 3);
+  int S, kp;
+  up_split(ho, wo, cin, cout, Bp, &S, &kp);
+  t.slab = cv.take<float>((size_t)4 * S * 4 * cout * cin);
+}
 
 size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int pad, char* base, Bufs* b, int* cs) {
   int ho, wo;
@@ -114,18 +155,12 @@ size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int 
   const long M = (long)B * ho * wo;
   t.tmp = cv.take<float>(std::max<size_t>(colsum_tmp_floats(M, cout), 1));
   if (c == CASE_UP) {
-    const int Bp = (B + 31) / 32 * 32;
-    const long P = (long)ho * wo;
-    const size_t n = (size_t)cin * cout * 16;
-    t.wf = cv.take<float>(n + n * 3 / 2);  // fp32 packing + its x3 copy (damc_pack_generator_layer layout)
-    t.wb = cv.take<float>(n + n * 3 / 2);
-    t.dy3 = cv.take<unsigned short>((size_t)M * cout * 3);
-    t.tin = cv.take<unsigned short>((size_t)cout * P * Bp * 3);
-    t.tdl = cv.take<unsigned short>((size_t)4 * cin * P * Bp * 3);
-    int S, kp;
-    up_split(ho, wo, cin, cout, Bp, &S, &kp);
-    t.slab = cv.take<float>((size_t)4 * S * 4 * cout * cin);
-  } else if (c == CASE_FIRST) {
+    carve_up(cv, B, ho, wo, cin, cout, t);
+  } else if (c == CASE_UP_ODD) {
+    t.xp = cv.take<float>((size_t)B * (hin + 1) * (win + 1) * cin);
+    t.dxp = cv.take<float>((size_t)B * (hin + 1) * (win + 1) * cin);
+    t.dyp = cv.take<float>((size_t)B * (ho + 1) * (wo + 1) * cout);
+    carve_up(cv, B, ho + 1, wo + 1, cin, cout, t);  } else if (c == CASE_FIRST) {
     damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
     L.kind = DAMC_LAYER_SMALLC;
     L.cin = cout;
@@ -143,6 +178,80 @@ size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int 
   }
   if (b) *b = t;
   return c == CASE_NONE ? 0 : cv.off;
+}
+
+// (A): dW by O_WGRAD with the transposed view's roles, dx by the transposed view's phase-split forward
+int backward_up(const float* x, const float* dy, const float* w, int B, int hin, int win, int cin, int cout, int ho,
+                int wo, float* dx, float* dw, const Bufs& t, hipStream_t s, void* stream) {
+  const long M = (long)B * ho * wo;
+  int rc;
+  const int Bp = (B + 31) / 32 * 32;
+  const long P = (long)ho * wo;
+  damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
+  // weight gradient: O_WGRAD with the transposed view's roles (input = dy, output gradient = x)
+  if ((rc = launch_transpose_x3(dy, nullptr, B, ho, wo, cout, ho, wo, 1, 1, 0, 0, Bp, t.tin, nullptr, s))) return rc;
+  for (int ph = 0; ph < 4; ++ph) {
+    rc = launch_transpose_x3(x, nullptr, B, hin, win, cin, ho, wo, 2, 2, ph >> 1, ph & 1, Bp,
+                             t.tdl + (size_t)ph * cin * P * Bp * 3, nullptr, s);
+    if (rc) return rc;
+  }
+  {
+    int S, kp;
+    up_split(ho, wo, cin, cout, Bp, &S, &kp);
+    GemmArgs a;
+    a.A3 = t.tin;
+    a.B3 = t.tdl;
+    a.Cg = cout;
+    a.Hin = ho;
+    a.Win = wo;
+    a.K = (int)(P * Bp);
+    a.wg_bp = Bp;
+    a.kw = 2;
+    a.wg_phases = 4;
+    a.M = 4 * cout;
+    a.N = cin;
+    a.ldc = cin;
+    a.c_zstride = (long)a.M * a.N;
+    a.b_zstride = (long)cin * a.K;
+    a.k_per_z = kp;
+    a.C = t.slab;
+    if ((rc = launch_wgrad_x3(a, S, "enc_wgrad", 2.0 * M * cout * cin * 16, s))) return rc;
+    if ((rc = launch_up2_wgrad_reduce(t.slab, S, cout, cin, dw, s))) return rc;
+  }
+  if (!dx) return 0;
+  // input gradient: the transposed view's forward (phase-split implicit GEMM) over dy
+  L.w_fwd = t.wf;
+  L.w_bwd = t.wb;
+  if ((rc = damc_pack_generator_layer(&L, w, t.wf, t.wb, stream))) return rc;
+  const size_t n = (size_t)cin * cout * 16;
+  GemmArgs a;
+  a.A = dy;
+  a.Hin = ho;
+  a.Win = wo;
+  a.Cg = cout;
+  a.Hq = ho;
+  a.Wq = wo;
+  a.kw = 2;
+  a.stride = 1;
+  a.B = t.wf;
+  a.b_kmajor = conv_kmajor_ok(cout);
+  a.ldb = a.b_kmajor ? 4L * cout : cin;
+  a.b_zstride = 4L * cout * cin;
+  a.C = dx;
+  a.ldc = cin;
+  a.M = (int)M;
+  a.N = cin;
+  a.K = 4 * cout;
+  a.Hout = hin;
+  a.Wout = win;
+  a.act = DAMC_ACT_NONE;
+  if (up_x3(cin, cout)) {
+    if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
+    a.A3 = t.dy3;
+    a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
+    a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy
+  }
+  return launch_gemm(a, A_CONV, EPI_BIAS_ACT, O_PHASE, 4, "enc_dgrad", 2.0 * M * cout * cin * 16, s);
 }
 
 }  // namespace
@@ -224,72 +333,12 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     }
     return (int)hipGetLastError();
   }
-  // CASE_UP
-  const int Bp = (B + 31) / 32 * 32;
-  const long P = (long)ho * wo;
-  damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
-  // weight gradient: O_WGRAD with the transposed view's roles (input = dy, output gradient = x)
-  if ((rc = launch_transpose_x3(dy, nullptr, B, ho, wo, cout, ho, wo, 1, 1, 0, 0, Bp, t.tin, nullptr, s))) return rc;
-  for (int ph = 0; ph < 4; ++ph) {
-    rc = launch_transpose_x3(x, nullptr, B, hin, win, cin, ho, wo, 2, 2, ph >> 1, ph & 1, Bp,
-                             t.tdl + (size_t)ph * cin * P * Bp * 3, nullptr, s);
-    if (rc) return rc;
-  }
-  {
-    int S, kp;
-    up_split(ho, wo, cin, cout, Bp, &S, &kp);
-    GemmArgs a;
-    a.A3 = t.tin;
-    a.B3 = t.tdl;
-    a.Cg = cout;
-    a.Hin = ho;
-    a.Win = wo;
-    a.K = (int)(P * Bp);
-    a.wg_bp = Bp;
-    a.kw = 2;
-    a.wg_phases = 4;
-    a.M = 4 * cout;
-    a.N = cin;
-    a.ldc = cin;
-    a.c_zstride = (long)a.M * a.N;
-    a.b_zstride = (long)cin * a.K;
-    a.k_per_z = kp;
-    a.C = t.slab;
-    if ((rc = launch_wgrad_x3(a, S, "enc_wgrad", 2.0 * M * cout * cin * 16, s))) return rc;
-    if ((rc = launch_up2_wgrad_reduce(t.slab, S, cout, cin, dw, s))) return rc;
-  }
-  if (!dx) return 0;
-  // input gradient: the transposed view's forward (phase-split implicit GEMM) over dy
-  L.w_fwd = t.wf;
-  L.w_bwd = t.wb;
-  if ((rc = damc_pack_generator_layer(&L, w, t.wf, t.wb, stream))) return rc;
-  const size_t n = (size_t)cin * cout * 16;
-  GemmArgs a;
-  a.A = dy;
-  a.Hin = ho;
-  a.Win = wo;
-  a.Cg = cout;
-  a.Hq = ho;
-  a.Wq = wo;
-  a.kw = 2;
-  a.stride = 1;
-  a.B = t.wf;
-  a.b_kmajor = conv_kmajor_ok(cout);
-  a.ldb = a.b_kmajor ? 4L * cout : cin;
-  a.b_zstride = 4L * cout * cin;
-  a.C = dx;
-  a.ldc = cin;
-  a.M = (int)M;
-  a.N = cin;
-  a.K = 4 * cout;
-  a.Hout = hin;
-  a.Wout = win;
-  a.act = DAMC_ACT_NONE;
-  if (up_x3(cin, cout)) {
-    if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
-    a.A3 = t.dy3;
-    a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
-    a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy
-  }
-  return launch_gemm(a, A_CONV, EPI_BIAS_ACT, O_PHASE, 4, "enc_dgrad", 2.0 * M * cout * cin * 16, s);
+  if (cs == CASE_UP) return backward_up(x, dy, w, B, hin, win, cin, cout, ho, wo, dx, dw, t, s, stream);
+  // CASE_UP_ODD: (A) on the padded tensors, then the crop
+  if ((rc = pad_crop(x, B, hin, win, cin, t.xp, hin + 1, win + 1, s))) return rc;
+  if ((rc = pad_crop(dy, B, ho, wo, cout, t.dyp, ho + 1, wo + 1, s))) return rc;
+  if ((rc = backward_up(t.xp, t.dyp, w, B, hin + 1, win + 1, cin, cout, ho + 1, wo + 1, dx ? t.dxp : nullptr, dw, t, s,
+                        stream)))
+    return rc;
+  return dx ? pad_crop(t.dxp, B, hin + 1, win + 1, cin, dx, hin, win, s) : 0;
 }

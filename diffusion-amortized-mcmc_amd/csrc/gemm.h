@@ -80,6 +80,9 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
 // negated (exact); the GEMM launches that read it set GemmArgs::b_negblk
 constexpr int X3_NEGK = 256;
 int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s);
+// the same reordered for the channel-major K walk: a row's K = taps * Cg values [tap][c] are stored
+// [c / sw][tap][c % sw] (sw channels per slice), sign blocks counted in that order
+int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s);
 
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);

@@ -976,6 +976,30 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < X3_BJ; ++j) *reinterpret_cast<u32x4*>(base + blds[j]) = rb[j];
   };
+  // channel-major walk: the next tile's (slice, tap), advanced after the tile's barrier (its VALU work then
+  // overlaps the trailing MFMAs; before the DMA issue it delayed the next tile, before the barrier it kept the
+  // barrier from being hoisted)
+  constexpr bool CMAJ = (V & 8) != 0 && OM != O_WGRAD;
+  constexpr int CMAJ_SW = X3_BK;  // channels per slice of the channel-major walk (64 measured the same)
+  int cmaj_h = 0;  // K tile within the current slice (slices of CMAJ_SW channels)
+  auto advance_cmaj = [&]() {
+    if (++cmaj_h < CMAJ_SW / X3_BK) {
+      ci0 += X3_BK;
+      return;
+    }
+    cmaj_h = 0;
+    ci0 -= CMAJ_SW - X3_BK;
+    ++tap;
+    if (++tkx == kw) {
+      tkx = 0;
+      if (++tky == kh) {
+        tky = 0;
+        tap = 0;
+        ci0 += CMAJ_SW;
+      }
+    }
+    set_tap();
+  };
   // LDS-DMA form: chunk id -> LDS byte 16 id, so each wave-instruction fills 1 KiB at a wave-uniform base
   typedef __attribute__((address_space(3))) void* lds_t;
   const int wbase = (tid & ~63) * 16;
@@ -994,6 +1018,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16,
                                                  live ? (int)(abase[j] + k0 * 6) : (int)KM_OOB, 0, 0, 0);
       }
+    } else if constexpr (CMAJ) {
+      // K tile kt = (channel slice kt / taps, tap kt % taps), walked incrementally; the weights are stored in
+      // the same slice-major order (launch_split_x3_cmaj), so B stays the sequential column k0
+#pragma unroll
+      for (int j = 0; j < X3_AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < X3_AJ; ++j)
@@ -1003,7 +1033,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     for (int j = 0; j < X3_BJ; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
                                                k0 * 6, 0, 0);
-    if constexpr (OM != O_WGRAD) {
+    if constexpr (OM != O_WGRAD && !CMAJ) {
       ci0 += X3_BK;
       if (ci0 == Cg) {
         ci0 = 0;
@@ -1052,8 +1082,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   {
   constexpr bool DMA = (V & 4) != 0;
   static_assert(OM != O_WGRAD || DMA, "O_WGRAD runs on the LDS-DMA staging path only");
+  static_assert(!CMAJ || DMA, "the channel-major walk runs on the LDS-DMA staging path only");
   if (DMA) {
     if (nk > 0) dma_ab(kbeg, 0);
+    if constexpr (CMAJ) advance_cmaj();
   } else if (nk > 0) {
     load_ab(0);
     store_ab(0);
@@ -1126,6 +1158,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       if (V & 2) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
+    if constexpr (CMAJ) advance_cmaj();
     // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
     // (a flush between them and the barrier measured 6-8 % slower)
     if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
@@ -1301,6 +1334,39 @@ int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hip
   const long n8 = n / 8;
   if (n8 == 0) return 0;
   hipLaunchKernelGGL(split_x3_negblk_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, y);
+  return (int)hipGetLastError();
+}
+
+// weight rows of K = taps * Cg values in tap-major order [tap][c] -> x3 in slice-major order
+// [c / 32][tap][c % 32] (the channel-major K walk, V & 8), odd X3_NEGK-blocks of the new order negated
+__global__ void split_x3_cmaj_kernel(const float* __restrict__ x, long n8, int K8, int Cg8, int taps, int sw8,
+                                     unsigned short* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // source octet
+  if (i >= n8) return;
+  const long row = i / K8;
+  const int k8 = (int)(i - row * K8);
+  const int tp = k8 / Cg8, c8 = k8 - tp * Cg8;  // octet c8 of tap tp
+  const int d8 = (c8 / sw8) * taps * sw8 + tp * sw8 + c8 % sw8;  // destination octet within the row
+  const float sg = ((d8 * 8 / X3_NEGK) & 1) ? -1.f : 1.f;
+  const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
+  const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
+  const float v[8] = {sg * v0.x, sg * v0.y, sg * v0.z, sg * v0.w, sg * v1.x, sg * v1.y, sg * v1.z, sg * v1.w};
+  bf16x8 h, m, l;
+  split3_octet(v, h, m, l);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * (row * K8 + d8);
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
+int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s) {
+  if (K <= 0 || Cg <= 0 || sw <= 0 || sw % 8 != 0 || Cg % sw != 0 || K % Cg != 0 || n % K != 0 ||
+      ((uintptr_t)x | (uintptr_t)y) % 16 != 0)
+    return DAMC_ERR_ARG;
+  const long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(split_x3_cmaj_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, Cg / 8,
+                     K / Cg, sw / 8, y);
   return (int)hipGetLastError();
 }
 

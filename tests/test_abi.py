@@ -91,7 +91,8 @@ def test_training_shape_support_host_only():
     assert ws(128, 16, 16, 64, 128, 4, 2, 1) > 0       # k4 s2 p1, H = 2 Ho: limb-engine path
     assert ws(128, 32, 32, 3, 64, 3, 1, 1) > 0         # first conv (Cin <= 4)
     assert ws(128, 4, 4, 512, 1024, 4, 1, 0) > 0       # last conv covering its input
-    assert ws(128, 7, 7, 64, 128, 4, 2, 1) == 0        # mnist 7 -> 3: H != 2 Ho
+    assert ws(128, 7, 7, 64, 128, 4, 2, 1) > 0         # mnist 7 -> 3 (H = 2 Ho + 1): the zero-padded path
+    assert ws(128, 7, 7, 4, 128, 4, 2, 1) == 0         # ... whose transposed view needs Cin % 8 == 0
     assert ws(128, 32, 32, 64, 64, 3, 1, 1) == 0       # a k3 conv that is not the first
     assert L.damc_conv2d_workspace_floats(128, 8, 8, 256, 512, 4, 2, 1) > 0  # under-filled: split-K slabs
     d = _lib.DenoiserTrain()
@@ -101,7 +102,7 @@ def test_training_shape_support_host_only():
 
 
 def test_encoder_training_dispatch_host_only():
-    """encoder_train_supported: CIFAR / CelebA topologies take the HIP path, mnist's does not (host logic)."""
+    """encoder_train_supported: the CIFAR / CelebA / mnist topologies take the HIP path (host logic)."""
     import torch
 
     from damc import training
@@ -110,7 +111,7 @@ def test_encoder_training_dispatch_host_only():
     x32 = torch.empty(4, 3, 32, 32)
     assert training.encoder_train_supported(dn.Encoder_cifar10(nc=3, nemb=64, nif=8), x32)
     assert training.encoder_train_supported(dn.Encoder_celeba64(nc=3, nemb=64, nif=8), torch.empty(2, 3, 64, 64))
-    assert not training.encoder_train_supported(dn.Encoder_mnist(nc=1, nemb=64, nif=8), torch.empty(2, 1, 28, 28))
+    assert training.encoder_train_supported(dn.Encoder_mnist(nc=1, nemb=64, nif=8), torch.empty(2, 1, 28, 28))
 
 
 def test_adam_chunk_table_host_only():

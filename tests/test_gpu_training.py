@@ -116,9 +116,8 @@ def test_q_update_matches_reference(gpu_device, name):
         loss, grads, rec, meta = qtrain_run(name, gpu_device)
     finally:
         training.encoder_apply = orig
-    # the encoder ran on libdamc for every topology whose convs the C side covers (mnist's 7 -> 3 stride-2
-    # conv is not a k4 s2 p1 with H = 2 Ho: stock PyTorch there)
-    assert bool(calls) == (name != "q_mnist_s")
+    # the encoder ran on libdamc for every topology (mnist's 7 -> 3 conv through the zero-padded k4 s2 p1 path)
+    assert calls
     assert rel_l2(loss, rec["loss"]) < 1e-5
     # 1e-4: the time embedding sin/cos(1000 * f * t) (SinusoidalPosEmb, arguments up to ~1000 rad, whose own
     # fp32 rounding is ~3e-5 absolute) is torch's on each device, GPU vs the reference's CPU; with B = 3-4
@@ -175,6 +174,42 @@ def _stock_denoiser(p, z, t_in, xemb):
     for layer in p.out_layers:
         out = layer(ctx=ctx, x=F.leaky_relu(torch.cat([out, skips.pop()], dim=1), negative_slope=0.01))
     return z + out if p.residual else out
+
+
+@pytest.mark.parametrize("B,cin,cout", [(128, 256, 512), (5, 32, 64)])
+def test_odd_k4s2_conv_backward(gpu_device, B, cin, cout):
+    """Encoder_mnist's 7 -> 3 k4 s2 p1 conv (diffusion_net.py:374-413; nif 64 at B=128 and a ragged small case):
+    damc_conv2d_backward_nhwc through the zero-padded 8 -> 4 path, dW, db and dx against fp32 / fp64 autograd."""
+    import ctypes
+
+    import torch.nn.functional as F
+
+    from damc import _lib
+    from damc._lib import ptr
+
+    L = _lib.lib()
+    st = _lib.stream_ptr(gpu_device)
+    g = torch.Generator().manual_seed(B + cin)
+    x = torch.randn(B, 7, 7, cin, generator=g).to(gpu_device)
+    dy = torch.randn(B, 3, 3, cout, generator=g).to(gpu_device)
+    w = (torch.randn(cout, cin, 4, 4, generator=g) * (cin * 16) ** -0.5).to(gpu_device)
+    nb = int(L.damc_conv2d_backward_workspace_bytes(B, 7, 7, cin, cout, 4, 2, 1))
+    assert nb > 0
+    ws = torch.empty(nb, dtype=torch.uint8, device=gpu_device)
+    dx, dw, db = torch.empty_like(x), torch.empty_like(w), torch.empty(cout, device=gpu_device)
+    assert L.damc_conv2d_backward_nhwc(ptr(x), ptr(dy), ptr(w), B, 7, 7, cin, cout, 4, 2, 1, ptr(dx), ptr(dw), ptr(db),
+                                       ptr(ws), nb, st) == 0
+    refs = []
+    for dt in (torch.float32, torch.float64):
+        xx = x.cpu().to(dt).permute(0, 3, 1, 2).clone().requires_grad_(True)
+        ww = w.cpu().to(dt).clone().requires_grad_(True)
+        bb = torch.zeros(cout, dtype=dt, requires_grad=True)
+        F.conv2d(xx, ww, bb, 2, 1).backward(dy.cpu().to(dt).permute(0, 3, 1, 2))
+        refs.append((ww.grad, bb.grad, xx.grad.permute(0, 2, 3, 1)))
+    for nm, ours, r32, r64 in zip(("dw", "db", "dx"), (dw, db, dx), refs[0], refs[1]):
+        e, e32 = rel_l2(ours.double().cpu().numpy(), r64.numpy()), rel_l2(r32.double().numpy(), r64.numpy())
+        print("7->3 conv B=%d %s: |hip - fp64| %.2e  |torch32 - fp64| %.2e" % (B, nm, e, e32))
+        assert e <= 3 * e32 + 1e-6, (nm, e, e32)
 
 
 def test_encoder_train_stagewise_b128(gpu_device):

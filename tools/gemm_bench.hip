@@ -58,6 +58,7 @@ struct Shape {
   unsigned short* a3 = nullptr;  // limb-engine operands (x3 layout)
   unsigned short* b3 = nullptr;
   unsigned short* b3n = nullptr;  // the same with odd X3_NEGK-blocks negated (GemmArgs::b_negblk)
+  unsigned short* b3c = nullptr;  // slice-major (channel-major K walk, V & 8) with sign blocks
 };
 
 static unsigned short* split_dev(const float* d, size_t n) {
@@ -75,8 +76,8 @@ template <int V, int NEG = 0>
 static void run_x3(const Shape& sh, hipStream_t s) {
   GemmArgs a = sh.a;
   a.A3 = sh.a3;
-  a.B3 = NEG ? sh.b3n : sh.b3;
-  a.b_negblk = NEG;
+  a.B3 = (V & 8) ? sh.b3c : (NEG ? sh.b3n : sh.b3);
+  a.b_negblk = (V & 8) ? 1 : NEG;
   a.b_zstride = (long)a.N * a.K;
   if (sh.phase)
     launch_x3_t<EPI_BIAS_ACT, O_PHASE, V>(a, 4, s);
@@ -239,13 +240,18 @@ int main(int argc, char** argv) {
     sh.b3 = split_dev(sh.bt, (size_t)(sh.phase ? 4 : 1) * a.N * a.K);
     const size_t nb = (size_t)(sh.phase ? 4 : 1) * a.N * a.K;
     CK(hipMalloc(&sh.b3n, nb * 6));
+    CK(hipMalloc(&sh.b3c, nb * 6));
+    if (launch_split_x3_cmaj(sh.bt, (long)nb, a.K, a.Cg, 32, sh.b3c, 0) != 0) {
+      printf("split failed\n");
+      exit(1);
+    }
     if (launch_split_x3_negblk(sh.bt, (long)nb, a.K, sh.b3n, 0) != 0) {
       printf("split failed\n");
       exit(1);
     }
     CK(hipDeviceSynchronize());
   }
-  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v5neg", run_x3<5, 1>}, {"X3/v37(chain)", run_x3<37>}, {"X3/v69(flush32)", run_x3<69>}};
+  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v13(cmaj)", run_x3<13>}, {"X3/v21(raster)", run_x3<21>}, {"X3/v29(cmaj+raster)", run_x3<29>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {

@@ -27,6 +27,19 @@ __global__ void k(const float* A, const float* B, float* C, int trials, float sg
   for (int r = 0; r < 4; ++r) C[(long)t * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = sg * c[r];
 }
 
+// the same with v_mfma_f32_16x16x4_f32 (fp32 operands, 4 products): A [trial][16][4], B [trial][4][16]
+__global__ void k4(const float* A, const float* B, float* C, int trials, float sg) {
+  const int t = blockIdx.x;
+  if (t >= trials) return;
+  const int lane = threadIdx.x;
+  const float a = sg * A[(long)t * 512 + (lane & 15) * 32 + (lane >> 4)];
+  const float b = B[(long)t * 512 + (lane >> 4) * 16 + (lane & 15)];
+  f32x4 c;
+  for (int r = 0; r < 4; ++r) c[r] = sg * C[(long)t * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)];
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  for (int r = 0; r < 4; ++r) C[(long)t * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = sg * c[r];
+}
+
 static float bf(float x) {  // RNE to bf16
   unsigned u;
   memcpy(&u, &x, 4);
@@ -51,13 +64,21 @@ int main() {
   hipMalloc(&dC, C.size() * 4);
   hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(dB, B.data(), B.size() * 4, hipMemcpyHostToDevice);
-  for (int mode = 0; mode < 6; ++mode) {
-    const float sg = mode >= 3 ? -1.f : 1.f;
+  for (int mode = 0; mode < 12; ++mode) {
+    const bool f32 = mode >= 6;
+    const int kdep = f32 ? 4 : 32;
+    if (mode == 6)
+      for (auto& v : A) v = nrm();  // full fp32 operands for the fp32 MFMA
+    const float sg = mode % 6 >= 3 ? -1.f : 1.f;
     srand(7 + mode % 3);
     for (auto& v : C) v = mode % 3 == 0 ? 0.f : (mode % 3 == 1 ? 8.f * nrm() : 0.01f * nrm());
     C0 = C;
     hipMemcpy(dC, C.data(), C.size() * 4, hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(k, dim3(trials), dim3(64), 0, 0, dA, dB, dC, trials, sg);
+    if (mode == 6) hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice);
+    if (f32)
+      hipLaunchKernelGGL(k4, dim3(trials), dim3(64), 0, 0, dA, dB, dC, trials, sg);
+    else
+      hipLaunchKernelGGL(k, dim3(trials), dim3(64), 0, 0, dA, dB, dC, trials, sg);
     hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost);
     double sum = 0, sq = 0, sgn = 0, sum_rne = 0, sq_rne = 0;
     long n = 0;
@@ -65,7 +86,7 @@ int main() {
       for (int i = 0; i < 16; ++i)
         for (int j = 0; j < 16; ++j) {
           double ex = C0[t * 256 + i * 16 + j], mx = fabs(ex);
-          for (int kk = 0; kk < 32; ++kk) {
+          for (int kk = 0; kk < kdep; ++kk) {
             const double p = (double)A[t * 512 + i * 32 + kk] * B[t * 512 + kk * 16 + j];
             ex += p;
             mx = fmax(mx, fabs(p));
@@ -80,8 +101,8 @@ int main() {
           sq_rne += er * er;
           ++n;
         }
-    printf("%s C %-12s: mfma error mean %+.3f rms %.3f  (sign-relative mean %+.3f)   fp32-rne of exact: mean %+.3f rms %.3f"
-           "   [units 2^-24 max|term|]\n", sg > 0 ? "+" : "-(-A B - C)", mode % 3 == 0 ? "= 0" : (mode % 3 == 1 ? "~ 8 N(0,1)" : "~ .01 N(0,1)"), sum / n,
+    printf("%s %s C %-12s: mfma error mean %+.3f rms %.3f  (sign-relative mean %+.3f)   fp32-rne of exact: mean %+.3f rms %.3f"
+           "   [units 2^-24 max|term|]\n", f32 ? "f32 16x16x4 " : "bf16 16x16x32", sg > 0 ? "+" : "-(-A B - C)", mode % 3 == 0 ? "= 0" : (mode % 3 == 1 ? "~ 8 N(0,1)" : "~ .01 N(0,1)"), sum / n,
            sqrt(sq / n), sgn / n, sum_rne / n, sqrt(sq_rne / n));
   }
   return 0;
