@@ -334,40 +334,52 @@ __global__ void philox_normal_kernel(float* out, int n_steps, int B, int nz, uin
 constexpr int EB_THREADS = 1024, EB_WAVES = 16, EB_RW = 13, EB_K2 = 4, EB_K1 = 2;
 bool ebm_reg_ok(int nz, int nh) { return nz > 0 && nz <= 64 * EB_K1 && nh > 0 && nh <= EB_WAVES * EB_RW; }
 
+// cross-lane moves without the LDS crossbar: DPP within 16-lane rows, v_permlane16/32_swap across them
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1, DPP_QUAD_XOR2 = 0x4E, DPP_ROW_SHL4 = 0x104, DPP_ROW_SHR4 = 0x114,
+              DPP_ROW_ROR8 = 0x128;
+
+// the pair sum across lanes l and l ^ 32 (a in the lower half, b in the upper): one v_permlane32_swap moves the
+// upper lanes' a down and the lower lanes' b up, so own + partner is the sum of the two outputs in every lane
+__device__ __forceinline__ float pair_sum32(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// the same across l and l ^ 16 (v_permlane16_swap: odd 16-lane rows of the first operand <-> even rows of the
+// second)
+__device__ __forceinline__ float pair_sum16(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // v[16]: per-lane partial sums of 16 rows -> the sum over the 64 lanes of row (lane >> 2) & 15, in every lane
+// (a halving exchange: at each level a lane keeps half of its rows and adds its partner's copy of them; the
+// same additions in the same order as with __shfl_xor, without ds_bpermute's LDS round trips)
 __device__ __forceinline__ float reduce16_rows(float (&v)[16], int lane) {
-  {
-    const bool up = lane & 32;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float keep = up ? v[i + 8] : v[i], send = up ? v[i] : v[i + 8];
-      v[i] = keep + __shfl_xor(send, 32, 64);
-    }
-  }
-  {
-    const bool up = lane & 16;
+  for (int i = 0; i < 8; ++i) v[i] = pair_sum32(v[i], v[i + 8]);  // lane half 32: rows i (low) / i + 8 (high)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float keep = up ? v[i + 4] : v[i], send = up ? v[i] : v[i + 4];
-      v[i] = keep + __shfl_xor(send, 16, 64);
-    }
-  }
+  for (int i = 0; i < 4; ++i) v[i] = pair_sum16(v[i], v[i + 4]);
   {
     const bool up = lane & 8;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const float keep = up ? v[i + 2] : v[i], send = up ? v[i] : v[i + 2];
-      v[i] = keep + __shfl_xor(send, 8, 64);
+      v[i] = keep + dpp<DPP_ROW_ROR8>(send);  // row_ror:8 = lane ^ 8 within the 16-lane row
     }
   }
   {
     const bool up = lane & 4;
     const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
-    v[0] = keep + __shfl_xor(send, 4, 64);
+    const float from_hi = dpp<DPP_ROW_SHL4>(send), from_lo = dpp<DPP_ROW_SHR4>(send);
+    v[0] = keep + (up ? from_lo : from_hi);
   }
   float t = v[0];
-  t += __shfl_xor(t, 2, 64);
-  t += __shfl_xor(t, 1, 64);
+  t += dpp<DPP_QUAD_XOR2>(t);
+  t += dpp<DPP_QUAD_XOR1>(t);
   return t;
 }
 
@@ -407,6 +419,7 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chain = blockIdx.x;
   __shared__ float zs[64 * EB_K1];
+  __shared__ float xs[64 * EB_K1];  // this step's noise
   __shared__ float h1s[EB_WAVES * EB_RW];
   __shared__ float part2[EB_WAVES][64 * EB_K2];
   __shared__ float part1[EB_WAVES][64 * EB_K1];
@@ -439,6 +452,19 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
 
   const int nsteps = MODE == EB_PRIOR ? a.n_steps : 1;
   for (int it = 0; it < nsteps; ++it) {
+    // ---- this step's noise, off the update's critical path: drawn by the last two waves (wave 15 owns 5 live
+    // rows of 13 at nh = 200) into LDS before the FC work; the barriers below publish it to the update
+    const bool draw = MODE != EB_GRAD && a.with_noise && wave >= EB_WAVES - 2;
+    if (draw) {
+      const int c = tid - (EB_WAVES - 2) * 64;
+      if (c < nz) {
+        xs[c] = MODE == EB_PRIOR
+                    ? noise_at(a.noise, ((long)it * a.B + chain) * nz + c, 1, a.seed, a.chain_base + chain,
+                               a.step_offset + it, c, DAMC_STREAM_PRIOR)
+                    : noise_at(a.noise, (long)chain * nz + c, 1, a.seed, a.chain_base + chain, a.step_offset, c,
+                               DAMC_STREAM_POSTERIOR);
+      }
+    }
     // ---- layer 1 forward: a1 = W1 z + b1, h1 = lrelu(a1)
     float zl[EB_K1];
 #pragma unroll
@@ -495,8 +521,8 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
       const int j = EB_RW * wave + (lane >> 2), w0 = 4 * (lane & 3);
       if (j < nh) g1 = part2[w0][j] + part2[w0 + 1][j] + part2[w0 + 2][j] + part2[w0 + 3][j];
     }
-    g1 += __shfl_xor(g1, 1, 64);
-    g1 += __shfl_xor(g1, 2, 64);
+    g1 += dpp<DPP_QUAD_XOR1>(g1);
+    g1 += dpp<DPP_QUAD_XOR2>(g1);
     g1 *= m1;  // lane l < 52 holds row l >> 2 = rr: its own a1
     // ---- layer 1 backward: partial (W1^T g1)[c] over this wave's rows
     float q1[EB_K1] = {};
@@ -525,16 +551,7 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
         zsq = zv * zv;
         gsum = g;
         float zn = sub_rn(zv, mul_rn(a.c1, g));
-        if (a.with_noise) {
-          float xi;
-          if (MODE == EB_PRIOR) {
-            xi = noise_at(a.noise, ((long)it * a.B + chain) * nz + tid, 1, a.seed, a.chain_base + chain,
-                          a.step_offset + it, tid, DAMC_STREAM_PRIOR);
-          } else {
-            xi = noise_at(a.noise, gi, 1, a.seed, a.chain_base + chain, a.step_offset, tid, DAMC_STREAM_POSTERIOR);
-          }
-          zn = add_rn(zn, mul_rn(a.step, xi));
-        }
+        if (a.with_noise) zn = add_rn(zn, mul_rn(a.step, xs[tid]));
         zs[tid] = zn;
       }
     }

@@ -253,3 +253,23 @@ def stream_ptr(device=None):
     import torch
 
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class WorkspaceCache:
+    """A reusable device workspace per (thread, stream, key).  A library call's kernels are enqueued in order on
+    the caller's stream, so two calls may share scratch memory only if they are ordered on the same stream and
+    issued by the same thread: two threads on one stream interleave their launches (one call's kernels would
+    overwrite the other's intermediates), and two streams run concurrently."""
+
+    def __init__(self):
+        self._tls = threading.local()
+
+    def get(self, device, nbytes, key):
+        import torch
+
+        stream = torch.cuda.current_stream(device).cuda_stream
+        k = (key, str(device), stream)
+        cur = getattr(self._tls, "ws", None)
+        if cur is None or cur[0] != k or cur[1].numel() < nbytes:
+            self._tls.ws = cur = (k, torch.empty(nbytes, dtype=torch.uint8, device=device))
+        return cur[1]

@@ -168,10 +168,9 @@ class DenoiserPlan:
         nbytes = int(_lib.lib().damc_sweep_workspace_bytes(ctypes.byref(desc), B, n))
         if nbytes == 0:
             raise _lib.DamcError("unsupported denoiser configuration for the HIP path")
-        key = (int(B), int(n), str(device))
-        if self._ws is None or self._ws[0] != key or self._ws[1].numel() < nbytes:
-            self._ws = (key, torch.empty(nbytes, dtype=torch.uint8, device=device))
-        return self._ws[1], nbytes
+        if self._ws is None:
+            self._ws = _lib.WorkspaceCache()
+        return self._ws.get(device, nbytes, (int(B), int(n))), nbytes
 
 
 _ENC = weakref.WeakKeyDictionary()

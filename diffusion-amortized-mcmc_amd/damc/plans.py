@@ -155,11 +155,9 @@ class GeneratorPlan:
         nbytes = int(L.damc_posterior_workspace_bytes(ctypes.byref(self.desc), int(batch)))
         if nbytes == 0:
             raise _lib.DamcError("unsupported generator configuration for the HIP path")
-        key = (int(batch), str(self.device))
-        ws = getattr(self, "_ws", None)
-        if ws is None or ws[0] != key or ws[1].numel() < nbytes:
-            self._ws = (key, torch.empty(nbytes, dtype=torch.uint8, device=self.device))
-        return self._ws[1], nbytes
+        if getattr(self, "_ws", None) is None:
+            self._ws = _lib.WorkspaceCache()
+        return self._ws.get(self.device, nbytes, int(batch)), nbytes
 
 
 class EbmPlan:
