@@ -47,7 +47,8 @@ def _worker(rank, world, port, q):
     f.update(feats[s:s + c])
     mse = m.compute()
     mu, sigma = f.compute()
-    q.put((rank, mse, mu, sigma))
+    # numpy copies: a tensor on a spawn queue is a shared-memory handle that dies with this process
+    q.put((rank, mse, mu.numpy().copy(), sigma.numpy().copy()))
     d.destroy_process_group()
 
 
@@ -71,6 +72,7 @@ def test_reductions_match_single_process():
     want_mu = feats.mean(0)
     want_sigma = torch.cov(feats.t())
     for _, mse, mu, sigma in res:
+        mu, sigma = torch.from_numpy(mu), torch.from_numpy(sigma)
         assert abs(mse - want_mse) < 1e-12
         assert torch.allclose(mu, want_mu, atol=1e-12)
         assert torch.allclose(sigma, want_sigma, atol=1e-10)
@@ -106,8 +108,8 @@ def _plan_worker(rank, world, port, q):
     d.all_gather(bases, torch.tensor([plan["post_start"], plan["prior_start"]]))
     if rank == 0:
         n = [(int(c[0]), int(c[1])) for c in counts]
-        q.put((torch.cat([g[:c] for g, (c, _) in zip(gx, n)]), torch.cat([g[:c] for g, (c, _) in zip(gz, n)]),
-               torch.cat([g[:c] for g, (_, c) in zip(gp, n)]), [tuple(int(v) for v in b) for b in bases], n))
+        q.put((torch.cat([g[:c] for g, (c, _) in zip(gx, n)]).numpy(), torch.cat([g[:c] for g, (c, _) in zip(gz, n)]).numpy(),
+               torch.cat([g[:c] for g, (_, c) in zip(gp, n)]).numpy(), [tuple(int(v) for v in b) for b in bases], n))
     d.destroy_process_group()
 
 
@@ -130,6 +132,7 @@ def test_strong_scaling_plan_reassembles_the_global_block():
     for p in procs:
         p.start()
     x, z0, p0, bases, counts = q.get(timeout=180)
+    x, z0, p0 = (torch.from_numpy(a) for a in (x, z0, p0))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
