@@ -33,10 +33,14 @@
 
 namespace {
 
-constexpr int CH_THREADS = 256;  // 4 waves, K split in quarters
+#ifndef DAMC_CH_WAVES
+#define DAMC_CH_WAVES 4
+#endif
+constexpr int CH_WAVES = DAMC_CH_WAVES;  // waves per chain workgroup, splitting K
+constexpr int CH_THREADS = 64 * CH_WAVES;
 constexpr int TM = 16;           // rows per workgroup
 constexpr int TC = 8;            // output columns per workgroup (x 2 products)
-constexpr int KG = 64;           // K padding granule: 4 waves x one 16-deep k-group
+constexpr int KG = 16 * CH_WAVES;  // K padding granule: one 16-deep k-group per wave
 constexpr int CH_CHUNK = 8;      // k-groups whose loads a lane keeps in flight at once
 constexpr int EMB_G = 8;         // in0: 16-deep k-groups of z (nz <= 128)
 
@@ -68,6 +72,8 @@ struct ChainArgs {
   float c0, c1, c2, c3, c4;
   float* zt;          // == z
   const SweepCall* call;
+  uint64_t* trace;  // tools only (DAMC_CHAIN_TRACE): [launch][512][2] 100 MHz stamps {block start, block end}
+  int li;           // launch index in the sweep (trace row)
   int dbg;  // timing experiments only (DAMC_CHAIN_DBG, wrong results): 1 no x loads, 2 no weight loads, 4 no MFMA,
             // 8 no epilogue prefetch, 16 no output stores; in0: 32 no sin/cos, 64 no B loads, 128 no zB MFMA
 };
@@ -79,8 +85,10 @@ __host__ __device__ inline int emb_ld(int kp) { return kp + 8; }  // in0 LDS ima
 // the six other blocks' kernels carry no scratch segment
 template <bool EMB>
 __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[4][TM][16];
+  __shared__ __attribute__((aligned(16))) float red[CH_WAVES][TM][16];
   extern __shared__ __attribute__((aligned(16))) float embs[];  // in0: [TM][emb_ld(kp)]
+  if (a.trace && threadIdx.x == 0) { a.trace[((long)a.li * 512 + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime(); a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 2] = __builtin_amdgcn_s_memtime(); }
+  if (a.trace && (threadIdx.x == 64 || threadIdx.x == 192)) a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 6 + (threadIdx.x >> 7)] = __builtin_amdgcn_s_memtime();
   if (a.dbg & 512) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (a.dout + TC - 1) / TC;
@@ -101,17 +109,34 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
     bs = a.bls[tn * 16 + 8 + ec];
     if (a.final_) {
       zv = a.zt[(long)erow * a.nz + ecol];
-      if (!a.last && call->with_noise) {
-        if (call->noise) {
-          xi = call->noise[((long)a.noisy_k * a.B + erow) * a.nz + ecol];
+      // every per-call field in one round trip (not three dependent ones)
+      const int with_noise = call->with_noise;
+      const float* noise = call->noise;
+      const uint64_t seed = call->seed, chain_base = call->chain_base, step_offset = call->step_offset;
+      if (!a.last && with_noise) {
+        if (noise) {
+          xi = noise[((long)a.noisy_k * a.B + erow) * a.nz + ecol];
         } else {
           float n4[4];
-          philox_normal4(call->seed, call->chain_base + erow, call->step_offset + a.noisy_k, (uint32_t)(ecol >> 2),
+          philox_normal4(seed, chain_base + erow, step_offset + a.noisy_k, (uint32_t)(ecol >> 2),
                          DAMC_STREAM_SWEEP, n4);
           xi = pick4(n4, ecol);
         }
       }
     }
+  }
+
+  // ---- this wave's K range and, for in0, its first weight chunk now: the embedding below is a dependent
+  // load -> MFMA -> sin/cos phase, so the weights' memory round trip overlaps it instead of following it
+  const int kq = a.kp / CH_WAVES;
+  const int ng = kq >> 4;
+  const int kbase = wave * kq;
+  const float* wrow = a.w + ((long)tn * 16 + m) * a.kp + kbase + 4 * q;
+  f32x4 wpre[CH_CHUNK];
+  if (EMB) {
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c)
+      wpre[c] = (c < ng && !(a.dbg & 2)) ? *reinterpret_cast<const f32x4*>(wrow + 16 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
   // ---- in0: the Fourier input embedding of the 16 rows into LDS (zB on MFMA, wave w -> 16-column tiles w, w+4..)
@@ -127,7 +152,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       const int k = 16 * g + 4 * q;
       zv4[g] = (rok && k < nz) ? *reinterpret_cast<const f32x4*>(a.z + (long)row * nz + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int t = wave; t * 16 < half; t += 4) {
+    for (int t = wave; t * 16 < half; t += CH_WAVES) {
       const int col = t * 16 + m;
       const bool cok = col < half;
       f32x4 bv[EMB_G];  // a.bmat is B^T (half, nz): lane (m, q) reads B[16 g + 4 q + s][col] as one f32x4
@@ -176,12 +201,8 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   }
 
   // ---- main loop: wave w covers k in [w kq, (w+1) kq) of the padded K
-  const int kq = a.kp >> 2;
-  const int ng = kq >> 4;
-  const int kbase = wave * kq;
   const int xrow = r0 + m;
   const bool xok = xrow < a.B;
-  const float* wrow = a.w + ((long)tn * 16 + m) * a.kp + kbase + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int g0 = 0; g0 < ng; g0 += CH_CHUNK) {
     f32x4 xa[CH_CHUNK], wb[CH_CHUNK];
@@ -191,7 +212,8 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       const int k = kbase + 16 * g + 4 * q;
       f32x4 wv = {0.f, 0.f, 0.f, 0.f}, xv = {0.f, 0.f, 0.f, 0.f};
       if (g < ng) {
-        if (!(a.dbg & 2)) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * g);
+        if (EMB && g0 == 0) wv = wpre[c];
+        else if (!(a.dbg & 2)) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * g);
         if (EMB) {
           xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
         } else if (xok && k < a.din && !(a.dbg & 1)) {
@@ -201,6 +223,10 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       }
       wb[c] = wv;
       xa[c] = xv;
+    }
+    if ((a.dbg & 1024) && g0 == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (a.trace && tid == 0) a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 3] = __builtin_amdgcn_s_memtime();
     }
 #pragma unroll
     for (int c = 0; c < CH_CHUNK; ++c) {
@@ -225,11 +251,12 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
   __syncthreads();
+  if (a.trace && tid == 0) a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 4] = __builtin_amdgcn_s_memtime();
 
   if (!eok) return;
   float l = 0.f, sk = 0.f;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {  // fixed order: deterministic
+  for (int w = 0; w < CH_WAVES; ++w) {  // fixed order: deterministic
     l += red[w][er][ec];
     sk += red[w][er][8 + ec];
   }
@@ -237,6 +264,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   const float o = ((l + bl) * gate + hb) + (sk + bs);
   if (!a.final_) {
     if (!(a.dbg & 16)) a.out[(long)erow * a.dout + ecol] = o;
+    if (a.trace && tid == 0) { a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 1] = __builtin_amdgcn_s_memrealtime(); a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 5] = __builtin_amdgcn_s_memtime(); }
     return;
   }
   // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
@@ -252,6 +280,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
     if (call->with_noise) zn = add_rn(zn, mul_rn(a.c4, xi));
   }
   a.zt[zi] = zn;
+  if (a.trace && tid == 0) { a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 1] = __builtin_amdgcn_s_memrealtime(); a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 5] = __builtin_amdgcn_s_memtime(); }
 }
 
 // ------------------------------------------------------------------------------ persistent chain (one launch)
@@ -533,6 +562,89 @@ __global__ __launch_bounds__(PS_THREADS) void sweep_persistent_kernel(PsArgs a) 
   }
 }
 
+// ------------------------------------------------------------------------------ skinny GEMMs of the precompute
+// Y[m][n] = act(sum_k f(A[m][k]) W[n][k] + bias[n]) for the sweep's short-M products (the time MLP and qt over
+// n steps, px over B rows): the chain kernel's tile (16 rows x 16 columns, K split over 4 waves, every lane's
+// f32x4 loads of a chunk in flight together) so a product of a few hundred rows fills the chip with one memory
+// round trip per chunk, where 128 x 128 tiles would give it 9 workgroups walking K serially.  W is read in its
+// PyTorch (out, in) layout; the N columns are up to 7 segments with their own weight rows and bias (the 7
+// blocks' ctx Linears side by side).
+struct SkSeg {
+  const float* w;     // row n - n0 of the segment at w + (n - n0) * ldw
+  const float* bias;  // or null
+  long ldw;
+  int n0;
+};
+struct SkArgs {
+  const float* A;
+  long lda;
+  int M, N, K;
+  SkSeg seg[7];
+  int nseg;
+  int silu_a, silu_y;
+  float* Y;
+  long ldy;
+};
+
+__global__ __launch_bounds__(256) void skinny_gemm_kernel(SkArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[4][16][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int ntn = a.N >> 4;
+  const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
+  const int r0 = tm * 16, n0 = tn * 16;
+  int sg = 0;
+  while (sg + 1 < a.nseg && a.seg[sg + 1].n0 <= n0) ++sg;
+  const SkSeg& S = a.seg[sg];
+  const int kq = ((a.K + 63) >> 6) << 4;  // per-wave K span, whole 16-deep k-groups
+  const int kbase = wave * kq;
+  const int row = r0 + m, col = n0 + m;
+  const bool rok = row < a.M;
+  const float* arow = a.A + (long)row * a.lda;
+  const float* wrow = S.w + (long)(col - S.n0) * S.ldw;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < kq; g0 += 16 * CH_CHUNK) {
+    f32x4 xa[CH_CHUNK], wb[CH_CHUNK];
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      const int k = kbase + g0 + 16 * c + 4 * q;
+      const bool ok = g0 + 16 * c < kq && k < a.K;
+      xa[c] = (ok && rok) ? *reinterpret_cast<const f32x4*>(arow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      wb[c] = ok ? *reinterpret_cast<const f32x4*>(wrow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      f32x4 x = xa[c];
+      if (a.silu_a) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = x[e] / (1.f + expf(-x[e]));
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[e], wb[c][e], acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
+  __syncthreads();
+  const int er = tid >> 4, ec = tid & 15;
+  const int orow = r0 + er, ocol = n0 + ec;
+  if (orow >= a.M) return;
+  float v = ((red[0][er][ec] + red[1][er][ec]) + red[2][er][ec]) + red[3][er][ec];
+  if (S.bias) v += S.bias[ocol - S.n0];
+  if (a.silu_y) v = v / (1.f + expf(-v));
+  a.Y[(long)orow * a.ldy + ocol] = v;
+}
+
+int launch_skinny(const SkArgs& a, const char* prof, hipStream_t s) {
+  if (a.M <= 0 || (a.N & 15) || (a.K & 3) || (a.lda & 3) || a.nseg < 1 || a.nseg > 7) return DAMC_ERR_UNSUPPORTED;
+  for (int i = 0; i < a.nseg; ++i)
+    if ((a.seg[i].ldw & 3) || (a.seg[i].n0 & 15)) return DAMC_ERR_UNSUPPORTED;
+  ProfScope ps(prof, 2.0 * a.M * a.N * a.K, s);
+  const unsigned grid = (unsigned)(((a.M + 15) / 16) * (a.N / 16));
+  hipLaunchKernelGGL(skinny_gemm_kernel, dim3(grid), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------- per-call helpers
 __global__ void silu_kernel(const float* x, long n, float* y) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -716,6 +828,33 @@ struct Launch {
   size_t smem;
 };
 
+// tools only: DAMC_CHAIN_TRACE=<file> gives every chain launch a stamp row; chain_trace_dump writes them after the
+// sweep (host sync) as {launches, then [launch][512][2] stamps}
+uint64_t* g_trace = nullptr;
+long g_trace_rows = 0;
+uint64_t* chain_trace_buffer(long rows) {
+  static const bool on = getenv("DAMC_CHAIN_TRACE") != nullptr;
+  if (!on || rows > 4096) return nullptr;
+  if (!g_trace) {
+    if (hipMalloc(&g_trace, 4096L * 512 * 8 * sizeof(uint64_t)) != hipSuccess) g_trace = nullptr;
+  }
+  g_trace_rows = rows;
+  return g_trace;
+}
+void chain_trace_dump(hipStream_t s) {
+  if (!g_trace) return;
+  std::vector<uint64_t> h((size_t)g_trace_rows * 512 * 8);
+  if (hipStreamSynchronize(s) != hipSuccess) return;
+  if (hipMemcpy(h.data(), g_trace, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return;
+  if (FILE* f = fopen(getenv("DAMC_CHAIN_TRACE"), "wb")) {
+    const long rows = g_trace_rows;
+    fwrite(&rows, sizeof(rows), 1, f);
+    fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+    fclose(f);
+  }
+  (void)hipMemsetAsync(g_trace, 0, h.size() * sizeof(uint64_t), s);
+}
+
 // the chain launches of one sweep (n steps from step index k0), in order
 void chain_launches(const damc_denoiser_t* d, const SweepWs& w, int B, int n, const float* coef,
                     std::vector<Launch>& out) {
@@ -736,6 +875,7 @@ void chain_launches(const damc_denoiser_t* d, const SweepWs& w, int B, int n, co
     const char* e = getenv("DAMC_CHAIN_DBG");
     return e ? atoi(e) : 0;
   }();
+  uint64_t* trace = chain_trace_buffer(7L * n);
   int noisy_k = 0;
   for (int k = 0; k < n; ++k) {
     const float* c = coef + 6 * (size_t)k;
@@ -766,6 +906,8 @@ void chain_launches(const damc_denoiser_t* d, const SweepWs& w, int B, int n, co
       a.zt = w.z;
       a.call = w.call;
       a.dbg = dbg;
+      a.trace = trace;
+      a.li = 7 * k + j;
       if (a.final_) {
         a.residual = d->residual;
         a.last = last;
@@ -1034,10 +1176,15 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     pa.wctx_t = w.wctx_t;
     pa.wctx_x = w.wctx_x;
     pa.bctx = w.bctx;
-    hipLaunchKernelGGL(pack_denoiser_kernel, dim3((unsigned)((maxn + 255) / 256), 7, 3), dim3(256), 0, s, pa);
+    // the skinny precompute GEMMs read the time MLP and ctx Linears in their PyTorch layouts: no transposes
+    bool sk = (nt & 15) == 0 && (nx & 3) == 0;
+    for (int j = 0; j < 7; ++j) sk = sk && (d->blocks[j].dout & 15) == 0;
+    hipLaunchKernelGGL(pack_denoiser_kernel, dim3((unsigned)((maxn + 255) / 256), 7, sk ? 2 : 3), dim3(256), 0, s, pa);
     const long ntt = (long)nt * nt;
-    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw1, nt, nt, w.tw1t);
-    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw2, nt, nt, w.tw2t);
+    if (!sk) {
+      hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw1, nt, nt, w.tw1t);
+      hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntt + 255) / 256)), dim3(256), 0, s, d->tw2, nt, nt, w.tw2t);
+    }
     const long nb = (long)d->nz * (d->nz / 2);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, d->bmat, d->nz, d->nz / 2,
                        w.bmat);
@@ -1045,7 +1192,46 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   }
 
   // ---- 2. ctx: time MLP (n rows), xemb part (B rows), c for every (step, row)
-  {
+  bool skinny = (nt & 15) == 0 && (nx & 3) == 0;
+  for (int j = 0; j < 7; ++j) skinny = skinny && (d->blocks[j].dout & 15) == 0;
+  if (skinny) {
+    SkArgs g;
+    memset(&g, 0, sizeof(g));
+    g.M = n;
+    g.N = nt;
+    g.K = nt;
+    g.A = temb_in;
+    g.lda = nt;
+    g.nseg = 1;
+    g.seg[0] = SkSeg{d->tw1, d->tb1, nt, 0};
+    g.silu_y = 1;
+    g.Y = w.t1;
+    g.ldy = nt;
+    if ((rc = launch_skinny(g, "sweep_pre", s))) return rc;
+    g.A = w.t1;
+    g.seg[0] = SkSeg{d->tw2, d->tb2, nt, 0};
+    g.Y = w.t2;  // the ctx Linear consumes SiLU(temb)
+    if ((rc = launch_skinny(g, "sweep_pre", s))) return rc;
+    g.A = w.t2;
+    g.N = S;
+    g.nseg = 7;
+    for (int j = 0; j < 7; ++j) g.seg[j] = SkSeg{d->wctx[j], d->bctx[j], (long)nt + nx, coloff[j]};
+    g.silu_y = 0;
+    g.Y = w.qt;
+    g.ldy = S;
+    if ((rc = launch_skinny(g, "sweep_pre", s))) return rc;
+    g.A = xemb;
+    g.lda = nx;
+    g.M = B;
+    g.K = nx;
+    for (int j = 0; j < 7; ++j) g.seg[j] = SkSeg{d->wctx[j] + nt, nullptr, (long)nt + nx, coloff[j]};
+    g.silu_a = 1;
+    g.Y = w.px;
+    if ((rc = launch_skinny(g, "sweep_pre", s))) return rc;
+    const long tot = (long)n * B * S;
+    hipLaunchKernelGGL(ctx_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, w.px, w.qt, B, S, tot, w.cx);
+    DAMC_LAUNCH_CHECK();
+  } else {
     damc::GemmArgs g;
     g.M = n;
     g.N = nt;
@@ -1144,6 +1330,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
       if ((rc = run_chain_persistent(d, w, B, n, coef, s))) return rc;
     } else if (allow_graph && graphs_enabled()) {
       if ((rc = run_chain_graph(d, w, wsp, wsb, B, n, coef, s))) return rc;
+      chain_trace_dump(s);
     } else {
       std::vector<Launch> ls;
       chain_launches(d, w, B, n, coef, ls);
