@@ -8,6 +8,8 @@
 // FC layers are tiny-M GEMMs bound by latency, not FLOPs: each layer splits its K axis over the
 // 1024-thread workgroup (float4 weight columns x strided k-groups, all loads of a thread in flight
 // at once) and adds the k-group partials in a fixed order in LDS.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -581,6 +583,157 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
   if (MODE != EB_GRAD && tid < nz) a.z[(long)chain * nz + tid] = zs[tid];
 }
 
+// ------------------------------------------------------------------ MFMA prior chain for large batches
+// 16 chains per workgroup as one 16-row tile: every FC layer of _netE (and of its backward) is a real GEMM
+// [16 x K] . [K x N] on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).  The activations live in
+// LDS; the weights stream from L2 in PyTorch / packed-transpose layouts, each lane reading f32x4 runs through the
+// k-permutation of the MFMA steps (step s of k-group g reads k = 16 g + 4 (lane >> 4) + s on both operands).
+// Output tiles of 16 columns go round-robin to the 8 waves.  Per step: a1 = z W1^T, a2 = h1 W2^T, g1 = (g2 W2) *
+// lrelu'(a1), gz = g1 W1 (2,116 MFMAs per 16 chains at nz = 128, nh = 200).  The fp32 MFMA issues at the fp32 VALU
+// rate (MI355X_MICROARCH.md), so this pays only by batching: at B chains it runs ceil(B / 16) workgroups where the
+// register-resident VALU kernel runs B (one per CU at a time); damc_prior_langevin takes it from
+// DAMC_EBM_MFMA_MIN_B chains up (bench: tools/ebm_profile.py).
+constexpr int EM_THREADS = 512, EM_WAVES = 8, EM_ROWS = 16;
+constexpr int EM_MAXW = 256;         // nz, nh <= 256
+constexpr int EM_LD = EM_MAXW + 4;   // LDS row stride (floats)
+bool ebm_mfma_ok(int nz, int nh) { return nz > 0 && nh > 0 && nz <= EM_MAXW && nh <= EM_MAXW && (nz & 15) == 0; }
+
+// acc[r] (row 4 (lane >> 4) + r, column n0 + (lane & 15)) of x[16][K] . W^T, W row n at w + n * ldw (k contiguous,
+// rows >= N and k >= K read as zero); x rows in LDS with stride EM_LD, zero-padded to a multiple of 16
+__device__ __forceinline__ f32x4 em_tile(const float* xs, const float* __restrict__ w, long ldw, int n0, int N, int K) {
+  const int lane = threadIdx.x & 63, m = lane & 15, q = lane >> 4;
+  const int n = n0 + m;
+  const float* wr = w + (long)n * ldw;
+  const int ng = (K + 15) >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < ng; g0 += 8) {
+    f32x4 wv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int k = 16 * (g0 + c) + 4 * q;
+      wv[c] = (g0 + c < ng && n < N && k < K) ? *reinterpret_cast<const f32x4*>(wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (g0 + c < ng) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(xs + m * EM_LD + 16 * (g0 + c) + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[e], wv[c][e], acc, 0, 0, 0);
+      }
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(EM_THREADS) void prior_chain_mfma_kernel(EbArgs a) {
+  const damc_ebm_t& e = a.e;
+  const int nz = e.nz, nh = e.nh;
+  const float sl = e.slope;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int r0 = blockIdx.x * EM_ROWS;
+  __shared__ __attribute__((aligned(16))) float zs[EM_ROWS * EM_LD];
+  __shared__ __attribute__((aligned(16))) float h1[EM_ROWS * EM_LD];  // lrelu(a1), then g1
+  __shared__ __attribute__((aligned(16))) float a1s[EM_ROWS * EM_LD];
+  __shared__ __attribute__((aligned(16))) float g2[EM_ROWS * EM_LD];
+  __shared__ float red[2][EM_WAVES];
+  const int kz = (nz + 15) & ~15, kh = (nh + 15) & ~15;
+  // z of the 16 chains -> LDS, zero padding of the K tails (never written again)
+  for (int i = tid; i < EM_ROWS * EM_LD; i += EM_THREADS) {
+    const int r = i / EM_LD, c = i - r * EM_LD;
+    zs[i] = (r0 + r < a.B && c < nz) ? a.z[(long)(r0 + r) * nz + c] : 0.f;
+    h1[i] = 0.f;
+    g2[i] = 0.f;
+  }
+  __syncthreads();
+  const bool want_e = a.diag != nullptr;
+  for (int it = 0; it < a.n_steps; ++it) {
+    // ---- a1 = z W1^T + b1 -> h1 = lrelu(a1) (and a1 for the backward mask)
+    for (int t = wave; 16 * t < kh; t += EM_WAVES) {
+      const f32x4 acc = em_tile(zs, e.w1, nz, 16 * t, nh, nz);
+      const int n = 16 * t + m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = n < nh ? acc[r] + e.b1[n] : 0.f;
+        a1s[(4 * q + r) * EM_LD + n] = v;
+        h1[(4 * q + r) * EM_LD + n] = v > 0.f ? v : v * sl;
+      }
+    }
+    __syncthreads();
+    // ---- a2 = h1 W2^T + b2 -> g2 = w3 lrelu'(a2); energy terms w3 lrelu(a2)
+    float en = 0.f;
+    for (int t = wave; 16 * t < kh; t += EM_WAVES) {
+      const f32x4 acc = em_tile(h1, e.w2, nh, 16 * t, nh, nh);
+      const int n = 16 * t + m;
+      const float w3 = n < nh ? e.w3[n] : 0.f;
+      const float b2 = n < nh ? e.b2[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[r] + b2;
+        g2[(4 * q + r) * EM_LD + n] = n < nh ? (v > 0.f ? w3 : w3 * sl) : 0.f;
+        if (want_e && n < nh && r0 + 4 * q + r < a.B) en += w3 * (v > 0.f ? v : v * sl);
+      }
+    }
+    __syncthreads();
+    // ---- g1 = (g2 W2) * lrelu'(a1): reduction over layer-2 rows, B operand w2t[k][n] = W2[n][k]
+    for (int t = wave; 16 * t < kh; t += EM_WAVES) {
+      const f32x4 acc = em_tile(g2, e.w2t, nh, 16 * t, nh, nh);
+      const int k = 16 * t + m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a1 = a1s[(4 * q + r) * EM_LD + k];
+        h1[(4 * q + r) * EM_LD + k] = k < nh ? acc[r] * (a1 > 0.f ? 1.f : sl) : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- gz = g1 W1 (B operand w1t[c][n] = W1[n][c]); g = gz + z; z <- z - c1 g (+ step xi)
+    float zsq = 0.f;
+    for (int t = wave; 16 * t < kz; t += EM_WAVES) {
+      const f32x4 acc = em_tile(h1, e.w1t, nh, 16 * t, nz, nh);
+      const int c = 16 * t + m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 4 * q + r;
+        if (row < a.B && c < nz) {
+          const float zv = zs[(4 * q + r) * EM_LD + c];
+          const float g = acc[r] + zv;
+          zsq += zv * zv;
+          float zn = sub_rn(zv, mul_rn(a.c1, g));
+          if (a.with_noise) {
+            const float xi = noise_at(a.noise, ((long)it * a.B + row) * nz + c, 1, a.seed, a.chain_base + row,
+                                      a.step_offset + it, c, DAMC_STREAM_PRIOR);
+            zn = add_rn(zn, mul_rn(a.step, xi));
+          }
+          zs[(4 * q + r) * EM_LD + c] = zn;
+        }
+      }
+    }
+    if (want_e) {  // uniform branch: per-workgroup sums of E and |z|^2 / 2, added to the step's diagnostics
+      en = wave_sum(en);
+      zsq = wave_sum(zsq);
+      if (lane == 0) {
+        red[0][wave] = en;
+        red[1][wave] = zsq;
+      }
+    }
+    __syncthreads();
+    if (want_e && tid == 0) {
+      float et = 0.f, zt = 0.f;
+      for (int w = 0; w < EM_WAVES; ++w) {
+        et += red[0][w];
+        zt += red[1][w];
+      }
+      const int rows = min(EM_ROWS, a.B - r0);
+      atomicAdd(&a.diag[2 * it + 0], et + rows * e.b3[0]);
+      atomicAdd(&a.diag[2 * it + 1], 0.5f * zt);
+    }
+  }
+  for (int i = tid; i < EM_ROWS * nz; i += EM_THREADS) {
+    const int r = i / nz, c = i - r * nz;
+    if (r0 + r < a.B) a.z[(long)(r0 + r) * nz + c] = zs[r * EM_LD + c];
+  }
+}
+
 // rows per workgroup: per step a workgroup streams all four weight panels (~0.5 MB, L2-resident) once,
 // so few rows per workgroup = more workgroups in flight = lower latency for these tiny batches
 constexpr int RP = 2;  // prior chain
@@ -635,15 +788,39 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
 
 extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* stream);
 
-extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_steps, double step, int with_noise,
-                                   const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
-                                   float* diag, void* stream) {
+// engine: 0 = by batch size (MFMA from DAMC_EBM_MFMA_MIN_B chains up), 1 = register-resident VALU, 2 = MFMA
+static int prior_langevin_impl(const damc_ebm_t* e, float* z, int B, int n_steps, double step, int with_noise,
+                               const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                               float* diag, void* stream, int engine) {
   if (!e || !z || B <= 0 || n_steps < 0) return DAMC_ERR_ARG;
   if (!e->w1t || !e->w2t) return DAMC_ERR_ARG;
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
   if (n_steps == 0) return 0;
   const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
+  static const int mfma_min_b = [] {
+    const char* v = getenv("DAMC_EBM_MFMA_MIN_B");
+    return v ? atoi(v) : 2048;
+  }();
+  if (engine == 2 && !ebm_mfma_ok(e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
+  if (ebm_mfma_ok(e->nz, e->nh) && (engine == 2 || (engine == 0 && B >= mfma_min_b))) {
+    EbArgs a{};
+    a.e = *e;
+    a.z = z;
+    a.B = B;
+    a.n_steps = n_steps;
+    a.c1 = c1;
+    a.step = (float)step;
+    a.with_noise = with_noise;
+    a.noise = noise;
+    a.seed = seed;
+    a.step_offset = step_offset;
+    a.chain_base = chain_base;
+    a.diag = diag;
+    ProfScope ps("prior_chain_mfma", 4.0 * (double)B * n_steps * ((double)e->nz * e->nh + (double)e->nh * e->nh), s);
+    hipLaunchKernelGGL(prior_chain_mfma_kernel, dim3((B + EM_ROWS - 1) / EM_ROWS), dim3(EM_THREADS), 0, s, a);
+    return (int)hipGetLastError();
+  }
   if (ebm_reg_ok(e->nz, e->nh)) {
     EbArgs a{};
     a.e = *e;
@@ -668,6 +845,20 @@ extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_s
   hipLaunchKernelGGL((prior_chain_kernel<RP>), dim3((B + RP - 1) / RP), dim3(EBM_THREADS), sm, s, *e, z, B, n_steps, c1, (float)step,
                      with_noise, noise, seed, step_offset, chain_base, diag);
   return (int)hipGetLastError();
+}
+
+extern "C" int damc_prior_langevin(const damc_ebm_t* e, float* z, int B, int n_steps, double step, int with_noise,
+                                   const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                                   float* diag, void* stream) {
+  return prior_langevin_impl(e, z, B, n_steps, step, with_noise, noise, seed, step_offset, chain_base, diag, stream, 0);
+}
+
+extern "C" int damc_prior_langevin_engine(const damc_ebm_t* e, float* z, int B, int n_steps, double step,
+                                          int with_noise, const float* noise, uint64_t seed, uint64_t step_offset,
+                                          uint64_t chain_base, float* diag, int engine, void* stream) {
+  if (engine < 0 || engine > 2) return DAMC_ERR_ARG;
+  return prior_langevin_impl(e, z, B, n_steps, step, with_noise, noise, seed, step_offset, chain_base, diag, stream,
+                             engine);
 }
 
 extern "C" int damc_ebm_energy_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad,

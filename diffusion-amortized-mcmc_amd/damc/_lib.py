@@ -136,6 +136,7 @@ _SIGS = {
     "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
                                           _P, _P, _SZ, _P]),
     "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _P]),
+    "damc_prior_langevin_engine": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _I, _P]),
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_z_update": (_I, [_P, _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P]),
     "damc_philox_normal": (_I, [_P, _I, _I, _I, _U64, _U64, _U64, ctypes.c_uint32, _P]),

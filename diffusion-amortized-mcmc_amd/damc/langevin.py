@@ -88,11 +88,16 @@ def generator_forward(z, netG):
     return out
 
 
+PRIOR_ENGINES = {"auto": 0, "valu": 1, "mfma": 2}
+
+
 def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, step_offset=0, chain_base=0,
-                   diag=False):
+                   diag=False, engine="auto"):
     """In-place n-step prior Langevin (workspace/src/MCMC.py:27-46), one persistent launch.
 
-    Returns a (n_steps, 2) diagnostics tensor {sum E, |z|^2/2} if diag else None.
+    engine: "auto" (the library's choice by batch size), "valu" (one chain per workgroup, weights in registers)
+    or "mfma" (16-chain tiles on the fp32 MFMA).  Returns a (n_steps, 2) diagnostics tensor {sum E, |z|^2/2} if
+    diag else None.
     """
     _f32c(z, "z")
     dev = z.device
@@ -108,9 +113,12 @@ def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, st
     if seed is None:
         seed = new_seed() if (with_noise and noise is None) else 0
     dg = torch.zeros(max(n_steps, 1), 2, dtype=torch.float32, device=dev) if diag else None
-    check(_lib.lib().damc_prior_langevin(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
-                                         int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base, ptr(dg),
-                                         _lib.stream_ptr(dev)), "damc_prior_langevin")
+    if engine not in PRIOR_ENGINES:
+        raise ValueError("engine must be one of %s" % sorted(PRIOR_ENGINES))
+    check(_lib.lib().damc_prior_langevin_engine(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
+                                                int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base,
+                                                ptr(dg), PRIOR_ENGINES[engine], _lib.stream_ptr(dev)),
+          "damc_prior_langevin")
     return dg
 
 

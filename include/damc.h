@@ -161,6 +161,12 @@ int damc_generator_train_backward(const damc_generator_t* g, const float* z, con
 int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps, double step, int with_noise,
                         const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
                         float* diag, void* stream);
+/* the same with the engine chosen per call: 0 = by batch size (the default above: the 16-chain MFMA tile kernel
+ * from DAMC_EBM_MFMA_MIN_B = 2048 chains up, where the FC layers are real GEMMs), 1 = register-resident VALU
+ * (one chain per workgroup), 2 = MFMA (nz % 16 == 0, nz and nh <= 256, else DAMC_ERR_UNSUPPORTED) */
+int damc_prior_langevin_engine(const damc_ebm_t* ebm, float* z, int batch, int n_steps, double step, int with_noise,
+                               const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
+                               float* diag, int engine, void* stream);
 /* per-op hook: energy (B) and grad_z sum E (B,nz) */
 int damc_ebm_energy_grad(const damc_ebm_t* ebm, const float* z, int batch, float* energy, float* grad,
                          void* stream);

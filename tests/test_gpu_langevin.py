@@ -58,15 +58,42 @@ def test_posterior_langevin_matches_reference(lv, gpu_device, name):
     assert rel_l2(z.cpu().numpy(), rec["post_z30"]) < 2e-3
 
 
+@pytest.mark.parametrize("engine", ["auto", "valu", "mfma"])
 @pytest.mark.parametrize("name", ["cifar10_w16", "svhn_w16", "mnist_w16", "cifar10_full"])
-def test_prior_langevin_matches_reference(lv, gpu_device, name):
+def test_prior_langevin_matches_reference(lv, gpu_device, name, engine):
     c = build_g_case(name, gpu_device)
+    if engine == "mfma" and c["zp0"].shape[1] % 16:
+        pytest.skip("the MFMA prior engine needs nz % 16 == 0")
     z = c["zp0"].clone()
-    lv.prior_langevin(z, c["E"], 5, c["meta"]["prior_step"], False)
+    lv.prior_langevin(z, c["E"], 5, c["meta"]["prior_step"], False, engine=engine)
     assert rel_l2(z.cpu().numpy(), c["rec"]["prior_z5"]) < 1e-6
     z = c["zp0"].clone()
-    lv.prior_langevin(z, c["E"], 60, c["meta"]["prior_step"], True, noise=c["prior_noise"])
+    lv.prior_langevin(z, c["E"], 60, c["meta"]["prior_step"], True, noise=c["prior_noise"], engine=engine)
     assert rel_l2(z.cpu().numpy(), c["rec"]["prior_z60"]) < 1e-4
+
+
+def test_prior_mfma_engine_large_batch(lv, gpu_device):
+    """B = 2048 chains (past the MFMA engine's batch threshold): the 16-chain MFMA tiles against the fp64
+    oracle (5 no-noise steps; a 2,048-row tail tile of 16 is exact), against the VALU engine (20 Philox steps:
+    the same noise stream, so only summation order differs) and their step diagnostics."""
+    from damc import synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
+    z0 = torch.from_numpy(synth.normal_f32(41, 0, (2050, 128))).to(gpu_device)  # 2050: a partial last tile
+    ref = orc.prior_langevin(orc.ebm_params(E, torch.float64), z0.cpu().double(), 5, 0.4)
+    z = z0.clone()
+    lv.prior_langevin(z, E, 5, 0.4, False, engine="mfma")
+    assert rel_l2(z.cpu().numpy(), ref.numpy()) < 1e-6
+    za, zb = z0.clone(), z0.clone()
+    da = lv.prior_langevin(za, E, 20, 0.4, True, seed=9, diag=True, engine="mfma")
+    db = lv.prior_langevin(zb, E, 20, 0.4, True, seed=9, diag=True, engine="valu")
+    assert rel_l2(za.cpu().numpy(), zb.cpu().numpy()) < 1e-5
+    assert rel_l2(da.cpu().numpy(), db.cpu().numpy()) < 1e-5
+    zc = z0.clone()
+    lv.prior_langevin(zc, E, 20, 0.4, True, seed=9, engine="auto")  # 2050 >= the default threshold: MFMA
+    assert torch.equal(zc, za)
 
 
 def test_toy_posterior_matches_reference(lv, gpu_device):

@@ -13,14 +13,16 @@ from damc import langevin as lv  # noqa: E402
 
 dev = torch.device("cuda:0")
 G, E = bench.build(dev)
-for nchains in (256, 128, 512):
+for nchains in (256, 128, 512, 1024, 2048, 4096, 16384):
     z = torch.randn(nchains, 128, device=dev)
+    res = []
+    for engine in ("valu", "mfma"):
+        def prior():
+            lv.prior_langevin(z, E, 60, 0.4, True, seed=3, engine=engine)
 
-    def prior():
-        lv.prior_langevin(z, E, 60, 0.4, True, seed=3)
-
-    ms = bench.event_ms(prior, reps=7)
-    print("prior chain: %d chains x 60 steps: %.3f ms = %.2f us/step" % (nchains, ms, 1e3 * ms / 60))
+        ms = bench.event_ms(prior, reps=5)
+        res.append("%s %.3f ms = %.2f us/step" % (engine, ms, 1e3 * ms / 60))
+    print("prior chain: %5d chains x 60 steps: %s" % (nchains, "  |  ".join(res)))
 x = torch.rand(128, 3, 32, 32, device=dev) * 2 - 1
 z = torch.randn(128, 128, device=dev)
 from damc import _lib  # noqa: E402

@@ -1,7 +1,6 @@
+# EBM: prior-chain parity (both engines) and the engine timing sweep over batch sizes
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_langevin.py tests/test_gpu_ops.py tests/test_gpu_checkpoint.py -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_ebm.log 2>&1
-rc=$?
-tail -4 gpurun_out/gpu_tests_ebm.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python tools/ebm_profile.py > gpurun_out/ebm_profile.txt 2>&1; cat gpurun_out/ebm_profile.txt
-bash tools/chain_dbg.sh > gpurun_out/chain_dbg.txt 2>&1; cat gpurun_out/chain_dbg.txt
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_langevin.py -x -q -k "prior" --timeout 120 --timeout-method thread > gpurun_out/ebm_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/ebm_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 tools/ebm_profile.py
