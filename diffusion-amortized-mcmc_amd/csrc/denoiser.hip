@@ -562,6 +562,373 @@ __global__ __launch_bounds__(PS_THREADS) void sweep_persistent_kernel(PsArgs a) 
   }
 }
 
+// ------------------------------------------------------------------------------ team sweep (one launch, default)
+// The whole dependent chain of a sweep as ONE launch of P = 8 T workgroups, one per CU, with every chain weight
+// resident in LDS for the whole sweep.  Rows never mix, so the chain splits into independent row tiles; workgroup
+// b belongs to team b % 8 (the dispatcher deals blocks round-robin over the 8 XCDs, so a team shares one XCD and
+// one L2: speed only, never correctness) as slot b / 8, and team x owns row tiles x, x + 8, ...  Block j's
+// column tile tn belongs to slot (tn + toff_j) mod T for every step, so its 16 packed weight rows (8 Wl + 8 Ws)
+// are copied into that workgroup's LDS once, in MFMA fragment order (one ds_read_b128 per lane and k-group, no
+// bank conflicts).  toff_j staggers the blocks' first tiles so the LDS load is even across slots (106.5 KB per
+// workgroup at the CIFAR defaults, nf 4).
+// Per stage (block j of step k, s = 7 k + j) a workgroup waits until every slot of its team has published stage
+// s - 1, reads its row tile's block input, runs 16 x 16 v_mfma_f32_16x16x4_f32 tiles over K split in quarters by
+// its 4 waves, and publishes its 16 x 8 outputs.  A block whose input is cat(prev, skip) takes the skip half
+// (complete stages earlier) and its MFMAs BEFORE the wait, and only the prev half after it.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): every handed-off value
+// is stored sc1 and every storing wave drains vmcnt before the workgroup barrier, then ONE lane stores the
+// slot's flag (= stages done) sc1; a consumer's wave 0 polls its team's T flags with sc1 loads, the other waves
+// join it at a barrier, and every load of handed-off bytes is an sc1 load.  Outputs and z go to per-step ring
+// slots, so no address is ever rewritten within a sweep.  Every wait is bounded: past the budget (or once any
+// workgroup has failed) the workgroup records the failure in the error word and leaves, so the grid drains, and
+// the copy-out writes NaN into zt.
+constexpr int TS_THREADS = 320;  // waves 0-3 compute (K in quarters), wave 4 polls and publishes
+constexpr int TS_MAXT = 64;     // slots per team (CUs per XCD)
+
+struct TsBlock {
+  const float* w;    // packed [ntn][16][kp] (workspace)
+  const float* bls;  // [ntn][16]
+  int kp, dout, ntn;
+  int wa, wb;        // widths of the input halves (in0: wa = din, the embedding; wb = 0: no skip half)
+  int kpa, kpb;      // their K paddings (multiples of 64)
+  int srcA, srcB;    // producing blocks of the halves (-1: none)
+  long ooff;         // output (B, dout) within a step's ring slot, floats
+  int ghoff;         // 2 * coloff: gate columns in a gh row
+  int toff;          // column tile tn -> slot (tn + toff) % T
+};
+
+struct TsArgs {
+  TsBlock b[7];
+  const float* bmat;  // B^T (nz/2, nz)
+  int nz, B, G, n, residual, T;
+  const float* gh;    // (n, B, 2S)
+  long ldgh;
+  float* ring;        // (n, B*S): block outputs of step k at ring + k * ring_step
+  long ring_step;
+  float* zring;       // (n+1, B, nz): z before step k at zring + k * B * nz
+  const float* tab;   // (n, 8): c0..c4, is_last, noisy_k
+  const SweepCall* call;
+  unsigned* flags;    // [8][TS_MAXT]: stages published by (team, slot)
+  int* err;
+  long budget;        // wait budget in 100 MHz ticks
+  int wlds;           // weight LDS floats per workgroup (host maximum over slots)
+  uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin, wait end, reduced,
+                      // published}
+  int dbg;            // timing experiments only (DAMC_SWEEP_DBG, wrong results): 1 no drain before the flag,
+                      // 2 no payload loads, 4 no MFMA, 8 no epilogue operand loads, 16 no output stores
+};
+
+// number of column tiles of block b that slot t owns, and the first one
+__device__ __forceinline__ int ts_tiles(const TsBlock& b, int T, int t, int* tn0) {
+  const int f = ((t - b.toff) % T + T) % T;
+  *tn0 = f;
+  return f < b.ntn ? (b.ntn - f + T - 1) / T : 0;
+}
+
+// wave 4 (which issues no other loads, so nothing queues in front of its poll) polls the T flags of the team
+// until all have published `need` stages; every thread returns whether the wait succeeded (a barrier is inside)
+__device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need, int* err, long budget, int* sflag) {
+  if (threadIdx.x >= 256) {
+    const int lane = threadIdx.x - 256;
+    int ok = 1;
+    uint64_t t0 = 0;
+    for (unsigned it = 0;; ++it) {
+      const unsigned v = lane < T ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : need;
+      if (__all(v >= need)) break;
+      if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_sleep(1);
+      if ((it & 63) == 63) {
+        const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e || (long)(__builtin_amdgcn_s_memrealtime() - t0) > budget) {
+          if (!e && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+    }
+    if (lane == 0) *sflag = ok;
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
+// acc += lrelu(x[rows][k0 .. k0 + kps)) . W^T over one input half: wave w takes k in [w kps/4, (w+1) kps/4);
+// x rows come from src (width wsrc, zero past it) with sc1 loads, or from the in0 embedding image in LDS
+template <bool EMB>
+__device__ __forceinline__ void ts_half(f32x4& acc, const float* wl, int kps, const __amdgpu_buffer_rsrc_t& rs,
+                                        long soff, int wsrc, int row, bool rok, const float* embs, int ld, int dbg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int kq = kps >> 2, ng = kq >> 4, kbase = wave * kq;
+  const f32x4* wv = reinterpret_cast<const f32x4*>(wl) + (long)wave * ng * 64 + lane;
+  for (int g0 = 0; g0 < ng; g0 += CH_CHUNK) {
+    f32x4 xa[CH_CHUNK];
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      const int k = kbase + 16 * (g0 + c) + 4 * q;
+      f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+      if (g0 + c < ng) {
+        if (EMB) xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
+        else if (rok && k < wsrc && !(dbg & 2)) xv = ld_sc1(rs, (soff + (long)row * wsrc + k) * 4);
+      }
+      xa[c] = xv;
+    }
+#pragma unroll
+    for (int c = 0; c < CH_CHUNK; ++c) {
+      if (g0 + c >= ng) break;
+      f32x4 x = xa[c];
+      if (!EMB) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.01f * x[e];
+      }
+      const f32x4 w = wv[(g0 + c) * 64];
+      if (dbg & 4) {
+        acc[0] += x[0] * w[0];
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[e], w[e], acc, 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[4][TM][16];
+  __shared__ int sflag;
+  __shared__ int lbase[7];                       // LDS float offset of block j's first owned tile
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [wlds weights][TM][emb_ld(kpa0)] in0 image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int er = tid >> 3, ec = tid & 7;
+  const int T = a.T, team = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nz = a.nz, B = a.B, G = a.G;
+  if (team >= G || slot >= T) return;  // no row tile for this team (its flags are never waited on)
+  const int nrt = (G - team + 7) / 8;  // row tiles of the team: team + 8 i
+  unsigned* const myflag = a.flags + team * TS_MAXT + slot;
+  const unsigned* const teamflags = a.flags + team * TS_MAXT;
+  float* const embs = lds + a.wlds;
+  const int ld0 = emb_ld(a.b[0].kpa);
+
+  // ---- the owned weight tiles into LDS, fragment order: (half, wave, k-group, lane) -> f32x4
+  if (tid == 0) {
+    int off = 0;
+    for (int j = 0; j < 7; ++j) {
+      int tn0;
+      const int c = ts_tiles(a.b[j], T, slot, &tn0);
+      lbase[j] = off;
+      off += c * 16 * (a.b[j].kpa + a.b[j].kpb);
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < 7; ++j) {
+    const TsBlock& b = a.b[j];
+    int tn0;
+    const int c = ts_tiles(b, T, slot, &tn0);
+    for (int i = 0; i < c; ++i) {
+      const int tn = tn0 + i * T;
+      float* dst = lds + lbase[j] + (long)i * 16 * (b.kpa + b.kpb);
+      for (int h = 0; h < 2; ++h) {
+        const int kps = h ? b.kpb : b.kpa, wsrc = h ? b.wb : b.wa, k0 = h ? b.wa : 0;
+        const int ng = kps >> 6;  // k-groups per wave
+        const int units = 4 * ng * 64;
+        f32x4* d4 = reinterpret_cast<f32x4*>(dst + (h ? 16 * b.kpa : 0));
+        for (int u = tid; u < units; u += TS_THREADS) {
+          const int l = u & 63, g = (u >> 6) % ng, w = (u >> 6) / ng;
+          const int mm = l & 15, qq = l >> 4;
+          const int k = w * (kps >> 2) + 16 * g + 4 * qq;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (k < wsrc) v = *reinterpret_cast<const f32x4*>(b.w + ((long)tn * 16 + mm) * b.kp + k0 + k);
+          d4[u] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const SweepCall* call = a.call;
+  const int with_noise = call->with_noise;
+  const float* noise = call->noise;
+  float* eps_log = call->eps_log;
+  const int eps_log_steps = call->eps_log_steps;
+  const uint64_t seed = call->seed, chain_base = call->chain_base, step_offset = call->step_offset;
+  const long ring_bytes = a.ring_step * 4;
+  unsigned known = 0;  // stages known complete team-wide (the last wait's target)
+  const bool cw = wave < 4;  // compute wave
+  // in0: wave w's B^T column tile (columns 16 w .. 16 w + 15 of zB), in registers for the whole sweep
+  f32x4 bv[EMB_G];
+  {
+    const int half = nz >> 1, col = wave * 16 + m;
+    int tn0;
+    const bool own0 = ts_tiles(a.b[0], T, slot, &tn0) > 0;
+#pragma unroll
+    for (int g = 0; g < EMB_G; ++g) {
+      const int kk = 16 * g + 4 * q;
+      bv[g] = (own0 && cw && col < half && kk < nz) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * nz + kk)
+                                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  for (int k = 0; k < a.n; ++k) {
+    const float* tb = a.tab + 8 * k;
+    const float c0 = tb[0], c1 = tb[1], c2 = tb[2], c3 = tb[3], c4 = tb[4];
+    const bool last = tb[5] != 0.f;
+    const int noisy_k = (int)tb[6];
+    float* const rslot = a.ring + (long)k * a.ring_step;
+    const float* const zk = a.zring + (long)k * B * nz;
+    float* const zk1 = a.zring + (long)(k + 1) * B * nz;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)rslot, (short)0, (int)ring_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)zk, (short)0, B * nz * 4, 0x00020000);
+#pragma unroll 1
+    for (int j = 0; j < 7; ++j) {
+      const TsBlock& b = a.b[j];
+      const unsigned s = 7u * k + j;
+      int tn0;
+      const int nt = ts_tiles(b, T, slot, &tn0);
+      uint64_t* tr = (a.trace && tid == 256) ? a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4 : nullptr;
+      if (nt == 0) {  // nothing to compute: publish at once (this slot's earlier stores are drained)
+        if (tid == 256) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      const bool final_ = j == 6;
+      const float* wbase = lds + lbase[j];
+      // a skip half produced at stage sb is ready now when sb < known
+      const bool skip_early = b.kpb > 0 && (7u * k + b.srcB) < known;
+      bool waited = false;
+#pragma unroll 1
+      for (int rt = 0; rt < nrt; ++rt) {
+        const int tm = team + 8 * rt, r0 = tm * TM;
+#pragma unroll 1
+        for (int i = 0; i < nt; ++i) {
+          const int tn = tn0 + i * T, n0 = tn * TC;
+          const float* wl = wbase + (long)i * 16 * (b.kpa + b.kpb);
+          // ---- independent of the previous stage: epilogue operands, the skip half
+          const int erow = r0 + er, ecol = n0 + ec;
+          const bool eok = tid < TM * TC && erow < B && ecol < b.dout;
+          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f;
+          if (eok && !(a.dbg & 8)) {
+            const float* ghr = a.gh + ((long)k * B + erow) * a.ldgh + b.ghoff;
+            gate = ghr[ecol];
+            hb = ghr[b.dout + ecol];
+            bl = b.bls[tn * 16 + ec];
+            bs = b.bls[tn * 16 + 8 + ec];
+            if (final_ && !last && with_noise) {
+              if (noise) {
+                xi = noise[((long)noisy_k * B + erow) * nz + ecol];
+              } else {
+                float n4[4];
+                philox_normal4(seed, chain_base + erow, step_offset + noisy_k, (uint32_t)(ecol >> 2),
+                               DAMC_STREAM_SWEEP, n4);
+                xi = pick4(n4, ecol);
+              }
+            }
+          }
+          const int xrow = r0 + m;
+          const bool xok = xrow < B;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if (skip_early && cw)
+            ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg);
+          const int half = nz >> 1;
+
+          // ---- wait for stage s - 1 of the team (once per stage)
+          if (!waited) {
+            if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+            if (s > 0 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag)) return;
+            if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
+            known = s;
+            waited = true;
+          }
+
+          if (j == 0) {  // in0: [sin 2pi zB, cos 2pi zB, z] of the 16 rows into LDS (as chain_kernel<true>)
+            f32x4 zv4[EMB_G];
+#pragma unroll
+            for (int g = 0; g < EMB_G; ++g) {
+              const int kk = 16 * g + 4 * q;
+              zv4[g] = (cw && xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            if (cw && wave * 16 < half) {  // wave w: B^T columns 16 w .. 16 w + 15 (nz <= 128), in registers
+              const int tt = wave;
+              const int col = tt * 16 + m;
+              const bool cok = col < half;
+              f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) e4 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], e4, 0, 0, 0);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int rrow = 4 * q + r;
+                if (cok) {
+                  const float t = e4[r] - rintf(e4[r]);
+                  const bool ok = r0 + rrow < B;
+                  embs[rrow * ld0 + col] = ok ? __builtin_amdgcn_sinf(t) : 0.f;
+                  embs[rrow * ld0 + half + col] = ok ? __builtin_amdgcn_cosf(t) : 0.f;
+                }
+              }
+            }
+            if (wave == 0) {
+#pragma unroll
+              for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const int kk = 16 * g + 4 * q + e;
+                  if (kk < nz) embs[m * ld0 + 2 * half + kk] = zv4[g][e];
+                }
+            }
+            for (int c = 2 * half + nz + tid; c < b.kpa; c += TS_THREADS)
+#pragma unroll
+              for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
+            __syncthreads();
+            if (cw) ts_half<true>(acc, wl, b.kpa, rr, 0, 0, xrow, xok, embs, ld0, a.dbg);
+          } else if (cw) {
+            ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg);
+            if (b.kpb > 0 && !skip_early)
+              ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg);
+          }
+          if (cw) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
+          }
+          __syncthreads();
+          if (tr && i == 0 && rt == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
+          if (eok) {
+            float l = 0.f, sk = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {  // fixed order: deterministic
+              l += red[w][er][ec];
+              sk += red[w][er][8 + ec];
+            }
+            // ConcatSquashLinearSkipCtx.forward: ret = layer(x) * gate + bias; ret + skip(x)
+            const float o = ((l + bl) * gate + hb) + (sk + bs);
+            if (!final_) {
+              if (!(a.dbg & 16)) st_sc1_f(rslot + b.ooff + (long)erow * b.dout + ecol, o);
+            } else {  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
+              const long zi = (long)erow * nz + ecol;
+              const float zv = ld_sc1_f(zk + zi);
+              const float eps = a.residual ? zv + o : o;
+              if (eps_log && k < eps_log_steps) eps_log[(long)k * B * nz + zi] = eps;
+              const float pred = mul_rn(c0, sub_rn(zv, mul_rn(eps, c1)));
+              float zn;
+              if (last) {
+                zn = pred;
+              } else {
+                zn = add_rn(mul_rn(c2, zv), mul_rn(c3, pred));
+                if (with_noise) zn = add_rn(zn, mul_rn(c4, xi));
+              }
+              st_sc1_f(zk1 + zi, zn);
+            }
+          }
+          __syncthreads();  // red (and the in0 image) are reused by the next task
+        }
+      }
+      // publish: every storing wave has drained, then one lane stores the slot's flag
+      if (!(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 256) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ skinny GEMMs of the precompute
 // Y[m][n] = act(sum_k f(A[m][k]) W[n][k] + bias[n]) for the sweep's short-M products (the time MLP and qt over
 // n steps, px over B rows): the chain kernel's tile (16 rows x 16 columns, K split over 4 waves, every lane's
@@ -754,6 +1121,7 @@ struct SweepWs {
   // persistent chain: per-step ring slots of the block outputs and of z, the step table, the arrival counters
   float *ring, *zring, *tab;
   unsigned* cnt;
+  unsigned* tflags;
   int* err;
   size_t bytes;
 };
@@ -797,7 +1165,8 @@ size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
   t.zring = take((long)(n + 1) * B * d->nz);
   t.tab = take(8L * n);
   t.cnt = reinterpret_cast<unsigned*>(take(7L * n * G + 64));
-  t.err = reinterpret_cast<int*>(t.cnt + 7L * n * G);
+  t.tflags = reinterpret_cast<unsigned*>(take(8 * TS_MAXT + 64));  // team flags, then the error word
+  t.err = reinterpret_cast<int*>(t.tflags + 8 * TS_MAXT);
   t.bytes = off;
   if (w) *w = t;
   return off;
@@ -1093,6 +1462,7 @@ int run_chain_persistent(const damc_denoiser_t* d, const SweepWs& w, int B, int 
   }
   DAMC_CHECK(hipMemcpyAsync(w.tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
   DAMC_CHECK(hipMemsetAsync(w.cnt, 0, (7L * n * G + 64) * sizeof(unsigned), s));
+  DAMC_CHECK(hipMemsetAsync(w.err, 0, sizeof(int), s));
   static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
   const size_t tbytes = (size_t)P * 7 * n * 3 * sizeof(uint64_t);
   if (trace) {
@@ -1113,6 +1483,148 @@ int run_chain_persistent(const damc_denoiser_t* d, const SweepWs& w, int B, int 
     }
   }
   return (int)hipGetLastError();
+}
+
+// ---- team sweep host side
+bool team_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DAMC_SWEEP_TEAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+constexpr size_t TS_LDS_MAX = 160 * 1024 - 8 * 1024;  // dynamic LDS a workgroup may take (static red etc. aside)
+constexpr size_t TS_LDS_MIN = 84 * 1024;              // > half the CU's LDS: one workgroup per CU
+
+// slots per team on this device: CUs / 8 (0 when the CUs do not split into 8 XCD groups)
+int team_slots() {
+  static std::mutex mu;
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cached[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = (cus % 8 == 0 && cus >= 8) ? std::min(cus / 8, TS_MAXT) : -1;
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TS_LDS_MAX);
+  }
+  return std::max(cached[dev], 0);
+}
+
+inline int pad64(int v) { return (v + 63) / 64 * 64; }
+
+// the team launch of a sweep: 0, or DAMC_ERR_UNSUPPORTED when the weights do not fit the LDS of a team
+int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* a, int* P, size_t* smem) {
+  const int T = team_slots();
+  if (T < 1) return DAMC_ERR_UNSUPPORTED;
+  if ((long)B * sum_dout(d) * 4 >= (1L << 31) || (long)B * d->nz * 4 >= (1L << 31)) return DAMC_ERR_UNSUPPORTED;
+  memset(a, 0, sizeof(*a));
+  const int srcA[7] = {-1, 0, 1, 2, 3, 4, 5}, srcB[7] = {-1, -1, -1, -1, 2, 1, 0};
+  int coloff = 0, tiles = 0;
+  for (int j = 0; j < 7; ++j) {
+    const damc_csq_block_t& bk = d->blocks[j];
+    TsBlock& p = a->b[j];
+    p.w = w.w[j];
+    p.bls = w.bls[j];
+    p.kp = kpad(bk.din);
+    p.dout = bk.dout;
+    p.ntn = (bk.dout + TC - 1) / TC;
+    p.srcA = srcA[j];
+    p.srcB = srcB[j];
+    p.wa = j ? d->blocks[j - 1].dout : bk.din;
+    p.wb = srcB[j] >= 0 ? d->blocks[srcB[j]].dout : 0;
+    if (p.wa + p.wb != bk.din) return DAMC_ERR_UNSUPPORTED;
+    p.kpa = pad64(p.wa);
+    p.kpb = pad64(p.wb);
+    p.ooff = (long)B * coloff;
+    p.ghoff = 2 * coloff;
+    p.toff = tiles % T;
+    tiles += p.ntn;
+    coloff += bk.dout;
+  }
+  long wl = 0;
+  for (int t = 0; t < T; ++t) {
+    long s = 0;
+    for (int j = 0; j < 7; ++j) {
+      const TsBlock& p = a->b[j];
+      const int f = ((t - p.toff) % T + T) % T;
+      const int c = f < p.ntn ? (p.ntn - f + T - 1) / T : 0;
+      s += (long)c * 16 * (p.kpa + p.kpb);
+    }
+    wl = std::max(wl, s);
+  }
+  size_t sm = (size_t)(wl + (long)TM * emb_ld(a->b[0].kpa)) * sizeof(float);
+  if (sm > TS_LDS_MAX) return DAMC_ERR_UNSUPPORTED;
+  sm = std::max(sm, TS_LDS_MIN);
+  a->bmat = w.bmat;
+  a->nz = d->nz;
+  a->B = B;
+  a->G = (B + TM - 1) / TM;
+  a->n = n;
+  a->residual = d->residual;
+  a->T = T;
+  a->gh = w.gh;
+  a->ldgh = 2L * sum_dout(d);
+  a->ring = w.ring;
+  a->ring_step = (long)B * sum_dout(d);
+  a->zring = w.zring;
+  a->tab = w.tab;
+  a->call = w.call;
+  a->flags = w.tflags;
+  a->err = w.err;
+  a->budget = 2000000;  // 20 ms at 100 MHz per wait: a stage takes microseconds
+  a->wlds = (int)wl;
+  static const int dbg = [] {
+    const char* e = getenv("DAMC_SWEEP_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a->dbg = dbg;
+  *P = 8 * T;
+  *smem = sm;
+  return 0;
+}
+
+// NaN-marks the result of a sweep whose team launch failed a bounded wait
+__global__ void team_copyout_kernel(const float* src, float* dst, long n, const int* err) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = *err ? __builtin_nanf("") : src[i];
+}
+
+int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t s) {
+  const int n = a.n;
+  std::vector<float> tab(8 * (size_t)n, 0.f);  // c0..c4, is_last, noisy_k
+  for (int k = 0, noisy = 0; k < n; ++k) {
+    for (int i = 0; i < 6; ++i) tab[8 * k + i] = coef[6 * (size_t)k + i];
+    tab[8 * k + 6] = (float)noisy;
+    if (coef[6 * (size_t)k + 5] == 0.f) ++noisy;
+  }
+  DAMC_CHECK(hipMemcpyAsync(const_cast<float*>(a.tab), tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  DAMC_CHECK(hipMemsetAsync(a.flags, 0, (8 * TS_MAXT + 64) * sizeof(unsigned), s));  // flags + error word
+  static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
+  const size_t tbytes = (size_t)P * 7 * n * 4 * sizeof(uint64_t);
+  if (trace) {
+    DAMC_CHECK(hipMalloc(&a.trace, tbytes));
+    DAMC_CHECK(hipMemsetAsync(a.trace, 0, tbytes, s));
+  }
+  hipLaunchKernelGGL(sweep_team_kernel, dim3(P), dim3(TS_THREADS), smem, s, a);
+  DAMC_LAUNCH_CHECK();
+  if (trace) {  // tools/sweep_trace.py reads the dump: P, n, G, then the stamps
+    std::vector<uint64_t> h((size_t)P * 7 * n * 4);
+    DAMC_CHECK(hipStreamSynchronize(s));
+    DAMC_CHECK(hipMemcpy(h.data(), a.trace, tbytes, hipMemcpyDeviceToHost));
+    (void)hipFree(a.trace);
+    a.trace = nullptr;
+    if (FILE* f = fopen(getenv("DAMC_SWEEP_TRACE"), "wb")) {
+      const int hdr[3] = {P, n, a.G};
+      fwrite(hdr, sizeof(hdr), 1, f);
+      fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+      fclose(f);
+    }
+  }
+  return 0;
 }
 
 }  // namespace
@@ -1319,14 +1831,20 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   call.with_noise = with_noise ? 1 : 0;
   const long nzb = (long)B * d->nz;
   const bool persist = persistent_enabled();
+  TsArgs ta;
+  int tP = 0;
+  size_t tsm = 0;
+  const bool team = !persist && team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
   hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, call, w.call, zt,
-                     persist ? w.zring : w.z, nzb);
+                     (persist || team) ? w.zring : w.z, nzb);
   DAMC_LAUNCH_CHECK();
   double flops_step = 0;
   for (int j = 0; j < 7; ++j) flops_step += 2.0 * B * 2.0 * d->blocks[j].din * d->blocks[j].dout;
   {
     ProfScope ps("denoise_chain", flops_step * n, s);
-    if (persist) {
+    if (team) {
+      if ((rc = run_chain_team(ta, tP, tsm, coef, s))) return rc;
+    } else if (persist) {
       if ((rc = run_chain_persistent(d, w, B, n, coef, s))) return rc;
     } else if (allow_graph && graphs_enabled()) {
       if ((rc = run_chain_graph(d, w, wsp, wsb, B, n, coef, s))) return rc;
@@ -1337,8 +1855,12 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
       if ((rc = launch_chain(ls, s))) return rc;
     }
   }
-  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
-                     persist ? w.zring + (long)n * nzb : w.z, zt, nzb);
+  if (team)
+    hipLaunchKernelGGL(team_copyout_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
+                       w.zring + (long)n * nzb, zt, nzb, w.err);
+  else
+    hipLaunchKernelGGL(copy_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
+                       persist ? w.zring + (long)n * nzb : w.z, zt, nzb);
   return (int)hipGetLastError();
 }
 
