@@ -283,48 +283,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   if (a.trace && tid == 0) { a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 1] = __builtin_amdgcn_s_memrealtime(); a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 5] = __builtin_amdgcn_s_memtime(); }
 }
 
-// ------------------------------------------------------------------------------ persistent chain (one launch)
-// The 7n dependent block evaluations of a sweep as ONE launch of P resident workgroups.  Stage s = 7 k + j is
-// block j of step k; its tasks are the (row tile tm, column tile tn) pairs of chain_kernel, task t = tm * ntn + tn
-// run by workgroup t mod P (static, so with P and ntn multiples of 8 a column tile stays on one XCD for every step
-// and its weights stay in that XCD's L2, as in the launch chain).  Rows never mix, so stage s of row tile tm needs
-// only stage s-1 of the same row tile: one arrival counter per (stage, row tile), ntn arrivals each; the earlier
-// stages a block reads (skip inputs, z) are complete by transitivity.
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): every handed-off value is
-// stored sc1, every storing wave drains vmcnt before the workgroup barrier, then ONE lane adds to the counter
-// (agent scope); the consumer polls the counter with sc1 loads from one lane, joins the others at a barrier, and
-// reads the values with sc1 loads only.  Every step writes fresh ring slots (outputs and z), so no address is
-// rewritten while another XCD may hold it.  Each workgroup issues its next task's weight and epilogue loads before
-// it waits.  Every wait is bounded: past the budget (or once any workgroup has failed) the workgroup records
-// the failure in the error word and leaves, so the grid always drains.
-constexpr int PS_THREADS = 256;
-
-struct PsBlock {
-  const float* w;     // [ntn][16][kp]
-  const float* bls;   // [ntn][16]
-  int din, kp, dout, ntn, wa, wb;
-  int srcA, srcB;     // producing blocks of the input halves (-1: none)
-  long ooff;          // this block's output (B, dout) within a step's ring slot, floats
-  int ghoff;          // 2 * coloff: gate columns in a gh row
-};
-
-struct PsArgs {
-  PsBlock b[7];
-  const float* bmat;  // B^T (nz/2, nz)
-  int nz, B, G, n, residual;
-  const float* gh;    // (n, B, 2S)
-  long ldgh;
-  float* ring;        // (n, B*S): block outputs of step k at ring + k * ring_step
-  long ring_step;
-  float* zring;       // (n+1, B, nz): z before step k at zring + k * B * nz
-  const float* tab;   // (n, 8): c0..c4, is_last, noisy_k
-  const SweepCall* call;
-  unsigned* cnt;      // (7n, G)
-  int* err;
-  long budget;        // wait budget in 100 MHz ticks
-  uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][3] 100 MHz stamps {wait begin, wait end, published}
-};
-
+// sc1 (L1-bypassing) accesses of handed-off words (MI355X_MICROARCH.md, inter-workgroup visibility)
 __device__ __forceinline__ f32x4 ld_sc1(const __amdgpu_buffer_rsrc_t& r, long byte_off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16));
 }
@@ -333,233 +292,6 @@ __device__ __forceinline__ float ld_sc1_f(const float* p) {
 }
 __device__ __forceinline__ void st_sc1_f(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// lane 0 polls until *c >= need; every thread returns whether the wait succeeded (a barrier is inside)
-__device__ __forceinline__ bool ps_wait(const unsigned* c, unsigned need, int* err, long budget, int* sflag) {
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (unsigned it = 1;; ++it) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-        if ((it & 63) == 0) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            ok = 0;
-            break;
-          }
-          if ((long)(__builtin_amdgcn_s_memrealtime() - t0) > budget) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = 0;
-            break;
-          }
-        }
-      }
-    }
-    *sflag = ok;
-  }
-  __syncthreads();
-  return *sflag != 0;
-}
-
-__global__ __launch_bounds__(PS_THREADS) void sweep_persistent_kernel(PsArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[4][TM][16];
-  __shared__ int sflag;
-  extern __shared__ __attribute__((aligned(16))) float embs[];  // in0: [TM][emb_ld(kp0)]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m = lane & 15, q = lane >> 4;
-  const int er = tid >> 3, ec = tid & 7;
-  const SweepCall* call = a.call;
-  const int with_noise = call->with_noise;
-  const float* noise = call->noise;
-  float* eps_log = call->eps_log;
-  const int eps_log_steps = call->eps_log_steps;
-  const uint64_t seed = call->seed, chain_base = call->chain_base, step_offset = call->step_offset;
-  const int nz = a.nz, B = a.B, G = a.G;
-
-  for (int k = 0; k < a.n; ++k) {
-    const float* tb = a.tab + 8 * k;
-    const float c0 = tb[0], c1 = tb[1], c2 = tb[2], c3 = tb[3], c4 = tb[4];
-    const bool last = tb[5] != 0.f;
-    const int noisy_k = (int)tb[6];
-    float* const slot = a.ring + (long)k * a.ring_step;
-    const float* const zk = a.zring + (long)k * B * nz;
-    float* const zk1 = a.zring + (long)(k + 1) * B * nz;
-    const __amdgpu_buffer_rsrc_t rslot =
-        __builtin_amdgcn_make_buffer_rsrc((void*)slot, (short)0, (int)(a.ring_step * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)zk, (short)0, B * nz * 4, 0x00020000);
-#pragma unroll 1
-    for (int j = 0; j < 7; ++j) {
-      const PsBlock& b = a.b[j];
-      const int s = 7 * k + j;
-      const int T = G * b.ntn;
-      const unsigned need = (unsigned)(j ? a.b[j - 1].ntn : a.b[6].ntn);
-      const bool final_ = j == 6;
-#pragma unroll 1
-      for (int t = blockIdx.x; t < T; t += gridDim.x) {
-        const int tn = t % b.ntn, tm = t / b.ntn;
-        const int r0 = tm * TM, n0 = tn * TC;
-        // ---- independent of the previous stage: epilogue operands and the first weight chunk
-        const int erow = r0 + er, ecol = n0 + ec;
-        const bool eok = tid < TM * TC && erow < B && ecol < b.dout;
-        float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f;
-        if (eok) {
-          const float* ghr = a.gh + ((long)k * B + erow) * a.ldgh + b.ghoff;
-          gate = ghr[ecol];
-          hb = ghr[b.dout + ecol];
-          bl = b.bls[tn * 16 + ec];
-          bs = b.bls[tn * 16 + 8 + ec];
-          if (final_ && !last && with_noise) {
-            if (noise) {
-              xi = noise[((long)noisy_k * B + erow) * nz + ecol];
-            } else {
-              float n4[4];
-              philox_normal4(seed, chain_base + erow, step_offset + noisy_k, (uint32_t)(ecol >> 2),
-                             DAMC_STREAM_SWEEP, n4);
-              xi = pick4(n4, ecol);
-            }
-          }
-        }
-        const int kq = b.kp >> 2, ng = kq >> 4, kbase = wave * kq;
-        const float* wrow = b.w + ((long)tn * 16 + m) * b.kp + kbase + 4 * q;
-        f32x4 wb[CH_CHUNK];
-#pragma unroll
-        for (int c = 0; c < CH_CHUNK; ++c)
-          wb[c] = c < ng ? *reinterpret_cast<const f32x4*>(wrow + 16 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-
-        // ---- wait for the previous stage of this row tile
-        uint64_t* tr = (a.trace && t == (int)blockIdx.x && tid == 0) ? a.trace + ((long)blockIdx.x * 7 * a.n + s) * 3 : nullptr;
-        if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
-        if (s > 0 && !ps_wait(a.cnt + (long)(s - 1) * G + tm, need, a.err, a.budget, &sflag)) return;
-        if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
-
-        const int xrow = r0 + m;
-        const bool xok = xrow < B;
-        const int ld = emb_ld(b.kp);
-        if (j == 0) {  // in0: [sin 2pi zB, cos 2pi zB, z] of the 16 rows into LDS (as chain_kernel<true>)
-          const int half = nz >> 1;
-          f32x4 zv4[EMB_G];
-#pragma unroll
-          for (int g = 0; g < EMB_G; ++g) {
-            const int kk = 16 * g + 4 * q;
-            zv4[g] = (xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-          for (int tt = wave; tt * 16 < half; tt += 4) {
-            const int col = tt * 16 + m;
-            const bool cok = col < half;
-            f32x4 bv[EMB_G];
-#pragma unroll
-            for (int g = 0; g < EMB_G; ++g) {
-              const int kk = 16 * g + 4 * q;
-              bv[g] = (cok && kk < nz) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * nz + kk)
-                                       : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int g = 0; g < EMB_G; ++g)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], acc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int rr = 4 * q + r;
-              if (cok) {
-                const float tt2 = acc[r] - rintf(acc[r]);
-                const bool ok = r0 + rr < B;
-                embs[rr * ld + col] = ok ? __builtin_amdgcn_sinf(tt2) : 0.f;
-                embs[rr * ld + half + col] = ok ? __builtin_amdgcn_cosf(tt2) : 0.f;
-              }
-            }
-          }
-          if (wave == 0) {
-#pragma unroll
-            for (int g = 0; g < EMB_G; ++g)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int kk = 16 * g + 4 * q + e;
-                if (kk < nz) embs[m * ld + 2 * half + kk] = zv4[g][e];
-              }
-          }
-          for (int c = 2 * half + nz + tid; c < b.kp; c += PS_THREADS)
-#pragma unroll
-            for (int rr = 0; rr < TM; ++rr) embs[rr * ld + c] = 0.f;
-          __syncthreads();
-        }
-
-        // ---- main loop (wave w: k in [w kq, (w+1) kq)); x = lrelu(cat(A, B)) from the ring with sc1 loads
-        const long aoff = b.srcA >= 0 ? a.b[b.srcA].ooff : 0, boff = b.srcB >= 0 ? a.b[b.srcB].ooff : 0;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int g0 = 0; g0 < ng; g0 += CH_CHUNK) {
-          f32x4 xa[CH_CHUNK];
-          if (g0) {
-#pragma unroll
-            for (int c = 0; c < CH_CHUNK; ++c)
-              wb[c] = g0 + c < ng ? *reinterpret_cast<const f32x4*>(wrow + 16 * (g0 + c)) : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-#pragma unroll
-          for (int c = 0; c < CH_CHUNK; ++c) {
-            const int g = g0 + c;
-            const int kk = kbase + 16 * g + 4 * q;
-            f32x4 xv = {0.f, 0.f, 0.f, 0.f};
-            if (g < ng) {
-              if (j == 0) {
-                xv = *reinterpret_cast<const f32x4*>(embs + m * ld + kk);
-              } else if (xok && kk < b.din) {
-                xv = kk < b.wa ? ld_sc1(rslot, (aoff + (long)xrow * b.wa + kk) * 4)
-                               : ld_sc1(rslot, (boff + (long)xrow * b.wb + (kk - b.wa)) * 4);
-              }
-            }
-            xa[c] = xv;
-          }
-#pragma unroll
-          for (int c = 0; c < CH_CHUNK; ++c) {
-            f32x4 x = xa[c];
-            if (j) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.01f * x[e];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[e], wb[c][e], acc, 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
-        __syncthreads();
-
-        if (eok) {
-          float l = 0.f, sk = 0.f;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            l += red[w][er][ec];
-            sk += red[w][er][8 + ec];
-          }
-          const float o = ((l + bl) * gate + hb) + (sk + bs);
-          if (!final_) {
-            st_sc1_f(slot + b.ooff + (long)erow * b.dout + ecol, o);
-          } else {
-            const long zi = (long)erow * nz + ecol;
-            const float zv = ld_sc1_f(zk + zi);
-            const float eps = a.residual ? zv + o : o;
-            if (eps_log && k < eps_log_steps) eps_log[(long)k * B * nz + zi] = eps;
-            const float pred = mul_rn(c0, sub_rn(zv, mul_rn(eps, c1)));
-            float zn;
-            if (last) {
-              zn = pred;
-            } else {
-              zn = add_rn(mul_rn(c2, zv), mul_rn(c3, pred));
-              if (with_noise) zn = add_rn(zn, mul_rn(c4, xi));
-            }
-            st_sc1_f(zk1 + zi, zn);
-          }
-        }
-        // publish: every storing wave drains, then one lane counts this task for (stage s, row tile tm)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(a.cnt + (long)s * G + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------ team sweep (one launch, default)
@@ -608,7 +340,7 @@ struct TsArgs {
   float* zring;       // (n+1, B, nz): z before step k at zring + k * B * nz
   const float* tab;   // (n, 8): c0..c4, is_last, noisy_k
   const SweepCall* call;
-  unsigned* flags;    // [8][TS_MAXT]: stages published by (team, slot)
+  unsigned* flags;    // [8][TS_MAXT][TS_FS]: stages published by (team, slot)
   int* err;
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
@@ -625,17 +357,20 @@ __device__ __forceinline__ int ts_tiles(const TsBlock& b, int T, int t, int* tn0
   return f < b.ntn ? (b.ntn - f + T - 1) / T : 0;
 }
 
-// wave 4 (which issues no other loads, so nothing queues in front of its poll) polls the T flags of the team
-// until all have published `need` stages; every thread returns whether the wait succeeded (a barrier is inside)
+// wave 4 (which issues no other loads, so nothing queues in front of its poll) polls the T flags of the team (one
+// 128-B line each: a shared line would serialise the producers' stores and the pollers' loads on one memory
+// channel) until all have published `need` stages; every thread returns whether the wait succeeded (a barrier is
+// inside).  One poll in flight: three staggered ones measured 4-5 % slower per sweep.
+constexpr int TS_FS = 32;  // flag stride, unsigned
 __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need, int* err, long budget, int* sflag) {
   if (threadIdx.x >= 256) {
     const int lane = threadIdx.x - 256;
     int ok = 1;
-    uint64_t t0 = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned it = 0;; ++it) {
-      const unsigned v = lane < T ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : need;
+      const unsigned v =
+          lane < T ? __hip_atomic_load(fl + lane * TS_FS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : need;
       if (__all(v >= need)) break;
-      if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_sleep(1);
       if ((it & 63) == 63) {
         const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -692,6 +427,41 @@ __device__ __forceinline__ void ts_half(f32x4& acc, const float* wl, int kps, co
   }
 }
 
+// the two halves of ts_half for an input half of at most 64 N columns of K: this wave's x loads into registers
+// (issued early), then its MFMAs
+template <int N>
+__device__ __forceinline__ void ts_load(f32x4 (&x)[N], int kps, const __amdgpu_buffer_rsrc_t& rs, long soff, int wsrc,
+                                        int row, bool rok) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4;
+  const int kq = kps >> 2, ng = kq >> 4, kbase = wave * kq;
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    const int k = kbase + 16 * c + 4 * q;
+    x[c] = (c < ng && rok && k < wsrc) ? ld_sc1(rs, (soff + (long)row * wsrc + k) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+template <int N>
+__device__ __forceinline__ void ts_mfma(f32x4& acc, const float* wl, int kps, const f32x4 (&x)[N], int dbg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ng = kps >> 6;
+  const f32x4* wv = reinterpret_cast<const f32x4*>(wl) + (long)wave * ng * 64 + lane;
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    if (c >= ng) break;
+    f32x4 xv = x[c];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xv[e] = xv[e] > 0.f ? xv[e] : 0.01f * xv[e];
+    const f32x4 w = wv[c * 64];
+    if (dbg & 4) {
+      acc[0] += xv[0] * w[0];
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[e], w[e], acc, 0, 0, 0);
+  }
+}
+
 __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   __shared__ int sflag;
@@ -704,8 +474,8 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   const int nz = a.nz, B = a.B, G = a.G;
   if (team >= G || slot >= T) return;  // no row tile for this team (its flags are never waited on)
   const int nrt = (G - team + 7) / 8;  // row tiles of the team: team + 8 i
-  unsigned* const myflag = a.flags + team * TS_MAXT + slot;
-  const unsigned* const teamflags = a.flags + team * TS_MAXT;
+  unsigned* const myflag = a.flags + (team * TS_MAXT + slot) * TS_FS;
+  const unsigned* const teamflags = a.flags + team * TS_MAXT * TS_FS;
   float* const embs = lds + a.wlds;
   const int ld0 = emb_ld(a.b[0].kpa);
 
@@ -825,7 +595,12 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
           const int xrow = r0 + m;
           const bool xok = xrow < B;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          if (skip_early && cw)
+          // a skip half that is complete already: its loads now (they land during the wait), its MFMAs while the
+          // previous block's half is in flight
+          const bool pre = skip_early && b.kpb <= 64 * CH_CHUNK && b.kpa <= 64 * CH_CHUNK;
+          f32x4 xs[CH_CHUNK];
+          if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
+          if (skip_early && !pre && cw)
             ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg);
           const int half = nz >> 1;
 
@@ -879,6 +654,11 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
               for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
             __syncthreads();
             if (cw) ts_half<true>(acc, wl, b.kpa, rr, 0, 0, xrow, xok, embs, ld0, a.dbg);
+          } else if (cw && pre) {
+            f32x4 xa[CH_CHUNK];
+            ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
+            ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
+            ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw) {
             ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg);
             if (b.kpb > 0 && !skip_early)
@@ -1118,9 +898,8 @@ struct SweepWs {
   float *px, *qt, *t1, *t2, *xs, *cx, *gh, *z;
   float* outs[7];
   SweepCall* call;
-  // persistent chain: per-step ring slots of the block outputs and of z, the step table, the arrival counters
+  // team sweep: per-step ring slots of the block outputs and of z, the step table, the team flags, the error word
   float *ring, *zring, *tab;
-  unsigned* cnt;
   unsigned* tflags;
   int* err;
   size_t bytes;
@@ -1160,13 +939,11 @@ size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
   t.z = take((long)B * d->nz);
   for (int j = 0; j < 7; ++j) t.outs[j] = take((long)B * d->blocks[j].dout);
   t.call = reinterpret_cast<SweepCall*>(take(64));
-  const int G = (B + TM - 1) / TM;
   t.ring = take((long)n * B * S);
   t.zring = take((long)(n + 1) * B * d->nz);
   t.tab = take(8L * n);
-  t.cnt = reinterpret_cast<unsigned*>(take(7L * n * G + 64));
-  t.tflags = reinterpret_cast<unsigned*>(take(8 * TS_MAXT + 64));  // team flags, then the error word
-  t.err = reinterpret_cast<int*>(t.tflags + 8 * TS_MAXT);
+  t.tflags = reinterpret_cast<unsigned*>(take(8 * TS_MAXT * TS_FS + 64));  // team flags, then the error word
+  t.err = reinterpret_cast<int*>(t.tflags + 8 * TS_MAXT * TS_FS);
   t.bytes = off;
   if (w) *w = t;
   return off;
@@ -1381,117 +1158,11 @@ int run_chain_graph(const damc_denoiser_t* d, const SweepWs& w, void* wsp, size_
   return (int)hipGraphLaunch(exec, s);
 }
 
-bool persistent_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DAMC_SWEEP_PERSIST");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// resident workgroups the persistent chain may use on this device: 2 per CU at most (multiple of 8, so a
-// column tile keeps its XCD), never more than the occupancy the runtime reports for the kernel
-int persistent_grid(size_t smem) {
-  static std::mutex mu;
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!cached[dev]) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_persistent_kernel, PS_THREADS, smem) != hipSuccess)
-      return 0;
-    cached[dev] = std::max(0, std::min(per, 2) * cus / 8 * 8);
-  }
-  return cached[dev];
-}
-
-int run_chain_persistent(const damc_denoiser_t* d, const SweepWs& w, int B, int n, const float* coef, hipStream_t s) {
-  const int G = (B + TM - 1) / TM;
-  const int S = sum_dout(d);
-  PsArgs a;
-  memset(&a, 0, sizeof(a));
-  int coloff = 0, maxT = 0, kp0 = kpad(d->blocks[0].din);
-  const int srcA[7] = {-1, 0, 1, 2, 3, 4, 5}, srcB[7] = {-1, -1, -1, -1, 2, 1, 0};
-  for (int j = 0; j < 7; ++j) {
-    const damc_csq_block_t& bk = d->blocks[j];
-    PsBlock& p = a.b[j];
-    p.w = w.w[j];
-    p.bls = w.bls[j];
-    p.din = bk.din;
-    p.kp = kpad(bk.din);
-    p.dout = bk.dout;
-    p.ntn = (bk.dout + TC - 1) / TC;
-    p.srcA = srcA[j];
-    p.srcB = srcB[j];
-    p.wa = j ? d->blocks[j - 1].dout : 0;
-    p.wb = srcB[j] >= 0 ? d->blocks[srcB[j]].dout : 0;
-    p.ooff = (long)B * coloff;
-    p.ghoff = 2 * coloff;
-    coloff += bk.dout;
-    maxT = std::max(maxT, G * p.ntn);
-  }
-  const size_t smem = (size_t)TM * emb_ld(kp0) * sizeof(float);
-  int P = persistent_grid(smem);
-  if (P < 8) return DAMC_ERR_UNSUPPORTED;
-  P = std::min(P, (maxT + 7) / 8 * 8);
-  a.bmat = w.bmat;
-  a.nz = d->nz;
-  a.B = B;
-  a.G = G;
-  a.n = n;
-  a.residual = d->residual;
-  a.gh = w.gh;
-  a.ldgh = 2L * S;
-  a.ring = w.ring;
-  a.ring_step = (long)B * S;
-  a.zring = w.zring;
-  a.tab = w.tab;
-  a.call = w.call;
-  a.cnt = w.cnt;
-  a.err = w.err;
-  a.budget = 5000000;  // 50 ms at 100 MHz per wait: a stage takes microseconds
-  if ((long)B * S * 4 >= (1L << 31) || (long)B * d->nz * 4 >= (1L << 31)) return DAMC_ERR_UNSUPPORTED;
-  // the step table (c0..c4, is_last, noisy_k) travels to the device with the call
-  std::vector<float> tab(8 * (size_t)n, 0.f);
-  for (int k = 0, noisy = 0; k < n; ++k) {
-    for (int i = 0; i < 6; ++i) tab[8 * k + i] = coef[6 * (size_t)k + i];
-    tab[8 * k + 6] = (float)noisy;
-    if (coef[6 * (size_t)k + 5] == 0.f) ++noisy;
-  }
-  DAMC_CHECK(hipMemcpyAsync(w.tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
-  DAMC_CHECK(hipMemsetAsync(w.cnt, 0, (7L * n * G + 64) * sizeof(unsigned), s));
-  DAMC_CHECK(hipMemsetAsync(w.err, 0, sizeof(int), s));
-  static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
-  const size_t tbytes = (size_t)P * 7 * n * 3 * sizeof(uint64_t);
-  if (trace) {
-    DAMC_CHECK(hipMalloc(&a.trace, tbytes));
-    DAMC_CHECK(hipMemsetAsync(a.trace, 0, tbytes, s));
-  }
-  hipLaunchKernelGGL(sweep_persistent_kernel, dim3(P), dim3(PS_THREADS), smem, s, a);
-  if (trace) {  // tools/sweep_trace.py reads the dump: P, n, then the stamps
-    std::vector<uint64_t> h((size_t)P * 7 * n * 3);
-    DAMC_CHECK(hipStreamSynchronize(s));
-    DAMC_CHECK(hipMemcpy(h.data(), a.trace, tbytes, hipMemcpyDeviceToHost));
-    (void)hipFree(a.trace);
-    if (FILE* f = fopen(getenv("DAMC_SWEEP_TRACE"), "wb")) {
-      const int hdr[3] = {P, n, G};
-      fwrite(hdr, sizeof(hdr), 1, f);
-      fwrite(h.data(), sizeof(uint64_t), h.size(), f);
-      fclose(f);
-    }
-  }
-  return (int)hipGetLastError();
-}
-
 // ---- team sweep host side
+// DAMC_SWEEP_TEAM=0 selects the launch chain (read per call, so one process can A/B the two)
 bool team_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DAMC_SWEEP_TEAM");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = getenv("DAMC_SWEEP_TEAM");
+  return !(e && e[0] == '0');
 }
 
 constexpr size_t TS_LDS_MAX = 160 * 1024 - 8 * 1024;  // dynamic LDS a workgroup may take (static red etc. aside)
@@ -1602,7 +1273,7 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
     if (coef[6 * (size_t)k + 5] == 0.f) ++noisy;
   }
   DAMC_CHECK(hipMemcpyAsync(const_cast<float*>(a.tab), tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
-  DAMC_CHECK(hipMemsetAsync(a.flags, 0, (8 * TS_MAXT + 64) * sizeof(unsigned), s));  // flags + error word
+  DAMC_CHECK(hipMemsetAsync(a.flags, 0, (8 * TS_MAXT * TS_FS + 64) * sizeof(unsigned), s));  // flags + error word
   static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
   const size_t tbytes = (size_t)P * 7 * n * 4 * sizeof(uint64_t);
   if (trace) {
@@ -1830,13 +1501,12 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   call.step_offset = step_offset;
   call.with_noise = with_noise ? 1 : 0;
   const long nzb = (long)B * d->nz;
-  const bool persist = persistent_enabled();
   TsArgs ta;
   int tP = 0;
   size_t tsm = 0;
-  const bool team = !persist && team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
+  const bool team = team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
   hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, call, w.call, zt,
-                     (persist || team) ? w.zring : w.z, nzb);
+                     team ? w.zring : w.z, nzb);
   DAMC_LAUNCH_CHECK();
   double flops_step = 0;
   for (int j = 0; j < 7; ++j) flops_step += 2.0 * B * 2.0 * d->blocks[j].din * d->blocks[j].dout;
@@ -1844,8 +1514,6 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     ProfScope ps("denoise_chain", flops_step * n, s);
     if (team) {
       if ((rc = run_chain_team(ta, tP, tsm, coef, s))) return rc;
-    } else if (persist) {
-      if ((rc = run_chain_persistent(d, w, B, n, coef, s))) return rc;
     } else if (allow_graph && graphs_enabled()) {
       if ((rc = run_chain_graph(d, w, wsp, wsb, B, n, coef, s))) return rc;
       chain_trace_dump(s);
@@ -1860,7 +1528,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
                        w.zring + (long)n * nzb, zt, nzb, w.err);
   else
     hipLaunchKernelGGL(copy_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
-                       persist ? w.zring + (long)n * nzb : w.z, zt, nzb);
+                       w.z, zt, nzb);
   return (int)hipGetLastError();
 }
 

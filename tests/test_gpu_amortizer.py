@@ -8,6 +8,7 @@ steps amplify rounding by sqrt(1+e^-l) per step, and the reference's own fp32 re
 result's distance to the fp64 oracle must stay within 3x the reference golden's distance to it (+ a 1e-5 /
 1e-6 floor).  The golden itself is still bounded by conftest.Q_END_TOL.
 """
+import numpy as np
 import pytest
 import torch
 
@@ -133,3 +134,65 @@ def test_dropin_q_forward(gpu_device):
     G = synth.load_into(dn._netG_cifar10(nz=128, ngf=16, nc=3), 0).to(gpu_device)
     xs, zs = MCMC.gen_samples_with_diffusion_prior(b=6, device=gpu_device, netQ=Q, netG=G)
     assert xs.shape == (6, 3, 32, 32) and zs.shape == (6, 128)
+
+
+def _wide_q(gpu_device, n_interval):
+    from damc import synth
+    from src import diffusion_net as dn
+
+    Q = dn._netQ_U(nc=3, nz=128, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=n_interval,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, dataset="cifar10")
+    synth.load_into(Q, 20)
+    return Q.to(gpu_device).eval()
+
+
+@pytest.mark.parametrize("B", [1, 37, 128, 300])
+def test_team_sweep_matches_launch_chain(am, gpu_device, monkeypatch, B):
+    """The one-launch team sweep (default) against the per-block launch chain (DAMC_SWEEP_TEAM=0) at full CIFAR
+    width: B=300 gives teams 2-3 row tiles, B=37 a ragged last tile, B=1 one active team.  The two differ only in
+    the order of the K sum of the skip blocks, so eps of step 1 agrees to rel-L2 1e-6 and of step 2 to 1e-5; a
+    10-step sweep amplifies fp32 rounding far beyond that, so the end point is judged
+    against the fp64 oracle on the same injected noise: the team's distance within 3x the chain's (+1e-6)."""
+    from damc import synth
+    from oracle import damc_oracle as orc
+
+    n = 10
+    Q = _wide_q(gpu_device, n)
+    xemb = torch.from_numpy(synth.normal_f32(7, 0, (B, 1024))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(8, 0, (B, 128))).to(gpu_device)
+    noise = torch.from_numpy(synth.normal_f32(9, 0, (n - 1, B, 128))).to(gpu_device)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DAMC_SWEEP_TEAM", mode)
+        zt = zt0.clone()
+        eps = am.reverse_sweep(Q, xemb, zt, noise=noise, eps_log_steps=2)
+        torch.cuda.synchronize()
+        res[mode] = (zt.cpu().numpy(), eps.cpu().numpy())
+    (zt_t, eps_t), (zt_c, eps_c) = res["1"], res["0"]
+    Qd = Q.cpu().double()
+    with torch.no_grad():
+        z64, _ = orc.reverse_sweep(Qd, xemb.cpu().double(), zt0.cpu().double(), noise.cpu().double(), n, -5.1, 9.8,
+                                   "large")
+    z64 = z64.numpy()
+    e_t, e_c = rel_l2(zt_t, z64), rel_l2(zt_c, z64)
+    print("B=%d team vs chain: eps1 %.2e eps2 %.2e; end |team-fp64| %.2e |chain-fp64| %.2e"
+          % (B, rel_l2(eps_t[0], eps_c[0]), rel_l2(eps_t[1], eps_c[1]), e_t, e_c))
+    assert np.isfinite(zt_t).all()
+    assert rel_l2(eps_t[0], eps_c[0]) <= 1e-6
+    assert rel_l2(eps_t[1], eps_c[1]) <= 1e-5
+    assert e_t <= 3 * e_c + 1e-6
+
+
+def test_team_sweep_is_deterministic(am, gpu_device):
+    """Fixed-order reductions everywhere: two team sweeps of the same inputs are bitwise equal."""
+    from damc import synth
+
+    Q = _wide_q(gpu_device, 20)
+    xemb = torch.from_numpy(synth.normal_f32(7, 0, (128, 1024))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(8, 0, (128, 128))).to(gpu_device)
+    out = []
+    for _ in range(2):
+        zt = zt0.clone()
+        am.reverse_sweep(Q, xemb, zt, seed=99)
+        out.append(zt.cpu().numpy())
+    assert np.array_equal(out[0], out[1])
