@@ -812,14 +812,14 @@ constexpr int X3_AJ = X3_BM * X3_CHUNKS / 512, X3_BJ = X3_BN * X3_CHUNKS / 512;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// V: variant bits (tools/gemm_bench.hip A/B): 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
+// V: variant bits (tools/gemm_bench.hip A/B): 256 = fragment reads in MFMA order (below), 1 = v_mfma_f32_16x16x32_bf16 on a 4x4 grid of 16x16 tiles per
 // wave, 2 = s_setprio(1) around the MFMA cluster, 4 = LDS-DMA staging (buffer_load ... lds straight into
 // the lane-linear LDS image, issued one K tile ahead; no staging registers or ds_write), 16 = supertile
 // raster (32 = one MFMA accumulation chain over all of K: no blocking, no sign alternation; A/B only) (a 1-D grid; each XCD's 32 concurrent workgroups form a block of <= 8 M tiles x 4 (N tile, phase) pairs
 // with the 4 phases of an N tile adjacent, so the phases' overlapping input windows and the weight panels are
 // shared in L2 instead of every XCD streaming all phases' panels; DMA and non-WGRAD only)
 #ifndef DAMC_X3_VARIANT
-#define DAMC_X3_VARIANT 5  // measured best (profiles/r01/gemm_bench.txt)
+#define DAMC_X3_VARIANT 261  // measured best (profiles/r02/gemm_bench_rdorder.txt; round 1: 5)
 #endif
 // RNE limb split of 8 consecutive values: v = h + m + l (to 24 significand bits)
 __device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
@@ -1103,7 +1103,64 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     // barrier at the end of this tile (its vmcnt(0)) lands it
     // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
     if (DMA && kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
-    if (M16) {
+    if (M16 && (V & 256)) {
+      // 256: fragment reads one group ahead of the MFMAs that consume them, in the order those MFMAs run (A tile 0
+      // against B tiles 0..3, then A tiles 1..3), pinned by sched_group_barrier: the first MFMAs wait for 6 reads
+      // instead of the ~15 the default schedule puts in front of its first lgkmcnt(0).  2.5-3.9 % less time on
+      // the four CIFAR shapes, bit-identical results (profiles/r02/gemm_bench_rdorder.txt).  Measured and dropped:
+      // reading the next tile's first fragments after the barrier into the registers the trailing MFMAs free
+      // (cross-tile pipeline, 1-2 % slower than this), all reads issued by the end of A row 0 so the barrier moves
+      // up (5-8 % slower), A tile 3 read later so it moves down (0-2 % slower).
+      bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
+      auto rd_a = [&](int t) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
+      };
+      auto rd_b = [&](int t) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
+      };
+      auto mf = [&](int i, int j) {
+        f32x4 c = acc16[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+        acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+      };
+      rd_a(0);
+      rd_b(0);
+      rd_b(1);
+      mf(0, 0);
+      rd_b(2);
+      mf(0, 1);
+      rd_b(3);
+      mf(0, 2);
+      rd_a(1);
+      mf(0, 3);
+      rd_a(2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mf(1, j);
+      rd_a(3);
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mf(i, j);
+      constexpr int SG_MFMA = 0x8, SG_DS_RD = 0x100;
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 9, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 48, 0);
+    } else if (M16) {
       bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
 #pragma unroll
       for (int t = 0; t < 4; ++t)
