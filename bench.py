@@ -381,11 +381,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # DAMC_DIST_BACKEND=gloo (tests only): several ranks sharing one GPU (RCCL needs one GPU per rank); the
+    # driver's multi-GPU runs use the default, nccl = RCCL over xGMI
+    backend = os.environ.get("DAMC_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if dist:
         import torch.distributed as tdist
 
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     device = torch.device("cuda", local)
 
     from damc import _lib
@@ -446,7 +454,7 @@ def main():
 
     t_max = elapsed
     if dist:
-        t = torch.tensor([elapsed], device=device)
+        t = torch.tensor([elapsed], device=device if backend == "nccl" else "cpu")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         t_max = float(t.item())
 
@@ -535,6 +543,9 @@ def main():
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(out))
+    dump = os.environ.get("DAMC_BENCH_DUMP")
+    if dump:  # tests only: this rank's chains after its last block, with its slice of the global batch
+        torch.save({"z": zbuf.cpu(), "p": pbuf.cpu(), "plan": dict(plan)}, os.path.join(dump, "rank%d.pt" % rank))
     if dist:
         tdist.destroy_process_group()
 

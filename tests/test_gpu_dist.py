@@ -1,0 +1,69 @@
+"""The multi-GPU path of bench.py end to end on one MI355X: two ranks launched by torch.distributed.run share the
+GPU over the gloo backend (RCCL needs one GPU per rank; the driver's 8-GPU runs use nccl = RCCL).  Each rank runs
+its slice of the BASELINE Langevin block on the HIP path (damc.dist.block_plan, chain_base = the slice start) and
+the ranks' timings go through the MAX all-reduce.  Checks: the JSON line's multi-rank fields, and — strong
+scaling — the union of the two ranks' chains is bitwise the 1-rank block (posterior and prior chains), because
+the Philox noise is keyed by the global chain index and nothing else couples the chains."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(tmp, world, scaling):
+    env = dict(os.environ, DAMC_DIST_BACKEND="gloo", DAMC_BENCH_DUMP=str(tmp))
+    args = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
+            "--scaling", scaling]
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    r = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    return json.loads(line)
+
+
+def test_two_ranks_strong_scaling_union_is_the_one_rank_block(tmp_path, gpu_device):
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    j1 = _run(one, 1, "strong")
+    j2 = _run(two, 2, "strong")
+    assert j2["n_gpus"] == 2 and j2["scaling"] == "strong"
+    assert j2["config"]["global_batch"] == 128 and j2["config"]["per_rank_batch"] == 64
+    assert j2["value"] > 0 and j1["value"] > 0
+    ref = torch.load(one / "rank0.pt", weights_only=True)
+    parts = [torch.load(two / ("rank%d.pt" % r), weights_only=True) for r in range(2)]
+    assert [p["plan"]["post_start"] for p in parts] == [0, 64]
+    assert [p["plan"]["prior_start"] for p in parts] == [0, 128]
+    z = torch.cat([p["z"] for p in parts])
+    pz = torch.cat([p["p"] for p in parts])
+    assert torch.isfinite(z).all() and torch.isfinite(pz).all()
+    assert torch.equal(z, ref["z"]), "posterior chains of the 2-rank block differ from the 1-rank block"
+    assert torch.equal(pz, ref["p"]), "prior chains of the 2-rank block differ from the 1-rank block"
+
+
+def test_two_ranks_weak_scaling_line(tmp_path, gpu_device):
+    j = _run(tmp_path, 2, "weak")
+    assert j["n_gpus"] == 2 and j["scaling"] == "weak"
+    assert j["config"]["per_rank_batch"] == 128
+    parts = [torch.load(tmp_path / ("rank%d.pt" % r), weights_only=True) for r in range(2)]
+    assert [p["plan"]["post_start"] for p in parts] == [0, 128]
+    # distinct global chains: the two ranks' noise streams differ, so their chains do too
+    assert not torch.equal(parts[0]["z"], parts[1]["z"])
