@@ -83,6 +83,10 @@ int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hip
 // the same reordered for the channel-major K walk: a row's K = taps * Cg values [tap][c] are stored
 // [c / sw][tap][c % sw] (sw channels per slice), sign blocks counted in that order
 int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s);
+// the x3 copy of a conv weight (rows of K = taps * Cg) in the order the library's limb-engine kernels walk K:
+// slice-major with sign-alternating blocks when the default variant walks channel-major (DAMC_X3_VARIANT & 8),
+// else tap-major (launch_split_x3_negblk)
+int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s);
 
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);

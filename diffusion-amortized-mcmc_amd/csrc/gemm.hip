@@ -1432,6 +1432,11 @@ int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned
   return (int)hipGetLastError();
 }
 
+int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s) {
+  if ((DAMC_X3_VARIANT & 8) != 0 && Cg % 32 == 0) return launch_split_x3_cmaj(x, n, K, Cg, 32, y, s);
+  return launch_split_x3_negblk(x, n, K, y, s);
+}
+
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
   if (n % 8 != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0) return DAMC_ERR_ARG;
   const long n8 = n / 8;

@@ -1592,10 +1592,11 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
                          (int)damc::conv_kmajor_ok(L->cout), wf, wb);
       // x3 copies with sign-alternating K blocks (gemm.h GemmArgs::b_negblk): rows of 4 Cin (forward, per phase
       // and output channel) and 16 Cout (input gradient, per input channel)
+      // (in the K order the limb-engine kernels walk: damc::launch_split_x3_conv)
       if (x3_fwd_cap(*L))
-        DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wf, n, 4 * L->cin, reinterpret_cast<unsigned short*>(wf + n), s));
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wf, n, 4 * L->cin, L->cin, reinterpret_cast<unsigned short*>(wf + n), s));
       if (x3_bwd_cap(*L))
-        DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wb, n, 16 * L->cout, reinterpret_cast<unsigned short*>(wb + n), s));
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wb, n, 16 * L->cout, L->cout, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_SMALLC:
       if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));
