@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, 
 // of per-pixel global gathers; lanes own 4 channels of a pixel and each wave walks its pixels UNR at a
 // time (UNR activation loads in flight).  Output: the masked gradient as fp32 in place, or (h3) as x3
 // limbs only, lane pairs exchanging halves so every store is a whole 16-B limb octet.
-template <int NC, int UNR>
+template <int NC, int UNR, bool PF = false>
 __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict__ h, int Hin, int Win, int Cin,
                                                               int R, const float* __restrict__ wpk,
                                                               const float* __restrict__ delta, int mask_act,
@@ -535,6 +535,15 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
   __syncthreads();
   const int npix = rows * Win;
   const long pbase = ((long)b * Hin + y0) * Win;
+  // PF (sign-bit masks): the next iteration's mask nibbles are loaded while this one computes
+  unsigned mbn[UNR];
+  if (PF && hbits) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pl = wave * P * UNR + u * P + sub;
+      mbn[u] = pl < npix ? (hbits[((pbase + pl) * Cin + ci0) >> 3] >> (ci0 & 4)) & 15u : 0u;
+    }
+  }
   for (int p0 = wave * P * UNR; p0 < npix; p0 += 4 * P * UNR) {
     // the LReLU' mask source: the fp32 activation, or (hbits) its sign bits (nibble of this lane's 4 channels)
     f32x4 hv[UNR];
@@ -542,7 +551,12 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int pl = p0 + u * P + sub;
-      if (hbits) {
+      if (PF && hbits) {
+        mb[u] = mbn[u];
+        const int pn = pl + 4 * P * UNR;
+        mbn[u] = pn < npix ? (hbits[((pbase + pn) * Cin + ci0) >> 3] >> (ci0 & 4)) & 15u : 0u;
+        hv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else if (hbits) {
         mb[u] = pl < npix ? (hbits[((pbase + pl) * Cin + ci0) >> 3] >> (ci0 & 4)) & 15u : 0u;
         hv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
@@ -839,15 +853,17 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
   if (hbits_in && (!smallc_k3(L) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
   if (smallc_k3(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
-    const int R = 4;
+    // 8 rows per block with the next mask nibbles prefetched: 66.4 us vs 69.9 (4 rows, no prefetch) at the
+    // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us)
+    const int R = 8;
     const dim3 grid((unsigned)((L.hin + R - 1) / R), (unsigned)B);
     const size_t sm = sizeof(float) * (R + 2) * (L.win + 2) * 4;
     if (L.cout == 3)
-      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
-                         delta, mask_act, mask_slope, h3, hbits_in);
+      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, 4, true>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R,
+                         L.w_fwd, delta, mask_act, mask_slope, h3, hbits_in);
     else
-      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<1, 4>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R, L.w_fwd,
-                         delta, mask_act, mask_slope, h3, hbits_in);
+      hipLaunchKernelGGL((smallc_dgrad_k3_kernel<1, 4, true>), grid, dim3(256), sm, s, h, L.hin, L.win, L.cin, R,
+                         L.w_fwd, delta, mask_act, mask_slope, h3, hbits_in);
     return (int)hipGetLastError();
   }
   if (smallc_reg_ok(L)) {

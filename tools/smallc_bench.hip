@@ -3,17 +3,19 @@
 // forward, timed in one process.
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DDAMC_GEMM_NO_C_API tools/smallc_bench.hip -o tools/smallc_bench
 #include <cstdio>
+#include <type_traits>
 #include <vector>
 
 #include "../diffusion-amortized-mcmc_amd/csrc/gemm.hip"
 #include "../diffusion-amortized-mcmc_amd/csrc/generator.hip"
+#include "../diffusion-amortized-mcmc_amd/csrc/wgrad.hip"
 
 namespace damc_prof {
 bool enabled() { return false; }
 int begin(const char*, double, hipStream_t) { return -1; }
 void end(int, hipStream_t) {}
 }  // namespace damc_prof
-int damc_launch_posterior_update(const damc_ebm_t*, float*, const float*, int, long, int, int, float, int,
+int damc_launch_posterior_update(const damc_ebm_t*, float*, const float*, int, long, int, int, double, int,
                                  const float*, uint64_t, uint64_t, uint64_t, float*, hipStream_t) {
   return 0;
 }
@@ -98,6 +100,25 @@ int main() {
   timeit("dgrad bit mask, limb out", act * 1.5 + act / 32, [&] {
     smallc_dgrad(L, h, B, delta, DAMC_ACT_LRELU, 0.2f, h3, bits, s);
   });
+  // limb-output dgrad geometry sweep (rows per block R, pixels in flight per wave UNR) and the write floor
+  timeit("write floor: hipMemset of the limb out", act * 1.5, [&] { CK(hipMemsetAsync(h3, 0, npix * C * 6, s)); });
+  auto k3 = [&](int R, auto unr, auto pf) {
+    constexpr int U = decltype(unr)::value;
+    constexpr bool PFv = decltype(pf)::value;
+    const dim3 grid((unsigned)((H + R - 1) / R), (unsigned)B);
+    const size_t sm = sizeof(float) * (R + 2) * (H + 2) * 4;
+    hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, U, PFv>), grid, dim3(256), sm, s, h, H, H, C, R, L.w_fwd, delta,
+                       (int)DAMC_ACT_LRELU, 0.2f, h3, bits);
+  };
+  char nm[64];
+  for (int R : {4, 8, 16}) {
+    snprintf(nm, sizeof(nm), "k3 bits->limbs R=%d UNR=4", R);
+    timeit(nm, act * 1.5 + act / 32, [&] { k3(R, std::integral_constant<int, 4>(), std::false_type()); });
+    snprintf(nm, sizeof(nm), "k3 bits->limbs R=%d UNR=4 PF", R);
+    timeit(nm, act * 1.5 + act / 32, [&] { k3(R, std::integral_constant<int, 4>(), std::true_type()); });
+    snprintf(nm, sizeof(nm), "k3 bits->limbs R=%d UNR=2 PF", R);
+    timeit(nm, act * 1.5 + act / 32, [&] { k3(R, std::integral_constant<int, 2>(), std::true_type()); });
+  }
   CK(hipGetLastError());
   return 0;
 }
