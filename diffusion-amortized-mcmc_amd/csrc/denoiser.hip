@@ -314,8 +314,12 @@ __device__ __forceinline__ void st_sc1_f(float* p, float v) {
 // slots, so no address is ever rewritten within a sweep.  Every wait is bounded: past the budget (or once any
 // workgroup has failed) the workgroup records the failure in the error word and leaves, so the grid drains, and
 // the copy-out writes NaN into zt.
-constexpr int TS_THREADS = 320;  // waves 0-3 compute (K in quarters), wave 4 polls and publishes
+// waves 0-3 compute (K in quarters), wave 4 polls, wave 5 stores the slot's flag: a poll issued behind the same
+// wave's flag store would return only after that store's write-through ack (loads and stores share vmcnt, in order)
+constexpr int TS_THREADS = 384;
+constexpr int TS_PUB = 320;  // the publishing lane
 constexpr int TS_MAXT = 64;     // slots per team (CUs per XCD)
+constexpr int TS_TAB_STEPS = 256;  // steps whose schedule rows are kept in LDS
 
 struct TsBlock {
   const float* w;    // packed [ntn][16][kp] (workspace)
@@ -347,7 +351,8 @@ struct TsArgs {
   uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin, wait end, reduced,
                       // published}
   int dbg;            // timing experiments only (DAMC_SWEEP_DBG, wrong results): 1 no drain before the flag,
-                      // 2 no payload loads, 4 no MFMA, 8 no epilogue operand loads, 16 no output stores
+                      // 2 no payload loads, 4 no MFMA, 8 no epilogue operand loads, 16 no output stores,
+                      // 32 no zB / sin / cos (in0), 64 no z loads (in0)
 };
 
 // number of column tiles of block b that slot t owns, and the first one
@@ -363,7 +368,7 @@ __device__ __forceinline__ int ts_tiles(const TsBlock& b, int T, int t, int* tn0
 // inside).  One poll in flight: three staggered ones measured 4-5 % slower per sweep.
 constexpr int TS_FS = 32;  // flag stride, unsigned
 __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need, int* err, long budget, int* sflag) {
-  if (threadIdx.x >= 256) {
+  if (threadIdx.x >= 256 && threadIdx.x < 320) {
     const int lane = threadIdx.x - 256;
     int ok = 1;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -465,6 +470,8 @@ __device__ __forceinline__ void ts_mfma(f32x4& acc, const float* wl, int kps, co
 __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   __shared__ int sflag;
+  __shared__ uint64_t trs[3];                    // tools only: this stage's stamps
+  __shared__ float tabs[8 * TS_TAB_STEPS];       // the step table (n <= TS_TAB_STEPS)
   __shared__ int lbase[7];                       // LDS float offset of block j's first owned tile
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [wlds weights][TM][emb_ld(kpa0)] in0 image
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -479,6 +486,8 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   float* const embs = lds + a.wlds;
   const int ld0 = emb_ld(a.b[0].kpa);
 
+  if (a.n <= TS_TAB_STEPS)
+    for (int i = tid; i < 8 * a.n; i += TS_THREADS) tabs[i] = a.tab[i];
   // ---- the owned weight tiles into LDS, fragment order: (half, wave, k-group, lane) -> f32x4
   if (tid == 0) {
     int off = 0;
@@ -539,7 +548,16 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   }
 
   for (int k = 0; k < a.n; ++k) {
-    const float* tb = a.tab + 8 * k;
+    // the step's schedule row from LDS (a per-step scalar load from memory missed the scalar cache every step and
+    // held the in0 stage's first LDS wait ~1 us)
+    float tb[7];
+    if (a.n <= TS_TAB_STEPS) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) tb[i] = tabs[8 * k + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) tb[i] = a.tab[8 * k + i];
+    }
     const float c0 = tb[0], c1 = tb[1], c2 = tb[2], c3 = tb[3], c4 = tb[4];
     const bool last = tb[5] != 0.f;
     const int noisy_k = (int)tb[6];
@@ -554,9 +572,11 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       const unsigned s = 7u * k + j;
       int tn0;
       const int nt = ts_tiles(b, T, slot, &tn0);
-      uint64_t* tr = (a.trace && tid == 256) ? a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4 : nullptr;
+      // tools only: the poll wave keeps its stamps in LDS (a global store in front of its poll would delay it);
+      // the publishing lane writes them out after the flag
+      const bool tr = a.trace != nullptr && tid == 256;
       if (nt == 0) {  // nothing to compute: publish at once (this slot's earlier stores are drained)
-        if (tid == 256) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == TS_PUB) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
       const bool final_ = j == 6;
@@ -606,9 +626,9 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
 
           // ---- wait for stage s - 1 of the team (once per stage)
           if (!waited) {
-            if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+            if (tr) trs[0] = __builtin_amdgcn_s_memrealtime();
             if (s > 0 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag)) return;
-            if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
+            if (tr) trs[1] = __builtin_amdgcn_s_memrealtime();
             known = s;
             waited = true;
           }
@@ -618,9 +638,10 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
 #pragma unroll
             for (int g = 0; g < EMB_G; ++g) {
               const int kk = 16 * g + 4 * q;
-              zv4[g] = (cw && xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+              zv4[g] = (cw && xok && kk < nz && !(a.dbg & 64)) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4)
+                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            if (cw && wave * 16 < half) {  // wave w: B^T columns 16 w .. 16 w + 15 (nz <= 128), in registers
+            if (cw && wave * 16 < half && !(a.dbg & 32)) {  // wave w: B^T columns 16 w .. 16 w + 15 (nz <= 128), in registers
               const int tt = wave;
               const int col = tt * 16 + m;
               const bool cok = col < half;
@@ -669,7 +690,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
             for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
           }
           __syncthreads();
-          if (tr && i == 0 && rt == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
+          if (tr && i == 0 && rt == 0) trs[2] = __builtin_amdgcn_s_memrealtime();
           if (eok) {
             float l = 0.f, sk = 0.f;
 #pragma unroll
@@ -703,8 +724,14 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       // publish: every storing wave has drained, then one lane stores the slot's flag
       if (!(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 256) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+      if (tid == TS_PUB) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.trace && tid == TS_PUB) {
+        uint64_t* tg = a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4;
+        tg[0] = trs[0];
+        tg[1] = trs[1];
+        tg[2] = trs[2];
+        tg[3] = __builtin_amdgcn_s_memrealtime();
+      }
     }
   }
 }
@@ -1165,7 +1192,7 @@ bool team_enabled() {
   return !(e && e[0] == '0');
 }
 
-constexpr size_t TS_LDS_MAX = 160 * 1024 - 8 * 1024;  // dynamic LDS a workgroup may take (static red etc. aside)
+constexpr size_t TS_LDS_MAX = 160 * 1024 - 16 * 1024;  // dynamic LDS a workgroup may take (static red, tabs etc. aside)
 constexpr size_t TS_LDS_MIN = 84 * 1024;              // > half the CU's LDS: one workgroup per CU
 
 // slots per team on this device: CUs / 8 (0 when the CUs do not split into 8 XCD groups)
