@@ -1257,6 +1257,19 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
   size_t sm = (size_t)(wl + (long)TM * emb_ld(a->b[0].kpa)) * sizeof(float);
   if (sm > TS_LDS_MAX) return DAMC_ERR_UNSUPPORTED;
   sm = std::max(sm, TS_LDS_MIN);
+  {  // every workgroup must be resident (one per CU): otherwise the launch chain
+    static std::mutex mu;
+    static size_t ok_sm[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return DAMC_ERR_UNSUPPORTED;
+    std::lock_guard<std::mutex> lk(mu);
+    if (ok_sm[dev] != sm) {
+      int per = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel, TS_THREADS, sm) != hipSuccess || per < 1)
+        return DAMC_ERR_UNSUPPORTED;
+      ok_sm[dev] = sm;
+    }
+  }
   a->bmat = w.bmat;
   a->nz = d->nz;
   a->B = B;
