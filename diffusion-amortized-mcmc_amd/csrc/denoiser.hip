@@ -1304,15 +1304,52 @@ __global__ void team_copyout_kernel(const float* src, float* dst, long n, const 
   if (i < n) dst[i] = *err ? __builtin_nanf("") : src[i];
 }
 
-int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t s) {
-  const int n = a.n;
-  std::vector<float> tab(8 * (size_t)n, 0.f);  // c0..c4, is_last, noisy_k
+// the step table (c0..c4, is_last, noisy_k per step) of a schedule, uploaded once per (device, schedule) and kept:
+// a sweep then copies nothing from the host, so it can be captured into a HIP graph (after one eager call with
+// the same schedule, as torch.cuda.graphs' warm-up does)
+struct TabEntry {
+  int dev;
+  std::vector<float> key;
+  float* d;
+};
+std::mutex g_tab_mu;
+std::vector<TabEntry> g_tabs;
+
+int step_table(const float* coef, int n, hipStream_t s, const float** out) {
+  int dev = 0;
+  DAMC_CHECK(hipGetDevice(&dev));
+  std::vector<float> key(coef, coef + 6 * (size_t)n);
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  for (const TabEntry& e : g_tabs)
+    if (e.dev == dev && e.key == key) {
+      *out = e.d;
+      return 0;
+    }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  DAMC_CHECK(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) return DAMC_ERR_UNSUPPORTED;  // first use of a schedule inside a capture
+  std::vector<float> tab(8 * (size_t)n, 0.f);
   for (int k = 0, noisy = 0; k < n; ++k) {
     for (int i = 0; i < 6; ++i) tab[8 * k + i] = coef[6 * (size_t)k + i];
     tab[8 * k + 6] = (float)noisy;
     if (coef[6 * (size_t)k + 5] == 0.f) ++noisy;
   }
-  DAMC_CHECK(hipMemcpyAsync(const_cast<float*>(a.tab), tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  float* d = nullptr;
+  DAMC_CHECK(hipMalloc(&d, tab.size() * sizeof(float)));
+  DAMC_CHECK(hipMemcpy(d, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (g_tabs.size() >= 64) {  // a handful of schedules per process in practice
+    (void)hipFree(g_tabs.front().d);
+    g_tabs.erase(g_tabs.begin());
+  }
+  g_tabs.push_back(TabEntry{dev, std::move(key), d});
+  *out = d;
+  return 0;
+}
+
+int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t s) {
+  const int n = a.n;
+  int rc = step_table(coef, n, s, &a.tab);
+  if (rc) return rc;
   DAMC_CHECK(hipMemsetAsync(a.flags, 0, (8 * TS_MAXT * TS_FS + 64) * sizeof(unsigned), s));  // flags + error word
   static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
   const size_t tbytes = (size_t)P * 7 * n * 4 * sizeof(uint64_t);
@@ -1544,7 +1581,12 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   TsArgs ta;
   int tP = 0;
   size_t tsm = 0;
-  const bool team = team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
+  // inside a caller's stream capture the sweep records the launch chain's kernels eagerly into the caller's graph
+  // (a replayed team launch timed out its waits in tests/test_gpu_graph.py)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  DAMC_CHECK(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  const bool team = !capturing && team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
   hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, call, w.call, zt,
                      team ? w.zring : w.z, nzb);
   DAMC_LAUNCH_CHECK();
@@ -1554,7 +1596,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     ProfScope ps("denoise_chain", flops_step * n, s);
     if (team) {
       if ((rc = run_chain_team(ta, tP, tsm, coef, s))) return rc;
-    } else if (allow_graph && graphs_enabled()) {
+    } else if (allow_graph && graphs_enabled() && !capturing) {
       if ((rc = run_chain_graph(d, w, wsp, wsb, B, n, coef, s))) return rc;
       chain_trace_dump(s);
     } else {
