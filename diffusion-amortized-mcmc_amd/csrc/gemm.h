@@ -67,7 +67,15 @@ struct GemmArgs {
   // limb engine: B3 holds -B on the odd blocks of X3_NEGK consecutive k of every row (launch_split_x3_negblk),
   // and the kernel subtracts those blocks' sums (the MFMA's truncation bias then alternates sign; gemm.hip)
   int b_negblk = 0;
+  // limb engine, O_PHASE / O_DENSE: split-K over ksplit slices of k_per_z (a multiple of X3_NEGK) when the grid
+  // would under-fill the chip; the slices' fp32 tiles go to kslab [zdim * ksplit][M][N] and a fixed-order reduce
+  // applies the epilogue.  kslab = scratch the caller owns (kslab_floats of it); null: never split
+  int ksplit = 1;
+  float* kslab = nullptr;
+  long kslab_floats = 0;
 };
+// slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
+long x3_ksplit_floats(int M, int N, int K, int zdim);
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
 // channel count is a multiple of its K tile; weight packers pick the B layout with this predicate.

@@ -864,14 +864,21 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 
   int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
   const unsigned short* Bg = p.B3;
+  // split-K (O_PHASE / O_DENSE): z = phase * ksplit + slice
+  const bool KSPLIT = OM != O_WGRAD && p.ksplit > 1;
+  const int zph = KSPLIT ? z / p.ksplit : z, zsl = KSPLIT ? z - zph * p.ksplit : 0;
   if (OM == O_PHASE) {
-    py = z >> 1;
-    px = z & 1;
+    py = zph >> 1;
+    px = zph & 1;
     pad_y = 1 - py;
     pad_x = 1 - px;
-    Bg += (long)z * p.b_zstride * 3;
+    Bg += (long)zph * p.b_zstride * 3;
   }
   int kbeg = 0, kend = p.K;
+  if (KSPLIT) {
+    kbeg = zsl * p.k_per_z;
+    kend = min(p.K, kbeg + p.k_per_z);
+  }
   if constexpr (OM == O_WGRAD) {  // z = phase * slices + split-K slice
     const int nsl = gridDim.z / p.wg_phases;
     const int ph = z / nsl, sl = z - ph * nsl;
@@ -889,7 +896,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   const int Cg = p.Cg, kw = p.kw, Win = p.Win;
   const int kh = p.K / Cg / kw;
-  const int nk = (OM == O_WGRAD) ? max(kend - kbeg, 0) / X3_BK : p.K / X3_BK;
+  const int nk = (OM == O_WGRAD || KSPLIT) ? max(kend - kbeg, 0) / X3_BK : p.K / X3_BK;
+  const int kt0 = kbeg / X3_BK;  // global index of the first K tile (sign blocks follow the global index)
   const int hwq = p.Hq * p.Wq;
   const int nimg = (p.M + hwq - 1) / hwq;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
@@ -943,6 +951,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
 
   int tap = 0, ci0 = 0, tky = 0, tkx = 0;
+  if (OM != O_WGRAD && kbeg > 0) {  // a split slice starts mid-walk (tap-major: K tile = (tap, 32 channels))
+    tap = kbeg / Cg;
+    ci0 = kbeg - tap * Cg;
+    tky = tap / kw;
+    tkx = tap - tky * kw;
+  }
   unsigned aoff[X3_AJ];
   auto set_tap = [&]() {
     const int toff = (tky * Win + tkx) * Cg * 6;
@@ -1224,7 +1238,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
     // (a flush between them and the barrier measured 6-8 % slower)
     if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
-      const float sg = (p.b_negblk && ((kt / FLUSH) & 1)) ? -1.f : 1.f;
+      const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
       if (M16) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1250,7 +1264,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   // the last partial block
   {
-    const float sg = (p.b_negblk && nk > 0 && (((nk - 1) / FLUSH) & 1)) ? -1.f : 1.f;
+    const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
     if (M16) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -1293,6 +1307,19 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
               acc[i][j][r];
   }
   __syncthreads();
+  if (KSPLIT) {  // this slice's raw fp32 tile into the slab; x3_ksplit_reduce_kernel applies the epilogue
+    float* sl = p.kslab + (long)z * p.M * p.N;
+#pragma unroll 2
+    for (int it = 0; it < X3_BM * X3_BN / 8 / 512; ++it) {
+      const int id = tid + 512 * it, row = id >> 4, oct = id & 15;
+      const int m = m0 + row, n = n0 + oct * 8;
+      if (m >= p.M || n >= p.N) continue;
+      float* d = sl + (long)m * p.N + n;
+      *reinterpret_cast<f32x4*>(d) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8);
+      *reinterpret_cast<f32x4*>(d + 4) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8 + 4);
+    }
+    return;
+  }
   float* Cz = p.C;
   if ((OM == O_DENSE || OM == O_WGRAD) && Cz) Cz += (long)z * p.c_zstride;
 #pragma unroll 2
@@ -1350,9 +1377,107 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
 }
 
+// the split-K reduce: one thread per (phase, row, channel octet); the slices in fixed order, then the limb GEMM's
+// epilogue (bias + act or the LReLU' mask, sign bits, fp32 and limb outputs) on the sum
+template <int EPI, int OM>
+__global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int noct = p.N / 8;
+  if (i >= (long)zdim * p.M * noct) return;
+  const int oct = (int)(i % noct);
+  const long r = i / noct;
+  const int m = (int)(r % p.M), ph = (int)(r / p.M);
+  const int py = OM == O_PHASE ? ph >> 1 : 0, px = OM == O_PHASE ? ph & 1 : 0;
+  const int n = oct * 8;
+  // the blocks in order from 0: each add the kernel's fmaf(sign, block, tot) with the sign already applied
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int sl = 0; sl < p.ksplit; ++sl) {
+    const float* src = p.kslab + ((long)(ph * p.ksplit + sl) * p.M + m) * p.N + n;
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 t1 = *reinterpret_cast<const f32x4*>(src + 4);
+    v[0] += t0.x; v[1] += t0.y; v[2] += t0.z; v[3] += t0.w;
+    v[4] += t1.x; v[5] += t1.y; v[6] += t1.z; v[7] += t1.w;
+  }
+  const long idx = gemm_row_offset<OM>(p, m, py, px) + n;
+  if (EPI == EPI_BIAS_ACT) {
+    if (p.bias) {
+      const int nb = p.bias_mod < p.N ? n % p.bias_mod : n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.bias[nb + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = act_apply(v[e], p.act, p.slope);
+  } else if (EPI == EPI_MASK) {
+    if (p.mask_sgn) {
+      const unsigned bits = p.mask_sgn[idx >> 3];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= ((bits >> e) & 1u) ? 1.f : p.mask_slope;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= act_grad_from_out(p.mask[idx + e], p.mask_act, p.mask_slope);
+    }
+  }
+  if (p.sgn) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bits |= (v[e] > 0.f ? 1u : 0u) << e;
+    p.sgn[idx >> 3] = (unsigned char)bits;
+  }
+  if (p.C) {
+    *reinterpret_cast<f32x4*>(p.C + idx) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(p.C + idx + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+  if (p.C3) {
+    bf16x8 h, mm, l;
+    split3_octet(v, h, mm, l);
+    bf16x8* o = reinterpret_cast<bf16x8*>(p.C3 + 3 * idx);
+    o[0] = h;
+    o[1] = mm;
+    o[2] = l;
+  }
+}
+
+// split-K plan of a limb-engine conv: an under-filled grid (< 192 workgroups) splits K into its X3_NEGK sign blocks,
+// one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
+// the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
+// unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
+int x3_ksplit(int M, int N, int K, int zdim) {
+  // DAMC_X3_KSPLIT=0 disables; DAMC_X3_KSPLIT_WGS: the grid size below which a conv splits (A/B)
+  static const bool on = [] {
+    const char* e = getenv("DAMC_X3_KSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  static const long below = [] {
+    const char* e = getenv("DAMC_X3_KSPLIT_WGS");
+    return e ? atol(e) : 128L;
+  }();
+  const long wgs = (long)((M + X3_BM - 1) / X3_BM) * ((N + X3_BN - 1) / X3_BN) * zdim;
+  if (!on || wgs >= below || K % X3_NEGK != 0 || K / X3_NEGK < 2) return 1;
+  return K / X3_NEGK;
+}
+
+long x3_ksplit_floats(int M, int N, int K, int zdim) {
+  const int ks = x3_ksplit(M, N, K, zdim);
+  return ks > 1 ? (long)zdim * ks * M * N : 0;
+}
+
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
-static void launch_x3_t(const GemmArgs& a, int zdim, hipStream_t s) {
+static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
+  GemmArgs a = a0;
   const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
+  if (OM != O_WGRAD && a.kslab && !(V & 16)) {
+    const int ks = x3_ksplit(a.M, a.N, a.K, zdim);
+    if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
+      a.ksplit = ks;
+      a.k_per_z = a.K / ks;
+      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks), dim3(512), 0, s, a);
+      const long tot = (long)zdim * a.M * (a.N / 8);
+      hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, OM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
+                         zdim);
+      return;
+    }
+  }
+  a.ksplit = 1;
   if ((V & 16) && OM != O_WGRAD)  // supertile raster: phases folded into a 1-D grid
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
   else

@@ -1049,6 +1049,8 @@ struct Workspace {
   float* slabs;           // split-K partial gradients
   float* glik;            // their fixed-order sum: grad of the likelihood term (B, nz)
   float* pbuf;            // per-tap projections of the output layer (two-stage forward)
+  float* kslab;           // split-K slabs of the limb-engine convolutions at small batch (or nullptr)
+  long kslab_floats;
   int nslab;
   size_t bytes;
 };
@@ -1089,7 +1091,18 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   float* pb = (F.kind == DAMC_LAYER_SMALLC) ? take((long)B * F.hin * F.win * smallc_ntile(F) * 32) : nullptr;
   unsigned short* z3 =
       x3_proj_cap(L0) ? reinterpret_cast<unsigned short*>(take((long)B * g->nz * 3 / 2 + 4)) : nullptr;
+  // split-K slabs: the largest any UP2 forward / input gradient of this batch uses (damc::x3_ksplit)
+  long ksf = 0;
+  for (int i = 0; i < g->n_layers; ++i) {
+    const damc_layer_t& L = g->layers[i];
+    if (L.kind != DAMC_LAYER_UP2) continue;
+    if (x3_fwd_cap(L)) ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cout, 4 * L.cin, 4));
+    if (x3_bwd_cap(L)) ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cin, 16 * L.cout, 1));
+  }
+  float* ks = ksf ? take(ksf) : nullptr;
   if (w) {
+    w->kslab = ks;
+    w->kslab_floats = ksf;
     w->z3 = z3;
     w->delta = d;
     w->slabs = sl;
@@ -1203,6 +1216,8 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
         }
         if (hbits(g, i)) a.sgn = ws.hb[i];
         if (!h_f32(g, i)) a.C = nullptr;
+        a.kslab = ws.kslab;  // split-K when the batch leaves the grid under-filled
+        a.kslab_floats = ws.kslab_floats;
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
@@ -1298,6 +1313,8 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
         a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
         a.b_negblk = 1;
+        a.kslab = ws.kslab;
+        a.kslab_floats = ws.kslab_floats;
         if (hbits(g, i - 1)) {
           a.mask_sgn = ws.hb[i - 1];
           a.mask = nullptr;
