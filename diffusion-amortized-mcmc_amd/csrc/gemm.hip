@@ -1443,10 +1443,8 @@ __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
 // unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
 int x3_ksplit(int M, int N, int K, int zdim) {
   // DAMC_X3_KSPLIT=0 disables; DAMC_X3_KSPLIT_WGS: the grid size below which a conv splits (A/B)
-  static const bool on = [] {
-    const char* e = getenv("DAMC_X3_KSPLIT");
-    return !(e && e[0] == '0');
-  }();
+  const char* ev = getenv("DAMC_X3_KSPLIT");  // per call: tests compare both paths in one process
+  const bool on = !(ev && ev[0] == '0');
   static const long below = [] {
     const char* e = getenv("DAMC_X3_KSPLIT_WGS");
     return e ? atol(e) : 128L;

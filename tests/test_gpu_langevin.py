@@ -333,3 +333,26 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
     whole = grads(False)
     for a, b in zip(split, whole):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [4, 16])
+def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
+    """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one 256-k sign block per slice, reduced
+    in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
+    width with DAMC_X3_KSPLIT=0 vs the default."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=128, nc=3), 0).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, 128))).to(gpu_device)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_X3_KSPLIT", mode)
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
+        torch.cuda.synchronize()
+        out[mode] = z.cpu()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
