@@ -169,6 +169,8 @@ def langevin_breakdown(lv, G, E, x, z0, p0, zbuf, pbuf, plan):
 # SURVEY.md §8(d) per-config posterior work (4 B MAC_G FLOP per batch-step) and BASELINE configs 2/4/5 at
 # their per-rank sizes on one GPU: (name, generator ctor, nz, ngf, image, B, steps, sigma)
 CONFIG_LEGS = (
+    ("cifar10 B=16 (headline config, strong scaling per rank of 8)", "_netG_cifar10", 128, 128, 32, 16, 10, 0.1,
+     1089.2e6),
     ("svhn B=64 (config 2)", "_netG_svhn", 100, 64, 32, 64, 30, 0.1, 69.5e6),
     ("celeba64 B=32 (config 4, per rank of 8)", "_netG_celeba64", 100, 128, 64, 32, 10, 0.1, 410.6e6),
     ("celeba64 B=256 (config 4, one GPU)", "_netG_celeba64", 100, 128, 64, 256, 5, 0.1, 410.6e6),
