@@ -854,8 +854,11 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
   if (smallc_k3(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
     // 8 rows per block with the next mask nibbles prefetched: 66.4 us vs 69.9 (4 rows, no prefetch) at the
-    // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us)
-    const int R = 8;
+    // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us); fewer rows per block when the
+    // batch would leave fewer than 256 blocks (B=16: 60 us at 8 rows, 64 blocks).  Pixels are independent, so
+    // the row blocking never changes a result
+    int R = 8;
+    while (R > 1 && (long)((L.hin + R - 1) / R) * B < 256) R >>= 1;
     const dim3 grid((unsigned)((L.hin + R - 1) / R), (unsigned)B);
     const size_t sm = sizeof(float) * (R + 2) * (L.win + 2) * 4;
     if (L.cout == 3)
