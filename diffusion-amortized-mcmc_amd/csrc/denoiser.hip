@@ -1547,9 +1547,11 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   }
 
   // ---- 3. every block's gate and hyper bias for every (step, row): [sigmoid(c Wg^T + bg) | c Wb^T]
+  damc::GemmArgs hg[7];
+  double hflops = 0.0;
   for (int j = 0; j < 7; ++j) {
     const int dout = d->blocks[j].dout;
-    damc::GemmArgs g;
+    damc::GemmArgs& g = hg[j];
     g.M = n * B;
     g.N = 2 * dout;
     g.K = dout;
@@ -1563,9 +1565,23 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     g.bias = w.bg2[j];
     g.bias_mod = 2 * dout;
     g.gate_cols = dout;
-    if ((rc = damc::launch_gemm(g, damc::A_DENSE, damc::EPI_GATE, damc::O_DENSE, 1, "sweep_hyper",
-                                2.0 * n * B * dout * 2.0 * dout, s)))
-      return rc;
+    hflops += 2.0 * n * B * dout * 2.0 * dout;
+  }
+  // one grouped launch (its tiles fill the chip; seven launches of 200-400 tiles each left half of it idle in their
+  // last round); the general path when a block's rows are not float4-aligned
+  // DAMC_SWEEP_HYPER_GROUP=0 (read per call): seven launches (tests/test_gpu_amortizer.py checks both are bitwise equal)
+  const char* hge = getenv("DAMC_SWEEP_HYPER_GROUP");
+  rc = (hge && atoi(hge) == 0) ? DAMC_ERR_UNSUPPORTED
+                               : damc::launch_gemm_group(hg, 7, damc::EPI_GATE, "sweep_hyper", hflops, s);
+  if (rc == DAMC_ERR_UNSUPPORTED) {
+    for (int j = 0; j < 7; ++j) {
+      const int dout = d->blocks[j].dout;
+      if ((rc = damc::launch_gemm(hg[j], damc::A_DENSE, damc::EPI_GATE, damc::O_DENSE, 1, "sweep_hyper",
+                                  2.0 * n * B * dout * 2.0 * dout, s)))
+        return rc;
+    }
+  } else if (rc) {
+    return rc;
   }
 
   // ---- 4. the dependent chain

@@ -102,4 +102,14 @@ int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);
 
+// up to GEMM_GROUP_MAX independent A_DENSE / O_DENSE GEMMs (no split-K, float4-aligned rows) in one launch of the
+// generic engine; each result is bitwise the one launch_gemm gives it
+constexpr int GEMM_GROUP_MAX = 8;
+struct GemmGroup {
+  GemmArgs a[GEMM_GROUP_MAX];
+  int start[GEMM_GROUP_MAX + 1];
+  int n;
+};
+int launch_gemm_group(const GemmArgs* a, int n, Epi epi, const char* prof_name, double flops, hipStream_t s);
+
 }  // namespace damc

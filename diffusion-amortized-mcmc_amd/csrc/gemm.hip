@@ -145,8 +145,9 @@ __device__ __forceinline__ void supertile(int l, int T, int P, int& tm, int& p) 
   p = pb * SP + rem % sp;
 }
 
-template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT, int SCHED>
-__global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
+// one block tile of the generic engine: tile wgid (already XCD-remapped) of the (M, N) grid, z = blockIdx.z
+template <int AM, int EPI, int OM, bool BVEC, int BK, int MT, int SCHED>
+__device__ __forceinline__ void gemm_f32_tile(const GemmArgs& p, const int wgid, const int z) {
   typedef TileCfg<BK, MT> C;
   constexpr int BM = C::BM;
   __shared__ float As[2][BK * C::LDA];
@@ -157,12 +158,9 @@ __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
-  // ---- XCD-aware tile remap (bijective for any grid size)
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntn = (p.N + BN - 1) / BN;
   const int tm = wgid / ntn, tn = wgid - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int z = blockIdx.z;
 
   int pad_y = p.pad_y, pad_x = p.pad_x;
   const float* Bg = p.B;
@@ -396,6 +394,23 @@ __global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
   }
 
   gemm_epilogue<EPI, OM, MT>(p, acc, m0, n0, wm, wn, lane, z, py, px);
+}
+
+template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT, int SCHED>
+__global__ __launch_bounds__(256, OCC) void gemm_f32_kernel(GemmArgs p) {
+  // XCD-aware tile remap (bijective for any grid size)
+  gemm_f32_tile<AM, EPI, OM, BVEC, BK, MT, SCHED>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
+}
+
+// independent GEMMs of one shape class in one launch: group g owns the remapped tile ids [start[g], start[g+1]), so
+// the tiles of all of them share the chip instead of each launch's last partial round idling half of it
+template <int AM, int EPI, int OM, bool BVEC, int BK, int OCC, int MT, int SCHED>
+__global__ __launch_bounds__(256, OCC) void gemm_f32_group_kernel(GemmGroup g) {
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  int j = 0;
+#pragma unroll
+  for (int t = 1; t < GEMM_GROUP_MAX; ++t) j += (t < g.n && wgid >= g.start[t]) ? 1 : 0;
+  gemm_f32_tile<AM, EPI, OM, BVEC, BK, MT, SCHED>(g.a[j], wgid - g.start[j], 0);
 }
 
 // ================================================================================================
@@ -1661,6 +1676,35 @@ static void launch_t(const GemmArgs& a, int zdim, hipStream_t s) {
 #ifndef DAMC_GEMM_MT
 #define DAMC_GEMM_MT 2
 #endif
+
+int launch_gemm_group(const GemmArgs* a, int n, Epi epi, const char* prof_name, double flops, hipStream_t s) {
+  if (n < 1 || n > GEMM_GROUP_MAX) return DAMC_ERR_ARG;
+  if (epi != EPI_GATE && epi != EPI_STORE) return DAMC_ERR_UNSUPPORTED;
+  GemmGroup g;
+  const int bm = 64 * DAMC_GEMM_MT;
+  int tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& x = a[i];
+    if (x.M <= 0 || x.N <= 0 || x.K <= 0 || x.A3 || x.b_kmajor || x.k_per_z < x.K) return DAMC_ERR_ARG;
+    // the dense vector path only: float4 rows of A and B
+    if (x.lda % 4 || x.K % 4 || x.ldb % 4 || x.N % 4 || ((uintptr_t)x.A | (uintptr_t)x.B) % 16) return DAMC_ERR_UNSUPPORTED;
+    if ((double)x.M * x.lda >= 2147483647.0 || (double)x.K * x.ldb >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
+    g.a[i] = x;
+    g.start[i] = tot;
+    tot += ((x.M + bm - 1) / bm) * ((x.N + BN - 1) / BN);
+  }
+  for (int i = n; i <= GEMM_GROUP_MAX; ++i) g.start[i] = tot;
+  g.n = n;
+  ProfScope ps(prof_name, flops, s);
+  constexpr int BKc = DAMC_GEMM_BK, OCCc = DAMC_GEMM_OCC, MTc = DAMC_GEMM_MT;
+  if (epi == EPI_GATE)
+    hipLaunchKernelGGL((gemm_f32_group_kernel<A_DENSE, EPI_GATE, O_DENSE, true, BKc, OCCc, MTc, DAMC_GEMM_SCHED>),
+                       dim3(tot), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_group_kernel<A_DENSE, EPI_STORE, O_DENSE, true, BKc, OCCc, MTc, DAMC_GEMM_SCHED>),
+                       dim3(tot), dim3(256), 0, s, g);
+  return (int)hipGetLastError();
+}
 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s) {

@@ -196,3 +196,21 @@ def test_team_sweep_is_deterministic(am, gpu_device):
         am.reverse_sweep(Q, xemb, zt, seed=99)
         out.append(zt.cpu().numpy())
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.gpu
+def test_grouped_hyper_gemms_are_bitwise_the_separate_launches(am, gpu_device, monkeypatch):
+    """The seven hyper GEMMs run as one grouped launch; the same tiles as seven launches, bit for bit."""
+    from damc import synth
+
+    Q = _wide_q(gpu_device, 20)
+    xemb = torch.from_numpy(synth.normal_f32(7, 0, (128, 1024))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(8, 0, (128, 128))).to(gpu_device)
+    out = []
+    for grouped in ("1", "0"):
+        monkeypatch.setenv("DAMC_SWEEP_HYPER_GROUP", grouped)
+        zt = zt0.clone()
+        am.reverse_sweep(Q, xemb, zt, seed=99)
+        out.append(zt.cpu().numpy())
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[0], out[1])
