@@ -718,6 +718,66 @@ __global__ __launch_bounds__(256) void smallc_proj_kernel(const float* __restric
     }
 }
 
+// The same products in the same k order, with each wave's 32 pixels (one contiguous NHWC block) staged through LDS
+// 64 channels at a time: whole 256-B row spans per load instruction instead of 32 B of 32 rows, the next chunk's
+// loads in flight under the current chunk's MFMAs.  Row stride 68 floats: conflict-free ds_read_b128 fragments.
+constexpr int PJ_KC = 64, PJ_RS = PJ_KC + 4;
+template <int NTILE>
+__global__ __launch_bounds__(256) void smallc_proj_lds_kernel(const float* __restrict__ h, long npix, int Cin,
+                                                              const float* __restrict__ wp, float* __restrict__ P) {
+  __shared__ __attribute__((aligned(16))) float st[4][32 * PJ_RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long p0 = ((long)blockIdx.x * 4 + wave) * 32;
+  const int i = lane & 31, hh = lane >> 5;
+  float* ls = st[wave];
+  f32x16 acc[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const float* wrow[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) wrow[t] = wp + (long)(32 * t + i) * Cin + 4 * hh;
+  // staging: load q of a chunk covers rows 4q + lane/16, float4 lane%16 of the row's 64 channels
+  f32x4 g[8];
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = 4 * q + (lane >> 4);
+      const long pr = min(p0 + row, npix - 1);
+      g[q] = *reinterpret_cast<const f32x4*>(h + pr * Cin + c0 + 4 * (lane & 15));
+    }
+  };
+  gload(0);
+  for (int c0 = 0; c0 < Cin; c0 += PJ_KC) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      *reinterpret_cast<f32x4*>(ls + (4 * q + (lane >> 4)) * PJ_RS + 4 * (lane & 15)) = g[q];
+    __syncthreads();
+    if (c0 + PJ_KC < Cin) gload(c0 + PJ_KC);
+#pragma unroll
+    for (int j = 0; j < PJ_KC; j += 8) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(ls + i * PJ_RS + j + 4 * hh);
+      f32x4 b[NTILE];
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) b[t] = *reinterpret_cast<const f32x4*>(wrow[t] + c0 + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < NTILE; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], b[t][e], acc[t], 0, 0, 0);
+    }
+  }
+  const int ldp = NTILE * 32;
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long p = p0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (p < npix) P[p * ldp + 32 * t + i] = acc[t][r];
+    }
+}
+
 // Stage 2: out[b,oy,ox,co] = bias + sum over the valid taps of P[input pixel][tap*NC + co], then tanh,
 // x_hat (NCHW) and the residual delta = (x_hat - x)/s^2 * (1 - x_hat^2) (NHWC).  One thread per output pixel.
 template <int NC, int K, int S>
@@ -789,7 +849,14 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   const long npin = (long)B * L.hin * L.win;
   const int nt = smallc_ntile(L);
   const int g1 = (int)((npin + 127) / 128);
-  if (nt == 1)
+  // DAMC_SMALLC_PROJ_LDS=1 (read per call; opt-in): the LDS-staged kernel when Cin is whole 64-channel chunks
+  const char* pe = getenv("DAMC_SMALLC_PROJ_LDS");
+  const bool lds = pe && atoi(pe) == 1 && L.cin % PJ_KC == 0;
+  if (lds && nt == 1)
+    hipLaunchKernelGGL((smallc_proj_lds_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
+  else if (lds)
+    hipLaunchKernelGGL((smallc_proj_lds_kernel<2>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
+  else if (nt == 1)
     hipLaunchKernelGGL((smallc_proj_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
   else
     hipLaunchKernelGGL((smallc_proj_kernel<2>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
