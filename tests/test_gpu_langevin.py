@@ -358,18 +358,20 @@ def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [5, 128])
-def test_lds_staged_output_projection_is_bitwise_the_direct_kernel(lv, gpu_device, monkeypatch, B):
+@pytest.mark.parametrize("net,B", [("cifar10", 5), ("cifar10", 128), ("celeba64", 4)])
+def test_lds_staged_output_projection_is_bitwise_the_direct_kernel(lv, gpu_device, monkeypatch, net, B):
     """The output layer's projection stage staged through LDS (generator.hip smallc_proj_lds_kernel: same MFMA
-    sequence, operands from LDS) gives the same bits as the direct-load kernel: 2 posterior steps at full CIFAR width
-    (ragged last wave at B=5) with DAMC_SMALLC_PROJ_LDS=0 vs 1."""
+    sequence, operands from LDS) gives the same bits as the direct-load kernel: 2 posterior steps at full width
+    (CIFAR k3: one 32-column tile, ragged last wave at B=5; CelebA-64 k4 s2: two tiles) with
+    DAMC_SMALLC_PROJ_LDS=0 vs 1."""
     from damc import synth
     from src import diffusion_net as dn
 
-    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=128, nc=3), 0).to(gpu_device).eval()
-    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
-    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(gpu_device)
-    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, 128))).to(gpu_device)
+    nz, hw = (128, 32) if net == "cifar10" else (100, 64)
+    G = synth.load_into(getattr(dn, "_netG_" + net)(nz=nz, ngf=128, nc=3), 0).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=nz), 10).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, hw, hw))).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, nz))).to(gpu_device)
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_SMALLC_PROJ_LDS", mode)
