@@ -9,12 +9,14 @@ chains (sample_langevin_prior_z, s=.4, noise on).  `value` counts POSTERIOR z-st
 is charged but its (cheap) z-steps are not — conservative against the CPU-reference's 130
 posterior z-steps/s.
 
-Multi-GPU: one process per GPU (torchrun).  Chains never communicate, so there is no collective in
-the timed path (timing uses a barrier and a MAX all-reduce of the elapsed time only); noise is keyed
-by the GLOBAL chain index (damc.dist.block_plan):
-  --scaling weak   (default): B=128 chains per rank -> per-GPU work fixed, "scaling": "weak";
-  --scaling strong: the global B=128 (and 2B prior) chains split over the ranks (BASELINE.md's primary
-                    curve), "scaling": "strong"; the JSON records the per-rank batch.
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` with no launcher environment starts N ranks
+itself (torch.distributed.run as a child process, before any GPU call); under torchrun it is one rank.
+Chains never communicate, so there is no collective in the timed path (timing uses a barrier and a MAX
+all-reduce of the elapsed time only); noise is keyed by the GLOBAL chain index (damc.dist.block_plan):
+  --scaling strong (default): the global B=128 (and 2B prior) chains split over the ranks (BASELINE.md's
+                    primary curve), "scaling": "strong"; the JSON records the per-rank batch.  For N > 1 a
+                    weak-scaling pass (B=128 chains per rank) is timed after it and reported as "weak_scaling".
+  --scaling weak:   B=128 chains per rank -> per-GPU work fixed, "scaling": "weak".
 
 Data: synthetic (counter-hash weights / x ~ U[-1,1] / z0 ~ N(0,1); no datasets offline).
 """
@@ -73,7 +75,35 @@ def one_block(lv, G, E, x, z0, p0, zbuf, pbuf, seed, plan):
     zbuf.copy_(z0)
     lv.posterior_langevin(zbuf, x, G, E, POST_STEPS, SIGMA, S_POST, True, seed=seed, chain_base=plan["post_start"])
     pbuf.copy_(p0)
-    lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=seed + 1, chain_base=plan["prior_start"])
+    lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=seed + 1, chain_base=plan["prior_start"],
+                      global_batch=plan["prior_global"])
+
+
+def available_cores():
+    """(cores, basis): the host cores this process may run on — the affinity mask, capped by a cgroup CPU quota
+    (a GPU box's share of a large host), counted as physical cores when SMT siblings share the mask."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = list(range(os.cpu_count() or 1))
+    phys = set()
+    for c in cpus:
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c) as f:
+                phys.add(f.read().strip())
+        except OSError:
+            phys.add(str(c))
+    n, basis = len(phys), "%d physical cores in the affinity mask (%d logical)" % (len(phys), len(cpus))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            if quota < n:
+                n, basis = quota, "cgroup CPU quota %d (affinity: %s)" % (quota, basis)
+    except (OSError, ValueError):
+        pass
+    return n, basis
 
 
 def cpu_model():
@@ -100,7 +130,9 @@ def cpu_baseline(budget_s=12.0, full=False):
     from oracle import damc_oracle as orc
     from src import diffusion_net as dn
 
-    threads = torch.get_num_threads()
+    threads, basis = available_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     G = synth.load_into(dn._netG_cifar10(nz=NZ, ngf=NGF, nc=3), 0).eval()
     E = synth.load_into(dn._netE(nz=NZ), 10).eval()
     L, P = orc.generator_layers(G), orc.ebm_params(E)
@@ -124,11 +156,12 @@ def cpu_baseline(budget_s=12.0, full=False):
         el = time.perf_counter() - t0
         if (full and len(ts) >= 5) or (not full and ((el > budget_s and len(ts) >= 5) or len(ts) >= 200)):
             break
+    torch.set_num_threads(prev_threads)
     med = sorted(ts)[len(ts) // 2]
     what = ("%d full-length calls (30 posterior steps on B=128 + 60 prior steps on 2B=256) after 3 warm-ups"
             % len(ts)) if full else ("%d timed calls of 1 posterior step (B=128) + 2 prior steps (2B=256) after 1 "
                                       "warm-up, %.1f s" % (len(ts), el))
-    return dict(value=round(B * npost / med, 2), unit="z-steps/s", cores=threads, kind="port",
+    return dict(value=round(B * npost / med, 2), unit="z-steps/s", cores=threads, cores_basis=basis, kind="port",
                 cpu_model=cpu_model(), statistic="median per call",
                 sample="%s of the fp32 oracle restatement (CIFAR-10 _netG_cifar10 ngf=128 + _netE), torch %d threads"
                        % (what, threads))
@@ -156,7 +189,8 @@ def langevin_breakdown(lv, G, E, x, z0, p0, zbuf, pbuf, plan):
 
     def prior():
         pbuf.copy_(p0)
-        lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=8, chain_base=plan["prior_start"])
+        lv.prior_langevin(pbuf, E, PRIOR_STEPS, S_PRIOR, True, seed=8, chain_base=plan["prior_start"],
+                          global_batch=plan["prior_global"])
 
     tp, tq = event_ms(post), event_ms(prior)
     nb, nq = zbuf.shape[0], pbuf.shape[0]
@@ -357,13 +391,48 @@ def traffic_from_profiles(kernel_class):
         return None
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` outside a launcher: run N ranks under torch.distributed.run as a CHILD process (this
+    process has not touched the GPU, and is never replaced by exec) and return its exit code.  Rank 0 prints the
+    JSON line to the inherited stdout."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=dict(os.environ, DAMC_BENCH_LAUNCHED="1"))
+
+
+def dry_run(args, rank, world):
+    from damc import dist as ddist
+
+    if world > 1:
+        import torch.distributed as tdist
+
+        tdist.init_process_group("gloo")
+        if tdist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (tdist.get_world_size(), args.gpus))
+        plans = [None] * world
+        tdist.all_gather_object(plans, ddist.block_plan(B, rank, world, args.scaling))
+        tdist.destroy_process_group()
+    else:
+        plans = [ddist.block_plan(B, 0, 1, args.scaling)]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": args.scaling, "plans": plans}))
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: B=128 chains per rank (default); strong: the global B=128 split over the ranks")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): the global B=128 split over the ranks; weak: B=128 chains per rank")
+    ap.add_argument("--no-weak-extra", action="store_true", help="N > 1: skip the weak-scaling pass after the timed one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-full", action="store_true",
@@ -374,7 +443,16 @@ def main():
     ap.add_argument("--no-live-prof", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--exact-fp32", action="store_true",
                     help="run the generator convolutions on the fp32-MFMA engine instead of the limb engine")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: the ranks rendezvous over gloo, check the world size and "
+                         "print their block plans")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if os.environ.get("DAMC_BENCH_LAUNCHED"):
+            raise SystemExit("bench.py: the rank launcher did not set WORLD_SIZE")
+        return launch_ranks(args.gpus, sys.argv[1:])
     if args.exact_fp32:
         os.environ["DAMC_EXACT_FP32"] = "1"
     limb = os.environ.get("DAMC_EXACT_FP32", "0") != "1"
@@ -382,7 +460,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world))
     dist = world > 1
+    if args.dry_run:
+        return dry_run(args, rank, world)
     # DAMC_DIST_BACKEND=gloo (tests only): several ranks sharing one GPU (RCCL needs one GPU per rank); the
     # driver's multi-GPU runs use the default, nccl = RCCL over xGMI
     backend = os.environ.get("DAMC_DIST_BACKEND", "nccl")
@@ -396,6 +478,8 @@ def main():
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             tdist.init_process_group(backend)
+        if tdist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (tdist.get_world_size(), args.gpus))
     device = torch.device("cuda", local)
 
     from damc import _lib
@@ -414,6 +498,13 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize(device)
 
+    def max_over_ranks(v):
+        if not dist:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+
     for i in range(args.warmup):
         one_block(lv, G, E, x, z0, p0, zbuf, pbuf, 1000 + i, plan)
     L = _lib.lib()
@@ -430,6 +521,9 @@ def main():
     L.damc_prof_enable(0)
     if not torch.isfinite(zbuf).all() or not torch.isfinite(pbuf).all():
         raise RuntimeError("non-finite chains after the timed region")
+    dump = os.environ.get("DAMC_BENCH_DUMP")
+    if dump:  # tests only: this rank's chains after its last block, with its slice of the global batch
+        torch.save({"z": zbuf.cpu(), "p": pbuf.cpu(), "plan": dict(plan)}, os.path.join(dump, "rank%d.pt" % rank))
 
     # per-class kernel time from the live HIP events
     import ctypes
@@ -454,11 +548,31 @@ def main():
     L.damc_prof_enable(0)
     breakdown = query()
 
-    t_max = elapsed
-    if dist:
-        t = torch.tensor([elapsed], device=device if backend == "nccl" else "cpu")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        t_max = float(t.item())
+    t_max = max_over_ranks(elapsed)
+    # the dominant class's mean launch time, max over ranks (a strong-scaling rank's per-rank batch)
+    dom = max(("upconv_fwd", "upconv_dgrad"), key=lambda k: classes.get(k, {}).get("total_ms", 0.0))
+    dom_c = classes.get(dom)
+    dom_avg_ms = dom_c["total_ms"] / dom_c["launches"] if dom_c else float("nan")
+    dom_avg_ms_max = max_over_ranks(dom_avg_ms)
+
+    weak = None
+    if dist and args.scaling == "strong" and not args.no_weak_extra:
+        # secondary curve: B=128 chains per rank, its own timed pass after the headline one
+        wplan = ddist.block_plan(B, rank, world, "weak")
+        wx, wz0, wp0 = inputs(device, rank, wplan, "weak")
+        wz, wp = torch.empty_like(wz0), torch.empty_like(wp0)
+        for i in range(args.warmup):
+            one_block(lv, G, E, wx, wz0, wp0, wz, wp, 4000 + i, wplan)
+        barrier()
+        tw = time.perf_counter()
+        for i in range(args.steps):
+            one_block(lv, G, E, wx, wz0, wp0, wz, wp, 5000 + i, wplan)
+        barrier()
+        tw_max = max_over_ranks(time.perf_counter() - tw)
+        weak = {"value": round(world * B * POST_STEPS * args.steps / tw_max, 2), "unit": "z-steps/s",
+                "ms_per_step": round(1e3 * tw_max / args.steps, 3), "global_batch": world * B,
+                "per_rank_batch": B, "scaling": "weak"}
+        del wx, wz0, wp0, wz, wp
 
     extras = None
     if not args.no_extras and rank == 0:
@@ -477,7 +591,6 @@ def main():
         chains = world * B if args.scaling == "weak" else B
         zsteps = chains * POST_STEPS * args.steps
         value = zsteps / t_max
-        dom = max(("upconv_fwd", "upconv_dgrad"), key=lambda k: classes.get(k, {}).get("total_ms", 0.0))
         c = classes.get(dom, dict(total_ms=float("nan"), launches=1, flops=float("nan")))
         avg_s = c["total_ms"] / c["launches"] / 1e3
         flops_per_launch = c["flops"] / c["launches"]
@@ -533,6 +646,11 @@ def main():
             "batch_iterations_per_s": round(args.steps / t_max, 3),
             "cpu_baseline": None,
         }
+        if dist:
+            out["per_rank"] = {"dominant_class": dom, "avg_launch_ms_max_over_ranks": round(dom_avg_ms_max, 4),
+                               "backend": backend}
+        if weak:
+            out["weak_scaling"] = weak
         if extras:
             out["langevin_legs"] = {k: v for k, v in extras.items() if k not in ("amortizer", "g_update", "q_update")}
             out["amortizer"] = extras["amortizer"]
@@ -545,12 +663,9 @@ def main():
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(out))
-    dump = os.environ.get("DAMC_BENCH_DUMP")
-    if dump:  # tests only: this rank's chains after its last block, with its slice of the global batch
-        torch.save({"z": zbuf.cpu(), "p": pbuf.cpu(), "plan": dict(plan)}, os.path.join(dump, "rank%d.pt" % rank))
     if dist:
         tdist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

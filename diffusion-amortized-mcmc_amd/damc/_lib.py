@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("DAMC_LIB_PATH") or os.path.join(_HERE, "libdamc.so")
 ABI_VERSION = 2
 MAX_LAYERS = 10
 ENGINE_LIMB, ENGINE_FP32 = 0, 1
+# include/damc.h error codes
+DAMC_ERR_ARG, DAMC_ERR_WORKSPACE, DAMC_ERR_UNSUPPORTED = 1001, 1002, 1003
 LAYER_PROJ, LAYER_UP2, LAYER_SMALLC, LAYER_LINEAR = 1, 2, 3, 4
 ACT_NONE, ACT_LRELU, ACT_TANH = 0, 1, 2
 

@@ -29,15 +29,18 @@ def block_plan(global_batch, rank, world, scaling="weak"):
             global chains [r B, (r+1) B) and [2 r B, 2 (r+1) B) -> noise streams never collide.
     strong: the global batch is split: posterior rows shard(B) and prior rows shard(2B) of the global
             arrays; chain_base = the slice start, so the union over ranks is the 1-GPU block bit for bit.
-    Returns dict(post_start, post_count, prior_start, prior_count) — *_start are the chain_base values (and,
-    for strong, the slice offsets into the global inputs)."""
+    Returns dict(post_start, post_count, prior_start, prior_count, post_global, prior_global) — *_start are the
+    chain_base values (and, for strong, the slice offsets into the global inputs); *_global the chain count of the
+    block a rank's slice belongs to (what a shape-dependent engine choice must key on: langevin.prior_langevin's
+    global_batch)."""
     B = int(global_batch)
     if scaling == "weak":
-        return dict(post_start=rank * B, post_count=B, prior_start=rank * 2 * B, prior_count=2 * B)
+        return dict(post_start=rank * B, post_count=B, prior_start=rank * 2 * B, prior_count=2 * B,
+                    post_global=B, prior_global=2 * B)
     if scaling == "strong":
         ps, pc = shard(B, rank, world)
         qs, qc = shard(2 * B, rank, world)
-        return dict(post_start=ps, post_count=pc, prior_start=qs, prior_count=qc)
+        return dict(post_start=ps, post_count=pc, prior_start=qs, prior_count=qc, post_global=B, prior_global=2 * B)
     raise ValueError("scaling must be 'weak' or 'strong', got %r" % (scaling,))
 
 
@@ -47,10 +50,10 @@ def _dist():
     return d if d.is_available() and d.is_initialized() else None
 
 
-def all_reduce_sum_(t):
+def all_reduce_sum_(t, group=None):
     d = _dist()
-    if d is not None and d.get_world_size() > 1:
-        d.all_reduce(t, op=d.ReduceOp.SUM)
+    if d is not None and d.get_world_size(group) > 1:
+        d.all_reduce(t, op=d.ReduceOp.SUM, group=group)
     return t
 
 

@@ -3,8 +3,9 @@ Frechet distance of pytorch-fid 0.2.1 (the algorithm pytorch_fid_wrapper's ``pfw
 workspace/src/MCMC.py:130-176).
 
   acc = FidAccumulator(dim, device); acc.update(features) per batch  -> damc_fid_accumulate (fp64 s1, s2)
-  mu, sigma = acc.compute()                                        -> all_reduce(SUM) over the ranks (RCCL
-                                                                      for backend "nccl"), damc_fid_mean_cov
+  mu, sigma = acc.compute()                                        -> this rank's samples, damc_fid_mean_cov
+  mu, sigma = acc.compute(reduce=True, group=g)                    -> sharded FID: all_reduce(SUM) of s1, s2, n
+                                                                      over the group first (RCCL for "nccl")
   fid = frechet_distance(mu, sigma, real_m, real_s)                -> host fp64 (scipy.linalg.sqrtm), exactly
                                                                       pytorch-fid's calculate_frechet_distance
 
@@ -42,13 +43,19 @@ class FidAccumulator:
                                              _lib.stream_ptr(self.device)), "damc_fid_accumulate")
         self.n += f.shape[0]
 
-    def compute(self):
-        """(mu, sigma) as fp64 device tensors over every rank's samples (one all_reduce of s1, s2 and n)."""
-        from .dist import all_reduce_sum_
+    def compute(self, reduce=False, group=None):
+        """(mu, sigma) as fp64 device tensors.
 
+        reduce=False (default): this accumulator's samples only, like the reference's single ``pfw.fid`` call; no
+        collective, so a driver that computes FID on rank 0 alone cannot deadlock.  reduce=True: the sharded FID,
+        every rank of ``group`` (default: the world) calls compute(reduce=True) and gets the statistics of the
+        union of their samples (one all_reduce of s1, s2 and n; each rank's tensors stay on its own device)."""
         flat = torch.cat([self.s1, self.s2.reshape(-1),
                           torch.tensor([float(self.n)], dtype=torch.float64, device=self.device)])
-        all_reduce_sum_(flat)
+        if reduce:
+            from .dist import all_reduce_sum_
+
+            all_reduce_sum_(flat, group=group)
         d = self.dim
         s1, s2, n = flat[:d].contiguous(), flat[d:d + d * d].contiguous(), float(flat[-1].item())
         mu = torch.empty(d, dtype=torch.float64, device=self.device)

@@ -91,13 +91,22 @@ def generator_forward(z, netG):
 PRIOR_ENGINES = {"auto": 0, "valu": 1, "mfma": 2}
 
 
+def mfma_min_chains():
+    """Chain count from which "auto" picks the MFMA prior engine (the library reads the same variable)."""
+    import os
+
+    return int(os.environ.get("DAMC_EBM_MFMA_MIN_B", "2048"))
+
+
 def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, step_offset=0, chain_base=0,
-                   diag=False, engine="auto"):
+                   diag=False, engine="auto", global_batch=None):
     """In-place n-step prior Langevin (workspace/src/MCMC.py:27-46), one persistent launch.
 
-    engine: "auto" (the library's choice by batch size), "valu" (one chain per workgroup, weights in registers)
-    or "mfma" (16-chain tiles on the fp32 MFMA).  Returns a (n_steps, 2) diagnostics tensor {sum E, |z|^2/2} if
-    diag else None.
+    engine: "auto" (by chain count), "valu" (one chain per workgroup, weights in registers) or "mfma" (16-chain
+    tiles on the fp32 MFMA).  The two engines sum in different orders, so "auto" decides from ``global_batch``
+    (the chain count of the whole sharded block; default: this call's) — every shard of a block then runs the
+    engine the unsharded block runs, and the union of the shards stays bitwise the one-GPU result.  Returns a
+    (n_steps, 2) diagnostics tensor {sum E, |z|^2/2} if diag else None.
     """
     _f32c(z, "z")
     dev = z.device
@@ -115,10 +124,19 @@ def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, st
     dg = torch.zeros(max(n_steps, 1), 2, dtype=torch.float32, device=dev) if diag else None
     if engine not in PRIOR_ENGINES:
         raise ValueError("engine must be one of %s" % sorted(PRIOR_ENGINES))
-    check(_lib.lib().damc_prior_langevin_engine(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
-                                                int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base,
-                                                ptr(dg), PRIOR_ENGINES[engine], _lib.stream_ptr(dev)),
-          "damc_prior_langevin")
+    code = PRIOR_ENGINES[engine]
+    if engine == "auto":  # resolved here from the global chain count, never from the shard's
+        code = 2 if int(global_batch if global_batch is not None else B) >= mfma_min_chains() else 1
+
+    def run(c):
+        return _lib.lib().damc_prior_langevin_engine(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
+                                                     int(bool(with_noise)), ptr(noise), seed, step_offset,
+                                                     chain_base, ptr(dg), c, _lib.stream_ptr(dev))
+
+    rc = run(code)
+    if rc == _lib.DAMC_ERR_UNSUPPORTED and engine == "auto":  # the shape has no kernel of that engine: the other
+        rc = run(1 if code == 2 else 2)
+    check(rc, "damc_prior_langevin")
     return dg
 
 

@@ -104,7 +104,10 @@ def _fid(fid_samples, real_m, real_s, save_name):
 
     fid_samples = torch.cat(fid_samples, dim=0)
     fid_samples = (1.0 + torch.clamp(fid_samples, min=-1.0, max=1.0)) / 2.0
-    fid = _dfid.fid_of_samples(fid_samples.to("cuda:0"), real_m, real_s)
+    # the samples' own device when they are on a GPU (the reference's pfw.fid used cuda:0, MCMC.py:139); no
+    # collective: a driver that computes FID on one rank must not block on the others
+    dev = fid_samples.device if fid_samples.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+    fid = _dfid.fid_of_samples(fid_samples.to(dev), real_m, real_s)
     if save_name is not None:
         import torchvision
 

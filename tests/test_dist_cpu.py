@@ -145,3 +145,35 @@ def test_strong_scaling_plan_reassembles_the_global_block():
     weak = [ddist.block_plan(bench.B, r, 4, "weak") for r in range(4)]
     assert [w["post_start"] for w in weak] == [0, 128, 256, 384]
     assert [w["prior_start"] for w in weak] == [0, 256, 512, 768]
+
+
+def test_bench_gpus_n_launches_n_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` (the driver's command form, no torchrun around it) starts 2 ranks itself: they
+    rendezvous (gloo, --dry-run: no GPU here) and see a world of 2; strong scaling splits the global B=128."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import REPO
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j["n_gpus"] == 2 and j["scaling"] == "strong"
+    assert [p["post_count"] for p in j["plans"]] == [64, 64]
+    assert [p["prior_start"] for p in j["plans"]] == [0, 128]
+    assert all(p["prior_global"] == 256 for p in j["plans"])
+
+
+def test_bench_refuses_a_world_that_disagrees_with_gpus():
+    import subprocess
+    import sys
+
+    from conftest import REPO
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--dry-run"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpus 3" in r.stderr

@@ -1,5 +1,5 @@
-"""The multi-GPU path of bench.py end to end on one MI355X: two ranks launched by torch.distributed.run share the
-GPU over the gloo backend (RCCL needs one GPU per rank; the driver's 8-GPU runs use nccl = RCCL).  Each rank runs
+"""The multi-GPU path of bench.py end to end on one MI355X: `python bench.py --gpus 2` (no launcher around it, the
+driver's command form) starts two ranks itself; they share the GPU over the gloo backend (RCCL needs one GPU per rank; the driver's 8-GPU runs use nccl = RCCL).  Each rank runs
 its slice of the BASELINE Langevin block on the HIP path (damc.dist.block_plan, chain_base = the slice start) and
 the ranks' timings go through the MAX all-reduce.  Checks: the JSON line's multi-rank fields, and — strong
 scaling — the union of the two ranks' chains is bitwise the 1-rank block (posterior and prior chains), because
@@ -24,11 +24,13 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(tmp, world, scaling):
-    env = dict(os.environ, DAMC_DIST_BACKEND="gloo", DAMC_BENCH_DUMP=str(tmp))
+def _run(tmp, world, scaling, torchrun=False, **extra_env):
+    env = dict(os.environ, DAMC_DIST_BACKEND="gloo", DAMC_BENCH_DUMP=str(tmp), **extra_env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     args = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
             "--scaling", scaling]
-    if world > 1:
+    if torchrun:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     else:
@@ -47,6 +49,8 @@ def test_two_ranks_strong_scaling_union_is_the_one_rank_block(tmp_path, gpu_devi
     j2 = _run(two, 2, "strong")
     assert j2["n_gpus"] == 2 and j2["scaling"] == "strong"
     assert j2["config"]["global_batch"] == 128 and j2["config"]["per_rank_batch"] == 64
+    assert j2["weak_scaling"]["per_rank_batch"] == 128 and j2["weak_scaling"]["global_batch"] == 256
+    assert j2["per_rank"]["avg_launch_ms_max_over_ranks"] > 0
     assert j2["value"] > 0 and j1["value"] > 0
     ref = torch.load(one / "rank0.pt", weights_only=True)
     parts = [torch.load(two / ("rank%d.pt" % r), weights_only=True) for r in range(2)]
@@ -59,8 +63,23 @@ def test_two_ranks_strong_scaling_union_is_the_one_rank_block(tmp_path, gpu_devi
     assert torch.equal(pz, ref["p"]), "prior chains of the 2-rank block differ from the 1-rank block"
 
 
+def test_strong_scaling_union_keeps_the_prior_engine_of_the_global_block(tmp_path, gpu_device):
+    """the prior engine is chosen from the GLOBAL chain count.  With the MFMA threshold at 200 the
+    1-rank block (256 prior chains) runs the MFMA engine; each rank of 2 holds 128 chains and must run it too, or
+    the union is no longer bitwise the 1-rank block."""
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    _run(one, 1, "strong", DAMC_EBM_MFMA_MIN_B="200")
+    _run(two, 2, "strong", DAMC_EBM_MFMA_MIN_B="200")
+    ref = torch.load(one / "rank0.pt", weights_only=True)
+    parts = [torch.load(two / ("rank%d.pt" % r), weights_only=True) for r in range(2)]
+    assert torch.equal(torch.cat([p["p"] for p in parts]), ref["p"])
+    assert torch.equal(torch.cat([p["z"] for p in parts]), ref["z"])
+
+
 def test_two_ranks_weak_scaling_line(tmp_path, gpu_device):
-    j = _run(tmp_path, 2, "weak")
+    j = _run(tmp_path, 2, "weak", torchrun=True)
     assert j["n_gpus"] == 2 and j["scaling"] == "weak"
     assert j["config"]["per_rank_batch"] == 128
     parts = [torch.load(tmp_path / ("rank%d.pt" % r), weights_only=True) for r in range(2)]
