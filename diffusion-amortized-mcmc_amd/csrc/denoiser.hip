@@ -346,13 +346,15 @@ struct TsArgs {
   const SweepCall* call;
   unsigned* flags;    // [8][TS_MAXT][TS_FS]: stages published by (team, slot)
   int* err;
+  int* diag;          // [P][4]: a failed wait's {stage needed, flag of the first late slot, late-slot mask lo, hi}
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
   uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin, wait end, reduced,
                       // published}
   int dbg;            // timing experiments only (DAMC_SWEEP_DBG, wrong results): 1 no drain before the flag,
                       // 2 no payload loads, 4 no MFMA, 8 no epilogue operand loads, 16 no output stores,
-                      // 32 no zB / sin / cos (in0), 64 no z loads (in0)
+                      // 32 no zB / sin / cos (in0), 64 no z loads (in0); tests: 4096 every workgroup reports a
+                      // failed wait at once (exercises the rescue in team_finish_kernel)
 };
 
 // number of column tiles of block b that slot t owns, and the first one
@@ -367,7 +369,8 @@ __device__ __forceinline__ int ts_tiles(const TsBlock& b, int T, int t, int* tn0
 // channel) until all have published `need` stages; every thread returns whether the wait succeeded (a barrier is
 // inside).  One poll in flight: three staggered ones measured 4-5 % slower per sweep.
 constexpr int TS_FS = 32;  // flag stride, unsigned
-__device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need, int* err, long budget, int* sflag) {
+__device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need, int* err, long budget, int* sflag,
+                                        int* diag) {
   if (threadIdx.x >= 256 && threadIdx.x < 320) {
     const int lane = threadIdx.x - 256;
     int ok = 1;
@@ -381,6 +384,17 @@ __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need
         const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e || (long)(__builtin_amdgcn_s_memrealtime() - t0) > budget) {
           if (!e && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // diagnostics: which slots of the team had not published `need` stages when this wait gave up
+          const uint64_t late = __ballot(v < need);
+          const int first = late ? __builtin_ctzll(late) : 0;
+          const unsigned vf = __shfl(v, first);
+          if (lane == 0) {
+            int* dg = diag + blockIdx.x * 4;
+            dg[0] = (int)need;
+            dg[1] = e ? -1 : (int)vf;  // -1: gave up because another workgroup had failed
+            dg[2] = (int)(unsigned)late;
+            dg[3] = (int)(unsigned)(late >> 32);
+          }
           ok = 0;
           break;
         }
@@ -480,6 +494,10 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   const int T = a.T, team = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nz = a.nz, B = a.B, G = a.G;
   if (team >= G || slot >= T) return;  // no row tile for this team (its flags are never waited on)
+  if (a.dbg & 4096) {  // tests only: report a failed wait at once
+    if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   const int nrt = (G - team + 7) / 8;  // row tiles of the team: team + 8 i
   unsigned* const myflag = a.flags + (team * TS_MAXT + slot) * TS_FS;
   const unsigned* const teamflags = a.flags + team * TS_MAXT * TS_FS;
@@ -581,8 +599,14 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       }
       const bool final_ = j == 6;
       const float* wbase = lds + lbase[j];
-      // a skip half produced at stage sb is ready now when sb < known
-      const bool skip_early = b.kpb > 0 && (7u * k + b.srcB) < known;
+      // a skip half (produced at stage sb = 7 k + srcB, two or more stages back) always goes first, so every slot sums
+      // in the same order (team_finish_kernel's rescue relies on it); it is normally known complete already (sb <
+      // known); a slot that owned no tile of the stages since waits for it here
+      const bool skip_early = b.kpb > 0;
+      if (skip_early && !(7u * k + b.srcB < known)) {
+        if (!ts_wait(teamflags, T, 7u * k + b.srcB + 1, a.err, a.budget, &sflag, a.diag)) return;
+        known = 7u * k + b.srcB + 1;
+      }
       bool waited = false;
 #pragma unroll 1
       for (int rt = 0; rt < nrt; ++rt) {
@@ -627,7 +651,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
           // ---- wait for stage s - 1 of the team (once per stage)
           if (!waited) {
             if (tr) trs[0] = __builtin_amdgcn_s_memrealtime();
-            if (s > 0 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag)) return;
+            if (s > 0 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
             if (tr) trs[1] = __builtin_amdgcn_s_memrealtime();
             known = s;
             waited = true;
@@ -682,8 +706,6 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
             ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw) {
             ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg);
-            if (b.kpb > 0 && !skip_early)
-              ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg);
           }
           if (cw) {
 #pragma unroll
@@ -734,6 +756,187 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       }
     }
   }
+}
+
+// ---- after the team launch: copy-out, or (a failed wait) the rescue
+// acc += f(x) . W^T over one input half like ts_half, with the weight fragments read from the packed global array
+// (the values and order the team's LDS copy holds): wrow = the lane's weight row at the half's first column
+template <bool EMB>
+__device__ __forceinline__ void rs_half(f32x4& acc, const float* wrow, int kps, int wsrc, const __amdgpu_buffer_rsrc_t& rs,
+                                        long soff, int row, bool rok, const float* embs, int ld) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int kq = kps >> 2, ng = kq >> 4, kbase = wave * kq;
+  for (int c = 0; c < ng; ++c) {
+    const int k = kbase + 16 * c + 4 * q;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+    if (EMB) x = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
+    else if (rok && k < wsrc) x = ld_sc1(rs, (soff + (long)row * wsrc + k) * 4);
+    if (k < wsrc) w = *reinterpret_cast<const f32x4*>(wrow + k);
+    if (!EMB) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.01f * x[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[e], w[e], acc, 0, 0, 0);
+  }
+}
+
+// One workgroup (4 waves) per row tile.  err == 0: copy the sweep's result (zring[n]) to zt.  err != 0 (a team
+// member's bounded wait gave up: a workgroup never became resident, e.g. another process or stream held CUs): the
+// workgroup recomputes its row tile's whole sweep alone — every (step, block, column tile) with the team's
+// arithmetic (same fragments and MFMA order, skip half first, the same fixed-order wave sum and epilogue), so the
+// result is bitwise the team's — and marks the failure in host-visible memory (the library then runs the launch
+// chain for the rest of the process).  A team failure costs time, never correctness, and never NaN.
+__global__ __launch_bounds__(256) void team_finish_kernel(TsArgs a, float* zt, int* hostflag) {
+  __shared__ __attribute__((aligned(16))) float red[4][TM][16];
+  __shared__ __attribute__((aligned(16))) float embs[TM * (256 + 8)];  // in0 image (kpa of in0 <= 256: nz <= 128)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int er = tid >> 3, ec = tid & 7;
+  const int nz = a.nz, B = a.B;
+  const int r0 = blockIdx.x * TM;
+  const int rows = min(TM, B - r0);
+  const int err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float* const zfin = a.zring + (long)a.n * B * nz;
+  if (err) {
+    if (blockIdx.x == 0 && tid == 0 && hostflag) __hip_atomic_store(hostflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const SweepCall* call = a.call;
+    const int with_noise = call->with_noise;
+    const float* noise = call->noise;
+    float* eps_log = call->eps_log;
+    const int eps_log_steps = call->eps_log_steps;
+    const uint64_t seed = call->seed, chain_base = call->chain_base, step_offset = call->step_offset;
+    const long ring_bytes = a.ring_step * 4;
+    const int half = nz >> 1, ld0 = emb_ld(a.b[0].kpa);
+    const int xrow = r0 + m;
+    const bool xok = xrow < B;
+    // B^T tile of in0's Fourier projection (wave w: columns 16 w .. 16 w + 15), as the team holds it
+    f32x4 bv[EMB_G];
+#pragma unroll
+    for (int g = 0; g < EMB_G; ++g) {
+      const int kk = 16 * g + 4 * q, col = wave * 16 + m;
+      bv[g] = (col < half && kk < nz) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * nz + kk)
+                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int k = 0; k < a.n; ++k) {
+      const float* tb = a.tab + 8 * k;
+      const float c0 = tb[0], c1 = tb[1], c2 = tb[2], c3 = tb[3], c4 = tb[4];
+      const bool last = tb[5] != 0.f;
+      const int noisy_k = (int)tb[6];
+      float* const rslot = a.ring + (long)k * a.ring_step;
+      const float* const zk = a.zring + (long)k * B * nz;
+      float* const zk1 = a.zring + (long)(k + 1) * B * nz;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)rslot, (short)0, (int)ring_bytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)zk, (short)0, B * nz * 4, 0x00020000);
+      // in0 image: [sin 2 pi zB, cos 2 pi zB, z] of the 16 rows (the team's in0 code)
+      {
+        f32x4 zv4[EMB_G];
+#pragma unroll
+        for (int g = 0; g < EMB_G; ++g) {
+          const int kk = 16 * g + 4 * q;
+          zv4[g] = (xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (wave * 16 < half) {
+          const int col = wave * 16 + m;
+          f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) e4 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], e4, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rrow = 4 * q + r;
+            if (col < half) {
+              const float t = e4[r] - rintf(e4[r]);
+              const bool ok = r0 + rrow < B;
+              embs[rrow * ld0 + col] = ok ? __builtin_amdgcn_sinf(t) : 0.f;
+              embs[rrow * ld0 + half + col] = ok ? __builtin_amdgcn_cosf(t) : 0.f;
+            }
+          }
+        }
+        if (wave == 0) {
+#pragma unroll
+          for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int kk = 16 * g + 4 * q + e;
+              if (kk < nz) embs[m * ld0 + 2 * half + kk] = zv4[g][e];
+            }
+        }
+        for (int c = 2 * half + nz + tid; c < a.b[0].kpa; c += 256)
+#pragma unroll
+          for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
+        __syncthreads();
+      }
+      for (int j = 0; j < 7; ++j) {
+        const TsBlock& b = a.b[j];
+        const bool final_ = j == 6;
+        for (int tn = 0; tn < b.ntn; ++tn) {
+          const int n0 = tn * TC, erow = r0 + er, ecol = n0 + ec;
+          const bool eok = tid < TM * TC && erow < B && ecol < b.dout;
+          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f;
+          if (eok) {
+            const float* ghr = a.gh + ((long)k * B + erow) * a.ldgh + b.ghoff;
+            gate = ghr[ecol];
+            hb = ghr[b.dout + ecol];
+            bl = b.bls[tn * 16 + ec];
+            bs = b.bls[tn * 16 + 8 + ec];
+            if (final_ && !last && with_noise) {
+              if (noise) {
+                xi = noise[((long)noisy_k * B + erow) * nz + ecol];
+              } else {
+                float n4[4];
+                philox_normal4(seed, chain_base + erow, step_offset + noisy_k, (uint32_t)(ecol >> 2), DAMC_STREAM_SWEEP, n4);
+                xi = pick4(n4, ecol);
+              }
+            }
+          }
+          const float* wrow = b.w + ((long)tn * 16 + m) * b.kp;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if (j == 0) {
+            rs_half<true>(acc, wrow, b.kpa, b.wa, rr, 0, xrow, xok, embs, ld0);
+          } else {
+            if (b.kpb > 0) rs_half<false>(acc, wrow + b.wa, b.kpb, b.wb, rr, a.b[b.srcB].ooff, xrow, xok, nullptr, 0);
+            rs_half<false>(acc, wrow, b.kpa, b.wa, rr, a.b[b.srcA].ooff, xrow, xok, nullptr, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
+          __syncthreads();
+          if (eok) {
+            float l = 0.f, sk = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              l += red[w][er][ec];
+              sk += red[w][er][8 + ec];
+            }
+            const float o = ((l + bl) * gate + hb) + (sk + bs);
+            if (!final_) {
+              rslot[b.ooff + (long)erow * b.dout + ecol] = o;
+            } else {
+              const long zi = (long)erow * nz + ecol;
+              const float zv = ld_sc1_f(zk + zi);
+              const float eps = a.residual ? zv + o : o;
+              if (eps_log && k < eps_log_steps) eps_log[(long)k * B * nz + zi] = eps;
+              const float pred = mul_rn(c0, sub_rn(zv, mul_rn(eps, c1)));
+              float zn;
+              if (last) {
+                zn = pred;
+              } else {
+                zn = add_rn(mul_rn(c2, zv), mul_rn(c3, pred));
+                if (with_noise) zn = add_rn(zn, mul_rn(c4, xi));
+              }
+              zk1[zi] = zn;
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's outputs are in L2 before any wave reads them
+          __syncthreads();
+        }
+      }
+    }
+  }
+  // copy-out of the row tile (sc1: a rescue's own stores are read back past L1)
+  for (int i = tid; i < rows * nz; i += 256) zt[(long)r0 * nz + i] = ld_sc1_f(zfin + (long)r0 * nz + i);
 }
 
 // ------------------------------------------------------------------------------ skinny GEMMs of the precompute
@@ -902,10 +1105,14 @@ __global__ void transpose_kernel(const float* in, int rows, int cols, float* out
   out[c * rows + r] = in[i];
 }
 
-__global__ void sweep_setup_kernel(SweepCall c, SweepCall* dst, const float* zt, float* zw, long n) {
+// the call's per-call record and z, and (team launch) the team flags, error word and diagnostics zeroed: a kernel in
+// the stream, not a memset node, so a captured sweep orders it like every other kernel
+__global__ void sweep_setup_kernel(SweepCall c, SweepCall* dst, const float* zt, float* zw, long n, unsigned* zero,
+                                   long nzero) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *dst = c;
   if (i < n) zw[i] = zt[i];
+  if (i < nzero) zero[i] = 0u;
 }
 
 __global__ void copy_kernel(const float* src, float* dst, long n) {
@@ -929,8 +1136,10 @@ struct SweepWs {
   float *ring, *zring, *tab;
   unsigned* tflags;
   int* err;
+  int* diag;
   size_t bytes;
 };
+constexpr long TS_CTL_WORDS = 8L * TS_MAXT * TS_FS + 64 + 8L * TS_MAXT * 4;
 
 size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
   size_t off = 0;
@@ -969,8 +1178,10 @@ size_t carve(const damc_denoiser_t* d, int B, int n, char* base, SweepWs* w) {
   t.ring = take((long)n * B * S);
   t.zring = take((long)(n + 1) * B * d->nz);
   t.tab = take(8L * n);
-  t.tflags = reinterpret_cast<unsigned*>(take(8 * TS_MAXT * TS_FS + 64));  // team flags, then the error word
+  // team flags, then the error word, then the failed waits' diagnostics
+  t.tflags = reinterpret_cast<unsigned*>(take(TS_CTL_WORDS));
   t.err = reinterpret_cast<int*>(t.tflags + 8 * TS_MAXT * TS_FS);
+  t.diag = reinterpret_cast<int*>(t.tflags + 8 * TS_MAXT * TS_FS + 64);
   t.bytes = off;
   if (w) *w = t;
   return off;
@@ -1286,6 +1497,7 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
   a->call = w.call;
   a->flags = w.tflags;
   a->err = w.err;
+  a->diag = w.diag;
   a->budget = 2000000;  // 20 ms at 100 MHz per wait: a stage takes microseconds
   a->wlds = (int)wl;
   static const int dbg = [] {
@@ -1293,16 +1505,13 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
     return e ? atoi(e) : 0;
   }();
   a->dbg = dbg;
+  const char* ff = getenv("DAMC_SWEEP_FORCE_FAIL");  // tests (read per call): every wait fails, the rescue runs
+  if (ff && ff[0] == '1') a->dbg |= 4096;
   *P = 8 * T;
   *smem = sm;
   return 0;
 }
 
-// NaN-marks the result of a sweep whose team launch failed a bounded wait
-__global__ void team_copyout_kernel(const float* src, float* dst, long n, const int* err) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = *err ? __builtin_nanf("") : src[i];
-}
 
 // the step table (c0..c4, is_last, noisy_k per step) of a schedule, uploaded once per (device, schedule) and kept:
 // a sweep then copies nothing from the host, so it can be captured into a HIP graph (after one eager call with
@@ -1350,7 +1559,6 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
   const int n = a.n;
   int rc = step_table(coef, n, s, &a.tab);
   if (rc) return rc;
-  DAMC_CHECK(hipMemsetAsync(a.flags, 0, (8 * TS_MAXT * TS_FS + 64) * sizeof(unsigned), s));  // flags + error word
   static const bool trace = getenv("DAMC_SWEEP_TRACE") != nullptr;
   const size_t tbytes = (size_t)P * 7 * n * 4 * sizeof(uint64_t);
   if (trace) {
@@ -1375,7 +1583,76 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
   return 0;
 }
 
+// A failed team launch (rescued on the device by team_finish_kernel) is reported through one host-visible word per
+// device; the next sweep on that device reads it (no synchronisation: a failure still in flight is seen a call
+// later) and the process keeps to the launch chain from then on.
+struct TeamHealth {
+  int* host = nullptr;  // pinned, mapped: host view
+  int* dev = nullptr;   // its device address
+  bool disabled = false;
+  long failures = 0;
+};
+std::mutex g_health_mu;
+TeamHealth g_health[64];
+
+// the device's health word (allocated on first use outside a capture; null inside one: the rescue still runs)
+int* team_health_word(int dev, bool capturing) {
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  TeamHealth& h = g_health[dev];
+  if (!h.host && !capturing) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+      h.host = static_cast<int*>(p);
+      *reinterpret_cast<volatile int*>(h.host) = 0;
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) h.dev = static_cast<int*>(d);
+    }
+  }
+  return h.dev;
+}
+
+// true when the team launch may be used on this device: no earlier team launch has needed the rescue
+bool team_healthy(int dev) {
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  TeamHealth& h = g_health[dev];
+  if (h.disabled) return false;
+  if (h.host && *reinterpret_cast<volatile int*>(h.host)) {
+    *reinterpret_cast<volatile int*>(h.host) = 0;
+    ++h.failures;
+    static const bool keep = [] {
+      const char* e = getenv("DAMC_SWEEP_TEAM_KEEP");  // tests: stay on the team launch after a rescue
+      return e && e[0] == '1';
+    }();
+    if (!keep) {
+      h.disabled = true;
+      fprintf(stderr, "damc: a team reverse-sweep launch on device %d could not keep all its workgroups resident; "
+                      "its result was recomputed on the device, and this process now uses the launch chain\n", dev);
+      return false;
+    }
+  }
+  return true;
+}
+
 }  // namespace
+
+extern "C" long damc_sweep_team_failures(int device) {
+  if (device < 0 || device >= 64) return -1;
+  (void)team_healthy(device);  // picks up a failure that has completed since the last sweep
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  return g_health[device].failures;
+}
+
+extern "C" int damc_sweep_team_words(const damc_denoiser_t* d, int B, int n, const void* wsp, size_t wsb, int* out,
+                                     int nwords) {
+  if (validate(d) || B <= 0 || n <= 0 || !wsp || !out || nwords <= 0) return DAMC_ERR_ARG;
+  if (wsb < carve(d, B, n, nullptr, nullptr)) return DAMC_ERR_WORKSPACE;
+  SweepWs w;
+  carve(d, B, n, reinterpret_cast<char*>(const_cast<void*>(wsp)), &w);
+  const long cnt = std::min<long>(nwords, TS_CTL_WORDS);
+  DAMC_CHECK(hipDeviceSynchronize());
+  DAMC_CHECK(hipMemcpy(out, w.tflags, cnt * sizeof(int), hipMemcpyDeviceToHost));
+  return 0;
+}
 
 extern "C" size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int B, int n) {
   if (validate(d) || B <= 0 || n <= 0) return 0;
@@ -1602,9 +1879,23 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   DAMC_CHECK(hipStreamIsCapturing(s, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  const bool team = !capturing && team_enabled() && team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
-  hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s, call, w.call, zt,
-                     team ? w.zring : w.z, nzb);
+  int dev = 0;
+  DAMC_CHECK(hipGetDevice(&dev));
+  // inside a caller's capture the team launch is recorded like any kernel (DAMC_SWEEP_CAPTURE_TEAM=0, read per
+  // call: the launch chain instead).  Round 2 recorded the launch chain there because a replayed team launch timed
+  // out: its flags were zeroed by a hipMemsetAsync node, which the replay did not order before the team kernel
+  // (DAMC_SWEEP_MEMSET_FLAGS=1 restores that form for tools/diag_team_capture.py); the setup kernel zeroes them now.
+  const char* tic = getenv("DAMC_SWEEP_CAPTURE_TEAM");
+  const bool team_in_capture = !(tic && tic[0] == '0');
+  const bool team = (!capturing || team_in_capture) && team_enabled() && dev < 64 && team_healthy(dev) &&
+                    team_plan(d, w, B, n, &ta, &tP, &tsm) == 0;
+  int* health = team ? team_health_word(dev, capturing) : nullptr;
+  const char* mf = getenv("DAMC_SWEEP_MEMSET_FLAGS");  // diagnosis only: round 2's memset form (see above)
+  const bool memset_flags = team && mf && mf[0] == '1';
+  if (memset_flags) DAMC_CHECK(hipMemsetAsync(w.tflags, 0, TS_CTL_WORDS * sizeof(unsigned), s));
+  const long nzero = (team && !memset_flags) ? TS_CTL_WORDS : 0;
+  hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((std::max(nzb, nzero) + 255) / 256)), dim3(256), 0, s, call,
+                     w.call, zt, team ? w.zring : w.z, nzb, w.tflags, nzero);
   DAMC_LAUNCH_CHECK();
   double flops_step = 0;
   for (int j = 0; j < 7; ++j) flops_step += 2.0 * B * 2.0 * d->blocks[j].din * d->blocks[j].dout;
@@ -1622,8 +1913,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     }
   }
   if (team)
-    hipLaunchKernelGGL(team_copyout_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
-                       w.zring + (long)n * nzb, zt, nzb, w.err);
+    hipLaunchKernelGGL(team_finish_kernel, dim3((unsigned)ta.G), dim3(256), 0, s, ta, zt, health);
   else
     hipLaunchKernelGGL(copy_kernel, dim3((unsigned)((nzb + 255) / 256)), dim3(256), 0, s,
                        w.z, zt, nzb);

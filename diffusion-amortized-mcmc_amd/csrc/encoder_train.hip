@@ -22,7 +22,7 @@ namespace {
 
 using namespace damc;
 
-enum { CASE_NONE = 0, CASE_UP = 1, CASE_FIRST = 2, CASE_DENSE = 3, CASE_UP_ODD = 4 };
+enum { CASE_NONE = 0, CASE_UP = 1, CASE_FIRST = 2, CASE_DENSE = 3, CASE_UP_ODD = 4, CASE_UP_CPAD = 5 };
 
 int conv_case(int hin, int win, int cin, int cout, int k, int stride, int pad, int* ho_, int* wo_) {
   const int ho = (hin + 2 * pad - k) / stride + 1, wo = (win + 2 * pad - k) / stride + 1;
@@ -32,6 +32,9 @@ int conv_case(int hin, int win, int cin, int cout, int k, int stride, int pad, i
   if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho && win == 2 * wo && cin % 8 == 0) return CASE_UP;
   if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho + 1 && win == 2 * wo + 1 && cin % 8 == 0) return CASE_UP_ODD;
   if (k == 3 && stride == 1 && pad == 1 && cin <= 4) return CASE_FIRST;
+  // a k4 s2 p1 conv whose input channels are not a multiple of 8 (Encoder_celebaHQ at nif = 4: 4 -> 8): the CASE_UP
+  // path on zero channels padded up to the next multiple of 8, then the crop
+  if (k == 4 && stride == 2 && pad == 1 && hin == 2 * ho && win == 2 * wo && cin % 8 != 0) return CASE_UP_CPAD;
   if (pad == 0 && ho == 1 && wo == 1 && k == hin && k == win) return CASE_DENSE;
   return CASE_NONE;
 }
@@ -129,7 +132,38 @@ struct Bufs {
   unsigned short *dy3 = nullptr, *tin = nullptr, *tdl = nullptr;
   float* part = nullptr;
   float *xp = nullptr, *dyp = nullptr, *dxp = nullptr;  // CASE_UP_ODD: padded x, dy and dx
+  float *wc = nullptr, *dwc = nullptr;                   // CASE_UP_CPAD: channel-padded weight and its gradient
 };
+
+inline int cpad8(int c) { return (c + 7) / 8 * 8; }
+
+// NHWC channel pad / crop: y (rows, C2) from x (rows, C1), zero past C1
+__global__ void chan_pad_kernel(const float* __restrict__ x, long rows, int C1, int C2, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * C2) return;
+  const long r = i / C2;
+  const int c = (int)(i - r * C2);
+  y[i] = c < C1 ? x[r * C1 + c] : 0.f;
+}
+// conv weight (cout, C1, k, k) <-> (cout, C2, k, k), zero past C1
+__global__ void wchan_pad_kernel(const float* __restrict__ w, int cout, int C1, int C2, int kk, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)cout * C2 * kk) return;
+  const int t = (int)(i % kk);
+  const long r = i / kk;
+  const int c = (int)(r % C2), co = (int)(r / C2);
+  y[i] = c < C1 ? w[((long)co * C1 + c) * kk + t] : 0.f;
+}
+int chan_pad(const float* x, long rows, int C1, int C2, float* y, hipStream_t s) {
+  const long n = rows * C2;
+  hipLaunchKernelGGL(chan_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, rows, C1, C2, y);
+  return (int)hipGetLastError();
+}
+int wchan_pad(const float* w, int cout, int C1, int C2, int kk, float* y, hipStream_t s) {
+  const long n = (long)cout * C2 * kk;
+  hipLaunchKernelGGL(wchan_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, cout, C1, C2, kk, y);
+  return (int)hipGetLastError();
+}
 
 void carve_up(Carve& cv, int B, int ho, int wo, int cin, int cout, Bufs& t) {
   const long M = (long)B * ho * wo;
@@ -160,7 +194,15 @@ size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int 
     t.xp = cv.take<float>((size_t)B * (hin + 1) * (win + 1) * cin);
     t.dxp = cv.take<float>((size_t)B * (hin + 1) * (win + 1) * cin);
     t.dyp = cv.take<float>((size_t)B * (ho + 1) * (wo + 1) * cout);
-    carve_up(cv, B, ho + 1, wo + 1, cin, cout, t);  } else if (c == CASE_FIRST) {
+    carve_up(cv, B, ho + 1, wo + 1, cin, cout, t);
+  } else if (c == CASE_UP_CPAD) {
+    const int cp = cpad8(cin);
+    t.xp = cv.take<float>((size_t)B * hin * win * cp);
+    t.dxp = cv.take<float>((size_t)B * hin * win * cp);
+    t.wc = cv.take<float>((size_t)cout * cp * 16);
+    t.dwc = cv.take<float>((size_t)cout * cp * 16);
+    carve_up(cv, B, ho, wo, cp, cout, t);
+  } else if (c == CASE_FIRST) {
     damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
     L.kind = DAMC_LAYER_SMALLC;
     L.cin = cout;
@@ -334,6 +376,16 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     return (int)hipGetLastError();
   }
   if (cs == CASE_UP) return backward_up(x, dy, w, B, hin, win, cin, cout, ho, wo, dx, dw, t, s, stream);
+  if (cs == CASE_UP_CPAD) {  // CASE_UP on channels padded with zeros to a multiple of 8, then the crops
+    const int cp = cpad8(cin);
+    const long rows = (long)B * hin * win;
+    if ((rc = chan_pad(x, rows, cin, cp, t.xp, s))) return rc;
+    if ((rc = wchan_pad(w, cout, cin, cp, 16, t.wc, s))) return rc;
+    if ((rc = backward_up(t.xp, dy, t.wc, B, hin, win, cp, cout, ho, wo, dx ? t.dxp : nullptr, t.dwc, t, s, stream)))
+      return rc;
+    if ((rc = wchan_pad(t.dwc, cout, cp, cin, 16, dw, s))) return rc;  // (cout, cp, 4, 4) -> (cout, cin, 4, 4)
+    return dx ? chan_pad(t.dxp, rows, cp, cin, dx, s) : 0;
+  }
   // CASE_UP_ODD: (A) on the padded tensors, then the crop
   if ((rc = pad_crop(x, B, hin, win, cin, t.xp, hin + 1, win + 1, s))) return rc;
   if ((rc = pad_crop(dy, B, ho, wo, cout, t.dyp, ho + 1, wo + 1, s))) return rc;

@@ -1126,12 +1126,15 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     if (nk > 1) load_ab(X3_BK);
   }
   __syncthreads();
+  bf16x8 pfa[4][3], pfb[4][3];  // the read-order path's fragments
   for (int kt = 0; kt < nk; ++kt) {
     const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
     // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
     // barrier at the end of this tile (its vmcnt(0)) lands it
     // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
-    if (DMA && kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+    // timing probes (tools/gemm_bench.hip only, wrong results): 512 no DMA after the first tile, 1024 fragment reads
+    // of the first tile only
+    if (DMA && kt + 1 < nk && !(V & 512)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
     if (M16 && (V & 256)) {
       // 256: fragment reads one group ahead of the MFMAs that consume them, in the order those MFMAs run (A tile 0
       // against B tiles 0..3, then A tiles 1..3), pinned by sched_group_barrier: the first MFMAs wait for 6 reads
@@ -1140,12 +1143,15 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       // reading the next tile's first fragments after the barrier into the registers the trailing MFMAs free
       // (cross-tile pipeline, 1-2 % slower than this), all reads issued by the end of A row 0 so the barrier moves
       // up (5-8 % slower), A tile 3 read later so it moves down (0-2 % slower).
-      bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
+      bf16x8 (&fa)[4][3] = pfa, (&fb)[4][3] = pfb;  // [tile][limb]
+      const bool rd = !(V & 1024) || kt == 0;
       auto rd_a = [&](int t) {
+        if (!rd) return;
 #pragma unroll
         for (int l = 0; l < 3; ++l) fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
       };
       auto rd_b = [&](int t) {
+        if (!rd) return;
 #pragma unroll
         for (int l = 0; l < 3; ++l) fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
       };

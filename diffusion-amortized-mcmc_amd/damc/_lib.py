@@ -157,6 +157,8 @@ _SIGS = {
     "damc_q_encoder_fwd": (_I, [ctypes.POINTER(Encoder), _P, _I, _P, _P, _SZ, _P]),
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
+    "damc_sweep_team_failures": (ctypes.c_long, [_I]),
+    "damc_sweep_team_words": (_I, [ctypes.POINTER(Denoiser), _I, _I, _P, _SZ, _P, _I]),
     "damc_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,
                                 _SZ, _P]),
     "damc_q_reverse_sweep": (_I, [ctypes.POINTER(Denoiser), _P, _P, _I, _I, _P, _P, _I, _P, _U64, _U64, _P, _I, _P,

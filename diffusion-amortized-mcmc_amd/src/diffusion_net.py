@@ -199,11 +199,22 @@ class SinusoidalPosEmb(nn.Module):
         self.dim = dim
         self.max_time = max_time
 
+    _FREQS = {}
+
     def forward(self, x):
         x *= 1000.0 / self.max_time
         half = self.dim // 2
-        freqs = torch.exp(torch.arange(half, device=x.device) * (-math.log(10000) / (half - 1)))
+        # the frequencies by the reference's fp32 ops on the host CPU (its golden path), cached per device: a
+        # device's own exp may differ by an ulp, which the ~1000 rad angles below amplify to ~1e-4 in sin / cos
+        key = (half, str(x.device))
+        freqs = self._FREQS.get(key)
+        if freqs is None:
+            freqs = torch.exp(torch.arange(half) * (-math.log(10000) / (half - 1))).to(x.device)
+            self._FREQS[key] = freqs
         ang = x[:, None] * freqs[None, :]
+        if ang.device.type == "cuda":  # sin / cos of the fp32 angle rounded once (the host's libm is within 1 ulp)
+            a64 = ang.double()
+            return torch.cat((a64.sin(), a64.cos()), dim=-1).to(ang.dtype)
         return torch.cat((ang.sin(), ang.cos()), dim=-1)
 
 

@@ -270,8 +270,9 @@ size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch, int n_ste
  * steps at once: the time MLP (batch-invariant), the ctx Linear's xemb part (step-invariant), and for every
  * (step, row) a block's ctx c = SiLU(Lc(SiLU(cat(temb, xemb)))), its gate sigmoid(c Wg^T + bg) and hyper
  * bias c Wb^T (fp32 MFMA GEMMs over n*B rows).  The dependent chain — per step the 7 blocks'
- * x Wl^T / x Ws^T products plus the reverse-step update — then runs as 7 launches per step, replayed from a
- * HIP graph cached per (workspace, shapes, schedule) so the host does not bound the ~2 us kernels.
+ * x Wl^T / x Ws^T products plus the reverse-step update — then runs as ONE team launch (weights LDS-resident,
+ * flag hand-offs between the workgroups of a team); DAMC_SWEEP_TEAM=0 runs it as 7 launches per step replayed
+ * from a HIP graph cached per (workspace, shapes, schedule).
  *   eps = p(zt, l_t, xemb); pred = c0 * (zt - eps * c1); zt <- last ? pred : c2*zt + c3*pred (+ c4*xi)
  * temb_in (n_steps, ntemb): SinusoidalPosEmb of the step's logsnr input (host, fp32, as the reference);
  * coef (n_steps, 6), a HOST pointer: {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std,
@@ -288,6 +289,16 @@ int damc_q_reverse_sweep(const damc_denoiser_t* d, const float* xemb, float* zt,
                          const float* temb_in, const float* coef, int with_noise, const float* noise, uint64_t seed,
                          uint64_t chain_base, float* eps_log, int eps_log_steps, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* The team reverse sweep (default) needs all its workgroups resident at once.  If a member never starts (another
+ * process or stream holding CUs), its bounded waits give up and the library recomputes the affected sweep on the
+ * device (bitwise the team's arithmetic; never NaN), flags the device, and runs later sweeps on the launch chain.
+ * damc_sweep_team_failures: how many such rescued launches this process has seen on a device (a rescue still in
+ * flight is counted once it completes).  damc_sweep_team_words (tools; synchronises the device): the workspace's
+ * team control words (flags [8][64][32], error word, then per workgroup {stage needed, first late flag, late-slot
+ * mask lo, hi} of a failed wait). */
+long damc_sweep_team_failures(int device);
+int damc_sweep_team_words(const damc_denoiser_t* d, int batch, int n_steps, const void* workspace,
+                          size_t workspace_bytes, int* out, int nwords);
 /* per-op hook (SURVEY.md §8b damc_denoise_step): ONE reverse step = damc_reverse_sweep with n_steps = 1 on the
  * step's temb_row (ntemb) and coef_row (6, HOST); noise (B, nz) injected or NULL for Philox at step index
  * noise_step (the k-th noisy step of a sweep uses k); eps (B, nz) receives the denoiser output or NULL.

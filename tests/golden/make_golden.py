@@ -251,7 +251,7 @@ def capture_checkpoint(dn, torch):
     np.savez(os.path.join(HERE, "ckpt_cifar10_tiny.npz"), meta=json.dumps(meta), **rec)
 
 
-QTRAIN_CONFIGS = ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"]
+QTRAIN_CONFIGS = ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full", "q_celeba64_s", "q_celebaHQ_s"]
 SEED_QT = 7
 
 
@@ -400,9 +400,13 @@ def main():
 
     torch.set_num_threads(8)
     dn, mc = import_reference()
-    capture_checkpoint(dn, torch)
+    if "--qtrain-only" not in sys.argv:
+        capture_checkpoint(dn, torch)
     for name, (rec, meta) in capture_qtrain(dn, torch).items():
         np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
+    if "--qtrain-only" in sys.argv:
+        print("done")
+        return
     for name, (rec, meta) in capture_gtrain(dn, torch).items():
         np.savez(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **rec)
     if "--gtrain-only" in sys.argv:

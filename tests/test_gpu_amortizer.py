@@ -214,3 +214,36 @@ def test_grouped_hyper_gemms_are_bitwise_the_separate_launches(am, gpu_device, m
         out.append(zt.cpu().numpy())
     assert np.isfinite(out[0]).all()
     assert np.array_equal(out[0], out[1])
+
+
+def test_failed_team_launch_is_rescued_bitwise(am, gpu_device, monkeypatch):
+    """A team member that never becomes resident makes the bounded waits give up (forced here: every wait fails
+    at once).  The sweep is then recomputed on the device by team_finish_kernel with the team's own arithmetic:
+    the result is bitwise the healthy team sweep (no NaN), eps_log included, and the failure is reported to the
+    host (damc_sweep_team_failures) at the next sweep."""
+    from damc import _lib, synth
+
+    Q = _wide_q(gpu_device, 12)
+    xemb = torch.from_numpy(synth.normal_f32(7, 0, (37, 1024))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(8, 0, (37, 128))).to(gpu_device)
+    L = _lib.lib()
+    dev = gpu_device.index or 0
+    zt = zt0.clone()
+    eps = am.reverse_sweep(Q, xemb, zt, seed=5, eps_log_steps=3)
+    torch.cuda.synchronize()
+    before = L.damc_sweep_team_failures(dev)
+    monkeypatch.setenv("DAMC_SWEEP_TEAM_KEEP", "1")
+    monkeypatch.setenv("DAMC_SWEEP_FORCE_FAIL", "1")
+    zr = zt0.clone()
+    epr = am.reverse_sweep(Q, xemb, zr, seed=5, eps_log_steps=3)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("DAMC_SWEEP_FORCE_FAIL")
+    assert torch.isfinite(zr).all()
+    assert torch.equal(zr, zt), "the rescued sweep differs from the team sweep"
+    assert torch.equal(epr, eps)
+    assert L.damc_sweep_team_failures(dev) == before + 1
+    zt2 = zt0.clone()  # the team launch is still used (DAMC_SWEEP_TEAM_KEEP) and healthy again
+    am.reverse_sweep(Q, xemb, zt2, seed=5)
+    torch.cuda.synchronize()
+    assert torch.equal(zt2, zt)
+    assert L.damc_sweep_team_failures(dev) == before + 1

@@ -100,14 +100,22 @@ def test_generator_forward_no_grad_is_hip(gpu_device):
 
 
 # ------------------------------------------------------------------------------------------ Q update
-@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"])
+@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full", "q_celeba64_s",
+                                  "q_celebaHQ_s"])
 def test_q_update_matches_reference(gpu_device, name):
-    """The Q update's loss and gradients (train_gen_recon.py:211-217) with the denoiser forward/backward on
-    libdamc (damc_denoiser_train_*), the encoder / prior_emb / noising on PyTorch, vs the reference's autograd
-    on the same injected noise and a mixed mask.  Tolerance as for the G update."""
-    from conftest import qtrain_run
+    """The Q update's loss and gradients (train_gen_recon.py:211-217) with the denoiser and encoder forward/backward
+    on libdamc (damc_denoiser_train_*, the encoder training kernels), prior_emb / noising on PyTorch, vs the
+    reference's autograd on the same injected noise and a mixed mask.  Per tensor the bound is 1e-4 or twice the
+    error of the reference's own ops run on this GPU (stock PyTorch), whichever is larger: at B = 2 a few
+    gradients are ill-conditioned (q_celeba64_s: in_layers.2._skip.weight sits 4.8e-5 from the golden with the
+    reference's ops on the CPU and 2.1e-4 on the GPU, tools/diag_qtrain.py)."""
+    from conftest import gtrain_errors, qtrain_run
 
     from damc import training
+
+    with training.stock_pytorch():
+        _, g_ref_dev, rec0, meta0 = qtrain_run(name, gpu_device)
+    tol = [max(1e-4, 2.0 * max(e)) for e in gtrain_errors(g_ref_dev, rec0, meta0)]
 
     calls = []
     orig = training.encoder_apply
@@ -122,8 +130,8 @@ def test_q_update_matches_reference(gpu_device, name):
     # 1e-4: the time embedding sin/cos(1000 * f * t) (SinusoidalPosEmb, arguments up to ~1000 rad, whose own
     # fp32 rounding is ~3e-5 absolute) is torch's on each device, GPU vs the reference's CPU; with B = 3-4
     # samples that difference reaches time_mlp[1].weight's gradient unaveraged (its norm agrees to ~1e-6)
-    worst = gtrain_check(grads, rec, meta, 1e-4)
-    print("%s worst rel err vs reference %.2e" % (name, worst))
+    worst = gtrain_check(grads, rec, meta, tol)
+    print("%s worst rel err vs reference %.2e (largest bound %.2e)" % (name, worst, max(tol)))
 
 
 def test_denoiser_train_vs_autograd_b128(gpu_device):
@@ -212,8 +220,12 @@ def test_odd_k4s2_conv_backward(gpu_device, B, cin, cout):
         assert e <= 3 * e32 + 1e-6, (nm, e, e32)
 
 
-def test_encoder_train_stagewise_b128(gpu_device):
-    """Bench-size encoder training (CIFAR-10 Encoder, nif 64, nemb 1024, B=128): the libdamc backward replayed
+@pytest.mark.parametrize("name,B,nif", [("cifar10", 128, 64), ("celeba64", 8, 64), ("celebaHQ", 8, 64),
+                                        ("celebaHQ", 2, 4)])
+def test_encoder_train_stagewise(gpu_device, name, B, nif):
+    """Encoder training at full width (nif 64, nemb 1024): CIFAR-10 at the bench size B=128, and the CelebA-64 /
+    CelebA-HQ encoders (diffusion_net.py:268-372; 64x64 and 256x256 inputs, 5 and 7 convolutions) at B=8, their
+    per-rank batch.  The libdamc backward replayed
     stage by stage, each op (InstanceNorm+LReLU backward; Conv2d backward: dense last conv, k4 s2 p1 convs on
     the limb engine with swapped roles, first conv via the direct kernel) fed the SAME inputs as an fp64 and an
     fp32 PyTorch autograd evaluation.  Per output: |hip - fp64| <= 3 |torch fp32 - fp64| + 1e-6.
@@ -229,9 +241,9 @@ def test_encoder_train_stagewise_b128(gpu_device):
     from damc._lib import ptr
     from src import diffusion_net as dn
 
-    B = 128
-    enc = synth.load_into(dn.Encoder_cifar10(nc=3, nemb=1024, nif=64), 4).to(gpu_device).train()
-    x = torch.from_numpy(synth.uniform_f32(6, 0, (B, 3, 32, 32))).to(gpu_device)
+    hw = {"cifar10": 32, "celeba64": 64, "celebaHQ": 256}[name]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=nif), 4).to(gpu_device).train()
+    x = torch.from_numpy(synth.uniform_f32(6, 0, (B, 3, hw, hw))).to(gpu_device)
     g = torch.from_numpy(synth.normal_f32(6, 1, (B, 1024))).to(gpu_device)
     assert training.encoder_train_supported(enc, x)
     cap = {}
@@ -253,9 +265,10 @@ def test_encoder_train_stagewise_b128(gpu_device):
     def check3(name, ours, t32, t64):
         e, e32 = rel_l2(ours.double().cpu().numpy(), t64.cpu().numpy()), rel_l2(t32.double().cpu().numpy(),
                                                                              t64.cpu().numpy())
-        print("%s: |hip - fp64| %.2e  |torch32 - fp64| %.2e" % (name, e, e32))
-        assert e <= 3 * e32 + 1e-6, (name, e, e32)
+        print("%s %s: |hip - fp64| %.2e  |torch32 - fp64| %.2e" % (enc_name, name, e, e32))
+        assert e <= 3 * e32 + 1e-6, (enc_name, name, e, e32)
 
+    enc_name = "Encoder_%s nif=%d B=%d" % (name, nif, B)
     dh = g.contiguous()
     stages, saved = cap["stages"], cap["saved"]
     for i in range(len(stages) - 1, -1, -1):

@@ -171,7 +171,7 @@ def test_reference_checkpoint_loads():
         assert rel_l2(orc.encoder_forward(Q.encoder, x).numpy(), d["xemb"]) < 1e-5
 
 
-@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full"])
+@pytest.mark.parametrize("name", ["q_cifar10_s", "q_svhn_s", "q_mnist_s", "q_cifar10_full", "q_celeba64_s", "q_celebaHQ_s"])
 def test_q_update_loss_and_grads_cpu(name):
     """Q update (train_gen_recon.py:211-217) of the drop-in Q on CPU (stock ops) vs the reference's autograd."""
     loss, grads, rec, meta = qtrain_run(name, "cpu")

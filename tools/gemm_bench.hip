@@ -251,7 +251,7 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
   }
-  V vars[] = {{"X3/v5", run_x3<5>}, {"X3/v261(rd-order)", run_x3<261>}, {"X3/v389(rd-order+prio)", run_x3<389>}};
+  V vars[] = {{"v261", run_x3<261>}, {"noDMA", run_x3<261 | 512>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
