@@ -278,6 +278,45 @@ def amortizer_bench(device):
             "sweep_reference_equivalent_tflops": round(sweep_flop / (t_sw / 1e3) / 1e12, 2)}
 
 
+def hq_q_legs(device):
+    """BASELINE config 5's named workload: CelebA-HQ Q(x) = Encoder_celebaHQ(nif=64) + the 100-step 'large' reverse
+    sweep (nxemb 1024, ntemb 128; train_gen_recon.py:360-380, diffusion_net.py:315-372,585-622), at the per-rank batch
+    of 8 GPUs (B=8) and the whole batch on one GPU (B=64).  Encoder FLOP = 2 B x 6,362.8 M MAC."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    n_int = 100
+    Q = dn._netQ_U(nc=3, nz=NZ, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=n_int,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                   dataset="celebaHQ")
+    synth.load_into(Q, 20)
+    Q.to(device).eval()
+    for p in Q.parameters():
+        p.requires_grad_(False)
+    out = {}
+    for bsz in (8, 64):
+        x = torch.from_numpy(synth.uniform_f32(33, 0, (bsz, 3, 256, 256))).to(device)
+        zt = torch.from_numpy(synth.normal_f32(34, 0, (bsz, NZ))).to(device)
+        xemb = amortizer.encoder_forward(Q.encoder, x)
+        zw = torch.empty_like(zt)
+
+        def sweep():
+            zw.copy_(zt)
+            amortizer.reverse_sweep(Q, xemb, zw, seed=5)
+
+        t_enc = event_ms(lambda: amortizer.encoder_forward(Q.encoder, x), reps=3)
+        t_sw = event_ms(sweep, reps=3)
+        t_q = event_ms(lambda: amortizer.q_forward(Q, x=x), reps=3)
+        enc_flop = 2.0 * bsz * 6362.8e6
+        out["celebaHQ Q(x) B=%d" % bsz] = {
+            "q_forward_ms": round(t_q, 3), "encoder_ms": round(t_enc, 3), "sweep_ms": round(t_sw, 3),
+            "us_per_denoise_step": round(1e3 * t_sw / n_int, 2),
+            "encoder_tflops": round(enc_flop / (t_enc / 1e3) / 1e12, 1)}
+        del x, zt, xemb, zw
+        torch.cuda.empty_cache()
+    return out
+
+
 def g_update_bench(device, with_torch=True):
     """SURVEY.md §8(f) row 1, the G update of a training iteration (train_gen_recon.py:222-231) at the bench
     config: x_hat = G(z); sum((x_hat - x)^2, [1,2,3]).mean().backward() with the drop-in _netG_cifar10
@@ -579,6 +618,7 @@ def main():
         # outside the timed region (after the max-over-ranks reduction): does not enter `value`; rank 0 only
         extras = langevin_breakdown(lv, G, E, x, z0, p0, zbuf, pbuf, plan)
         extras["amortizer"] = amortizer_bench(device)
+        extras["amortizer"]["celebaHQ"] = hq_q_legs(device)
         extras["g_update"] = g_update_bench(device, with_torch=not args.no_torch_g)
         extras["q_update"] = q_update_bench(device, with_torch=not args.no_torch_g)
 

@@ -65,7 +65,21 @@ __global__ __launch_bounds__(256) void in_stats_kernel(const float* y, int B, in
   const int p0 = (int)((long)HW * s / S), p1 = (int)((long)HW * (s + 1) / S);
   Wf w{0.f, 0.f, 0.f};
   if (c < C) {
-    for (int p = p0 + prow; p < p1; p += 4) {
+    // four loads in flight, then their updates in pixel order (the same Welford chain as one at a time)
+    int p = p0 + prow;
+    for (; p + 12 < p1; p += 16) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = y[((long)b * HW + p + 4 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w.n += 1.f;
+        const float d = v[u] - w.mean;
+        w.mean += d / w.n;
+        w.m2 += d * (v[u] - w.mean);
+      }
+    }
+    for (; p < p1; p += 4) {
       const float v = y[((long)b * HW + p) * C + c];
       w.n += 1.f;
       const float d = v - w.mean;
@@ -116,6 +130,189 @@ __global__ __launch_bounds__(256) void in_apply_kernel(float* y, int B, int HW, 
     float* q = y + ((long)b * HW + p) * C + c;
     const float v = fmaf(*q, scl, shf);
     *q = v > 0.f ? v : v * slope;
+  }
+}
+
+// (scale, shift) of every (sample, channel) from the S statistics partials, merged once (in_apply_kernel's merge,
+// same order): ss [B][2][C]
+__global__ void in_merge_kernel(const float* __restrict__ part, int B, int C, int S, const float* gamma,
+                                const float* beta, float eps, float* __restrict__ ss) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  const float* pp = part + (long)i * S * 3;
+  Wf a{pp[0], pp[1], pp[2]};
+  for (int s = 1; s < S; ++s) a = wmerge(a, Wf{pp[3 * s], pp[3 * s + 1], pp[3 * s + 2]});
+  const float var = a.m2 / a.n;
+  const float rstd = 1.f / sqrtf(var + eps);
+  const float scale = rstd * gamma[c];
+  ss[(long)b * 2 * C + c] = scale;
+  ss[(long)b * 2 * C + C + c] = beta[c] - a.mean * scale;
+}
+
+// the normalise + affine + LeakyReLU of in_apply_kernel (same fmaf), written as the next convolution's limbs (x3
+// octets) instead of fp32 in place: the limb engine reads nothing else.  One thread per (pixel, channel octet).
+__global__ __launch_bounds__(256) void in_apply_x3_kernel(const float* __restrict__ y, long n8, int HW, int C,
+                                                          const float* __restrict__ ss, float slope,
+                                                          unsigned short* __restrict__ y3) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const int C8 = C / 8;
+  const long pix = i / C8;
+  const int c0 = (int)(i - pix * C8) * 8;
+  const int b = (int)(pix / HW);
+  const float* sc = ss + (long)b * 2 * C + c0;
+  const f32x4 v0 = *reinterpret_cast<const f32x4*>(y + 8 * i), v1 = *reinterpret_cast<const f32x4*>(y + 8 * i + 4);
+  const f32x4 a0 = *reinterpret_cast<const f32x4*>(sc), a1 = *reinterpret_cast<const f32x4*>(sc + 4);
+  const f32x4 h0 = *reinterpret_cast<const f32x4*>(sc + C), h1 = *reinterpret_cast<const f32x4*>(sc + C + 4);
+  float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  const float sa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const float sb[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t = fmaf(v[e], sa[e], sb[e]);
+    v[e] = t > 0.f ? t : t * slope;
+  }
+  damc::store_x3_octet(v, y3 + 24 * i);
+}
+
+// ---- the first layer (Conv2d k3 s1 p1 on the nc <= 4 image channels, then InstanceNorm + LeakyReLU) in two passes
+// that recompute the convolution (9 nc MACs per output) instead of storing it: pass 1 its per-(sample, channel)
+// statistics, pass 2 the normalised activation as the next convolution's limbs.  The conv output, the largest
+// tensor of the encoder (1 GB at CelebA-HQ B=64), never reaches HBM.  A block = R image rows of one sample, the
+// (R+2) x (W+2) x CIN input window staged in LDS (read from the caller's NCHW image).  A wave owns one channel
+// octet at a time (its 8 x 9 CIN weights wave-uniform: scalar loads, no LDS traffic) and its lanes own pixels, whose
+// 9 CIN window values are read from LDS once for the 8 channels.  Both passes evaluate y with conv3_octet (fixed tap
+// order, one fmaf chain per channel), so the statistics describe exactly the values pass 2 normalises.
+template <int CIN>
+__device__ __forceinline__ void conv3_octet(const float* __restrict__ win, int ld, int r, int x,
+                                            const float* __restrict__ wl, int C, int c0, const float* __restrict__ bl,
+                                            float (&y)[8]) {
+  float xv[9 * CIN];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci) xv[(ky * 3 + kx) * CIN + ci] = win[((r + ky) * ld + x + kx) * CIN + ci];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9 * CIN; ++t) {  // wl: the LDS copy of damc_pack_conv2d's [(ky, kx, ci)][co] (a wave-uniform
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(wl + t * C + c0);  // address: broadcast reads)
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(wl + t * C + c0 + 4);
+    acc[0] = fmaf(w0.x, xv[t], acc[0]);
+    acc[1] = fmaf(w0.y, xv[t], acc[1]);
+    acc[2] = fmaf(w0.z, xv[t], acc[2]);
+    acc[3] = fmaf(w0.w, xv[t], acc[3]);
+    acc[4] = fmaf(w1.x, xv[t], acc[4]);
+    acc[5] = fmaf(w1.y, xv[t], acc[5]);
+    acc[6] = fmaf(w1.z, xv[t], acc[6]);
+    acc[7] = fmaf(w1.w, xv[t], acc[7]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) y[e] = acc[e] + bl[c0 + e];
+}
+// the strip's input window: rows r0-1 .. r0+R of sample b, columns -1 .. W, zero outside, [row][col][ci] in LDS
+template <int CIN>
+__device__ __forceinline__ void conv3_stage(const float* __restrict__ x, int b, int H, int W, int r0, int R, float* win) {
+  const int ld = W + 2, n = (R + 2) * ld * CIN;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int ci = i % CIN, rc = i / CIN, rr = rc / ld, cc = rc - rr * ld;
+    const int iy = r0 - 1 + rr, ix = cc - 1;
+    win[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? x[(((long)b * CIN + ci) * H + iy) * W + ix] : 0.f;
+  }
+}
+
+// pass 1: grid (B, S strips of R rows); wave w takes octets w, w+4, ...; each lane a Welford chain over its pixels per
+// channel, then the 64 lanes merged (Chan, fixed butterfly order); part [B][C][S][3] as in_stats_kernel's
+template <int CIN>
+__global__ __launch_bounds__(256) void conv3_stats_kernel(const float* __restrict__ x, int H, int W, int C, int R,
+                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                          float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float sm3[];  // [9 CIN][C] weights, [C] bias, then the window
+  const int b = blockIdx.x, s = blockIdx.y, S = gridDim.y, r0 = s * R, rows = min(R, H - r0);
+  float* wl = sm3;
+  float* bl = wl + 9 * CIN * C;
+  float* win = bl + C;
+  for (int i = threadIdx.x; i < 9 * CIN * C; i += blockDim.x) wl[i] = w[i];
+  for (int i = threadIdx.x; i < C; i += blockDim.x) bl[i] = bias ? bias[i] : 0.f;
+  conv3_stage<CIN>(x, b, H, W, r0, R, win);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, npix = rows * W;
+  for (int o = wave; o < C / 8; o += 4) {
+    const int c0 = __builtin_amdgcn_readfirstlane(o * 8);
+    Wf a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = Wf{0.f, 0.f, 0.f};
+    float n = 0.f;
+    for (int p = lane; p < npix; p += 64) {
+      // the weights are re-read from LDS per pixel (broadcast reads); held in registers across the loop they took
+      // 216 VGPRs and left one wave per SIMD
+      asm volatile("" ::: "memory");
+      const int r = p / W, xx = p - r * W;
+      float y[8];
+      conv3_octet<CIN>(win, W + 2, r, xx, wl, C, c0, bl, y);
+      n += 1.f;
+      const float inv = 1.f / n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = y[e] - a[e].mean;
+        a[e].mean += d * inv;
+        a[e].m2 += d * (y[e] - a[e].mean);
+        a[e].n = n;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const Wf t{__shfl_xor(a[e].n, off), __shfl_xor(a[e].mean, off), __shfl_xor(a[e].m2, off)};
+        a[e] = (lane & off) ? wmerge(t, a[e]) : wmerge(a[e], t);  // both partners form the same (lower, upper) merge
+      }
+    if (lane < 8) {
+      Wf t = a[0];
+#pragma unroll
+      for (int e = 1; e < 8; ++e)
+        if (lane == e) t = a[e];
+      float* op = part + (((long)b * C + c0 + lane) * S + s) * 3;
+      op[0] = t.n;
+      op[1] = t.mean;
+      op[2] = t.m2;
+    }
+  }
+}
+
+// pass 2: grid (B, S strips); wave w takes octets w, w+4, ..., lanes pixels; writes the limbs of lrelu(IN(y))
+template <int CIN>
+__global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __restrict__ x, int H, int W, int C, int R,
+                                                             const float* __restrict__ w, const float* __restrict__ bias,
+                                                             const float* __restrict__ ss, float slope,
+                                                             unsigned short* __restrict__ y3) {
+  extern __shared__ __attribute__((aligned(16))) float sm3[];  // [9 CIN][C] weights, [C] bias, then the window
+  const int b = blockIdx.x, s = blockIdx.y, r0 = s * R, rows = min(R, H - r0);
+  float* wl = sm3;
+  float* bl = wl + 9 * CIN * C;
+  float* win = bl + C;
+  for (int i = threadIdx.x; i < 9 * CIN * C; i += blockDim.x) wl[i] = w[i];
+  for (int i = threadIdx.x; i < C; i += blockDim.x) bl[i] = bias ? bias[i] : 0.f;
+  conv3_stage<CIN>(x, b, H, W, r0, R, win);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, npix = rows * W;
+  const float* sb = ss + (long)b * 2 * C;
+  for (int o = wave; o < C / 8; o += 4) {
+    const int c0 = __builtin_amdgcn_readfirstlane(o * 8);
+    for (int p = lane; p < npix; p += 64) {
+      asm volatile("" ::: "memory");  // weights re-read from LDS per pixel (see conv3_stats_kernel)
+      const int r = p / W, xx = p - r * W;
+      float v[8];
+      conv3_octet<CIN>(win, W + 2, r, xx, wl, C, c0, bl, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = fmaf(v[e], sb[c0 + e], sb[C + c0 + e]);
+        v[e] = t > 0.f ? t : t * slope;
+      }
+      damc::store_x3_octet(v, y3 + 3 * ((((long)b * H + r0 + r) * W + xx) * C + c0));
+    }
   }
 }
 
@@ -407,45 +604,122 @@ extern "C" int damc_instnorm_lrelu_backward_nhwc(const float* y, const float* st
   return 0;
 }
 
-// ---- the whole encoder forward in one call (damc_q_encoder_fwd): NCHW -> NHWC, then per layer the conv
-// (split-K slabs when its tiles would not fill the chip) and InstanceNorm + LeakyReLU in place; two
-// ping-pong activation buffers, the last conv writes xemb directly
+// ---- the whole encoder forward in one call (damc_q_encoder_fwd): NCHW -> NHWC, then per layer the conv and
+// InstanceNorm + LeakyReLU in place; two ping-pong activation buffers, the last conv writes xemb directly.
+// Convolutions with cin % 32 == 0 (all but the first 3x3 at the reference's nif) run on the limb engine
+// (gemm_x3_kernel, A_CONV gather with stride / pad, bias epilogue; split-K into the sign blocks when the grid would
+// not fill the chip): the input activation is split into limbs per call, the weights' limb copy comes from the
+// caller (damc_pack_conv2d_x3) or is split into the workspace.  The rest on the fp32 MFMA engine.
 namespace {
 struct EncShapes {
   int h[DAMC_MAX_ENC_LAYERS + 1], w[DAMC_MAX_ENC_LAYERS + 1];
   size_t act_max = 0, slab_max = 0, in_max = 0;
+  size_t a3_max = 0, w3_max = 0, ks_max = 0;  // limb engine: activation limbs, weight limbs, split-K slabs
+  bool limb[DAMC_MAX_ENC_LAYERS] = {};
+  bool first_fused = false;  // layer 0 as conv3_stats + conv3_apply_x3 (no stored conv output, no NHWC copy)
+  int first_rows = 1, first_strips = 1;
 };
+bool enc_limb_layer(const damc_encoder_t* e, const damc_enc_layer_t& L) {
+  return e->engine == DAMC_ENGINE_LIMB && damc::conv_kmajor_ok(L.cin) && L.cout % 8 == 0 && L.k * L.k <= 32;
+}
 bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
   if (!e || B <= 0 || e->n_layers < 1 || e->n_layers > DAMC_MAX_ENC_LAYERS || e->nc <= 0 || e->h <= 0 || e->w <= 0)
     return false;
+  if (e->engine != DAMC_ENGINE_LIMB && e->engine != DAMC_ENGINE_FP32) return false;
   sh->h[0] = e->h;
   sh->w[0] = e->w;
   int c = e->nc;
   sh->act_max = (size_t)B * e->h * e->w * e->nc;
   for (int i = 0; i < e->n_layers; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
-    if (L.cin != c || L.cout <= 0 || L.k <= 0 || L.stride <= 0 || L.pad < 0 || !L.w_packed) return false;
+    if (L.cin != c || L.cout <= 0 || L.k <= 0 || L.stride <= 0 || L.pad < 0) return false;
     if ((L.in_gamma == nullptr) != (L.in_beta == nullptr)) return false;
     const int ho = (sh->h[i] + 2 * L.pad - L.k) / L.stride + 1, wo = (sh->w[i] + 2 * L.pad - L.k) / L.stride + 1;
     if (ho <= 0 || wo <= 0) return false;
     sh->h[i + 1] = ho;
     sh->w[i + 1] = wo;
     if (i + 1 < e->n_layers) sh->act_max = std::max(sh->act_max, (size_t)B * ho * wo * L.cout);
-    sh->slab_max = std::max(sh->slab_max,
-                            damc_conv2d_workspace_floats(B, sh->h[i], sh->w[i], L.cin, L.cout, L.k, L.stride, L.pad));
-    if (L.in_gamma) sh->in_max = std::max(sh->in_max, damc_instnorm_workspace_floats(B, ho * wo, L.cout));
+    sh->limb[i] = enc_limb_layer(e, L);
+    if (!L.w_packed && !(sh->limb[i] && L.w_x3)) return false;  // the engine's weight operand
+    if (sh->limb[i]) {
+      const long M = (long)B * ho * wo, K = (long)L.k * L.k * L.cin;
+      sh->a3_max = std::max(sh->a3_max, (size_t)B * sh->h[i] * sh->w[i] * L.cin * 6);
+      if (!L.w_x3) sh->w3_max = std::max(sh->w3_max, (size_t)L.cout * K * 6);
+      sh->ks_max = std::max(sh->ks_max, (size_t)damc::x3_ksplit_floats((int)M, L.cout, (int)K, 1));
+    } else {
+      sh->slab_max = std::max(sh->slab_max,
+                              damc_conv2d_workspace_floats(B, sh->h[i], sh->w[i], L.cin, L.cout, L.k, L.stride, L.pad));
+    }
+    if (L.in_gamma)
+      sh->in_max = std::max(sh->in_max, damc_instnorm_workspace_floats(B, ho * wo, L.cout) + (size_t)B * L.cout * 2);
     c = L.cout;
+  }
+  const damc_enc_layer_t& F0 = e->layers[0];
+  sh->first_fused = e->n_layers > 1 && sh->limb[1] && F0.k == 3 && F0.stride == 1 && F0.pad == 1 &&
+                    (F0.cin == 1 || F0.cin == 3 || F0.cin == 4) && F0.cout % 64 == 0 && F0.cout <= 512 &&
+                    F0.in_gamma && F0.w_packed && !damc::conv_kmajor_ok(F0.cin) && e->w <= 1024;
+  if (sh->first_fused) {
+    // ~1024 blocks over the batch (each strip's lanes merge their statistics once, a butterfly per channel octet),
+    // at most 64 strips per sample, at least 128 pixels per strip
+    const int want = std::max(1, std::min(64, 1024 / B));
+    sh->first_rows = std::max((e->h + want - 1) / want, (128 + e->w - 1) / e->w);
+    sh->first_strips = (e->h + sh->first_rows - 1) / sh->first_rows;
+    sh->in_max = std::max(sh->in_max, (size_t)B * F0.cout * (sh->first_strips * 3 + 2));
+    sh->a3_max = std::max(sh->a3_max, (size_t)B * e->h * e->w * F0.cout * 6);
   }
   return true;
 }
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
+
+// y (B, ho, wo, cout) NHWC = conv(x3 limbs of x) + bias on the limb engine
+int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_enc_layer_t& L, const void* w3, float* y,
+                float* kslab, size_t kslab_floats, hipStream_t s) {
+  const int hout = (hin + 2 * L.pad - L.k) / L.stride + 1, wout = (win + 2 * L.pad - L.k) / L.stride + 1;
+  damc::GemmArgs a;
+  a.A3 = a3;
+  a.Hin = hin;
+  a.Win = win;
+  a.Cg = L.cin;
+  a.Hq = hout;
+  a.Wq = wout;
+  a.kw = L.k;
+  a.stride = L.stride;
+  a.pad_y = L.pad;
+  a.pad_x = L.pad;
+  a.B3 = static_cast<const unsigned short*>(w3);
+  a.b_negblk = 1;  // damc::launch_split_x3_conv's layout (sign-alternating blocks)
+  a.C = y;
+  a.ldc = L.cout;
+  a.M = B * hout * wout;
+  a.N = L.cout;
+  a.K = L.k * L.k * L.cin;
+  a.k_per_z = a.K;
+  a.bias = L.bias;
+  a.bias_mod = L.cout;
+  a.act = DAMC_ACT_NONE;
+  a.kslab = kslab;
+  a.kslab_floats = (long)kslab_floats;
+  return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
+                           2.0 * a.M * (double)L.cout * a.K, s);
+}
 }  // namespace
+
+extern "C" size_t damc_conv2d_x3_bytes(int cout, int cin, int k) {
+  if (cout <= 0 || cin <= 0 || k <= 0 || !damc::conv_kmajor_ok(cin) || cout % 8 != 0 || k * k > 32) return 0;
+  return (size_t)cout * k * k * cin * 6;
+}
+
+extern "C" int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream) {
+  if (!w || !w_x3 || !damc_conv2d_x3_bytes(cout, cin, k)) return DAMC_ERR_ARG;
+  return damc::launch_pack_conv_x3(w, cout, cin, k, static_cast<unsigned short*>(w_x3), as_stream(stream));
+}
 
 extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B) {
   EncShapes sh;
   if (!enc_shapes(e, B, &sh)) return 0;
   return 2 * round256(sh.act_max * 4) + round256(std::max<size_t>(sh.slab_max, 1) * 4) +
-         round256(std::max<size_t>(sh.in_max, 1) * 4);
+         round256(std::max<size_t>(sh.in_max, 1) * 4) + round256(sh.a3_max) + round256(sh.w3_max) +
+         round256(sh.ks_max * 4);
 }
 
 extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B, float* xemb, void* wsp, size_t wsb,
@@ -456,23 +730,89 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   if (sh.h[n] != 1 || sh.w[n] != 1) return DAMC_ERR_UNSUPPORTED;  // NHWC flatten == NCHW flatten only at 1 x 1
   if (!wsp || wsb < damc_q_encoder_workspace_bytes(e, B)) return DAMC_ERR_WORKSPACE;
   char* base = reinterpret_cast<char*>(wsp);
-  float* buf[2] = {reinterpret_cast<float*>(base), reinterpret_cast<float*>(base + round256(sh.act_max * 4))};
-  float* slabs = reinterpret_cast<float*>(base + 2 * round256(sh.act_max * 4));
-  float* inws = reinterpret_cast<float*>(base + 2 * round256(sh.act_max * 4) +
-                                         round256(std::max<size_t>(sh.slab_max, 1) * 4));
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base + off;
+    off += round256(bytes);
+    return p;
+  };
+  float* buf[2];
+  buf[0] = reinterpret_cast<float*>(take(sh.act_max * 4));
+  buf[1] = reinterpret_cast<float*>(take(sh.act_max * 4));
+  float* slabs = reinterpret_cast<float*>(take(std::max<size_t>(sh.slab_max, 1) * 4));
+  float* inws = reinterpret_cast<float*>(take(std::max<size_t>(sh.in_max, 1) * 4));
+  unsigned short* a3 = reinterpret_cast<unsigned short*>(take(sh.a3_max));
+  unsigned short* w3 = reinterpret_cast<unsigned short*>(take(sh.w3_max));
+  float* kslab = reinterpret_cast<float*>(take(sh.ks_max * 4));
+  hipStream_t s = as_stream(stream);
   int rc;
-  if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) return rc;
-  for (int i = 0; i < n; ++i) {
+  bool a3_ready = false;  // a3 holds the limbs of the current layer's input (written by the previous layer's norm)
+  int i0 = 0;
+  if (sh.first_fused) {  // layer 0: conv3 + InstanceNorm + LeakyReLU straight to layer 1's limbs
+    const damc_enc_layer_t& L = e->layers[0];
+    const int H = e->h, W = e->w, C = L.cout, R = sh.first_rows, S = sh.first_strips;
+    const size_t sm = ((size_t)(R + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * C + C) * sizeof(float);
+    if (sm > 65536) return DAMC_ERR_UNSUPPORTED;
+    float* ssb = inws + (size_t)B * C * S * 3;
+    ProfScope ps("enc_first", 2.0 * B * H * W * (double)C * 9 * L.cin * 2, s);
+#define DAMC_C3(CIN_)                                                                                               \
+  if (L.cin == CIN_) {                                                                                              \
+    hipLaunchKernelGGL(conv3_stats_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,    \
+                       inws);                                                                                       \
+    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
+                       L.in_beta, L.in_eps, ssb);                                                                   \
+    hipLaunchKernelGGL(conv3_apply_x3_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,   \
+                       ssb, L.slope, a3);                                                                           \
+  }
+    DAMC_C3(1) DAMC_C3(3) DAMC_C3(4)
+#undef DAMC_C3
+    DAMC_LAUNCH_CHECK();
+    a3_ready = true;
+    i0 = 1;
+  } else if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) {
+    return rc;
+  }
+  for (int i = i0; i < n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
-    const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
-    if ((rc = damc_conv2d_nhwc(buf[i & 1], B, sh.h[i], sh.w[i], L.cin, L.w_packed, L.bias, L.cout, L.k, L.stride,
-                               L.pad, out, nsl ? slabs : nullptr, nsl, stream)))
+    if (sh.limb[i]) {
+      if (!a3_ready) {
+        const long na = (long)B * sh.h[i] * sh.w[i] * L.cin;
+        if ((rc = damc::launch_split_x3(buf[i & 1], na, a3, s))) return rc;
+      }
+      const void* wl = L.w_x3;
+      if (!wl) {  // the limb copy from the fp32 packing
+        const int K = L.k * L.k * L.cin;
+        if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;
+        wl = w3;
+      }
+      if ((rc = enc_conv_x3(a3, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max, s))) return rc;
+    } else {
+      const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
+      if ((rc = damc_conv2d_nhwc(buf[i & 1], B, sh.h[i], sh.w[i], L.cin, L.w_packed, L.bias, L.cout, L.k, L.stride,
+                                 L.pad, out, nsl ? slabs : nullptr, nsl, stream)))
+        return rc;
+    }
+    a3_ready = false;
+    if (!L.in_gamma) continue;
+    const int hw = sh.h[i + 1] * sh.w[i + 1];
+    if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
+      const int S = in_splits(hw), cg = (L.cout + 63) / 64;
+      float* ssb = inws + (size_t)B * L.cout * S * 3;
+      ProfScope ps("instnorm", 0.0, s);
+      hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, out, B, hw, L.cout, S, inws);
+      hipLaunchKernelGGL(in_merge_kernel, dim3((B * L.cout + 255) / 256), dim3(256), 0, s, inws, B, L.cout, S,
+                         L.in_gamma, L.in_beta, L.in_eps, ssb);
+      const long n8 = (long)B * hw * (L.cout / 8);
+      hipLaunchKernelGGL(in_apply_x3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, out, n8, hw, L.cout,
+                         ssb, L.slope, a3);
+      DAMC_LAUNCH_CHECK();
+      a3_ready = true;
+    } else if ((rc = damc_instnorm_lrelu_nhwc(out, B, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps, L.slope, inws,
+                                              stream))) {
       return rc;
-    if (L.in_gamma &&
-        (rc = damc_instnorm_lrelu_nhwc(out, B, sh.h[i + 1] * sh.w[i + 1], L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                                       L.slope, inws, stream)))
-      return rc;
+    }
   }
   return 0;
 }
+

@@ -96,6 +96,30 @@ int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned
 // else tap-major (launch_split_x3_negblk)
 int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s);
 
+// a PyTorch Conv2d weight (cout, cin, k, k), cin % 8 == 0, straight to the limb B operand of the conv (the order
+// launch_split_x3_conv gives damc_pack_conv2d's K-major packing)
+int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s);
+
+// the limb form of 8 consecutive fp32 values (the engine's RNE split: v = hi + mid + lo to 24 significand bits),
+// stored as one x3 octet [3][8] bf16 at dst (16-B aligned)
+__device__ __forceinline__ void store_x3_octet(const float (&v)[8], unsigned short* dst) {
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  bf16x8_t h, m, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 b0 = (__bf16)v[e];
+    const float r1 = v[e] - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)(r1 - (float)b1);
+  }
+  bf16x8_t* o = reinterpret_cast<bf16x8_t*>(dst);
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);
 

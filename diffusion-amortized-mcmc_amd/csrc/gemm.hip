@@ -1581,6 +1581,34 @@ int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* 
   return launch_split_x3_negblk(x, n, K, y, s);
 }
 
+// a PyTorch Conv2d weight (cout, cin, k, k) straight to the limb engine's B operand of the conv, [co][(ky, kx, ci)]
+// with sign-alternating blocks (launch_split_x3_negblk of damc_pack_conv2d's K-major packing, in one pass)
+__global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int cin, int k, unsigned short* __restrict__ y) {
+  const int K = k * k * cin, K8 = K / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)cout * K8) return;
+  const int co = (int)(i / K8), k8 = (int)(i - (long)co * K8);
+  const int kk = k8 * 8, tap = kk / cin, ci0 = kk - tap * cin;  // cin % 8 == 0: an octet never straddles a tap
+  const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = sg * w[((long)co * cin + ci0 + e) * k * k + tap];
+  bf16x8 h, m, l;
+  split3_octet(v, h, m, l);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * i;
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
+int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s) {
+  if ((DAMC_X3_VARIANT & 8) != 0) return DAMC_ERR_UNSUPPORTED;  // the channel-major walk needs the slice-major order
+  if (cout <= 0 || cin % 8 != 0 || k <= 0 || (uintptr_t)y % 16 != 0) return DAMC_ERR_ARG;
+  const long n = (long)cout * k * k * cin / 8;
+  hipLaunchKernelGGL(pack_conv_x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, cout, cin, k, y);
+  return (int)hipGetLastError();
+}
+
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
   if (n % 8 != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0) return DAMC_ERR_ARG;
   const long n8 = n / 8;

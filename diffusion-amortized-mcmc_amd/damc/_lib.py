@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DAMC_LIB_PATH: an alternative in-tree build for A/B timing (tools/); the default is the product library
 LIB_PATH = os.environ.get("DAMC_LIB_PATH") or os.path.join(_HERE, "libdamc.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_LAYERS = 10
 ENGINE_LIMB, ENGINE_FP32 = 0, 1
 # include/damc.h error codes
@@ -90,12 +90,12 @@ class EncLayer(ctypes.Structure):  # damc_enc_layer_t
     _fields_ = [("cin", ctypes.c_int), ("cout", ctypes.c_int), ("k", ctypes.c_int), ("stride", ctypes.c_int),
                 ("pad", ctypes.c_int), ("w_packed", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("in_gamma", ctypes.c_void_p), ("in_beta", ctypes.c_void_p), ("in_eps", ctypes.c_float),
-                ("slope", ctypes.c_float)]
+                ("slope", ctypes.c_float), ("w_x3", ctypes.c_void_p)]
 
 
 class Encoder(ctypes.Structure):  # damc_encoder_t
     _fields_ = [("n_layers", ctypes.c_int), ("nc", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
-                ("layers", EncLayer * MAX_ENC_LAYERS)]
+                ("layers", EncLayer * MAX_ENC_LAYERS), ("engine", ctypes.c_int)]
 
 
 class AdamHparams(ctypes.Structure):
@@ -156,6 +156,8 @@ _SIGS = {
     "damc_q_encoder_workspace_bytes": (_SZ, [ctypes.POINTER(Encoder), _I]),
     "damc_q_encoder_fwd": (_I, [ctypes.POINTER(Encoder), _P, _I, _P, _P, _SZ, _P]),
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
+    "damc_conv2d_x3_bytes": (_SZ, [_I, _I, _I]),
+    "damc_pack_conv2d_x3": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
     "damc_sweep_team_failures": (ctypes.c_long, [_I]),
     "damc_sweep_team_words": (_I, [ctypes.POINTER(Denoiser), _I, _I, _P, _SZ, _P, _I]),

@@ -106,9 +106,33 @@ class EncoderPlan:
                 i += 1
             self.stages.append((conv, norm, slope))
         self.nemb = enc.nemb
+        self._wcache = {}
+        self._ws = _lib.WorkspaceCache()
+
+    def _packed(self, i, conv, dev, L, stream):
+        """The conv's weight operand, repacked per call from the live parameter: the nets train between calls,
+        and the reference updates its EMA target Q_dummy through param.data.copy_ (train_gen_recon.py:258-261),
+        which leaves the parameter's version counter unchanged, so no version-keyed cache could see it.  A layer on
+        the limb engine is one pass from the PyTorch layout straight to limbs (damc_pack_conv2d_x3); the first 3x3
+        conv keeps the fp32 packing.  Buffers are reused across calls."""
+        k, cout, cin = conv.kernel_size[0], conv.out_channels, conv.in_channels
+        w = _dev(conv.weight, dev)
+        nb = int(L.damc_conv2d_x3_bytes(cout, cin, k)) if _lib.current_engine() == _lib.ENGINE_LIMB else 0
+        key = (str(dev), nb)
+        hit = self._wcache.get(i)
+        if hit is None or hit[0] != key:
+            buf = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else \
+                torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
+            hit = self._wcache[i] = (key, buf)
+        buf = hit[1]
+        if nb:
+            check(L.damc_pack_conv2d_x3(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d x3")
+            return None, buf, w
+        check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d")
+        return buf, None, w
 
     def forward(self, x):
-        """The whole encoder in one damc_q_encoder_fwd call (weights packed from the live modules per call)."""
+        """The whole encoder in one damc_q_encoder_fwd call (packed weights cached per parameter version)."""
         L = _lib.lib()
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -117,18 +141,17 @@ class EncoderPlan:
             raise NotImplementedError("encoder with %d convolutions" % len(self.stages))
         d = _lib.Encoder()
         d.n_layers, d.nc, d.h, d.w = len(self.stages), C, H, W
+        d.engine = _lib.current_engine()
         keep = []
         for i, (conv, norm, slope) in enumerate(self.stages):
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             cout, cin = conv.out_channels, conv.in_channels
-            w = _dev(conv.weight, dev)
-            wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
-            check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(wp), stream), "pack conv2d")
+            wp, w3, w = self._packed(i, conv, dev, L, stream)
             bias = _dev(conv.bias, dev) if conv.bias is not None else None
             e = d.layers[i]
             e.cin, e.cout, e.k, e.stride, e.pad = cin, cout, k, s, p
-            e.w_packed, e.bias = ptr(wp), ptr(bias)
-            keep += [w, wp, bias]
+            e.w_packed, e.bias, e.w_x3 = ptr(wp), ptr(bias), ptr(w3)
+            keep += [bias, w]
             if norm is not None:
                 g, b = _dev(norm.weight, dev), _dev(norm.bias, dev)
                 e.in_gamma, e.in_beta, e.in_eps, e.slope = ptr(g), ptr(b), float(norm.eps), slope
@@ -136,7 +159,7 @@ class EncoderPlan:
         nbytes = int(L.damc_q_encoder_workspace_bytes(ctypes.byref(d), B))
         if nbytes == 0:
             raise _lib.DamcError("unsupported encoder configuration for the HIP path")
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        ws = self._ws.get(dev, nbytes, ("encoder", B, H, W))
         conv = self.stages[-1][0]
         out = torch.empty(B, conv.out_channels, dtype=torch.float32, device=dev)
         check(L.damc_q_encoder_fwd(ctypes.byref(d), ptr(x), B, ptr(out), ptr(ws), nbytes, stream), "damc_q_encoder_fwd")

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DAMC_ABI_VERSION 2
+#define DAMC_ABI_VERSION 3
 #define DAMC_MAX_LAYERS 10
 
 enum {
@@ -220,19 +220,30 @@ int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* 
 /* The whole Encoder_* forward of _netQ_U (SURVEY.md §8b damc_q_encoder_fwd; diffusion_net.py:227-372, a10):
  * [Conv2d -> InstanceNorm2d(affine) -> LeakyReLU]* -> Conv2d on the kernels above, x (B, nc, h, w) NCHW ->
  * xemb (B, nemb) with nemb = cout * ho * wo of the last conv (1 x 1 in every Encoder_*, where the NHWC and
- * the reference's NCHW flattening agree; other output sizes return DAMC_ERR_UNSUPPORTED). */
+ * the reference's NCHW flattening agree; other output sizes return DAMC_ERR_UNSUPPORTED).
+ * engine DAMC_ENGINE_LIMB: the convolutions whose input channel count is a multiple of 32 (every one but the
+ * first 3x3 at the reference's nif) run on the limb engine (fp32-accurate, bf16 MFMA; see DAMC_ENGINE_*), the
+ * input activation split into limbs per call; w_x3 = damc_pack_conv2d_x3 of the layer's weight (then w_packed
+ * may be NULL for that layer), or NULL (the library splits w_packed into the workspace per call). */
 #define DAMC_MAX_ENC_LAYERS 8
 typedef struct {
   int cin, cout, k, stride, pad;
-  const float* w_packed;          /* damc_pack_conv2d layout                                          */
+  const float* w_packed;          /* damc_pack_conv2d layout (NULL allowed for a limb layer with w_x3) */
   const float* bias;              /* (cout) or NULL                                                   */
   const float *in_gamma, *in_beta; /* InstanceNorm2d affine (cout); NULL: no norm / activation after it */
   float in_eps, slope;
+  const void* w_x3;               /* the limb B operand (damc_pack_conv2d_x3) or NULL                 */
 } damc_enc_layer_t;
 typedef struct {
   int n_layers, nc, h, w;
   damc_enc_layer_t layers[DAMC_MAX_ENC_LAYERS];
+  int engine; /* DAMC_ENGINE_* */
 } damc_encoder_t;
+/* bytes of the limb copy of a packed conv weight (0: the layer does not run on the limb engine) */
+size_t damc_conv2d_x3_bytes(int cout, int cin, int k);
+/* a Conv2d weight in its PyTorch layout (cout, cin, k, k), cin % 32 == 0 -> the limb engine's B operand of the
+ * conv (damc_conv2d_x3_bytes bytes), in one pass */
+int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream);
 size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* enc, int batch);
 int damc_q_encoder_fwd(const damc_encoder_t* enc, const float* x, int batch, float* xemb, void* workspace,
                        size_t workspace_bytes, void* stream);

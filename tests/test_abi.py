@@ -34,7 +34,7 @@ def test_host_only_calls():
     from damc import _lib
 
     L = _lib.lib()
-    assert L.damc_abi_version() == _lib.ABI_VERSION == 2
+    assert L.damc_abi_version() == _lib.ABI_VERSION == 3
     assert b"invalid" in L.damc_error_string(1001)
     # descriptor validation runs on the host: an empty generator has no workspace
     g = _lib.Generator()

@@ -131,6 +131,26 @@ def test_full_width_encoder_vs_fp64(gpu_device, name, B):
     _check("Encoder_%s nif=64 B=%d xemb" % (name, B), got, e32, e64, 1e-7)
 
 
+def test_encoder_limb_engine_vs_fp32_engine_b128(gpu_device):
+    """The bench's Encoder_cifar10(nif=64) at B=128: the default engine (the k4 s2 and the final convs on the limb
+    engine) and the fp32-MFMA engine (damc._lib.exact_fp32) against fp64, both within 3x the fp32 reference's."""
+    from damc import _lib, amortizer, synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    B = 128
+    enc = synth.load_into(dn.Encoder_cifar10(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 1, (B, 3, 32, 32))).to(gpu_device)
+    got = amortizer.encoder_forward(enc, x).cpu().numpy()
+    with _lib.exact_fp32():
+        got32 = amortizer.encoder_forward(enc, x).cpu().numpy()
+    with torch.no_grad():
+        e32 = orc.encoder_forward(enc.cpu(), x.cpu()).numpy()
+        e64 = orc.encoder_forward(enc.double(), x.cpu().double()).numpy()
+    _check("Encoder_cifar10 nif=64 B=128 xemb, limb engine", got, e32, e64, 1e-7)
+    _check("Encoder_cifar10 nif=64 B=128 xemb, fp32 engine", got32, e32, e64, 1e-7)
+
+
 def test_celebaHQ_q_sweep_vs_fp64(gpu_device):
     """CelebA-HQ Q(x) at its per-rank size (B=8 of 64): Encoder_celebaHQ(nif=64) + the 100-step 'large' reverse sweep
     (nxemb 1024, ntemb 128; train_gen_recon.py:360-380 defaults) with injected noise, vs the fp64 oracle."""

@@ -116,6 +116,14 @@ def test_q_update_matches_reference(gpu_device, name):
     with training.stock_pytorch():
         _, g_ref_dev, rec0, meta0 = qtrain_run(name, gpu_device)
     tol = [max(1e-4, 2.0 * max(e)) for e in gtrain_errors(g_ref_dev, rec0, meta0)]
+    # an encoder pre-activation within fp32 rounding of the LeakyReLU kink takes either branch under any fp32
+    # summation order (q_celebaHQ_s: one value at |a| = 1.5e-7 in the 16x16 stage, tools/diag_kink.py), which moves
+    # the encoder's gradients by ~1e-2 at B = 2; for such a case the encoder's parameters are checked per op against
+    # fp64 instead (test_encoder_train_stagewise, the same nif = 4 topology) and everything else as above
+    kink = _encoder_kink(name, gpu_device)
+    if kink is not None:
+        print("%s: encoder pre-activation %.2e from the kink: encoder gradients not compared end to end" % (name, kink))
+        tol = [1e30 if p[0].startswith("encoder.") else t for p, t in zip(meta0["params"], tol)]
 
     calls = []
     orig = training.encoder_apply
@@ -132,6 +140,36 @@ def test_q_update_matches_reference(gpu_device, name):
     # samples that difference reaches time_mlp[1].weight's gradient unaveraged (its norm agrees to ~1e-6)
     worst = gtrain_check(grads, rec, meta, tol)
     print("%s worst rel err vs reference %.2e (largest bound %.2e)" % (name, worst, max(tol)))
+
+
+def _encoder_kink(name, device, rel=1e-6):
+    """The smallest |pre-activation| of the case's encoder (fp64 forward) if it is below rel times the stage's RMS,
+    else None."""
+    import torch.nn.functional as F
+
+    from conftest import build_q_case, load_golden
+
+    _, meta = load_golden(name + "_qtrain")
+    c = build_q_case(meta["q"], device)
+    h = c["x"].double()
+    worst = None
+    mods = list(c["Q"].encoder.net)
+    with torch.no_grad():
+        i = 0
+        while i < len(mods):
+            conv = mods[i]
+            h = F.conv2d(h, conv.weight.double(), conv.bias.double(), conv.stride, conv.padding)
+            if i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.InstanceNorm2d):
+                nm = mods[i + 1]
+                a = F.instance_norm(h, weight=nm.weight.double(), bias=nm.bias.double(), eps=nm.eps)
+                m = float(a.abs().min() / a.pow(2).mean().sqrt())
+                if m < rel:
+                    worst = m if worst is None else min(worst, m)
+                h = F.leaky_relu(a, mods[i + 2].negative_slope)
+                i += 3
+            else:
+                i += 1
+    return worst
 
 
 def test_denoiser_train_vs_autograd_b128(gpu_device):
