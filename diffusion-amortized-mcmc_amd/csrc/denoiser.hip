@@ -81,6 +81,21 @@ struct ChainArgs {
 __host__ __device__ inline int kpad(int din) { return (din + KG - 1) / KG * KG; }
 __host__ __device__ inline int emb_ld(int kp) { return kp + 8; }  // in0 LDS image row stride (floats)
 
+// in0's z B (16 rows x the wave's 16 columns, K = nz <= 128) as two independent MFMA chains over the even and the odd
+// k-groups, then their sum: half the dependent-MFMA latency of one chain on the stage's critical path (chain_kernel, the team
+// kernel and its rescue all use this function)
+__device__ __forceinline__ f32x4 emb_zb(const f32x4 (&zv4)[EMB_G], const f32x4 (&bv)[EMB_G]) {
+  f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < EMB_G; g += 2)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g + 1][e], bv[g + 1][e], e1, 0, 0, 0);
+    }
+  return e0 + e1;
+}
+
 // EMB: the in0 block (Fourier embedding, sin / cos with their large-argument path) is its own instantiation, so
 // the six other blocks' kernels carry no scratch segment
 template <bool EMB>
@@ -163,12 +178,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
       }
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (!(a.dbg & 128)) {
-#pragma unroll
-        for (int g = 0; g < EMB_G; ++g)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][s], bv[g][s], acc, 0, 0, 0);
-      }
+      if (!(a.dbg & 128)) acc = emb_zb(zv4, bv);
       // sin / cos (2 pi zB) on the hardware units, whose argument is in revolutions: t = zB - rint(zB) is exact,
       // so the only rounding is the unit's (the reference rounds 2 pi zB to fp32 first, ~4e-6 rad at |zB| ~ 10;
       // both are below the spread of zB itself between summation orders)
@@ -347,6 +357,8 @@ struct TsArgs {
   unsigned* flags;    // [8][TS_MAXT][TS_FS]: stages published by (team, slot)
   int* err;
   int* diag;          // [P][4]: a failed wait's {stage needed, flag of the first late slot, late-slot mask lo, hi}
+  int sent;           // 1: sentinel hand-offs (TS_SENT): no drain before the flag, every handed-off load re-read until
+                      // it holds no sentinel; 0: the drained-flag protocol (DAMC_SWEEP_SENT=0, read per call)
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
   uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin, wait end, reduced,
@@ -406,26 +418,80 @@ __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need
   return *sflag != 0;
 }
 
+// Sentinel hand-offs.  Every ring slot (block outputs and z of every step) is written exactly once per sweep, and
+// the setup kernel fills all of them with a NaN bit pattern no arithmetic produces (hardware NaNs are canonical,
+// 0x7FC00000) before the launch.  A handed-off 4-B value is then either the sentinel or final (aligned 4-B stores
+// do not tear), so the producer publishes its flag right behind its stores without draining them (one memory round
+// trip less per stage), and a consumer that has seen the flag re-reads (sc1) any load group that still holds a
+// sentinel.  The flag stays the cheap "probably ready" signal; the data itself proves readiness.
+constexpr unsigned TS_SENT = 0x7FC0DEADu;
+// a re-read loop gives up past the budget (setting the error word) or once another workgroup has failed
+__device__ __forceinline__ bool ts_giveup(uint64_t t0, unsigned it, int* err, long budget) {
+  if ((it & 15) != 15) return false;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  if ((long)(__builtin_amdgcn_s_memrealtime() - t0) > budget) {
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+__device__ __forceinline__ bool is_sent(float v) { return __builtin_bit_cast(unsigned, v) == TS_SENT; }
+template <int N>
+__device__ __forceinline__ bool any_sent(const f32x4 (&x)[N]) {
+  bool b = false;
+#pragma unroll
+  for (int c = 0; c < N; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b = b || is_sent(x[c][e]);
+  return b;
+}
+// wave-uniform: re-issue ts_load<N> until its registers hold no sentinel; past the budget the error word is set
+// (the team then drains and team_finish_kernel recomputes the sweep)
 // acc += lrelu(x[rows][k0 .. k0 + kps)) . W^T over one input half: wave w takes k in [w kps/4, (w+1) kps/4);
 // x rows come from src (width wsrc, zero past it) with sc1 loads, or from the in0 embedding image in LDS
 template <bool EMB>
 __device__ __forceinline__ void ts_half(f32x4& acc, const float* wl, int kps, const __amdgpu_buffer_rsrc_t& rs,
-                                        long soff, int wsrc, int row, bool rok, const float* embs, int ld, int dbg) {
+                                        long soff, int wsrc, int row, bool rok, const float* embs, int ld, int dbg,
+                                        int sent = 0, int* err = nullptr, long budget = 0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, q = lane >> 4;
   const int kq = kps >> 2, ng = kq >> 4, kbase = wave * kq;
   const f32x4* wv = reinterpret_cast<const f32x4*>(wl) + (long)wave * ng * 64 + lane;
   for (int g0 = 0; g0 < ng; g0 += CH_CHUNK) {
     f32x4 xa[CH_CHUNK];
+    auto load = [&]() {
 #pragma unroll
-    for (int c = 0; c < CH_CHUNK; ++c) {
-      const int k = kbase + 16 * (g0 + c) + 4 * q;
-      f32x4 xv = {0.f, 0.f, 0.f, 0.f};
-      if (g0 + c < ng) {
-        if (EMB) xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
-        else if (rok && k < wsrc && !(dbg & 2)) xv = ld_sc1(rs, (soff + (long)row * wsrc + k) * 4);
+      for (int c = 0; c < CH_CHUNK; ++c) {
+        const int k = kbase + 16 * (g0 + c) + 4 * q;
+        f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+        if (g0 + c < ng) {
+          if (EMB) xv = *reinterpret_cast<const f32x4*>(embs + m * ld + k);
+          else if (rok && k < wsrc && !(dbg & 2)) xv = ld_sc1(rs, (soff + (long)row * wsrc + k) * 4);
+        }
+        xa[c] = xv;
       }
-      xa[c] = xv;
+    };
+    load();
+    if (!EMB && sent) {  // sentinel hand-off (see TS_SENT): re-read the chunk until it holds no sentinel
+      bool bad = false;
+#pragma unroll
+      for (int c = 0; c < CH_CHUNK; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bad = bad || (__builtin_bit_cast(unsigned, xa[c][e]) == 0x7FC0DEADu);
+      if (__any(bad)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned it = 0;
+        do {
+          __builtin_amdgcn_s_sleep(1);
+          if (ts_giveup(t0, ++it, err, budget)) break;
+          load();
+          bad = false;
+#pragma unroll
+          for (int c = 0; c < CH_CHUNK; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bad = bad || (__builtin_bit_cast(unsigned, xa[c][e]) == 0x7FC0DEADu);
+        } while (__any(bad));
+      }
     }
 #pragma unroll
     for (int c = 0; c < CH_CHUNK; ++c) {
@@ -479,6 +545,19 @@ __device__ __forceinline__ void ts_mfma(f32x4& acc, const float* wl, int kps, co
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[e], w[e], acc, 0, 0, 0);
   }
+}
+
+template <int N>
+__device__ __forceinline__ void ts_ready(f32x4 (&x)[N], int kps, const __amdgpu_buffer_rsrc_t& rs, long soff, int wsrc,
+                                         int row, bool rok, int* err, long budget) {
+  if (!__any(any_sent(x))) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned it = 0;
+  do {
+    __builtin_amdgcn_s_sleep(1);
+    if (ts_giveup(t0, ++it, err, budget)) return;
+    ts_load<N>(x, kps, rs, soff, wsrc, row, rok);
+  } while (__any(any_sent(x)));
 }
 
 __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
@@ -594,7 +673,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       // the publishing lane writes them out after the flag
       const bool tr = a.trace != nullptr && tid == 256;
       if (nt == 0) {  // nothing to compute: publish at once (this slot's earlier stores are drained)
-        if (tid == TS_PUB) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
       const bool final_ = j == 6;
@@ -603,7 +682,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       // in the same order (team_finish_kernel's rescue relies on it); it is normally known complete already (sb <
       // known); a slot that owned no tile of the stages since waits for it here
       const bool skip_early = b.kpb > 0;
-      if (skip_early && !(7u * k + b.srcB < known)) {
+      if (skip_early && a.sent < 2 && !(7u * k + b.srcB < known)) {
         if (!ts_wait(teamflags, T, 7u * k + b.srcB + 1, a.err, a.budget, &sflag, a.diag)) return;
         known = 7u * k + b.srcB + 1;
       }
@@ -645,13 +724,14 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
           f32x4 xs[CH_CHUNK];
           if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
           if (skip_early && !pre && cw)
-            ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg);
+            ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
+                           a.sent, a.err, a.budget);
           const int half = nz >> 1;
 
           // ---- wait for stage s - 1 of the team (once per stage)
           if (!waited) {
             if (tr) trs[0] = __builtin_amdgcn_s_memrealtime();
-            if (s > 0 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
+            if (s > 0 && a.sent < 2 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
             if (tr) trs[1] = __builtin_amdgcn_s_memrealtime();
             known = s;
             waited = true;
@@ -665,15 +745,24 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
               zv4[g] = (cw && xok && kk < nz && !(a.dbg & 64)) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4)
                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
             }
+            if (a.sent && cw && __any(any_sent(zv4))) {  // z of this step not landed yet: re-read (bounded)
+              const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+              unsigned it = 0;
+              do {
+                __builtin_amdgcn_s_sleep(1);
+                if (ts_giveup(t0, ++it, a.err, a.budget)) break;
+#pragma unroll
+                for (int g = 0; g < EMB_G; ++g) {
+                  const int kk = 16 * g + 4 * q;
+                  zv4[g] = (xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+              } while (__any(any_sent(zv4)));
+            }
             if (cw && wave * 16 < half && !(a.dbg & 32)) {  // wave w: B^T columns 16 w .. 16 w + 15 (nz <= 128), in registers
               const int tt = wave;
               const int col = tt * 16 + m;
               const bool cok = col < half;
-              f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int g = 0; g < EMB_G; ++g)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) e4 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], e4, 0, 0, 0);
+              const f32x4 e4 = emb_zb(zv4, bv);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const int rrow = 4 * q + r;
@@ -702,10 +791,13 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
           } else if (cw && pre) {
             f32x4 xa[CH_CHUNK];
             ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
+            if (a.sent) ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
             ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
+            if (a.sent) ts_ready<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, a.err, a.budget);
             ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw) {
-            ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg);
+            ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg, a.sent, a.err,
+                           a.budget);
           }
           if (cw) {
 #pragma unroll
@@ -726,7 +818,16 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
               if (!(a.dbg & 16)) st_sc1_f(rslot + b.ooff + (long)erow * b.dout + ecol, o);
             } else {  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
               const long zi = (long)erow * nz + ecol;
-              const float zv = ld_sc1_f(zk + zi);
+              float zv = ld_sc1_f(zk + zi);
+              if (a.sent && is_sent(zv)) {  // this thread's own store of the previous step, not landed yet
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                unsigned it = 0;
+                do {
+                  __builtin_amdgcn_s_sleep(1);
+                  if (ts_giveup(t0, ++it, a.err, a.budget)) break;
+                  zv = ld_sc1_f(zk + zi);
+                } while (is_sent(zv));
+              }
               const float eps = a.residual ? zv + o : o;
               if (eps_log && k < eps_log_steps) eps_log[(long)k * B * nz + zi] = eps;
               const float pred = mul_rn(c0, sub_rn(zv, mul_rn(eps, c1)));
@@ -743,10 +844,10 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
           __syncthreads();  // red (and the in0 image) are reused by the next task
         }
       }
-      // publish: every storing wave has drained, then one lane stores the slot's flag
-      if (!(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // publish: (drained-flag protocol) every storing wave drains first; one lane then stores the slot's flag
+      if (!a.sent && !(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == TS_PUB) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == TS_PUB) {
         uint64_t* tg = a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4;
         tg[0] = trs[0];
@@ -839,11 +940,7 @@ __global__ __launch_bounds__(256) void team_finish_kernel(TsArgs a, float* zt, i
         }
         if (wave * 16 < half) {
           const int col = wave * 16 + m;
-          f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int g = 0; g < EMB_G; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) e4 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], e4, 0, 0, 0);
+          const f32x4 e4 = emb_zb(zv4, bv);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int rrow = 4 * q + r;
@@ -1108,11 +1205,17 @@ __global__ void transpose_kernel(const float* in, int rows, int cols, float* out
 // the call's per-call record and z, and (team launch) the team flags, error word and diagnostics zeroed: a kernel in
 // the stream, not a memset node, so a captured sweep orders it like every other kernel
 __global__ void sweep_setup_kernel(SweepCall c, SweepCall* dst, const float* zt, float* zw, long n, unsigned* zero,
-                                   long nzero) {
+                                   long nzero, f32x4* s1, long ns1, f32x4* s2, long ns2) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *dst = c;
   if (i < n) zw[i] = zt[i];
   if (i < nzero) zero[i] = 0u;
+  // sentinel hand-offs: every ring slot of the sweep (grid-stride over the two ranges, 16 B per store)
+  const float sv = __builtin_bit_cast(float, 0x7FC0DEADu);
+  const f32x4 s4 = {sv, sv, sv, sv};
+  const long st = (long)gridDim.x * blockDim.x;
+  for (long j = i; j < ns1; j += st) s1[j] = s4;
+  for (long j = i; j < ns2; j += st) s2[j] = s4;
 }
 
 __global__ void copy_kernel(const float* src, float* dst, long n) {
@@ -1453,6 +1556,17 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
     p.toff = tiles % T;
     tiles += p.ntn;
     coloff += bk.dout;
+  }
+  const char* lay = getenv("DAMC_SWEEP_LAYOUT");  // (read per call) 1: in0 placed after out2 (below); 0: in order
+  if (!(lay && lay[0] == '0')) {
+    for (int j = 1, t = 0; j < 7; ++j) {
+      a->b[j].toff = t % T;
+      t += a->b[j].ntn;
+    }
+  // block 0 (in0) right after out2's tiles: out2 -> in0 crosses the step, and a slot that has just published out2 would
+  // otherwise start its in0 wait a publish + poll round trip late; with disjoint slots the in0 owners are already
+  // polling when out2 completes (blocks 1..6 are placed in order from slot 0, which also keeps out1 / out2 disjoint)
+    a->b[0].toff = (a->b[6].toff + a->b[6].ntn) % T;
   }
   long wl = 0;
   for (int t = 0; t < T; ++t) {
@@ -1894,8 +2008,16 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   const bool memset_flags = team && mf && mf[0] == '1';
   if (memset_flags) DAMC_CHECK(hipMemsetAsync(w.tflags, 0, TS_CTL_WORDS * sizeof(unsigned), s));
   const long nzero = (team && !memset_flags) ? TS_CTL_WORDS : 0;
-  hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((std::max(nzb, nzero) + 255) / 256)), dim3(256), 0, s, call,
-                     w.call, zt, team ? w.zring : w.z, nzb, w.tflags, nzero);
+  // hand-off protocol (read per call): 2 (default) data-driven sentinel hand-offs, no flags; 1 flags without drain +
+  // sentinel checks; 0 drained flags.  Bitwise the same results; same-box A/B at B=128 (tools/sweep_ab.py): 2 is
+  // 6-7 % faster than 0, 1 is 4-5 % slower than 0
+  const char* se = getenv("DAMC_SWEEP_SENT");
+  if (team) ta.sent = se ? atoi(se) : 2;
+  const long ns1 = (team && ta.sent) ? (long)n * B * S / 4 : 0, ns2 = (team && ta.sent) ? (long)n * nzb / 4 : 0;
+  const long sgrid = std::min<long>(std::max<long>(std::max(nzb, nzero), (ns1 + ns2) / 8), 1L << 16);
+  hipLaunchKernelGGL(sweep_setup_kernel, dim3((unsigned)((sgrid + 255) / 256)), dim3(256), 0, s, call, w.call, zt,
+                     team ? w.zring : w.z, nzb, w.tflags, nzero, reinterpret_cast<f32x4*>(w.ring), ns1,
+                     reinterpret_cast<f32x4*>(w.zring + nzb), ns2);
   DAMC_LAUNCH_CHECK();
   double flops_step = 0;
   for (int j = 0; j < 7; ++j) flops_step += 2.0 * B * 2.0 * d->blocks[j].din * d->blocks[j].dout;

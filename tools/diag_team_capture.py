@@ -17,6 +17,7 @@ from damc import synth  # noqa: E402
 from src import diffusion_net as dn  # noqa: E402
 
 os.environ["DAMC_SWEEP_TEAM_KEEP"] = "1"
+os.environ["DAMC_SWEEP_SENT"] = "0"  # the flag protocol (round 2's): the data-driven default polls no flags
 dev = torch.device("cuda:0")
 n, B = 20, 128
 Q = dn._netQ_U(nc=3, nz=128, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=n, logsnr_min=-5.1,
