@@ -14,6 +14,7 @@
 // along M.  tools/gemm_bench.hip A/B-tests them on the generator's convolutions.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm.h"
 
@@ -1127,92 +1128,63 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   __syncthreads();
   bf16x8 pfa[4][3], pfb[4][3];  // the read-order path's fragments
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
-    // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
-    // barrier at the end of this tile (its vmcnt(0)) lands it
-    // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
-    // timing probes (tools/gemm_bench.hip only, wrong results): 512 no DMA after the first tile, 1024 fragment reads
-    // of the first tile only
-    if (DMA && kt + 1 < nk && !(V & 512)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
-    if (M16 && (V & 256)) {
-      // 256: fragment reads one group ahead of the MFMAs that consume them, in the order those MFMAs run (A tile 0
-      // against B tiles 0..3, then A tiles 1..3), pinned by sched_group_barrier: the first MFMAs wait for 6 reads
-      // instead of the ~15 the default schedule puts in front of its first lgkmcnt(0).  2.5-3.9 % less time on
-      // the four CIFAR shapes, bit-identical results (profiles/r02/gemm_bench_rdorder.txt).  Measured and dropped:
-      // reading the next tile's first fragments after the barrier into the registers the trailing MFMAs free
-      // (cross-tile pipeline, 1-2 % slower than this), all reads issued by the end of A row 0 so the barrier moves
-      // up (5-8 % slower), A tile 3 read later so it moves down (0-2 % slower).
-      bf16x8 (&fa)[4][3] = pfa, (&fb)[4][3] = pfb;  // [tile][limb]
-      const bool rd = !(V & 1024) || kt == 0;
-      auto rd_a = [&](int t) {
-        if (!rd) return;
+  // 2048: waves 4-7 run half a tile behind (the stagger of MI355X_MICROARCH.md, two waves per SIMD, item 9); every
+  // accumulator still takes its tiles' MFMAs in the same order and is flushed at the same block ends: bitwise the
+  // unstaggered kernel
+  const bool stag = M16 && (V & 256) && (V & 2048) && DMA && __builtin_amdgcn_readfirstlane(tid) >= 256;
+  auto flush16 = [&](int ktd) {  // block flush after the MFMAs of K tile ktd
+    const float sg = (p.b_negblk && (((ktd + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
 #pragma unroll
-        for (int l = 0; l < 3; ++l) fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
-      };
-      auto rd_b = [&](int t) {
-        if (!rd) return;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int l = 0; l < 3; ++l) fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
-      };
-      auto mf = [&](int i, int j) {
-        f32x4 c = acc16[i][j];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
-        acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
-      };
-      rd_a(0);
-      rd_b(0);
-      rd_b(1);
-      mf(0, 0);
-      rd_b(2);
-      mf(0, 1);
-      rd_b(3);
-      mf(0, 2);
-      rd_a(1);
-      mf(0, 3);
-      rd_a(2);
+      for (int j = 0; j < 4; ++j) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mf(1, j);
-      rd_a(3);
-#pragma unroll
-      for (int i = 2; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mf(i, j);
-      constexpr int SG_MFMA = 0x8, SG_DS_RD = 0x100;
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 9, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 48, 0);
-    } else if (M16) {
-      bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int l = 0; l < 3; ++l) {
-          fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
-          fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
-        }
-      if (!DMA && kt + 1 < nk) {
-        store_ab((kt + 1) & 1);
-        if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+        for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
+        acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (V & 2) __builtin_amdgcn_s_setprio(1);
+  };
+  auto mfp = [&](int i, int j) {  // the six limb products of A tile i x B tile j, smallest first
+    f32x4 c = acc16[i][j];
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][2], pfb[j][0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][1], pfb[j][1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][0], pfb[j][2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][1], pfb[j][0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][0], pfb[j][1], c, 0, 0, 0);
+    acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][0], pfb[j][0], c, 0, 0, 0);
+  };
+  // one loop per wave role (a runtime branch inside a shared loop made the compiler keep both roles' fragment sets
+  // live: 316 VGPRs spilled)
+  auto kloop = [&](auto S_) {
+    constexpr bool S = decltype(S_)::value;
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
+      // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
+      // barrier at the end of this tile (its vmcnt(0)) lands it
+      // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
+      // timing probes (tools/gemm_bench.hip only, wrong results): 512 no DMA after the first tile, 1024 fragment reads
+      // of the first tile only
+      if (DMA && kt + 1 < nk && !(V & 512)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+      if (M16 && (V & 256)) {
+        // 256: fragment reads one group ahead of the MFMAs that consume them, in the order those MFMAs run (A tile 0
+        // against B tiles 0..3, then A tiles 1..3), pinned by sched_group_barrier: the first MFMAs wait for 6 reads
+        // instead of the ~15 the default schedule puts in front of its first lgkmcnt(0).  2.5-3.9 % less time on
+        // the four CIFAR shapes, bit-identical results (profiles/r02/gemm_bench_rdorder.txt).  Measured and dropped:
+        // reading the next tile's first fragments after the barrier into the registers the trailing MFMAs free
+        // (cross-tile pipeline, 1-2 % slower than this), all reads issued by the end of A row 0 so the barrier moves
+        // up (5-8 % slower), A tile 3 read later so it moves down (0-2 % slower).
+        bf16x8 (&fa)[4][3] = pfa, (&fb)[4][3] = pfb;  // [tile][limb]
+        const bool rd = !(V & 1024) || kt == 0;
+        auto rd_a = [&](int t) {
+          if (!rd) return;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+          for (int l = 0; l < 3; ++l) fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
+        };
+        auto rd_b = [&](int t) {
+          if (!rd) return;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+          for (int l = 0; l < 3; ++l) fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
+        };
+        auto mf = [&](int i, int j) {
           f32x4 c = acc16[i][j];
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
@@ -1220,68 +1192,179 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
           acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+        };
+        constexpr int SG_MFMA = 0x8, SG_DS_RD = 0x100;
+        if constexpr (S) {
+          // 2048, waves 4-7: the second half (A tiles 2, 3) of the previous tile's MFMAs from the registers its
+          // fragments still hold, that tile's block flush, then this tile's reads and its first half, so that on every
+          // SIMD one wave is at MFMAs while its partner waits for its fragment reads after the barrier
+          if (kt > 0) {
+#pragma unroll
+            for (int i = 2; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) mf(i, j);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!(V & 32) && (kt & (FLUSH - 1)) == 0) flush16(kt - 1);
+          }
+          rd_a(0);
+          rd_b(0);
+          rd_b(1);
+          mf(0, 0);
+          rd_b(2);
+          mf(0, 1);
+          rd_b(3);
+          mf(0, 2);
+          rd_a(1);
+          mf(0, 3);
+          rd_a(2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mf(1, j);
+          rd_a(3);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 9, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __syncthreads();
+          if constexpr (CMAJ) advance_cmaj();
+          continue;
         }
-      if (V & 2) __builtin_amdgcn_s_setprio(0);
-    } else {
-      bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
+        rd_a(0);
+        rd_b(0);
+        rd_b(1);
+        mf(0, 0);
+        rd_b(2);
+        mf(0, 1);
+        rd_b(3);
+        mf(0, 2);
+        rd_a(1);
+        mf(0, 3);
+        rd_a(2);
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+        for (int j = 0; j < 4; ++j) mf(1, j);
+        rd_a(3);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int i = 2; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mf(i, j);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 9, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 48, 0);
+      } else if (M16) {
+        bf16x8 fa[4][3], fb[4][3];  // [tile][limb]
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int l = 0; l < 3; ++l) {
-            fa[s][t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 32 * X3_ROWB + oct32[s] + l * 16);
-            fb[s][t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 32 * X3_ROWB + oct32[s] + l * 16);
+            fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 16 * X3_ROWB + oct16 + l * 16);
+            fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 16 * X3_ROWB + oct16 + l * 16);
           }
-      if (!DMA && kt + 1 < nk) {
-        store_ab((kt + 1) & 1);
-        if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
-      }
-      if (V & 2) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            f32x16 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][2], fb[s][j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][1], c, 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
-          }
-      if (V & 2) __builtin_amdgcn_s_setprio(0);
-    }
-    __syncthreads();
-    if constexpr (CMAJ) advance_cmaj();
-    // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
-    // (a flush between them and the barrier measured 6-8 % slower)
-    if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
-      const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
-      if (M16) {
+        if (!DMA && kt + 1 < nk) {
+          store_ab((kt + 1) & 1);
+          if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+        }
+        if (V & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
-            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 c = acc16[i][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+            acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
           }
+        if (V & 2) __builtin_amdgcn_s_setprio(0);
       } else {
+        bf16x8 fa[2][2][3], fb[2][2][3];  // [s][tile][limb]
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              tot[i][j][r] = __builtin_fmaf(sg, acc[i][j][r], tot[i][j][r]);
-              acc[i][j][r] = 0.f;
+            for (int l = 0; l < 3; ++l) {
+              fa[s][t][l] = *reinterpret_cast<const bf16x8*>(base + afr + t * 32 * X3_ROWB + oct32[s] + l * 16);
+              fb[s][t][l] = *reinterpret_cast<const bf16x8*>(base + bfr + t * 32 * X3_ROWB + oct32[s] + l * 16);
             }
+        if (!DMA && kt + 1 < nk) {
+          store_ab((kt + 1) & 1);
+          if (kt + 2 < nk) load_ab((kt + 2) * X3_BK);
+        }
+        if (V & 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              f32x16 c = acc[i][j];
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][2], fb[s][j][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][2], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][1], fb[s][j][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][1], c, 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][0], fb[s][j][0], c, 0, 0, 0);
+            }
+        if (V & 2) __builtin_amdgcn_s_setprio(0);
+      }
+      __syncthreads();
+      if constexpr (CMAJ) advance_cmaj();
+      // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
+      // (a flush between them and the barrier measured 6-8 % slower)
+      if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
+        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        if (M16) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
+              acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                tot[i][j][r] = __builtin_fmaf(sg, acc[i][j][r], tot[i][j][r]);
+                acc[i][j][r] = 0.f;
+              }
+        }
       }
     }
-  }
+    if (S && nk > 0) {  // the staggered waves' trailing half tile
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mfp(i, j);
+      if (!(V & 32) && (nk & (FLUSH - 1)) == 0) flush16(nk - 1);
+    }
+  };
+  if (stag)
+    kloop(std::true_type{});
+  else
+    kloop(std::false_type{});
+
   }
   // the last partial block
   {
@@ -1458,8 +1541,8 @@ __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
   }
 }
 
-// split-K plan of a limb-engine conv: an under-filled grid (< 192 workgroups) splits K into its X3_NEGK sign blocks,
-// one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
+// split-K plan of a limb-engine conv: an under-filled grid (< DAMC_X3_KSPLIT_WGS, default 128 workgroups) splits K
+// into its X3_NEGK sign blocks, one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
 // the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
 // unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
 int x3_ksplit(int M, int N, int K, int zdim) {

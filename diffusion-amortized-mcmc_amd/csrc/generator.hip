@@ -10,7 +10,6 @@
 // dgrad outputs overwrite the activation they are masked with (same thread reads h, writes dh).
 #include <cstdlib>
 #include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "gemm.h"
@@ -1904,10 +1903,21 @@ static int setup_train(const damc_generator_t* g, int B, void* wsp, size_t wsb, 
 // activations), so the backward must run on the same one: train_forward records (batch, engine) per
 // workspace and train_backward refuses a descriptor that disagrees (DAMC_ERR_ARG) instead of reading
 // buffers the forward never wrote.  Keyed by the caller's workspace, so concurrent streams / threads with
-// their own workspaces do not interfere.
+// their own workspaces do not interfere.  The backward consumes the record: it overwrites activation buffers
+// as it goes, so a second backward of one forward (retain_graph) is refused rather than run on clobbered
+// inputs.  The table is a bounded ring: a forward that is never backpropagated holds one slot until 64 newer
+// workspaces have been recorded.
 static std::mutex g_train_mu;
-static std::unordered_map<const void*, long> g_train_rec;
+constexpr int TRAIN_REC_SLOTS = 64;
+static const void* g_train_ws[TRAIN_REC_SLOTS];
+static long g_train_key[TRAIN_REC_SLOTS];
+static int g_train_next = 0;
 static long train_key(const damc_generator_t* g, int B) { return (long)B * 4 + g->layers[0].engine; }
+static int train_rec_find(const void* wsp) {
+  for (int i = 0; i < TRAIN_REC_SLOTS; ++i)
+    if (g_train_ws[i] == wsp) return i;
+  return -1;
+}
 
 extern "C" int damc_generator_train_forward(const damc_generator_t* g, const float* z, int B, float* xhat, void* wsp,
                                             size_t wsb, void* stream) {
@@ -1920,7 +1930,13 @@ extern "C" int damc_generator_train_forward(const damc_generator_t* g, const flo
   if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
   if ((rc = forward_final(g, B, z, nullptr, 1.f, ws, xhat, nullptr, false, s))) return rc;
   std::lock_guard<std::mutex> lk(g_train_mu);
-  g_train_rec[wsp] = train_key(g, B);
+  int i = train_rec_find(wsp);
+  if (i < 0) {
+    i = g_train_next;
+    g_train_next = (g_train_next + 1) % TRAIN_REC_SLOTS;
+    g_train_ws[i] = wsp;
+  }
+  g_train_key[i] = train_key(g, B);
   return 0;
 }
 
@@ -1934,9 +1950,9 @@ extern "C" int damc_generator_train_backward(const damc_generator_t* g, const fl
   if (!z || !xhat || !grad_xhat || !grads) return DAMC_ERR_ARG;
   {
     std::lock_guard<std::mutex> lk(g_train_mu);
-    auto it = g_train_rec.find(wsp);
-    if (it == g_train_rec.end() || it->second != train_key(g, B)) return DAMC_ERR_ARG;
-    g_train_rec.erase(it);
+    const int i = train_rec_find(wsp);
+    if (i < 0 || g_train_key[i] != train_key(g, B)) return DAMC_ERR_ARG;
+    g_train_ws[i] = nullptr;
   }
   return train_backward(g, B, z, xhat, grad_xhat, grads, grad_z, ws, tw, as_stream(stream));
 }

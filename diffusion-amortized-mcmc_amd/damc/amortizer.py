@@ -132,7 +132,7 @@ class EncoderPlan:
         return buf, None, w
 
     def forward(self, x):
-        """The whole encoder in one damc_q_encoder_fwd call (packed weights cached per parameter version)."""
+        """The whole encoder in one damc_q_encoder_fwd call (weights re-packed per call into reused buffers)."""
         L = _lib.lib()
         dev = x.device
         stream = _lib.stream_ptr(dev)

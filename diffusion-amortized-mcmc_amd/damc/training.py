@@ -77,6 +77,9 @@ class _GeneratorTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx):
         zc, xh = ctx.saved_tensors[:2]
+        if ctx.ws is None:
+            raise RuntimeError("the HIP generator backward overwrites its forward's activations as it goes: "
+                               "backward through the same G(z) twice (retain_graph=True) is not supported")
         plan = ctx.plan
         dev = zc.device
         # the saved parameters are the modules' own and autograd has checked they were not modified in place,

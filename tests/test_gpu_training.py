@@ -300,9 +300,11 @@ def test_encoder_train_stagewise(gpu_device, name, B, nif):
     L = _lib.lib()
     st = _lib.stream_ptr(gpu_device)
 
-    def check3(name, ours, t32, t64):
-        e, e32 = rel_l2(ours.double().cpu().numpy(), t64.cpu().numpy()), rel_l2(t32.double().cpu().numpy(),
-                                                                             t64.cpu().numpy())
+    def check3(name, ours, t32, t64, keep=None):
+        o, a, b = (t.double().cpu().numpy() for t in (ours, t32, t64))
+        if keep is not None:
+            o, a, b = o[keep], a[keep], b[keep]
+        e, e32 = rel_l2(o, b), rel_l2(a, b)
         print("%s %s: |hip - fp64| %.2e  |torch32 - fp64| %.2e" % (enc_name, name, e, e32))
         assert e <= 3 * e32 + 1e-6, (enc_name, name, e, e32)
 
@@ -329,8 +331,23 @@ def test_encoder_train_stagewise(gpu_device, name, B, nif):
                 F.leaky_relu(F.instance_norm(yy, weight=gm, bias=bt, eps=norm.eps), slope).backward(
                     dh.to(dt).reshape(B, Ho, Wo, cout).permute(0, 3, 1, 2))
                 refs.append((yy.grad.permute(0, 2, 3, 1), gm.grad, bt.grad))
-            for nm, ours, r32, r64 in zip(("dy", "dgamma", "dbeta"), (dy, dgm, dbt), refs[0], refs[1]):
-                check3("stage %d IN %s" % (i, nm), ours, r32, r64)
+            # a pre-activation within fp32 rounding of the LeakyReLU kink takes either branch in any fp32 evaluation
+            # (the HIP kernel normalises with the forward's saved statistics, torch with its own): one flip moves the
+            # dy of its whole (sample, channel) slab through the slab means, and dgamma / dbeta of its channel.  Those
+            # slabs and channels are left out (the expected count: ~0.8e-6 of the elements; the rest must meet the bound)
+            with torch.no_grad():
+                a64 = F.instance_norm(y.double().permute(0, 3, 1, 2), weight=norm.weight.double(),
+                                      bias=norm.bias.double(), eps=norm.eps)
+                kink = (a64.abs() < 1e-6 * a64.pow(2).mean().sqrt()).flatten(2).any(2).cpu()  # (B, C)
+            nk = int(kink.sum())
+            assert nk <= max(4, 3e-6 * a64.numel()), (enc_name, i, nk)
+            if nk:
+                print("%s stage %d: %d (sample, channel) slab(s) at the LeakyReLU kink left out" % (enc_name, i, nk))
+            keep_dy = (~kink).numpy()[:, None, None, :].repeat(Ho, 1).repeat(Wo, 2)
+            keep_c = (~kink.any(0)).numpy()
+            for nm, ours, r32, r64, keep in zip(("dy", "dgamma", "dbeta"), (dy, dgm, dbt), refs[0], refs[1],
+                                                (keep_dy, keep_c, keep_c)):
+                check3("stage %d IN %s" % (i, nm), ours, r32, r64, keep if nk else None)
         else:
             dy = dh.reshape(B, Ho, Wo, cout)
         dx = torch.empty(B, H, W, cin, device=gpu_device) if i > 0 else None
@@ -351,3 +368,23 @@ def test_encoder_train_stagewise(gpu_device, name, B, nif):
         if dx is not None:
             check3("stage %d conv dx" % i, dx, refs[0][2], refs[1][2])
         dh = dx
+
+
+def test_generator_second_backward_is_refused(gpu_device):
+    """The HIP G-update backward consumes its forward's workspace (it overwrites activations as it walks the layers),
+    so a second backward through the same graph raises instead of reading clobbered buffers; a fresh forward after it
+    backpropagates normally (the per-workspace record is consumed, not leaked)."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=16, nc=3), 0).to(gpu_device)
+    z = torch.from_numpy(synth.normal_f32(2, 13, (8, 128))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(1, 13, (8, 3, 32, 32))).to(gpu_device)
+    loss = torch.sum((G(z) - x) ** 2)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="retain_graph"):
+        loss.backward()
+    a, _, _ = _hip_grads(G, z, x)
+    b, _, _ = _hip_grads(G, z, x)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)

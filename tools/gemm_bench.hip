@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../diffusion-amortized-mcmc_amd/csrc/gemm.hip"
@@ -251,7 +252,9 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
   }
-  V vars[] = {{"v261", run_x3<261>}, {"noDMA", run_x3<261 | 512>}};
+  // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only
+  V vars[] = {{"v261", run_x3<261, 1>}, {"noDMA", run_x3<261 | 512, 1>}, {"rd1", run_x3<261 | 1024, 1>},
+              {"mfma", run_x3<261 | 512 | 1024, 1>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
@@ -266,6 +269,7 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&c, nout * 4));
       std::vector<float> hmask = to_host(mk, nout);
       printf("accuracy %-28s", sh.name);
+      std::vector<float> h0;
       for (int v = 0; v < NV; ++v) {
         Shape s2 = sh;
         s2.a.C = c;
@@ -274,6 +278,8 @@ int main(int argc, char** argv) {
         vars[v].fn(s2, s);
         CK(hipStreamSynchronize(s));
         std::vector<float> hc = to_host(c, nout);
+        if (v == 0) h0 = hc;
+        else printf("  [%s bitwise v0: %s]", vars[v].name, memcmp(h0.data(), hc.data(), nout * 4) ? "NO" : "yes");
         double emax, emean, ebias;
         ref_check(sh, B, hA, hB, hbias, hmask, hc, &emax, &emean, &ebias);
         printf("  %s max %.2e mean %.2e bias %+.1e", vars[v].name, emax, emean, ebias);
