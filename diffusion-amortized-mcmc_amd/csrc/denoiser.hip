@@ -1988,8 +1988,8 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
   TsArgs ta;
   int tP = 0;
   size_t tsm = 0;
-  // inside a caller's stream capture the sweep records the launch chain's kernels eagerly into the caller's graph
-  // (a replayed team launch timed out its waits in tests/test_gpu_graph.py)
+  // inside a caller's stream capture the launch chain (when it is used) records its kernels eagerly into the caller's
+  // graph instead of replaying its own cached graph
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   DAMC_CHECK(hipStreamIsCapturing(s, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;

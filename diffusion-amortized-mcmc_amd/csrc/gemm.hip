@@ -854,6 +854,10 @@ __device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf1
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool M16 = (V & 1) != 0;
+  // 262144: 16-deep K stages in a 4-slot LDS ring (three stages in flight across raw barriers, counted vmcnt), each
+  // MFMA taking two limb products over 16 k (P16 main loop below)
+  constexpr bool P16 = (V & 262144) != 0;
+  constexpr bool DMA_OK_P16 = (V & 4) != 0;
   constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (X3_BM + X3_BN) * X3_ROWB];
   const int tid = threadIdx.x;
@@ -927,7 +931,9 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   int alds[X3_AJ], blds[X3_BJ];
 #pragma unroll
   for (int j = 0; j < X3_AJ; ++j) {
-    const int id = tid + 512 * j, row = id / X3_CHUNKS, ch = id - row * X3_CHUNKS;
+    // P16: 16-deep K stages, rows of 6 chunks in global order (the first X3P_AJ entries are used)
+    const int nch = P16 ? 6 : X3_CHUNKS;
+    const int id = tid + 512 * j, row = id / nch, ch = id - row * nch;
     const int m = m0 + row;
     unsigned msk = 0;
     int base = 0;
@@ -954,15 +960,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
             msk |= 1u << (ky * kw + kx);
     }
     const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;  // logical octet of physical chunk ch
-    abase[j] = base * 6 + q * 48 + limb * 16;
+    abase[j] = P16 ? base * 6 + ch * 16 : base * 6 + q * 48 + limb * 16;
     amask[j] = msk;
     alds[j] = row * X3_ROWB + ch * 16;
   }
 #pragma unroll
   for (int j = 0; j < X3_BJ; ++j) {
-    const int id = tid + 512 * j, row = id / X3_CHUNKS, ch = id - row * X3_CHUNKS;
+    const int nch = P16 ? 6 : X3_CHUNKS;
+    const int id = tid + 512 * j, row = id / nch, ch = id - row * nch;
     const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;
-    boff[j] = (unsigned)((n0 + row) * p.K * 6 + q * 48 + limb * 16);  // rows >= N fall out of range
+    boff[j] = (unsigned)((n0 + row) * p.K * 6 + (P16 ? ch * 16 : q * 48 + limb * 16));  // rows >= N fall out of range
     blds[j] = (X3_BM + row) * X3_ROWB + ch * 16;
   }
 
@@ -1054,6 +1061,20 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < X3_AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+    } else if constexpr ((V & 16384) != 0) {
+      // timing probe (wrong results): no A DMA after the first tile
+      if (k0 == kbeg) {
+#pragma unroll
+        for (int j = 0; j < X3_AJ; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+      }
+    } else if constexpr ((V & 4096) != 0) {
+      // timing probe (tools/gemm_bench.hip only, wrong results): every workgroup loads the same 64 KB, so the DMA
+      // is served by a hot L2 (issue cost and L2 latency only)
+#pragma unroll
+      for (int j = 0; j < X3_AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (tid * 16 + 8192 * j) & 0xFFFF,
+                                                 0, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < X3_AJ; ++j)
@@ -1061,9 +1082,40 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     }
 #pragma unroll
     for (int j = 0; j < X3_BJ; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
-                                               k0 * 6, 0, 0);
+      if (!(V & 32768) || k0 == kbeg)  // 32768: timing probe (wrong results), no B DMA after the first tile
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16,
+                                               (V & 4096) ? ((tid * 16 + 8192 * j) & 0xFFFF) : (int)boff[j],
+                                               (V & 4096) ? 0 : k0 * 6, 0, 0);
     if constexpr (OM != O_WGRAD && !CMAJ) {
+      ci0 += X3_BK;
+      if (ci0 == Cg) {
+        ci0 = 0;
+        ++tap;
+        if (++tkx == kw) {
+          tkx = 0;
+          ++tky;
+        }
+        set_tap();
+      }
+    }
+  };
+
+  // 65536 / 131072 (A/B): the default path's DMA in two parts, B and half of A at the tile start, the other half of A
+  // after a quarter / half of the tile's MFMAs
+  auto dma_part = [&](int k0, int buf, int part) {
+    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
+    if (part == 0) {
+#pragma unroll
+      for (int j = 0; j < X3_BJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
+                                                 k0 * 6, 0, 0);
+#pragma unroll
+      for (int j = 0; j < X3_AJ / 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = X3_AJ / 2; j < X3_AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
       ci0 += X3_BK;
       if (ci0 == Cg) {
         ci0 = 0;
@@ -1114,7 +1166,145 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   if constexpr ((V & 128) != 0) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
-  {
+  auto flush16 = [&](int ktd) {  // block flush after the MFMAs of K tile ktd
+    const float sg = (p.b_negblk && (((ktd + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
+        acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  };
+  if constexpr (P16) {
+    // ---- 16-deep K stages: stage s (16 k) of the A and B tiles is 384 rows x 96 B (three limbs of two octets, global
+    // order, conflict-free for every fragment pattern below without a swizzle), slot s & 3 of a 4-slot ring; the DMA
+    // of stage s + 3 is issued at the start of stage s, so three stages are in flight across each raw barrier and a
+    // wave waits (counted vmcnt) only for the stage the next one reads.  Per (A tile, B tile) three MFMAs, each over 16
+    // k of two limb products: [h|l].[l|h] (hl + lh), [h|m].[m|h] (hm + mh), [h|m].[h|m] (hh + mm).
+    static_assert(DMA_OK_P16 && !CMAJ && M16, "P16: LDS-DMA, tap-major walk, 16x16 tiles");
+    constexpr int PROWB = 96, PSLOT = (X3_BM + X3_BN) * PROWB;
+    static_assert(4 * PSLOT <= 2 * (X3_BM + X3_BN) * X3_ROWB, "P16 ring exceeds the LDS");
+    const int nks = 2 * nk;
+    const bool lo4 = __builtin_amdgcn_readfirstlane(tid) < 256;  // waves 0-3 also issue the second B piece
+    auto pdma = [&](int s) {
+      const int k0 = kbeg + s * 16;
+      unsigned char* base = smem + (s & 3) * PSLOT + wbase;
+      if constexpr (OM == O_WGRAD) {
+        const int pix = k0 / p.wg_bp;
+        const int qy = pix / Win, qx = pix - qy * Win;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int dy = (int)(amask[j] & 3u) - 1, dx = (int)((amask[j] >> 2) & 3u) - 1;
+          const bool live = amask[j] != 0xFFFFFFFFu && (unsigned)(qy + dy) < (unsigned)p.Hin &&
+                            (unsigned)(qx + dx) < (unsigned)Win;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16,
+                                                   live ? (int)(abase[j] + k0 * 6) : (int)KM_OOB, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * PROWB), 16, (int)boff[0], k0 * 6, 0, 0);
+      if (lo4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * PROWB + 512 * 16), 16, (int)boff[1], k0 * 6,
+                                                 0, 0);
+      if constexpr (OM != O_WGRAD) {
+        ci0 += 16;
+        if (ci0 == Cg) {
+          ci0 = 0;
+          ++tap;
+          if (++tkx == kw) {
+            tkx = 0;
+            ++tky;
+          }
+          set_tap();
+        }
+      }
+    };
+    // wait until at most `younger` stage groups issued after the one needed are still in flight (5 pieces per stage
+    // on waves 0-3, 4 on waves 4-7)
+    auto vwait = [&](int younger) {
+      if (lo4) {
+        if (younger >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    };
+    for (int s = 0; s < 3; ++s)
+      if (s < nks) pdma(s);
+    vwait((1 < nks) + (2 < nks));
+    __builtin_amdgcn_s_barrier();
+    // fragment byte offsets of this lane: row m = lane & 15, k-group q = lane >> 4 reads octet q & 1 of limb h (q < 2)
+    // or the pattern's second limb
+    const int lrow16 = lane & 15, q4 = lane >> 4, o3 = (q4 & 1) * 3;
+    const int cA1 = (o3 + (q4 < 2 ? 0 : 1)) * 16, cA2 = (o3 + (q4 < 2 ? 0 : 2)) * 16;
+    const int cB2 = (o3 + (q4 < 2 ? 1 : 0)) * 16, cB3 = (o3 + (q4 < 2 ? 2 : 0)) * 16;
+    const int arow = (wm * 64 + lrow16) * PROWB, brow = (X3_BM + wn * 64 + lrow16) * PROWB;
+    bf16x8 fa1[4], fa2[4], fb1[4], fb2[4], fb3[4];
+    constexpr int SG_MFMA = 0x8, SG_DS_RD = 0x100;
+    for (int s = 0; s < nks; ++s) {
+      if (s + 3 < nks) pdma(s + 3);
+      const unsigned char* sb = smem + (s & 3) * PSLOT;
+      auto rd_a = [&](int t) {
+        fa1[t] = *reinterpret_cast<const bf16x8*>(sb + arow + t * 16 * PROWB + cA1);
+        fa2[t] = *reinterpret_cast<const bf16x8*>(sb + arow + t * 16 * PROWB + cA2);
+      };
+      auto rd_b = [&](int t) {
+        fb1[t] = *reinterpret_cast<const bf16x8*>(sb + brow + t * 16 * PROWB + cA1);
+        fb2[t] = *reinterpret_cast<const bf16x8*>(sb + brow + t * 16 * PROWB + cB2);
+        fb3[t] = *reinterpret_cast<const bf16x8*>(sb + brow + t * 16 * PROWB + cB3);
+      };
+      auto mf = [&](int i, int j) {
+        f32x4 c = acc16[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[i], fb3[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb2[j], c, 0, 0, 0);
+        acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], c, 0, 0, 0);
+      };
+      rd_a(0);
+      rd_b(0);
+      rd_b(1);
+      mf(0, 0);
+      rd_b(2);
+      mf(0, 1);
+      rd_b(3);
+      mf(0, 2);
+      rd_a(1);
+      mf(0, 3);
+      rd_a(2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mf(1, j);
+      rd_a(3);
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mf(i, j);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 12, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
+      // the next stage's DMA has landed (this wave's pieces; the barrier covers the other waves'), and this stage's
+      // reads are retired before any wave re-fills its slot
+      vwait((s + 2 < nks) + (s + 3 < nks));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (!(V & 32) && ((s + 1) & (2 * FLUSH - 1)) == 0) flush16(s >> 1);
+    }
+  } else {
   constexpr bool DMA = (V & 4) != 0;
   static_assert(OM != O_WGRAD || DMA, "O_WGRAD runs on the LDS-DMA staging path only");
   static_assert(!CMAJ || DMA, "the channel-major walk runs on the LDS-DMA staging path only");
@@ -1132,17 +1322,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // accumulator still takes its tiles' MFMAs in the same order and is flushed at the same block ends: bitwise the
   // unstaggered kernel
   const bool stag = M16 && (V & 256) && (V & 2048) && DMA && __builtin_amdgcn_readfirstlane(tid) >= 256;
-  auto flush16 = [&](int ktd) {  // block flush after the MFMAs of K tile ktd
-    const float sg = (p.b_negblk && (((ktd + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
-        acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-  };
+
   auto mfp = [&](int i, int j) {  // the six limb products of A tile i x B tile j, smallest first
     f32x4 c = acc16[i][j];
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pfa[i][2], pfb[j][0], c, 0, 0, 0);
@@ -1163,7 +1343,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
       // timing probes (tools/gemm_bench.hip only, wrong results): 512 no DMA after the first tile, 1024 fragment reads
       // of the first tile only
-      if (DMA && kt + 1 < nk && !(V & 512)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+      // 8192 (with the stagger): the staggered waves issue their share of the DMA after their trailing half tile, so
+      // the two waves of a SIMD never issue DMA at the same time (each covers the other's DMA issue with MFMAs)
+      constexpr bool LATE = S && (V & 8192) != 0;
+      constexpr int SPLIT = (V & 65536) ? 1 : (V & 131072) ? 2 : 0;
+      static_assert(SPLIT == 0 || (OM != O_WGRAD && !CMAJ && !(V & (512 | 2048 | 4096 | 16384 | 32768))), "probe mix");
+      const bool dnext = DMA && kt + 1 < nk && !(V & 512);
+      if (SPLIT && dnext) dma_part(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1, 0);
+      else if (dnext && !(LATE && kt > 0)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
       if (M16 && (V & 256)) {
         // 256: fragment reads one group ahead of the MFMAs that consume them, in the order those MFMAs run (A tile 0
         // against B tiles 0..3, then A tiles 1..3), pinned by sched_group_barrier: the first MFMAs wait for 6 reads
@@ -1205,6 +1392,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
               for (int j = 0; j < 4; ++j) mf(i, j);
             __builtin_amdgcn_sched_barrier(0);
             if (!(V & 32) && (kt & (FLUSH - 1)) == 0) flush16(kt - 1);
+            if (LATE && kt + 1 < nk && !(V & 512)) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
           }
           rd_a(0);
           rd_b(0);
@@ -1233,6 +1421,46 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
           __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
           __syncthreads();
           if constexpr (CMAJ) advance_cmaj();
+          continue;
+        }
+        if constexpr (SPLIT != 0) {
+          rd_a(0);
+          rd_b(0);
+          rd_b(1);
+          mf(0, 0);
+          rd_b(2);
+          mf(0, 1);
+          rd_b(3);
+          mf(0, 2);
+          rd_a(1);
+          mf(0, 3);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 9, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 6, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (SPLIT == 1 && dnext) dma_part(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          rd_a(2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mf(1, j);
+          rd_a(3);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 24, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (SPLIT == 2 && dnext) dma_part(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 2; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mf(i, j);
+          __syncthreads();
+          if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) flush16(kt);
           continue;
         }
         rd_a(0);

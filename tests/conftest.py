@@ -28,11 +28,14 @@ SEED_X, SEED_Z0, SEED_POST, SEED_PRIOR, SEED_PRIOR_INIT, SEED_QN = 1, 2, 3, 4, 5
 G_NAMES = ["svhn_w16", "cifar10_w16", "celeba64_w16", "celebaHQ_w8", "mnist_w16", "cifar10_full"]
 Q_NAMES = ["q_cifar10_s", "q_cifar10_small", "q_svhn_s", "q_celeba64_s", "q_celebaHQ_s", "q_mnist_s",
            "q_cifar10_full"]
-# End-point tolerance (rel-L2) of a full reverse sweep: 2x the reference's own fp32 rounding spread,
-# measured as |fp64 oracle - reference golden| per case (n_interval 10-20 sweeps amplify rounding
-# through sqrt(1+e^-l) every step; 100-step 'large' sweeps are far better conditioned).
-Q_END_TOL = {"q_cifar10_s": 2e-2, "q_cifar10_small": 1.6e-1, "q_svhn_s": 5e-3, "q_celeba64_s": 1.1e-1,
-             "q_celebaHQ_s": 1.1e-1, "q_mnist_s": 1e-1, "q_cifar10_full": 2e-2}
+# End-point backstop (rel-L2 from the reference golden) of a full reverse sweep; the real criterion is accuracy-relative
+# (|hip - fp64| <= 3 |reference - fp64|, tests/test_gpu_amortizer.py).  n_interval 10-20 sweeps amplify rounding through
+# sqrt(1+e^-l) every step, so the reference's own fp32 result sits 3e-4 .. 8e-2 from an fp64 evaluation of the same
+# sweep (|reference - fp64|, per case).  Bound: 1.5x the largest |hip - reference| measured over the posterior and
+# prior sweeps of two rounds' GPU runs (profiles/r02/sweep_end_distances.txt, profiles/r03/sweep_end_distances.txt),
+# rounded up (q_cifar10_s / q_cifar10_full keep round 2's tighter 2e-2: measured 1.64e-2 / 1.67e-2).
+Q_END_TOL = {"q_cifar10_s": 2e-2, "q_cifar10_small": 1.35e-1, "q_svhn_s": 1.1e-3, "q_celeba64_s": 1.0e-1,
+             "q_celebaHQ_s": 9e-2, "q_mnist_s": 9e-2, "q_cifar10_full": 2e-2}
 
 
 def pytest_configure(config):

@@ -252,9 +252,10 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
   }
-  // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only
-  V vars[] = {{"v261", run_x3<261, 1>}, {"noDMA", run_x3<261 | 512, 1>}, {"rd1", run_x3<261 | 1024, 1>},
-              {"mfma", run_x3<261 | 512 | 1024, 1>}};
+  // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only,
+  // 4096 = DMA from one L2-hot 64 KB window
+  V vars[] = {{"v261", run_x3<261, 1>}, {"noDMA", run_x3<261 | 512, 1>}, {"mfma", run_x3<261 | 512 | 1024, 1>},
+              {"l2dma", run_x3<261 | 4096, 1>}, {"noAdma", run_x3<261 | 16384, 1>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
