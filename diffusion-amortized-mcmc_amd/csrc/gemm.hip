@@ -858,19 +858,25 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // MFMA taking two limb products over 16 k (P16 main loop below)
   constexpr bool P16 = (V & 262144) != 0;
   constexpr bool DMA_OK_P16 = (V & 4) != 0;
+  // 524288: a 128 x 256 block tile (waves 2 along M x 4 along N, each still 64 x 64) instead of 256 x 128: no
+  // half-empty tile at M = 128 (the first layer, M = B) and half the A gather per K tile
+  constexpr bool WIDE = (V & 524288) != 0;
+  static_assert(!(WIDE && P16), "one layout variant at a time");
+  constexpr int BM = WIDE ? 128 : X3_BM, BN = WIDE ? 256 : X3_BN;
+  constexpr int AJ = BM * X3_CHUNKS / 512, BJ = BN * X3_CHUNKS / 512;
   constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (X3_BM + X3_BN) * X3_ROWB];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * X3_ROWB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = WIDE ? wave >> 2 : wave >> 1, wn = WIDE ? wave & 3 : wave & 1;
   constexpr bool RASTER = (V & 16) != 0 && OM != O_WGRAD;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntn = (p.N + X3_BN - 1) / X3_BN;
+  const int ntn = (p.N + BN - 1) / BN;
   int tm, tn, z;
   if constexpr (RASTER) {
     const int nph = OM == O_PHASE ? 4 : 1;
-    const int ntm = (p.M + X3_BM - 1) / X3_BM;
+    const int ntm = (p.M + BM - 1) / BM;
     int pr;
     supertile(wgid, ntm, ntn * nph, tm, pr);
     tn = pr / nph;
@@ -880,7 +886,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     tn = wgid - tm * ntn;
     z = blockIdx.z;
   }
-  const int m0 = tm * X3_BM, n0 = tn * X3_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
   const unsigned short* Bg = p.B3;
@@ -926,11 +932,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       __builtin_amdgcn_make_buffer_rsrc((void*)Bg, (short)0, p.N * p.K * 6, 0x00020000);
 
   // ---- per-thread chunks: chunk id = tid + 512 j -> (row id / 12, 16-B chunk id % 12)
-  int abase[X3_AJ];
-  unsigned amask[X3_AJ], boff[X3_BJ];
-  int alds[X3_AJ], blds[X3_BJ];
+  int abase[AJ];
+  unsigned amask[AJ], boff[BJ];
+  int alds[AJ], blds[BJ];
 #pragma unroll
-  for (int j = 0; j < X3_AJ; ++j) {
+  for (int j = 0; j < AJ; ++j) {
     // P16: 16-deep K stages, rows of 6 chunks in global order (the first X3P_AJ entries are used)
     const int nch = P16 ? 6 : X3_CHUNKS;
     const int id = tid + 512 * j, row = id / nch, ch = id - row * nch;
@@ -965,12 +971,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     alds[j] = row * X3_ROWB + ch * 16;
   }
 #pragma unroll
-  for (int j = 0; j < X3_BJ; ++j) {
+  for (int j = 0; j < BJ; ++j) {
     const int nch = P16 ? 6 : X3_CHUNKS;
     const int id = tid + 512 * j, row = id / nch, ch = id - row * nch;
     const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;
     boff[j] = (unsigned)((n0 + row) * p.K * 6 + (P16 ? ch * 16 : q * 48 + limb * 16));  // rows >= N fall out of range
-    blds[j] = (X3_BM + row) * X3_ROWB + ch * 16;
+    blds[j] = (BM + row) * X3_ROWB + ch * 16;
   }
 
   int tap = 0, ci0 = 0, tky = 0, tkx = 0;
@@ -980,20 +986,20 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     tky = tap / kw;
     tkx = tap - tky * kw;
   }
-  unsigned aoff[X3_AJ];
+  unsigned aoff[AJ];
   auto set_tap = [&]() {
     const int toff = (tky * Win + tkx) * Cg * 6;
 #pragma unroll
-    for (int j = 0; j < X3_AJ; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
+    for (int j = 0; j < AJ; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
   };
   set_tap();
-  u32x4 ra[X3_AJ], rb[X3_BJ];
+  u32x4 ra[AJ], rb[BJ];
   auto load_ab = [&](int k0) {
 #pragma unroll
-    for (int j = 0; j < X3_AJ; ++j)
+    for (int j = 0; j < AJ; ++j)
       ra[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)aoff[j], ci0 * 6, 0));
 #pragma unroll
-    for (int j = 0; j < X3_BJ; ++j)
+    for (int j = 0; j < BJ; ++j)
       rb[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)boff[j], k0 * 6, 0));
     ci0 += X3_BK;
     if (ci0 == Cg) {
@@ -1007,11 +1013,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     }
   };
   auto store_ab = [&](int buf) {
-    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB;
+    unsigned char* base = smem + buf * (BM + BN) * X3_ROWB;
 #pragma unroll
-    for (int j = 0; j < X3_AJ; ++j) *reinterpret_cast<u32x4*>(base + alds[j]) = ra[j];
+    for (int j = 0; j < AJ; ++j) *reinterpret_cast<u32x4*>(base + alds[j]) = ra[j];
 #pragma unroll
-    for (int j = 0; j < X3_BJ; ++j) *reinterpret_cast<u32x4*>(base + blds[j]) = rb[j];
+    for (int j = 0; j < BJ; ++j) *reinterpret_cast<u32x4*>(base + blds[j]) = rb[j];
   };
   // channel-major walk: the next tile's (slice, tap), advanced after the tile's barrier (its VALU work then
   // overlaps the trailing MFMAs; before the DMA issue it delayed the next tile, before the barrier it kept the
@@ -1041,14 +1047,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   typedef __attribute__((address_space(3))) void* lds_t;
   const int wbase = (tid & ~63) * 16;
   auto dma_ab = [&](int k0, int buf) {
-    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
+    unsigned char* base = smem + buf * (BM + BN) * X3_ROWB + wbase;
     if constexpr (OM == O_WGRAD) {
       // the K tile is 32 samples of ONE pixel (wg_bp % 32 == 0): a chunk is live when its shifted pixel
       // lies inside the grid
       const int pix = k0 / p.wg_bp;
       const int qy = pix / Win, qx = pix - qy * Win;
 #pragma unroll
-      for (int j = 0; j < X3_AJ; ++j) {
+      for (int j = 0; j < AJ; ++j) {
         const int dy = (int)(amask[j] & 3u) - 1, dx = (int)((amask[j] >> 2) & 3u) - 1;
         const bool live = amask[j] != 0xFFFFFFFFu && (unsigned)(qy + dy) < (unsigned)p.Hin &&
                           (unsigned)(qx + dx) < (unsigned)Win;
@@ -1059,31 +1065,31 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       // K tile kt = (channel slice kt / taps, tap kt % taps), walked incrementally; the weights are stored in
       // the same slice-major order (launch_split_x3_cmaj), so B stays the sequential column k0
 #pragma unroll
-      for (int j = 0; j < X3_AJ; ++j)
+      for (int j = 0; j < AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     } else if constexpr ((V & 16384) != 0) {
       // timing probe (wrong results): no A DMA after the first tile
       if (k0 == kbeg) {
 #pragma unroll
-        for (int j = 0; j < X3_AJ; ++j)
+        for (int j = 0; j < AJ; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
       }
     } else if constexpr ((V & 4096) != 0) {
       // timing probe (tools/gemm_bench.hip only, wrong results): every workgroup loads the same 64 KB, so the DMA
       // is served by a hot L2 (issue cost and L2 latency only)
 #pragma unroll
-      for (int j = 0; j < X3_AJ; ++j)
+      for (int j = 0; j < AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (tid * 16 + 8192 * j) & 0xFFFF,
                                                  0, 0, 0);
     } else {
 #pragma unroll
-      for (int j = 0; j < X3_AJ; ++j)
+      for (int j = 0; j < AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < X3_BJ; ++j)
+    for (int j = 0; j < BJ; ++j)
       if (!(V & 32768) || k0 == kbeg)  // 32768: timing probe (wrong results), no B DMA after the first tile
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * X3_ROWB + 512 * 16 * j), 16,
                                                (V & 4096) ? ((tid * 16 + 8192 * j) & 0xFFFF) : (int)boff[j],
                                                (V & 4096) ? 0 : k0 * 6, 0, 0);
     if constexpr (OM != O_WGRAD && !CMAJ) {
@@ -1103,18 +1109,18 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // 65536 / 131072 (A/B): the default path's DMA in two parts, B and half of A at the tile start, the other half of A
   // after a quarter / half of the tile's MFMAs
   auto dma_part = [&](int k0, int buf, int part) {
-    unsigned char* base = smem + buf * (X3_BM + X3_BN) * X3_ROWB + wbase;
+    unsigned char* base = smem + buf * (BM + BN) * X3_ROWB + wbase;
     if (part == 0) {
 #pragma unroll
-      for (int j = 0; j < X3_BJ; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
+      for (int j = 0; j < BJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
                                                  k0 * 6, 0, 0);
 #pragma unroll
-      for (int j = 0; j < X3_AJ / 2; ++j)
+      for (int j = 0; j < AJ / 2; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
     } else {
 #pragma unroll
-      for (int j = X3_AJ / 2; j < X3_AJ; ++j)
+      for (int j = AJ / 2; j < AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
       ci0 += X3_BK;
       if (ci0 == Cg) {
@@ -1157,7 +1163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // (tile bases are multiples of 16 rows, so the row swizzle is a function of lrow alone)
   const int lrow = M16 ? (lane & 15) : (lane & 31), loct = M16 ? (lane >> 4) : (lane >> 5);
   const int sw = x3_swz(lrow);
-  const int afr = (wm * 64 + lrow) * X3_ROWB, bfr = (X3_BM + wn * 64 + lrow) * X3_ROWB;
+  const int afr = (wm * 64 + lrow) * X3_ROWB, bfr = (BM + wn * 64 + lrow) * X3_ROWB;
   const int oct16 = (loct ^ sw) * 48;                                         // 16x16x32
   const int oct32[2] = {((loct) ^ sw) * 48, ((2 + loct) ^ sw) * 48};          // 32x32x16, k16 step s
 
@@ -1184,8 +1190,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     // wave waits (counted vmcnt) only for the stage the next one reads.  Per (A tile, B tile) three MFMAs, each over 16
     // k of two limb products: [h|l].[l|h] (hl + lh), [h|m].[m|h] (hm + mh), [h|m].[h|m] (hh + mm).
     static_assert(DMA_OK_P16 && !CMAJ && M16, "P16: LDS-DMA, tap-major walk, 16x16 tiles");
-    constexpr int PROWB = 96, PSLOT = (X3_BM + X3_BN) * PROWB;
-    static_assert(4 * PSLOT <= 2 * (X3_BM + X3_BN) * X3_ROWB, "P16 ring exceeds the LDS");
+    constexpr int PROWB = 96, PSLOT = (BM + BN) * PROWB;
+    static_assert(4 * PSLOT <= 2 * (BM + BN) * X3_ROWB, "P16 ring exceeds the LDS");
     const int nks = 2 * nk;
     const bool lo4 = __builtin_amdgcn_readfirstlane(tid) < 256;  // waves 0-3 also issue the second B piece
     auto pdma = [&](int s) {
@@ -1207,9 +1213,9 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         for (int j = 0; j < 3; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * PROWB), 16, (int)boff[0], k0 * 6, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * PROWB), 16, (int)boff[0], k0 * 6, 0, 0);
       if (lo4)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + X3_BM * PROWB + 512 * 16), 16, (int)boff[1], k0 * 6,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * PROWB + 512 * 16), 16, (int)boff[1], k0 * 6,
                                                  0, 0);
       if constexpr (OM != O_WGRAD) {
         ci0 += 16;
@@ -1246,7 +1252,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     const int lrow16 = lane & 15, q4 = lane >> 4, o3 = (q4 & 1) * 3;
     const int cA1 = (o3 + (q4 < 2 ? 0 : 1)) * 16, cA2 = (o3 + (q4 < 2 ? 0 : 2)) * 16;
     const int cB2 = (o3 + (q4 < 2 ? 1 : 0)) * 16, cB3 = (o3 + (q4 < 2 ? 2 : 0)) * 16;
-    const int arow = (wm * 64 + lrow16) * PROWB, brow = (X3_BM + wn * 64 + lrow16) * PROWB;
+    const int arow = (wm * 64 + lrow16) * PROWB, brow = (BM + wn * 64 + lrow16) * PROWB;
     bf16x8 fa1[4], fa2[4], fb1[4], fb2[4], fb3[4];
     constexpr int SG_MFMA = 0x8, SG_DS_RD = 0x100;
     for (int s = 0; s < nks; ++s) {
@@ -1337,7 +1343,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   auto kloop = [&](auto S_) {
     constexpr bool S = decltype(S_)::value;
     for (int kt = 0; kt < nk; ++kt) {
-      const unsigned char* base = smem + (kt & 1) * (X3_BM + X3_BN) * X3_ROWB;
+      const unsigned char* base = smem + (kt & 1) * (BM + BN) * X3_ROWB;
       // DMA: the next tile goes into the other buffer (read before the previous barrier) now; the
       // barrier at the end of this tile (its vmcnt(0)) lands it
       // (issuing it later — after the fragment reads, or mid-MFMA — measured 10-15 % slower)
@@ -1615,11 +1621,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   // ---- epilogue through LDS: the block's 256 x 128 fp32 tile, then one thread per (row, channel octet):
   // 2 x 16-B fp32 stores and (C3) 3 x 16-B limb stores per octet, each row's 128 channels contiguous
-  constexpr int TS = X3_BN + 4;  // tile row stride (floats): 4-row groups of a 16x16 store land 16 banks apart
-  static_assert(X3_BM * TS * 4 + X3_BM * 8 <= 2 * (X3_BM + X3_BN) * X3_ROWB, "epilogue tile exceeds the LDS");
+  constexpr int TS = BN + 4;  // tile row stride (floats): 4-row groups of a 16x16 store land 16 banks apart
+  static_assert(BM * TS * 4 + BM * 8 <= 2 * (BM + BN) * X3_ROWB, "epilogue tile exceeds the LDS");
   float* tile = reinterpret_cast<float*>(smem);
-  long* rowtab = reinterpret_cast<long*>(smem + X3_BM * TS * 4);
-  if (tid < X3_BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
+  long* rowtab = reinterpret_cast<long*>(smem + BM * TS * 4);
+  if (tid < BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
   if (M16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1642,8 +1648,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   if (KSPLIT) {  // this slice's raw fp32 tile into the slab; x3_ksplit_reduce_kernel applies the epilogue
     float* sl = p.kslab + (long)z * p.M * p.N;
 #pragma unroll 2
-    for (int it = 0; it < X3_BM * X3_BN / 8 / 512; ++it) {
-      const int id = tid + 512 * it, row = id >> 4, oct = id & 15;
+    for (int it = 0; it < BM * BN / 8 / 512; ++it) {
+      const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
       const int m = m0 + row, n = n0 + oct * 8;
       if (m >= p.M || n >= p.N) continue;
       float* d = sl + (long)m * p.N + n;
@@ -1655,8 +1661,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   float* Cz = p.C;
   if ((OM == O_DENSE || OM == O_WGRAD) && Cz) Cz += (long)z * p.c_zstride;
 #pragma unroll 2
-  for (int it = 0; it < X3_BM * X3_BN / 8 / 512; ++it) {
-    const int id = tid + 512 * it, row = id >> 4, oct = id & 15;
+  for (int it = 0; it < BM * BN / 8 / 512; ++it) {
+    const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
     const int n = n0 + oct * 8;
     const long rowoff = rowtab[row];
     if (rowoff < 0 || n >= p.N) continue;
@@ -1773,7 +1779,7 @@ __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
 // into its X3_NEGK sign blocks, one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
 // the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
 // unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
-int x3_ksplit(int M, int N, int K, int zdim) {
+int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn) {
   // DAMC_X3_KSPLIT=0 disables; DAMC_X3_KSPLIT_WGS: the grid size below which a conv splits (A/B)
   const char* ev = getenv("DAMC_X3_KSPLIT");  // per call: tests compare both paths in one process
   const bool on = !(ev && ev[0] == '0');
@@ -1781,22 +1787,23 @@ int x3_ksplit(int M, int N, int K, int zdim) {
     const char* e = getenv("DAMC_X3_KSPLIT_WGS");
     return e ? atol(e) : 128L;
   }();
-  const long wgs = (long)((M + X3_BM - 1) / X3_BM) * ((N + X3_BN - 1) / X3_BN) * zdim;
+  const long wgs = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * zdim;
   if (!on || wgs >= below || K % X3_NEGK != 0 || K / X3_NEGK < 2) return 1;
   return K / X3_NEGK;
 }
 
-long x3_ksplit_floats(int M, int N, int K, int zdim) {
-  const int ks = x3_ksplit(M, N, K, zdim);
+long x3_ksplit_floats(int M, int N, int K, int zdim) {  // either block layout (gemm_x3_kernel, V & 524288)
+  const int ks = std::max(x3_ksplit(M, N, K, zdim, X3_BM, X3_BN), x3_ksplit(M, N, K, zdim, 128, 256));
   return ks > 1 ? (long)zdim * ks * M * N : 0;
 }
 
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   GemmArgs a = a0;
-  const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
+  constexpr int BM = (V & 524288) ? 128 : X3_BM, BN = (V & 524288) ? 256 : X3_BN;
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   if (OM != O_WGRAD && a.kslab && !(V & 16)) {
-    const int ks = x3_ksplit(a.M, a.N, a.K, zdim);
+    const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
       a.ksplit = ks;
       a.k_per_z = a.K / ks;
@@ -1993,7 +2000,8 @@ int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double
   if (a.N % 8 != 0 || a.ldc % 8 != 0 || a.ldc < a.N || a.c_zstride < (long)a.M * a.ldc) return DAMC_ERR_ARG;
   if (((uintptr_t)a.A3 | (uintptr_t)a.B3 | (uintptr_t)a.C) % 16 != 0) return DAMC_ERR_ARG;
   if ((double)a.Cg * a.K * 6 >= 2147483647.0 || (double)a.N * a.K * 6 >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
-  const int ntm = (a.M + X3_BM - 1) / X3_BM, ntn = (a.N + X3_BN - 1) / X3_BN;
+  constexpr int BM = (DAMC_X3_VARIANT & 524288) ? 128 : X3_BM, BN = (DAMC_X3_VARIANT & 524288) ? 256 : X3_BN;
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   ProfScope ps(prof_name, flops, s);
   hipLaunchKernelGGL((gemm_x3_kernel<EPI_STORE, O_WGRAD>), dim3(ntm * ntn, 1, a.wg_phases * slices), dim3(512), 0, s,
                      a);

@@ -631,6 +631,130 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
   }
 }
 
+// k3 s1 p1 output-layer dgrad on the limb engine (sign-bit mask in, x3 limbs out).  Per 16 pixels it is the product
+// dh^T (Cin x 16) = W^T (Cin x 9 NC) . D (9 NC x 16), D = the pixels' 3x3 delta windows (k = tap NC + o, zero past
+// 9 NC <= 32 and outside the image): one 16x16x32 tile per 16 channels, six bf16 limb products each (fp32-accurate,
+// as gemm_x3_kernel).  W^T's limb fragments sit in LDS for the whole grid-stride loop; D's are gathered per 16 pixels
+// from the L2-resident delta.  Output lane l holds channels 16 i + 4 (l >> 4) + r of pixel l & 15: the LReLU' nibble
+// of the sign bits applies directly, and each limb leaves as one 8-B store (4 channels), so the kernel is bound by
+// the 6 B per element it writes.  Replaces the VALU form (smallc_dgrad_k3_kernel, 66 us -> see DESIGN.md) on the
+// Langevin path; the accumulation order differs (limb products per 32-deep k), not the accuracy.
+template <int NC>
+__global__ __launch_bounds__(256) void smallc_dgrad_k3_mfma_kernel(int npix, int Hin, int Win, int Cin,
+                                                                   const float* __restrict__ wpk,
+                                                                   const float* __restrict__ delta, float mask_slope,
+                                                                   unsigned short* __restrict__ h3,
+                                                                   const unsigned char* __restrict__ hbits) {
+  static_assert(9 * NC <= 32, "the 3x3 window of NC channels fills one 32-deep k tile");
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) bf16x8_t wfr[];  // [Cin / 16][3 limbs][64 lanes]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, m = lane & 15;
+  const int nti = Cin >> 4;
+  // W^T limb fragments: lane (row = channel 16 i + m, k-group q) holds k = 8 q .. 8 q + 7
+  for (int u = tid; u < nti * 64; u += 256) {
+    const int i = u >> 6, l = u & 63, ch = 16 * i + (l & 15), kq = 8 * (l >> 4);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kq + e, t = k / NC, o = k - t * NC;
+      v[e] = k < 9 * NC ? wpk[((long)t * Cin + ch) * NC + o] : 0.f;
+    }
+    bf16x8_t h, md, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const __bf16 b0 = (__bf16)v[e];
+      const float r1 = v[e] - (float)b0;
+      const __bf16 b1 = (__bf16)r1;
+      h[e] = b0;
+      md[e] = b1;
+      lo[e] = (__bf16)(r1 - (float)b1);
+    }
+    wfr[(i * 3 + 0) * 64 + l] = h;
+    wfr[(i * 3 + 1) * 64 + l] = md;
+    wfr[(i * 3 + 2) * 64 + l] = lo;
+  }
+  __syncthreads();
+  const int hw = Hin * Win;
+  const int units = (npix + 15) >> 4;
+  for (int un = blockIdx.x * 4 + wave; un < units; un += gridDim.x * 4) {
+    const int pix = un * 16 + m;
+    const bool live = pix < npix;
+    const int b = live ? pix / hw : 0, rem = live ? pix - b * hw : 0;
+    const int y = rem / Win, x = rem - y * Win;
+    // D's fragment: column = this lane's pixel, k = 8 q .. 8 q + 7
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * q + e, t = k / NC, o = k - t * NC;
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      dv[e] = (live && k < 9 * NC && (unsigned)yy < (unsigned)Hin && (unsigned)xx < (unsigned)Win)
+                  ? delta[(((long)b * Hin + yy) * Win + xx) * NC + o]
+                  : 0.f;
+    }
+    bf16x8_t d0, d1, d2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const __bf16 b0 = (__bf16)dv[e];
+      const float r1 = dv[e] - (float)b0;
+      const __bf16 b1 = (__bf16)r1;
+      d0[e] = b0;
+      d1[e] = b1;
+      d2[e] = (__bf16)(r1 - (float)b1);
+    }
+    const unsigned char* hb = hbits + (long)pix * (Cin >> 3);
+    unsigned short* out = h3 + (long)pix * 3 * Cin;
+    for (int i = 0; i < nti; ++i) {
+      const bf16x8_t a0 = wfr[(i * 3 + 0) * 64 + lane], a1 = wfr[(i * 3 + 1) * 64 + lane],
+                     a2 = wfr[(i * 3 + 2) * 64 + lane];
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, d0, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, d1, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d2, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, d0, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d1, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d0, c, 0, 0, 0);
+      if (!live) continue;
+      const int c0 = 16 * i + 4 * q;
+      const unsigned nib = (hb[c0 >> 3] >> (c0 & 4)) & 15u;
+      unsigned short lh[4], lm[4], ll[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = c[r] * (((nib >> r) & 1u) ? 1.f : mask_slope);
+        const __bf16 b0 = (__bf16)v;
+        const float r1 = v - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        lh[r] = __builtin_bit_cast(unsigned short, b0);
+        lm[r] = __builtin_bit_cast(unsigned short, b1);
+        ll[r] = __builtin_bit_cast(unsigned short, (__bf16)(r1 - (float)b1));
+      }
+      typedef unsigned u2 __attribute__((ext_vector_type(2)));
+      unsigned short* o8 = out + (c0 >> 3) * 24 + (c0 & 4);
+      *reinterpret_cast<u2*>(o8) = u2{lh[0] | ((unsigned)lh[1] << 16), lh[2] | ((unsigned)lh[3] << 16)};
+      *reinterpret_cast<u2*>(o8 + 8) = u2{lm[0] | ((unsigned)lm[1] << 16), lm[2] | ((unsigned)lm[3] << 16)};
+      *reinterpret_cast<u2*>(o8 + 16) = u2{ll[0] | ((unsigned)ll[1] << 16), ll[2] | ((unsigned)ll[3] << 16)};
+    }
+  }
+}
+
+// the limb-engine form applies to the Langevin path's output layer: sign bits in, limbs out, Cin a multiple of 16
+bool smallc_k3_mfma_ok(const damc_layer_t& L) { return L.cin % 16 == 0 && L.cin <= 1024; }
+
+int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta, float mask_slope,
+                                unsigned short* h3, const unsigned char* hbits, hipStream_t s) {
+  const int npix = B * L.hin * L.win;
+  const int units = (npix + 15) / 16;
+  const size_t sm = (size_t)L.cin / 16 * 3 * 64 * 16;
+  const int grid = std::max(1, std::min((units + 3) / 4, 768));
+  if (L.cout == 3)
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<3>), dim3(grid), dim3(256), sm, s, npix, L.hin, L.win, L.cin,
+                       L.w_fwd, delta, mask_slope, h3, hbits);
+  else
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<1>), dim3(grid), dim3(256), sm, s, npix, L.hin, L.win, L.cin,
+                       L.w_fwd, delta, mask_slope, h3, hbits);
+  return (int)hipGetLastError();
+}
+
 bool smallc_reg_ok(const damc_layer_t& L) {
   if (L.cout != 1 && L.cout != 3) return false;
   if (!((L.k == 3 && L.stride == 1) || (L.k == 4 && L.stride == 2))) return false;
@@ -920,6 +1044,11 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
   if (hbits_in && (!smallc_k3(L) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
   if (smallc_k3(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
+    // the Langevin path (sign bits in, limbs out) on the limb engine; DAMC_SMALLC_DGRAD_MFMA=0 (read per call)
+    // selects the VALU kernel below
+    const char* mf = getenv("DAMC_SMALLC_DGRAD_MFMA");
+    if (h3 && hbits_in && smallc_k3_mfma_ok(L) && !(mf && mf[0] == '0'))
+      return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, h3, hbits_in, s);
     // 8 rows per block with the next mask nibbles prefetched: 66.4 us vs 69.9 (4 rows, no prefetch) at the
     // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us); fewer rows per block when the
     // batch would leave fewer than 256 blocks (B=16: 60 us at 8 rows, 64 blocks).  Pixels are independent, so

@@ -254,8 +254,7 @@ int main(int argc, char** argv) {
   }
   // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only,
   // 4096 = DMA from one L2-hot 64 KB window
-  V vars[] = {{"v261", run_x3<261, 1>}, {"noDMA", run_x3<261 | 512, 1>}, {"mfma", run_x3<261 | 512 | 1024, 1>},
-              {"l2dma", run_x3<261 | 4096, 1>}, {"noAdma", run_x3<261 | 16384, 1>}};
+  V vars[] = {{"v261", run_x3<261, 1>}, {"wide", run_x3<261 | 524288, 1>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
@@ -315,6 +314,44 @@ int main(int argc, char** argv) {
     for (int v = 0; v < NV; ++v)
       printf("  %s %.3f (%.1f)", vars[v].name, best[si][v], shapes[si].flops / (best[si][v] * 1e-3) / 1e12);
     printf("\n");
+  }
+  // the first layer on the limb engine as the library runs it (z limbs . W limbs as a 1x1 conv, bias + LReLU, fp32 +
+  // limb outputs, sign bits), both block layouts
+  {
+    GemmArgs a;
+    a.A = zin; a.Cg = nz; a.Hin = a.Win = a.Hq = a.Wq = 1; a.kw = 1; a.stride = 1;
+    a.A3 = split_dev(zin, (size_t)B * nz);
+    a.B3 = split_dev(wpf, (size_t)NP * nz);
+    a.b_negblk = 1;
+    a.C = o1; a.ldc = NP; a.M = B; a.N = NP; a.K = nz; a.k_per_z = nz;
+    a.bias = bias; a.bias_mod = 8 * ngf; a.act = DAMC_ACT_LRELU; a.slope = 0.2f;
+    CK(hipMalloc(&a.C3, (size_t)B * NP * 6));
+    CK(hipMalloc(&a.sgn, (size_t)B * NP / 8));
+    float* c2;
+    CK(hipMalloc(&c2, (size_t)B * NP * 4));
+    GemmArgs a2 = a;
+    a2.C = c2;
+    launch_x3_t<EPI_BIAS_ACT, O_DENSE, 261>(a, 1, s);
+    launch_x3_t<EPI_BIAS_ACT, O_DENSE, 261 | 524288>(a2, 1, s);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> r1 = to_host(o1, (size_t)B * NP), r2 = to_host(c2, (size_t)B * NP);
+    printf("proj fwd x3: wide bitwise default: %s\n", memcmp(r1.data(), r2.data(), r1.size() * 4) ? "NO" : "yes");
+    float b1 = 1e30f, b2 = 1e30f;
+    for (int r = 0; r < rounds; ++r) {
+      for (int v = 0; v < 2; ++v) {
+        CK(hipEventRecord(e0, s));
+        for (int k = 0; k < reps; ++k) {
+          if (v == 0) launch_x3_t<EPI_BIAS_ACT, O_DENSE, 261>(a, 1, s);
+          else launch_x3_t<EPI_BIAS_ACT, O_DENSE, 261 | 524288>(a, 1, s);
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        (v == 0 ? b1 : b2) = std::min(v == 0 ? b1 : b2, ms / reps);
+      }
+    }
+    printf("proj fwd x3 128x65536x128      v261 %.4f ms  wide %.4f ms\n", b1, b2);
   }
   for (const Proj& pr : projs) {
     float best = 1e30f;

@@ -2,7 +2,9 @@
 // -> 3 ch, k3 s1 p1): the dgrad (fp32 mask / sign-bit mask, fp32 / limb output) and the two-stage
 // forward, timed in one process.
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DDAMC_GEMM_NO_C_API tools/smallc_bench.hip -o tools/smallc_bench
+#include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -118,6 +120,36 @@ int main() {
     timeit(nm, act * 1.5 + act / 32, [&] { k3(R, std::integral_constant<int, 4>(), std::true_type()); });
     snprintf(nm, sizeof(nm), "k3 bits->limbs R=%d UNR=2 PF", R);
     timeit(nm, act * 1.5 + act / 32, [&] { k3(R, std::integral_constant<int, 2>(), std::true_type()); });
+  }
+  // the limb-engine (MFMA) form vs the VALU form: same inputs, max |difference| relative to max |value| of the
+  // decoded limbs
+  {
+    unsigned short* h3b;
+    CK(hipMalloc(&h3b, npix * C * 6));
+    CK(hipMemset(h3, 0, npix * C * 6));
+    CK(hipMemset(h3b, 0, npix * C * 6));
+    const dim3 grid((unsigned)(H / 8), (unsigned)B);
+    hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, 4, true>), grid, dim3(256), sizeof(float) * 10 * (H + 2) * 4, s, h,
+                       H, H, C, 8, L.w_fwd, delta, (int)DAMC_ACT_LRELU, 0.2f, h3, bits);
+    CK((hipError_t)launch_smallc_dgrad_k3_mfma(L, B, delta, 0.2f, h3b, bits, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<unsigned short> a((size_t)npix * C * 3), bb((size_t)npix * C * 3);
+    CK(hipMemcpy(a.data(), h3, a.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(bb.data(), h3b, bb.size() * 2, hipMemcpyDeviceToHost));
+    auto bf = [](unsigned short u) { unsigned v = (unsigned)u << 16; float f; memcpy(&f, &v, 4); return f; };
+    double mx = 0, md = 0;
+    for (size_t oc = 0; oc < (size_t)npix * C / 8; ++oc)
+      for (int e = 0; e < 8; ++e) {
+        const size_t base = oc * 24 + e;
+        const double va = (double)bf(a[base]) + bf(a[base + 8]) + bf(a[base + 16]);
+        const double vb = (double)bf(bb[base]) + bf(bb[base + 8]) + bf(bb[base + 16]);
+        mx = std::max(mx, std::fabs(va));
+        md = std::max(md, std::fabs(va - vb));
+      }
+    printf("mfma vs valu dgrad: max |diff| %.3e, max |value| %.3e (rel %.2e)\n", md, mx, md / mx);
+    timeit("k3 bits->limbs MFMA", act * 1.5 + act / 32, [&] {
+      CK((hipError_t)launch_smallc_dgrad_k3_mfma(L, B, delta, 0.2f, h3b, bits, s));
+    });
   }
   CK(hipGetLastError());
   return 0;
