@@ -1973,6 +1973,16 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     if (a.mask_sgn) c.mask_sgn = a.mask_sgn + b0 * cimg / 8;
     if (a.mask) c.mask = a.mask + b0 * cimg;
     c.M = (int)(nb * hwq);
+    // at most 128 rows (the first layer, M = B <= 128): the 128 x 256 block layout, no half-empty 256-row tile
+    // (bitwise the default layout: every output takes the same MFMA sequence; 46.6 -> 35.7 us for CIFAR's B = 128
+    // first layer, tools/gemm_bench.hip).  DAMC_X3_WIDE=0 (read per call) keeps the default layout
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128) {
+      const char* ew = getenv("DAMC_X3_WIDE");
+      if (!(ew && ew[0] == '0')) {
+        launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        continue;
+      }
+    }
 #define DAMC_X3(E_, O_)                \
   if (epi == E_ && om == O_) {         \
     launch_x3_t<E_, O_>(c, zdim, s);   \

@@ -634,64 +634,82 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
 // k3 s1 p1 output-layer dgrad on the limb engine (sign-bit mask in, x3 limbs out).  Per 16 pixels it is the product
 // dh^T (Cin x 16) = W^T (Cin x 9 NC) . D (9 NC x 16), D = the pixels' 3x3 delta windows (k = tap NC + o, zero past
 // 9 NC <= 32 and outside the image): one 16x16x32 tile per 16 channels, six bf16 limb products each (fp32-accurate,
-// as gemm_x3_kernel).  W^T's limb fragments sit in LDS for the whole grid-stride loop; D's are gathered per 16 pixels
-// from the L2-resident delta.  Output lane l holds channels 16 i + 4 (l >> 4) + r of pixel l & 15: the LReLU' nibble
-// of the sign bits applies directly, and each limb leaves as one 8-B store (4 channels), so the kernel is bound by
-// the 6 B per element it writes.  Replaces the VALU form (smallc_dgrad_k3_kernel, 66 us -> see DESIGN.md) on the
-// Langevin path; the accumulation order differs (limb products per 32-deep k), not the accuracy.
-template <int NC>
-__global__ __launch_bounds__(256) void smallc_dgrad_k3_mfma_kernel(int npix, int Hin, int Win, int Cin,
-                                                                   const float* __restrict__ wpk,
-                                                                   const float* __restrict__ delta, float mask_slope,
-                                                                   unsigned short* __restrict__ h3,
-                                                                   const unsigned char* __restrict__ hbits) {
+// as gemm_x3_kernel; the accumulation order differs from the VALU form's fmaf chain, not the accuracy).
+// A workgroup's NG waves share a 16-pixel unit, wave w taking channels 64 w .. 64 w + 63 (four tiles): its W^T limb
+// fragments (12 registers) are loaded once, the unit's D fragment and sign bits are loaded one unit ahead, and the
+// unit's 16 x 384 B of limbs leave through a per-wave LDS image as whole 16-B chunks.  Output lane l holds channels
+// 16 i + 4 (l >> 4) + r of pixel l & 15, so the LReLU' nibble of the sign bits applies directly.
+template <int NC, int NG>
+__global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix, int Hin, int Win,
+                                                                      const float* __restrict__ wpk,
+                                                                      const float* __restrict__ delta,
+                                                                      float mask_slope, unsigned short* __restrict__ h3,
+                                                                      const unsigned char* __restrict__ hbits,
+                                                                      int probe = 0) {
+  // probe (tools/smallc_bench.hip only, wrong results): 1 no delta / sign-bit loads, 2 no output stores
   static_assert(9 * NC <= 32, "the 3x3 window of NC channels fills one 32-deep k tile");
   typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-  extern __shared__ __attribute__((aligned(16))) bf16x8_t wfr[];  // [Cin / 16][3 limbs][64 lanes]
+  constexpr int Cin = 64 * NG;
+  // per-wave output image, pixel rows padded 384 -> 392 B (98 dwords): the 16 lanes of a ds_write_b64 group (16
+  // pixels) then cover all 32 banks (at 384 B they all hit one: 16-way; at 400 B, 2-way); rows are 8-B aligned, so the
+  // copy-out reads 8 B at a time
+  constexpr int SROW = 392;
+  __shared__ __attribute__((aligned(16))) unsigned char stg_all[NG][16 * SROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, m = lane & 15;
-  const int nti = Cin >> 4;
-  // W^T limb fragments: lane (row = channel 16 i + m, k-group q) holds k = 8 q .. 8 q + 7
-  for (int u = tid; u < nti * 64; u += 256) {
-    const int i = u >> 6, l = u & 63, ch = 16 * i + (l & 15), kq = 8 * (l >> 4);
-    float v[8];
+  unsigned char* const stg = stg_all[wave];
+  // this wave's W^T limb fragments: tile t = channels 64 w + 16 t + m (rows), k = 8 q .. 8 q + 7
+  bf16x8_t wa[4][3];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ch = 64 * wave + 16 * t + m;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int k = kq + e, t = k / NC, o = k - t * NC;
-      v[e] = k < 9 * NC ? wpk[((long)t * Cin + ch) * NC + o] : 0.f;
-    }
-    bf16x8_t h, md, lo;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const __bf16 b0 = (__bf16)v[e];
-      const float r1 = v[e] - (float)b0;
+      const int k = 8 * q + e, tp = k / NC, o = k - tp * NC;
+      const float v = k < 9 * NC ? wpk[((long)tp * Cin + ch) * NC + o] : 0.f;
+      const __bf16 b0 = (__bf16)v;
+      const float r1 = v - (float)b0;
       const __bf16 b1 = (__bf16)r1;
-      h[e] = b0;
-      md[e] = b1;
-      lo[e] = (__bf16)(r1 - (float)b1);
+      wa[t][0][e] = b0;
+      wa[t][1][e] = b1;
+      wa[t][2][e] = (__bf16)(r1 - (float)b1);
     }
-    wfr[(i * 3 + 0) * 64 + l] = h;
-    wfr[(i * 3 + 1) * 64 + l] = md;
-    wfr[(i * 3 + 2) * 64 + l] = lo;
   }
-  __syncthreads();
   const int hw = Hin * Win;
   const int units = (npix + 15) >> 4;
-  for (int un = blockIdx.x * 4 + wave; un < units; un += gridDim.x * 4) {
+  // every global access is a buffer access whose out-of-range offset reads zero / drops the store, so no load or store
+  // sits in a branch (a store in a divergent branch made the compiler wait vmcnt(0) for it at every unit)
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)delta, (short)0, npix * NC * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)hbits, (short)0, npix * (Cin / 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)h3, (short)0, npix * 6 * Cin, 0x00020000);
+  constexpr int OOB = 0x7FFFFFF0;
+  // the unit's loads: D's column for this lane's pixel (k = 8 q .. 8 q + 7) and the pixel's 8 sign-bit bytes of this
+  // wave's 64 channels
+  float dv[8];
+  unsigned mw0 = 0u, mw1 = 0u;
+  auto load_unit = [&](int un) {
     const int pix = un * 16 + m;
-    const bool live = pix < npix;
+    const bool live = un < units && pix < npix && !(probe & 1);
     const int b = live ? pix / hw : 0, rem = live ? pix - b * hw : 0;
     const int y = rem / Win, x = rem - y * Win;
-    // D's fragment: column = this lane's pixel, k = 8 q .. 8 q + 7
-    float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int k = 8 * q + e, t = k / NC, o = k - t * NC;
-      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-      dv[e] = (live && k < 9 * NC && (unsigned)yy < (unsigned)Hin && (unsigned)xx < (unsigned)Win)
-                  ? delta[(((long)b * Hin + yy) * Win + xx) * NC + o]
-                  : 0.f;
+      const int k = 8 * q + e, tp = k / NC, o = k - tp * NC;
+      const int yy = y + tp / 3 - 1, xx = x + tp % 3 - 1;
+      const bool ok = live && k < 9 * NC && (unsigned)yy < (unsigned)Hin && (unsigned)xx < (unsigned)Win;
+      dv[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            rd, ok ? ((((b * Hin + yy) * Win + xx) * NC + o) * 4) : OOB, 0, 0));
     }
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    const u2 t = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rb, live ? pix * (Cin / 8) + 8 * wave : OOB,
+                                                                             0, 0));
+    mw0 = t[0];
+    mw1 = t[1];
+  };
+  int un = blockIdx.x;
+  load_unit(un);
+  const int nsh = 8 * (q >> 1) + 4 * (q & 1);
+  for (; un < units; un += gridDim.x) {
     bf16x8_t d0, d1, d2;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -702,25 +720,32 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_mfma_kernel(int npix, int
       d1[e] = b1;
       d2[e] = (__bf16)(r1 - (float)b1);
     }
-    const unsigned char* hb = hbits + (long)pix * (Cin >> 3);
-    unsigned short* out = h3 + (long)pix * 3 * Cin;
-    for (int i = 0; i < nti; ++i) {
-      const bf16x8_t a0 = wfr[(i * 3 + 0) * 64 + lane], a1 = wfr[(i * 3 + 1) * 64 + lane],
-                     a2 = wfr[(i * 3 + 2) * 64 + lane];
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, d0, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, d1, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d2, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, d0, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d1, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, d0, c, 0, 0, 0);
-      if (!live) continue;
-      const int c0 = 16 * i + 4 * q;
-      const unsigned nib = (hb[c0 >> 3] >> (c0 & 4)) & 15u;
+    const unsigned m0w = mw0, m1w = mw1;
+    load_unit(un + gridDim.x);  // the next unit's loads land under this one's MFMAs and stores
+    f32x4 c[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the four tiles' six-MFMA chains interleaved (independent accumulators), smallest limb products first
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][2], d0, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][1], d1, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d2, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][1], d0, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d1, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d0, c[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      // channels 64 w + 16 t + 4 q .. + 3: byte 2 t + (q >> 1) of the wave's 8, nibble q & 1
+      const unsigned nib = ((t < 2 ? m0w : m1w) >> (16 * (t & 1) + nsh)) & 15u;
       unsigned short lh[4], lm[4], ll[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = c[r] * (((nib >> r) & 1u) ? 1.f : mask_slope);
+        const float v = c[t][r] * (((nib >> r) & 1u) ? 1.f : mask_slope);
         const __bf16 b0 = (__bf16)v;
         const float r1 = v - (float)b0;
         const __bf16 b1 = (__bf16)r1;
@@ -728,30 +753,53 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_mfma_kernel(int npix, int
         lm[r] = __builtin_bit_cast(unsigned short, b1);
         ll[r] = __builtin_bit_cast(unsigned short, (__bf16)(r1 - (float)b1));
       }
+      // image [16 pixels][8 octets x 48 B]: this lane's 4 channels at octet 2 t + (q >> 1), half q & 1
       typedef unsigned u2 __attribute__((ext_vector_type(2)));
-      unsigned short* o8 = out + (c0 >> 3) * 24 + (c0 & 4);
-      *reinterpret_cast<u2*>(o8) = u2{lh[0] | ((unsigned)lh[1] << 16), lh[2] | ((unsigned)lh[3] << 16)};
-      *reinterpret_cast<u2*>(o8 + 8) = u2{lm[0] | ((unsigned)lm[1] << 16), lm[2] | ((unsigned)lm[3] << 16)};
-      *reinterpret_cast<u2*>(o8 + 16) = u2{ll[0] | ((unsigned)ll[1] << 16), ll[2] | ((unsigned)ll[3] << 16)};
+      unsigned char* sp = stg + m * SROW + (2 * t + (q >> 1)) * 48 + (q & 1) * 8;
+      *reinterpret_cast<u2*>(sp) = u2{lh[0] | ((unsigned)lh[1] << 16), lh[2] | ((unsigned)lh[3] << 16)};
+      *reinterpret_cast<u2*>(sp + 16) = u2{lm[0] | ((unsigned)lm[1] << 16), lm[2] | ((unsigned)lm[3] << 16)};
+      *reinterpret_cast<u2*>(sp + 32) = u2{ll[0] | ((unsigned)ll[1] << 16), ll[2] | ((unsigned)ll[3] << 16)};
     }
+    // the unit's 16 x 384 B of this wave's channels leave as whole 16-B chunks (6 wave-instructions)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int cidx = lane + 64 * j, px = cidx / 24, w = cidx - px * 24;
+      const u2 lo = *reinterpret_cast<const u2*>(stg + px * SROW + w * 16);
+      const u2 hi = *reinterpret_cast<const u2*>(stg + px * SROW + w * 16 + 8);
+      const bool ok = un * 16 + px < npix && !(probe & 2);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, u4{lo[0], lo[1], hi[0], hi[1]}), ro,
+                                             ok ? (un * 16 + px) * 6 * Cin + wave * 384 + w * 16 : OOB, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-// the limb-engine form applies to the Langevin path's output layer: sign bits in, limbs out, Cin a multiple of 16
-bool smallc_k3_mfma_ok(const damc_layer_t& L) { return L.cin % 16 == 0 && L.cin <= 1024; }
+// the limb-engine form applies to the Langevin path's output layer: sign bits in, limbs out, Cin = 128 or 256
+bool smallc_k3_mfma_ok(const damc_layer_t& L) { return L.cin == 128 || L.cin == 256; }
 
 int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta, float mask_slope,
                                 unsigned short* h3, const unsigned char* hbits, hipStream_t s) {
   const int npix = B * L.hin * L.win;
   const int units = (npix + 15) / 16;
-  const size_t sm = (size_t)L.cin / 16 * 3 * 64 * 16;
-  const int grid = std::max(1, std::min((units + 3) / 4, 768));
-  if (L.cout == 3)
-    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<3>), dim3(grid), dim3(256), sm, s, npix, L.hin, L.win, L.cin,
-                       L.w_fwd, delta, mask_slope, h3, hbits);
-  else
-    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<1>), dim3(grid), dim3(256), sm, s, npix, L.hin, L.win, L.cin,
-                       L.w_fwd, delta, mask_slope, h3, hbits);
+  static const int gmax = [] {  // DAMC_SMALLC_DGRAD_GRID: A/B of the persistent grid size
+    const char* e = getenv("DAMC_SMALLC_DGRAD_GRID");
+    return e ? atoi(e) : 512;
+  }();
+  const int grid = std::max(1, std::min(units, gmax));
+  const int ng = L.cin / 64;
+#define SDM(NC_, NG_)                                                                                              \
+  hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin, L.win, \
+                     L.w_fwd, delta, mask_slope, h3, hbits)
+  if (L.cout == 3 && ng == 4) SDM(3, 4);
+  else if (L.cout == 3) SDM(3, 2);
+  else if (ng == 4) SDM(1, 4);
+  else SDM(1, 2);
+#undef SDM
   return (int)hipGetLastError();
 }
 
@@ -1047,7 +1095,8 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
     // the Langevin path (sign bits in, limbs out) on the limb engine; DAMC_SMALLC_DGRAD_MFMA=0 (read per call)
     // selects the VALU kernel below
     const char* mf = getenv("DAMC_SMALLC_DGRAD_MFMA");
-    if (h3 && hbits_in && smallc_k3_mfma_ok(L) && !(mf && mf[0] == '0'))
+    if (h3 && hbits_in && smallc_k3_mfma_ok(L) && (double)B * L.hin * L.win * 6 * L.cin < 2147483647.0 &&
+        !(mf && mf[0] == '0'))
       return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, h3, hbits_in, s);
     // 8 rows per block with the next mask nibbles prefetched: 66.4 us vs 69.9 (4 rows, no prefetch) at the
     // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us); fewer rows per block when the

@@ -44,6 +44,20 @@ static float* rnd(size_t n, unsigned seed) {
   return d;
 }
 
+// store-path probes: the dgrad's 201 MB limb output written with zeros, (0) one 16-B store per thread over the whole
+// buffer, (1) the MFMA kernel's persistent 16-pixel units (768 x 256 threads), 24 contiguous 16-B stores per lane
+__global__ void store_flat_probe(uint4* o, long n16) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) o[i] = uint4{0u, 0u, 0u, 0u};
+}
+__global__ __launch_bounds__(256) void store_unit_probe(unsigned char* o, int units, int rowb) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int un = blockIdx.x * 4 + wave; un < units; un += gridDim.x * 4) {
+    uint4* d = reinterpret_cast<uint4*>(o + (long)un * 16 * rowb);
+    for (int j = lane; j < 16 * rowb / 16; j += 64) d[j] = uint4{0u, 0u, 0u, 0u};
+  }
+}
+
 int main() {
   const int B = 128, C = 256, H = 32;
   const long npix = (long)B * H * H;
@@ -112,6 +126,19 @@ int main() {
     hipLaunchKernelGGL((smallc_dgrad_k3_kernel<3, U, PFv>), grid, dim3(256), sm, s, h, H, H, C, R, L.w_fwd, delta,
                        (int)DAMC_ACT_LRELU, 0.2f, h3, bits);
   };
+  timeit("store probe: flat 16-B stores", act * 1.5, [&] {
+    const long n16 = npix * C * 6 / 16;
+    hipLaunchKernelGGL(store_flat_probe, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(h3), n16);
+  });
+  timeit("store probe: 16-pixel units, 768 blocks", act * 1.5, [&] {
+    hipLaunchKernelGGL(store_unit_probe, dim3(768), dim3(256), 0, s, reinterpret_cast<unsigned char*>(h3),
+                       (int)(npix / 16), C * 6);
+  });
+  timeit("store probe: 16-pixel units, 2048 blocks", act * 1.5, [&] {
+    hipLaunchKernelGGL(store_unit_probe, dim3(2048), dim3(256), 0, s, reinterpret_cast<unsigned char*>(h3),
+                       (int)(npix / 16), C * 6);
+  });
   char nm[64];
   for (int R : {4, 8, 16}) {
     snprintf(nm, sizeof(nm), "k3 bits->limbs R=%d UNR=4", R);
@@ -150,6 +177,15 @@ int main() {
     timeit("k3 bits->limbs MFMA", act * 1.5 + act / 32, [&] {
       CK((hipError_t)launch_smallc_dgrad_k3_mfma(L, B, delta, 0.2f, h3b, bits, s));
     });
+    const int units = (int)(npix / 16);
+    for (int pg : {256, 512, 1024, 2048})
+      for (int pr : {0, 1, 2, 3}) {
+        snprintf(nm, sizeof(nm), "k3 MFMA grid %d probe %d", pg, pr);
+        timeit(nm, act * 1.5, [&] {
+          hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<3, 4>), dim3(std::min(units, pg)), dim3(256), 0, s,
+                             (int)npix, H, H, L.w_fwd, delta, 0.2f, h3b, bits, pr);
+        });
+      }
   }
   CK(hipGetLastError());
   return 0;
