@@ -949,6 +949,107 @@ __global__ __launch_bounds__(256) void smallc_proj_lds_kernel(const float* __res
     }
 }
 
+// The same projection on the limb engine (round 3): per 32-deep k step a lane loads its pixel's 8 channels (2 x 16 B)
+// and splits them into bf16 limbs; Wp's limb fragments for the 32 columns (2 tiles x 8 k steps x 3 limbs) are staged in
+// LDS once per workgroup.  A wave owns 32 pixels (two 16-row tiles) x 32 columns; six limb-product MFMAs per tile pair
+// and k step (fp32-accurate, gemm_x3_kernel's products; the sum order differs from the fp32-MFMA kernel's).  Cin = 256.
+__global__ __launch_bounds__(256) void smallc_proj_x3_kernel(const float* __restrict__ h, long npix,
+                                                             const float* __restrict__ wp, float* __restrict__ P) {
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  constexpr int Cin = 256, KS = Cin / 32;
+  __shared__ __attribute__((aligned(16))) bf16x8_t wfr[2][KS][3][64];  // [N tile][k step][limb][lane]: 48 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  // Wp (32 x Cin, row n = tap * NC + co) as B fragments: lane (col n = 16 t + m, k-group q) holds k = 8 q .. 8 q + 7
+  for (int u = tid; u < 2 * KS * 64; u += 256) {
+    const int t = u / (KS * 64), ks = (u / 64) % KS, l = u & 63;
+    // k permutation shared with the A loads below: fragment element e of k-group q is k = 4 q + e (e < 4) or
+    // 16 + 4 q + e - 4, so each of a lane's two 16-B activation loads is a quarter of one contiguous 64-B span
+    const float* src = wp + (long)(16 * t + (l & 15)) * Cin + 32 * ks + 4 * (l >> 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 16);
+    const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    bf16x8_t hb, mb, lb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const __bf16 b0 = (__bf16)v[e];
+      const float r1 = v[e] - (float)b0;
+      const __bf16 b1 = (__bf16)r1;
+      hb[e] = b0;
+      mb[e] = b1;
+      lb[e] = (__bf16)(r1 - (float)b1);
+    }
+    wfr[t][ks][0][l] = hb;
+    wfr[t][ks][1][l] = mb;
+    wfr[t][ks][2][l] = lb;
+  }
+  __syncthreads();
+  // persistent: the Wp fragments are staged once per workgroup, each wave then walks 32-pixel tasks
+  for (long p0 = ((long)blockIdx.x * 4 + wave) * 32; p0 < npix; p0 += (long)gridDim.x * 128) {
+  f32x4 acc[2][2];  // [pixel tile][column tile]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* hrow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) hrow[i] = h + min(p0 + 16 * i + m, npix - 1) * Cin + 4 * q;
+  // the pixels' channels two k steps ahead (4 x 16 B per lane and step in flight)
+  f32x4 ga[KS][2][2];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ga[ks][i][0] = *reinterpret_cast<const f32x4*>(hrow[i] + 32 * ks);
+      ga[ks][i][1] = *reinterpret_cast<const f32x4*>(hrow[i] + 32 * ks + 16);
+    }
+  };
+  gload(0);
+  gload(1);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8_t a[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float v[8] = {ga[ks][i][0][0], ga[ks][i][0][1], ga[ks][i][0][2], ga[ks][i][0][3],
+                          ga[ks][i][1][0], ga[ks][i][1][1], ga[ks][i][1][2], ga[ks][i][1][3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const __bf16 b0 = (__bf16)v[e];
+        const float r1 = v[e] - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        a[i][0][e] = b0;
+        a[i][1][e] = b1;
+        a[i][2][e] = (__bf16)(r1 - (float)b1);
+      }
+    }
+    if (ks + 2 < KS) gload(ks + 2);  // lands under this and the next step's MFMAs
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16x8_t b0 = wfr[j][ks][0][lane], b1 = wfr[j][ks][1][lane], b2 = wfr[j][ks][2][lane];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b1, c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b0, c, 0, 0, 0);
+      }
+    }
+  }
+  // C layout (16x16): col = lane & 15, rows 4 q + r
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long p = p0 + 16 * i + 4 * q + r;
+        if (p < npix) P[p * 32 + 16 * j + m] = acc[i][j][r];
+      }
+  }
+}
+
 // Stage 2: out[b,oy,ox,co] = bias + sum over the valid taps of P[input pixel][tap*NC + co], then tanh,
 // x_hat (NCHW) and the residual delta = (x_hat - x)/s^2 * (1 - x_hat^2) (NHWC).  One thread per output pixel.
 template <int NC, int K, int S>
@@ -1024,7 +1125,14 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   // DAMC_SMALLC_PROJ_LDS=0 (read per call) selects the direct-load kernel
   const char* pe = getenv("DAMC_SMALLC_PROJ_LDS");
   const bool lds = !(pe && atoi(pe) == 0) && L.cin % PJ_KC == 0;
-  if (lds && nt == 1)
+  // Cin = 256 (CIFAR's to-RGB layer): the limb-engine projection; DAMC_SMALLC_PROJ_X3=0 (read per call) keeps the
+  // fp32-MFMA kernels
+  const char* px3 = getenv("DAMC_SMALLC_PROJ_X3");
+  if (nt == 1 && L.cin == 256 && !(px3 && px3[0] == '0'))
+    // one workgroup per CU measured fastest (CIFAR B=128: 31.3 us at 256 workgroups, 35.9 at 768, 38.4 at 1024;
+    // the fp32-MFMA kernel 36.6; tools/smallc_bench.hip)
+    hipLaunchKernelGGL(smallc_proj_x3_kernel, dim3(std::min(g1, 256)), dim3(256), 0, s, h, npin, L.w_bwd, Pbuf);
+  else if (lds && nt == 1)
     hipLaunchKernelGGL((smallc_proj_lds_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
   else if (lds)
     hipLaunchKernelGGL((smallc_proj_lds_kernel<2>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);

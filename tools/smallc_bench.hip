@@ -107,6 +107,33 @@ int main() {
   timeit("fwd two-stage", act, [&] {
     smallc_fwd(L, h, B, x, 100.f, delta, nullptr, nullptr, pbuf, s);
   });
+  {  // the output projection: limb engine vs the LDS-staged fp32-MFMA kernel
+    float* pb2;
+    CK(hipMalloc(&pb2, npix * 32 * 4));
+    const int g1 = (int)((npix + 127) / 128);
+    hipLaunchKernelGGL((smallc_proj_lds_kernel<1>), dim3(g1), dim3(256), 0, s, h, npix, C, L.w_bwd, pbuf);
+    hipLaunchKernelGGL(smallc_proj_x3_kernel, dim3(768), dim3(256), 0, s, h, npix, L.w_bwd, pb2);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> p1(npix * 32), p2(npix * 32);
+    CK(hipMemcpy(p1.data(), pbuf, p1.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(p2.data(), pb2, p2.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0, md = 0;
+    for (size_t i = 0; i < p1.size(); ++i) {
+      mx = std::max(mx, (double)std::fabs(p1[i]));
+      md = std::max(md, (double)std::fabs(p1[i] - p2[i]));
+    }
+    printf("proj x3 vs fp32: max |diff| %.3e, max |value| %.3e (rel %.2e)\n", md, mx, md / mx);
+    timeit("proj fp32-MFMA (LDS)", act, [&] {
+      hipLaunchKernelGGL((smallc_proj_lds_kernel<1>), dim3(g1), dim3(256), 0, s, h, npix, C, L.w_bwd, pbuf);
+    });
+    for (int pg : {256, 512, 768, 1024}) {
+      char nm2[64];
+      snprintf(nm2, sizeof(nm2), "proj limb engine grid %d", pg);
+      timeit(nm2, act, [&] {
+        hipLaunchKernelGGL(smallc_proj_x3_kernel, dim3(pg), dim3(256), 0, s, h, npix, L.w_bwd, pb2);
+      });
+    }
+  }
   timeit("dgrad fp32 mask, fp32 out", 2 * act, [&] {
     smallc_dgrad(L, hcopy, B, delta, DAMC_ACT_LRELU, 0.2f, nullptr, nullptr, s);
   });
