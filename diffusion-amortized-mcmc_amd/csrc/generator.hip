@@ -1125,13 +1125,19 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   // DAMC_SMALLC_PROJ_LDS=0 (read per call) selects the direct-load kernel
   const char* pe = getenv("DAMC_SMALLC_PROJ_LDS");
   const bool lds = !(pe && atoi(pe) == 0) && L.cin % PJ_KC == 0;
-  // Cin = 256 (CIFAR's to-RGB layer): the limb-engine projection; DAMC_SMALLC_PROJ_X3=0 (read per call) keeps the
-  // fp32-MFMA kernels
+  // Cin = 256: the limb-engine projection, opt-in (DAMC_SMALLC_PROJ_X3=1, read per call).  Standalone it is 14 %
+  // faster (31.3 vs 36.6 us, tools/smallc_bench.hip), but in the bench line, where h3 was just written by the layer
+  // before, projection + gather took 60.6 us against 52.4 us for the LDS-staged fp32-MFMA kernel (same-box A/B,
+  // profiles/r03/ab_output_proj.txt), so that stays the default
   const char* px3 = getenv("DAMC_SMALLC_PROJ_X3");
-  if (nt == 1 && L.cin == 256 && !(px3 && px3[0] == '0'))
+  if (nt == 1 && L.cin == 256 && px3 && px3[0] == '1')
     // one workgroup per CU measured fastest (CIFAR B=128: 31.3 us at 256 workgroups, 35.9 at 768, 38.4 at 1024;
     // the fp32-MFMA kernel 36.6; tools/smallc_bench.hip)
-    hipLaunchKernelGGL(smallc_proj_x3_kernel, dim3(std::min(g1, 256)), dim3(256), 0, s, h, npin, L.w_bwd, Pbuf);
+    {
+      const char* pg = getenv("DAMC_SMALLC_PROJ_GRID");  // A/B of the persistent grid (read per call)
+      const int gm = pg ? std::max(1, atoi(pg)) : 256;
+      hipLaunchKernelGGL(smallc_proj_x3_kernel, dim3(std::min(g1, gm)), dim3(256), 0, s, h, npin, L.w_bwd, Pbuf);
+    }
   else if (lds && nt == 1)
     hipLaunchKernelGGL((smallc_proj_lds_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
   else if (lds)
