@@ -46,11 +46,25 @@ def _oracles(G, E):
             (orc.generator_layers(G, torch.float64), orc.ebm_params(E, torch.float64)))
 
 
-def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0):
+def _kink_rows(L64, z, rel=1e-6):
+    """Samples with a hidden pre-activation within rel x its layer's RMS of the LeakyReLU kink (fp64 forward at z):
+    their derivative (1 vs 0.2) is decided by rounding in any fp32 evaluation."""
+    from oracle import damc_oracle as orc
+
+    hs = orc.generator_forward(L64, z.double())
+    kink = np.zeros(z.shape[0], dtype=bool)
+    for h in hs[:-1]:
+        a = h.abs().reshape(h.shape[0], -1)
+        kink |= (a.min(dim=1).values < rel * h.pow(2).mean().sqrt()).numpy()
+    return kink
+
+
+def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0, kink=None):
     """Distance to fp64 against the fp32 reference arithmetic's.  per_row: per-sample relative errors, judged by
-    their median and 90th percentile: a sample with a hidden pre-activation within fp32 rounding of the LeakyReLU
-    kink can take the other derivative (1 vs 0.2) under any summation order (the SVHN B=64 batch's sample 54 has
-    a first-layer unit at 1.2e-8), an ill-conditioned row that is only bounded (max row error < 5e-2)."""
+    their median and 90th percentile, and every row that is not a kink sample by the largest fp32-reference row
+    error: a sample with a hidden pre-activation within fp32 rounding of the LeakyReLU kink can take the other
+    derivative (1 vs 0.2) under any summation order (the SVHN B=64 batch's sample 54 has a first-layer unit at
+    1.2e-8), an ill-conditioned row that is only bounded (< 5e-2)."""
     if not per_row:
         e_hip, e_32 = rel_l2(got, ref64), rel_l2(ref32, ref64)
         print("%s: |hip-fp64| %.2e  |fp32 reference arithmetic-fp64| %.2e" % (what, e_hip, e_32))
@@ -64,6 +78,10 @@ def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0):
     assert q(eh, .5) <= factor * q(e3, .5) + floor, what
     assert q(eh, .9) <= factor * q(e3, .9) + floor, what
     assert eh.max() < 5e-2, what
+    if kink is not None and (~kink).any():
+        print("%s: %d kink sample(s); the other rows' max |hip-fp64| %.2e vs the fp32 reference's %.2e"
+              % (what, int(kink.sum()), eh[~kink].max(), e3[~kink].max()))
+        assert eh[~kink].max() <= factor * e3[~kink].max() + floor, what
 
 
 @pytest.mark.parametrize("name,B,steps,noise,sigma", [
@@ -88,7 +106,7 @@ def test_full_width_posterior_vs_fp64(gpu_device, name, B, steps, noise, sigma):
     # one step: per sample (a kink sample is bounded, not compared); several steps: the whole batch, whose rel-L2
     # both implementations grow chaotically
     _check("%s B=%d %d step(s) z" % (name, B, steps), z.cpu().numpy(), r32, r64, 1e-7 if steps == 1 else 1e-6,
-           per_row=steps == 1)
+           per_row=steps == 1, kink=_kink_rows(L64, zc) if steps == 1 else None)
     if steps == 10:  # eval path: reconstruction MSE of the 10-step no-noise posterior (eval_gen_recon.py:184-194)
         mse = ((lv.generator_forward(z, G) - x) ** 2).mean(dim=(1, 2, 3)).cpu().numpy()
         m32 = ((orc.generator_sample(L32, torch.from_numpy(r32)) - xc) ** 2).mean(dim=(1, 2, 3)).numpy()
