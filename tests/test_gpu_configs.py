@@ -196,3 +196,24 @@ def test_celebaHQ_q_sweep_vs_fp64(gpu_device):
         z64, _ = orc.reverse_sweep(Qd, orc.encoder_forward(Qd.encoder, x.cpu().double()), zt0.double(), eps.double(),
                                    *args)
     _check("celebaHQ Q(x) 100-step sweep B=8", zt.cpu().numpy(), z32.numpy(), z64.numpy(), 1e-6)
+
+
+def test_celebaHQ_b64_posterior_step_equals_its_b8_shards(gpu_device):
+    """BASELINE config 5 on one GPU: the whole CelebA-HQ B=64 batch takes a full posterior step (with in-kernel noise)
+    in one call, and the result is bitwise the eight per-rank B=8 calls of the same chains (chain_base keys the noise
+    by global chain index; the B=8 step itself is checked against fp64 in test_full_width_posterior_vs_fp64, and an
+    fp64 oracle at B=64 full width would take the CPU tens of minutes).  The B=64 call runs the unsplit limb GEMMs,
+    the B=8 calls the split-K ones, so this also checks that the split reproduces the unsplit sums bit for bit at
+    K = 16384."""
+    from damc import langevin as lv
+
+    G, E, x, z0 = _case("celebaHQ", 64, gpu_device)
+    za = z0.clone()
+    lv.posterior_langevin(za, x, G, E, 1, 1.0, 0.1, True, seed=123)
+    assert torch.isfinite(za).all() and not torch.equal(za, z0)
+    parts = []
+    for r in range(8):
+        zb = z0[8 * r:8 * r + 8].clone()
+        lv.posterior_langevin(zb, x[8 * r:8 * r + 8].contiguous(), G, E, 1, 1.0, 0.1, True, seed=123, chain_base=8 * r)
+        parts.append(zb)
+    assert torch.equal(za, torch.cat(parts))
