@@ -73,6 +73,9 @@ struct GemmArgs {
   int ksplit = 1;
   float* kslab = nullptr;
   long kslab_floats = 0;
+  // split-K: sign blocks per workgroup (each block's sum still goes to its own slab; ksplit / kbpw workgroups along
+  // K), so a small batch fills the chip without paying a prologue and epilogue per 256 k
+  int kbpw = 1;
 };
 // slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
 long x3_ksplit_floats(int M, int N, int K, int zdim);

@@ -890,9 +890,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 
   int pad_y = p.pad_y, pad_x = p.pad_x, py = 0, px = 0;
   const unsigned short* Bg = p.B3;
-  // split-K (O_PHASE / O_DENSE): z = phase * ksplit + slice
+  // split-K (O_PHASE / O_DENSE): z = phase * (ksplit / kbpw) + workgroup slice of kbpw sign blocks
   const bool KSPLIT = OM != O_WGRAD && p.ksplit > 1;
-  const int zph = KSPLIT ? z / p.ksplit : z, zsl = KSPLIT ? z - zph * p.ksplit : 0;
+  const int nslz = KSPLIT ? p.ksplit / p.kbpw : 1;
+  const int zph = KSPLIT ? z / nslz : z, zsl = KSPLIT ? z - zph * nslz : 0;
   if (OM == O_PHASE) {
     py = zph >> 1;
     px = zph & 1;
@@ -1562,7 +1563,24 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       if constexpr (CMAJ) advance_cmaj();
       // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
       // (a flush between them and the barrier measured 6-8 % slower)
-      if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
+      if (M16 && KSPLIT && p.kbpw > 1 && ((kt + 1) & (FLUSH - 1)) == 0 && kt + 1 < nk) {
+        // a split-K workgroup's earlier sign blocks: each block's signed sum straight from the accumulators into its
+        // own slab (the last block leaves through the LDS epilogue below), so the reduce sees one sum per block
+        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        float* sl = p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw + kt / FLUSH) * p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+              if (m < p.M && n < p.N) sl[(long)m * p.N + n] = sg * acc16[i][j][r];
+            }
+            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      } else if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
         const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
         if (M16) {
 #pragma unroll
@@ -1645,8 +1663,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
               acc[i][j][r];
   }
   __syncthreads();
-  if (KSPLIT) {  // this slice's raw fp32 tile into the slab; x3_ksplit_reduce_kernel applies the epilogue
-    float* sl = p.kslab + (long)z * p.M * p.N;
+  if (KSPLIT) {  // this slice's last block's fp32 tile into its slab; x3_ksplit_reduce_kernel applies the epilogue
+    float* sl = p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw + p.kbpw - 1) * p.M * p.N;
 #pragma unroll 2
     for (int it = 0; it < BM * BN / 8 / 512; ++it) {
       const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
@@ -1806,8 +1824,21 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
       a.ksplit = ks;
-      a.k_per_z = a.K / ks;
-      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks), dim3(512), 0, s, a);
+      // sign blocks per workgroup: the most (a power of two dividing ks) that still leaves >= 256 workgroups, so one
+      // round covers the chip (the default 16x16-tile path only); DAMC_X3_KSPLIT_BPW (read per call) pins it
+      int bpw = 1;
+      if (V == DAMC_X3_VARIANT && (V & 1) && !(V & (2048 | 65536 | 131072 | 262144))) {
+        const char* eb = getenv("DAMC_X3_KSPLIT_BPW");
+        if (eb) {
+          bpw = std::max(1, atoi(eb));
+          while (bpw > 1 && ks % bpw) bpw >>= 1;
+        } else {
+          while (ks % (2 * bpw) == 0 && (long)ntm * ntn * zdim * ks / (2 * bpw) >= 256) bpw *= 2;
+        }
+      }
+      a.kbpw = bpw;
+      a.k_per_z = a.K / ks * bpw;
+      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
       const long tot = (long)zdim * a.M * (a.N / 8);
       hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, OM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
                          zdim);
@@ -1815,6 +1846,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     }
   }
   a.ksplit = 1;
+  a.kbpw = 1;
   if ((V & 16) && OM != O_WGRAD)  // supertile raster: phases folded into a 1-D grid
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
   else
@@ -1976,10 +2008,20 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // at most 128 rows (the first layer, M = B <= 128): the 128 x 256 block layout, no half-empty 256-row tile
     // (bitwise the default layout: every output takes the same MFMA sequence; 46.6 -> 35.7 us for CIFAR's B = 128
     // first layer, tools/gemm_bench.hip).  DAMC_X3_WIDE=0 (read per call) keeps the default layout
+    const char* ew = getenv("DAMC_X3_WIDE");
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128) {
-      const char* ew = getenv("DAMC_X3_WIDE");
       if (!(ew && ew[0] == '0')) {
         launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        continue;
+      }
+    }
+    if (ew && ew[0] == '2') {  // A/B only: every limb GEMM on the 128 x 256 layout (bitwise the default)
+      if (epi == EPI_BIAS_ACT && om == O_PHASE) {
+        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        continue;
+      }
+      if (epi == EPI_MASK && om == O_DENSE) {
+        launch_x3_t<EPI_MASK, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
         continue;
       }
     }
