@@ -76,6 +76,9 @@ struct GemmArgs {
   // split-K: sign blocks per workgroup (each block's sum still goes to its own slab; ksplit / kbpw workgroups along
   // K), so a small batch fills the chip without paying a prologue and epilogue per 256 k
   int kbpw = 1;
+  // split-K slab layout: 0 row-major [M][N] per block; 1 the 256 x 128 kernel's register layout, per block
+  // [tile][wave][4 x 4 tiles][64 lanes] f32x4 (16-B stores straight from the accumulators; the reduce maps back)
+  int kslab_reg = 0;
 };
 // slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
 long x3_ksplit_floats(int M, int N, int K, int zdim);

@@ -892,6 +892,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const unsigned short* Bg = p.B3;
   // split-K (O_PHASE / O_DENSE): z = phase * (ksplit / kbpw) + workgroup slice of kbpw sign blocks
   const bool KSPLIT = OM != O_WGRAD && p.ksplit > 1;
+  // split-K into register-layout slabs (GemmArgs::kslab_reg; launched only split, 256 x 128 16x16-tile path): a
+  // compile-time variant, so the block-total registers of the unsplit kernel drop out
+  constexpr bool KREG = (V & 1048576) != 0;
+  static_assert(!KREG || (M16 && !(V & (32 | 2048 | 65536 | 131072 | 262144 | 524288))), "KREG: default tiles only");
   const int nslz = KSPLIT ? p.ksplit / p.kbpw : 1;
   const int zph = KSPLIT ? z / nslz : z, zsl = KSPLIT ? z - zph * nslz : 0;
   if (OM == O_PHASE) {
@@ -1563,21 +1567,25 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       if constexpr (CMAJ) advance_cmaj();
       // block flush after the barrier: the compiler keeps hoisting the barrier above the tile's trailing MFMAs
       // (a flush between them and the barrier measured 6-8 % slower)
-      if (M16 && KSPLIT && p.kbpw > 1 && ((kt + 1) & (FLUSH - 1)) == 0 && kt + 1 < nk) {
-        // a split-K workgroup's earlier sign blocks: each block's signed sum straight from the accumulators into its
-        // own slab (the last block leaves through the LDS epilogue below), so the reduce sees one sum per block
+      if (KREG) {
+        if (((kt + 1) & (FLUSH - 1)) != 0) continue;
+        // split-K: every sign block's signed sum straight from the accumulators into its own slab, in the register
+        // layout (one 16-B store per lane and tile: 1 KB per wave-instruction); x3_ksplit_reduce_kernel maps back
+        // buffer stores: one VGPR of offset (wave, lane), the rest scalar, so the 256 accumulator VGPRs do not spill
         const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
-        float* sl = p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw + kt / FLUSH) * p.M * p.N;
+        const int ntile = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+        const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw) * ntile * (BM * BN)), (short)0,
+            p.kbpw * ntile * (BM * BN) * 4, 0x00020000);
+        const int soff = ((kt / FLUSH) * ntile + tm * ntn + tn) * (BM * BN * 4);
+        const int voff = (wave * 1024 + lane) * 16;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-              if (m < p.M && n < p.N) sl[(long)m * p.N + n] = sg * acc16[i][j][r];
-            }
+            acc16[i][j] *= sg;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl, voff,
+                                                   soff + (i * 4 + j) * 1024, 0);
             acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
       } else if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
@@ -1618,6 +1626,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     kloop(std::false_type{});
 
   }
+  if (KREG) return;  // every block already in its slab
   // the last partial block
   {
     const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
@@ -1663,8 +1672,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
               acc[i][j][r];
   }
   __syncthreads();
-  if (KSPLIT) {  // this slice's last block's fp32 tile into its slab; x3_ksplit_reduce_kernel applies the epilogue
-    float* sl = p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw + p.kbpw - 1) * p.M * p.N;
+  if (KSPLIT) {  // row-major slabs (one block per workgroup): the fp32 tile into its slab; the reduce applies the epilogue
+    float* sl = p.kslab + ((long)zph * p.ksplit + zsl) * p.M * p.N;
 #pragma unroll 2
     for (int it = 0; it < BM * BN / 8 / 512; ++it) {
       const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
@@ -1735,9 +1744,47 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 
 // the split-K reduce: one thread per (phase, row, channel octet); the slices in fixed order, then the limb GEMM's
 // epilogue (bias + act or the LReLU' mask, sign bits, fp32 and limb outputs) on the sum
+// the epilogue of one output octet (8 consecutive channels n .. n + 7 of GEMM row m) from its fp32 sums
+template <int EPI, int OM>
+__device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int n, int py, int px, float (&v)[8]);
+
+// register slab layout (GemmArgs::kslab_reg): one thread per (phase, tile, wave, 16x16 tile, lane quarter, half) =
+// 4 rows x 8 channels; the 8 channels are 8 consecutive lanes' f32x4, read as 128 contiguous bytes per block
+template <int EPI, int OM>
+__device__ __forceinline__ void x3_ksplit_reduce_reg(const GemmArgs& p, int zdim, long i) {
+  const int ntm = (p.M + X3_BM - 1) / X3_BM, ntn = (p.N + X3_BN - 1) / X3_BN;
+  const long ntile = (long)ntm * ntn;
+  if (i >= (long)zdim * ntile * 1024) return;
+  const int half = (int)(i & 1), q = (int)((i >> 1) & 3), ij = (int)((i >> 3) & 15), wave = (int)((i >> 7) & 7);
+  const long tl = i >> 10;
+  const int tile = (int)(tl % ntile), ph = (int)(tl / ntile);
+  const int tm = tile / ntn, tn = tile - tm * ntn, wm = wave >> 1, wn = wave & 1, ti = ij >> 2, tj = ij & 3;
+  const int mb = tm * X3_BM + wm * 64 + ti * 16 + 4 * q, n = tn * X3_BN + wn * 64 + tj * 16 + 8 * half;
+  if (n >= p.N) return;
+  float v[4][8] = {};
+  const f32x4* base = reinterpret_cast<const f32x4*>(p.kslab) + (((long)tile * 8 + wave) * 16 + ij) * 64 + 16 * q + 8 * half;
+  for (int sl = 0; sl < p.ksplit; ++sl) {  // the blocks in order from 0, the sign already applied
+    const f32x4* src = base + (long)(ph * p.ksplit + sl) * ntile * (X3_BM * X3_BN / 4);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const f32x4 t = src[c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r][c] += t[r];
+    }
+  }
+  const int py = OM == O_PHASE ? ph >> 1 : 0, px = OM == O_PHASE ? ph & 1 : 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (mb + r < p.M) x3_octet_epilogue<EPI, OM>(p, mb + r, n, py, px, v[r]);
+}
+
 template <int EPI, int OM>
 __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p.kslab_reg) {
+    x3_ksplit_reduce_reg<EPI, OM>(p, zdim, i);
+    return;
+  }
   const int noct = p.N / 8;
   if (i >= (long)zdim * p.M * noct) return;
   const int oct = (int)(i % noct);
@@ -1754,6 +1801,11 @@ __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
     v[0] += t0.x; v[1] += t0.y; v[2] += t0.z; v[3] += t0.w;
     v[4] += t1.x; v[5] += t1.y; v[6] += t1.z; v[7] += t1.w;
   }
+  x3_octet_epilogue<EPI, OM>(p, m, n, py, px, v);
+}
+
+template <int EPI, int OM>
+__device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int n, int py, int px, float (&v)[8]) {
   const long idx = gemm_row_offset<OM>(p, m, py, px) + n;
   if (EPI == EPI_BIAS_ACT) {
     if (p.bias) {
@@ -1812,7 +1864,9 @@ int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn) {
 
 long x3_ksplit_floats(int M, int N, int K, int zdim) {  // either block layout (gemm_x3_kernel, V & 524288)
   const int ks = std::max(x3_ksplit(M, N, K, zdim, X3_BM, X3_BN), x3_ksplit(M, N, K, zdim, 128, 256));
-  return ks > 1 ? (long)zdim * ks * M * N : 0;
+  // the register slab layout covers whole 256 x 128 tiles
+  const long padded = (long)((M + X3_BM - 1) / X3_BM) * X3_BM * ((N + X3_BN - 1) / X3_BN) * X3_BN;
+  return ks > 1 ? (long)zdim * ks * std::max((long)M * N, padded) : 0;
 }
 
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
@@ -1836,10 +1890,28 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
           while (ks % (2 * bpw) == 0 && (long)ntm * ntn * zdim * ks / (2 * bpw) >= 256) bpw *= 2;
         }
       }
+      // the register slab layout on the default 16x16-tile path (256 x 128 tiles), row-major slabs (one block per
+      // workgroup) otherwise; DAMC_X3_KSLAB_REG=0, read per call, forces row-major
+      const char* er = getenv("DAMC_X3_KSLAB_REG");
+      a.kslab_reg = (!(er && er[0] == '0') && BM == X3_BM && BN == X3_BN && (V & 1) && (V & 4) &&
+                     !(V & (32 | 2048 | 65536 | 131072 | 262144)) && (long)zdim * ks * ntm * ntn * BM * BN <= a.kslab_floats &&
+                     (long)bpw * ntm * ntn * BM * BN * 4 < (1L << 31))
+                        ? 1 : 0;
+      if (!a.kslab_reg) bpw = 1;
       a.kbpw = bpw;
       a.k_per_z = a.K / ks * bpw;
-      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
-      const long tot = (long)zdim * a.M * (a.N / 8);
+      if constexpr (V == DAMC_X3_VARIANT && OM != O_WGRAD && (V & 1) && (V & 4) &&
+                    !(V & (32 | 2048 | 65536 | 131072 | 262144 | 524288))) {
+        if (a.kslab_reg)
+          hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | 1048576>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0,
+                             s, a);
+        else
+          hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
+      } else {
+        a.kslab_reg = 0;
+        hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
+      }
+      const long tot = a.kslab_reg ? (long)zdim * ntm * ntn * 1024 : (long)zdim * a.M * (a.N / 8);
       hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, OM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
                          zdim);
       return;
@@ -1847,6 +1919,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   }
   a.ksplit = 1;
   a.kbpw = 1;
+  a.kslab_reg = 0;
   if ((V & 16) && OM != O_WGRAD)  // supertile raster: phases folded into a 1-D grid
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
   else
