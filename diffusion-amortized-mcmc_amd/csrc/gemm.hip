@@ -1845,7 +1845,7 @@ __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int 
   }
 }
 
-// split-K plan of a limb-engine conv: an under-filled grid (< DAMC_X3_KSPLIT_WGS, default 128 workgroups) splits K
+// split-K plan of a limb-engine conv: an under-filled grid (see below; DAMC_X3_KSPLIT_WGS pins the bound) splits K
 // into its X3_NEGK sign blocks, one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
 // the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
 // unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
@@ -1855,11 +1855,15 @@ int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn) {
   const bool on = !(ev && ev[0] == '0');
   static const long below = [] {
     const char* e = getenv("DAMC_X3_KSPLIT_WGS");
-    return e ? atol(e) : 128L;
+    return e ? atol(e) : -1L;
   }();
   const long wgs = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * zdim;
-  if (!on || wgs >= below || K % X3_NEGK != 0 || K / X3_NEGK < 2) return 1;
-  return K / X3_NEGK;
+  if (!on || K % X3_NEGK != 0 || K / X3_NEGK < 2) return 1;
+  const int ks = K / X3_NEGK;
+  // default: below 128 workgroups always; below 256 (half the chip idle) when K has at most 16 sign blocks, since
+  // the slab bytes grow with K (CIFAR B=16/32 per-rank steps -2.6 / -1.5 %, B=64's K=8192 dgrad stays unsplit)
+  const bool split = below >= 0 ? wgs < below : (wgs < 128 || (wgs < 256 && ks <= 16));
+  return split ? ks : 1;
 }
 
 long x3_ksplit_floats(int M, int N, int K, int zdim) {  // either block layout (gemm_x3_kernel, V & 524288)
