@@ -2038,9 +2038,47 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
   o[2] = l;
 }
 
+// the same packing, one thread per (co, input-channel octet): its 8 channels' k*k taps are 8 * k * k contiguous
+// floats of the PyTorch layout, read 4 taps at a time as f32x4 (k * k % 4 == 0); adjacent threads write adjacent
+// 48-B limb octets of each tap (the thread-per-output-octet kernel above reads 4 B at a 64-B stride, every line 16x)
+__global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, int cin, int k,
+                                         unsigned short* __restrict__ y) {
+  const int cin8 = cin / 8, taps = k * k, K8 = taps * cin8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)cout * cin8) return;
+  const int co = (int)(i / cin8), c8 = (int)(i - (long)co * cin8);
+  const f32x4* src = reinterpret_cast<const f32x4*>(w + ((long)co * cin + c8 * 8) * taps);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * ((long)co * K8 + c8);
+  for (int t0 = 0; t0 < taps; t0 += 4) {
+    f32x4 q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = src[(e * taps + t0) / 4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kk = (t0 + t) * cin + c8 * 8;
+      const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = sg * q[e][t];
+      bf16x8 h, m, l;
+      split3_octet(v, h, m, l);
+      bf16x8* d = o + 3L * (t0 + t) * cin8;
+      d[0] = h;
+      d[1] = m;
+      d[2] = l;
+    }
+  }
+}
+
 int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s) {
   if ((DAMC_X3_VARIANT & 8) != 0) return DAMC_ERR_UNSUPPORTED;  // the channel-major walk needs the slice-major order
   if (cout <= 0 || cin % 8 != 0 || k <= 0 || (uintptr_t)y % 16 != 0) return DAMC_ERR_ARG;
+  if ((k * k) % 4 == 0 && (uintptr_t)w % 16 == 0) {
+    const long nt = (long)cout * (cin / 8);
+    hipLaunchKernelGGL(pack_conv_x3_taps_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, cout, cin, k,
+                       y);
+    return (int)hipGetLastError();
+  }
   const long n = (long)cout * k * k * cin / 8;
   hipLaunchKernelGGL(pack_conv_x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, cout, cin, k, y);
   return (int)hipGetLastError();

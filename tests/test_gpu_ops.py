@@ -150,3 +150,33 @@ def test_z_update_hook_vs_oracle(gpu_device):
     lv.z_update(z, g.to(gpu_device), s, True, seed=11, step_index=4, chain_base=100)
     xi_k = lv.philox_normal(1, 37, 128, seed=11, device=gpu_device, step_offset=4, chain_base=100)[0].cpu()
     assert torch.equal(z.cpu(), (z0 - torch.tensor(c1) * (g + z0)) + torch.tensor(np.float32(s)) * xi_k)
+
+
+@pytest.mark.parametrize("cout,cin,k", [(16, 64, 4), (24, 32, 4), (40, 512, 4), (8, 32, 3), (16, 64, 1), (8, 32, 5)])
+def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
+    """damc_pack_conv2d_x3 (the encoder's per-call weight operand, Encoder_* convs, diffusion_net.py:227-372):
+    PyTorch (cout, cin, k, k) -> K-major [co][(ky, kx, ci)] with the odd 256-k blocks negated, as three RNE bf16
+    limbs h = bf16(v), m = bf16(v - h), l = bf16(v - h - m) per 8-value octet; bit-exact against the same split in
+    torch (k * k % 4 == 0 takes the tap-vectorised kernel, the rest the per-octet one)."""
+    from damc import _lib
+    from damc._lib import ptr
+
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(cout * 7 + cin + k)
+    w = torch.randn(cout, cin, k, k, generator=g) * torch.exp(torch.randn(cout, cin, k, k, generator=g) * 3)
+    nb = int(L.damc_conv2d_x3_bytes(cout, cin, k))
+    assert nb == cout * k * k * cin * 6
+    out = torch.zeros(nb // 2, dtype=torch.int16, device=gpu_device)
+    wd = w.to(gpu_device)
+    _lib.check(L.damc_pack_conv2d_x3(ptr(wd), cout, cin, k, ptr(out), _lib.stream_ptr(gpu_device)), "pack x3")
+    torch.cuda.synchronize()
+    K = k * k * cin
+    v = w.permute(0, 2, 3, 1).reshape(cout, K)
+    sg = torch.where((torch.arange(K) // 256) % 2 == 1, -1.0, 1.0)
+    v = v * sg
+    h = v.to(torch.bfloat16)
+    r1 = v - h.float()
+    m = r1.to(torch.bfloat16)
+    lo = (r1 - m.float()).to(torch.bfloat16)
+    want = torch.stack([t.view(torch.int16).reshape(cout, K // 8, 8) for t in (h, m, lo)], dim=2).reshape(-1)
+    assert torch.equal(out.cpu(), want)
