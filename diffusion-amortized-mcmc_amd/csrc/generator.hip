@@ -415,15 +415,18 @@ __global__ __launch_bounds__(256) void smallc_fwd_s2_kernel(const float* __restr
   }
 }
 
-template <int NC, int K, int S, int CH>
+// UNI (Cin == 64 CH: one pixel per wave): the pixel index is made wave-uniform, so the K*K*NC delta gathers of a
+// pixel become scalar loads (s_load, scalar cache) instead of 64-lane vector loads of one address each
+template <int NC, int K, int S, int CH, bool UNI = false>
 __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, int Hin, int Win, int Cin, int pad,
                                                                int Hout, int Wout, const float* __restrict__ wpk,
                                                                const float* __restrict__ delta, int mask_act,
                                                                float mask_slope, unsigned short* __restrict__ h3) {
   typedef typename VecT<CH>::T V;
-  const int G = Cin / CH, P = 64 / G;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane % G, sub = lane / G;
+  const int G = UNI ? 64 : Cin / CH, P = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int wave = UNI ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (int)(threadIdx.x >> 6);
+  const int g = UNI ? lane : lane % G, sub = UNI ? 0 : lane / G;
   const int ci0 = g * CH;
   float w[K * K][CH][NC];
 #pragma unroll
@@ -812,6 +815,12 @@ bool smallc_reg_ok(const damc_layer_t& L) {
   return G <= 64 && (64 % G) == 0;
 }
 
+// DAMC_SMALLC_UNI=1 (read per call): the k4 s2 dgrad at Cin 128 with wave-uniform pixels (opt-in until measured)
+inline bool uni_dgrad() {
+  const char* e = getenv("DAMC_SMALLC_UNI");
+  return e && e[0] == '1';
+}
+
 // dispatch of a register-resident instantiation (caller checked smallc_reg_ok)
 template <int NC>
 bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, float* h_out, int B, const float* x,
@@ -835,6 +844,9 @@ bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, flo
   } else {
     if (L.k == 3)
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 3, 1, 4>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
+                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
+    else if (G == 64 && uni_dgrad())
+      hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2, true>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
                          L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
     else
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
