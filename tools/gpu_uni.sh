@@ -1,7 +1,7 @@
 # k4 s2 output-layer dgrad with wave-uniform pixels (scalar delta loads): parity, then A/B (DAMC_SMALLC_UNI)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_langevin.py tests/test_gpu_ops.py tests/test_gpu_training.py -x -v --timeout 250 --timeout-method thread > gpurun_out/uni_tests.log 2>&1
+DAMC_SMALLC_UNI=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_langevin.py tests/test_gpu_ops.py tests/test_gpu_training.py -x -v --timeout 250 --timeout-method thread > gpurun_out/uni_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/uni_tests.log; [ $rc -eq 0 ] || exit $rc
 for u in 0 1 0 1; do
   export DAMC_SMALLC_UNI=$u
