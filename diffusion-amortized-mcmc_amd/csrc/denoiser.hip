@@ -424,6 +424,10 @@ __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need
 // do not tear), so the producer publishes its flag right behind its stores without draining them (one memory round
 // trip less per stage), and a consumer that has seen the flag re-reads (sc1) any load group that still holds a
 // sentinel.  The flag stays the cheap "probably ready" signal; the data itself proves readiness.
+// The caller data that enters the ring unchanged is z; the setup kernel stores its NaNs canonical.  The other ring
+// values are computed, and a VALU op may carry a (quieted) input NaN's payload through, so a weight or xemb holding
+// exactly the TS_SENT pattern could still reach the ring.  Then the consumers' bounded wait expires (20 ms),
+// team_finish_kernel recomputes the sweep bitwise and the process stays on the launch chain: slow, never wrong.
 constexpr unsigned TS_SENT = 0x7FC0DEADu;
 // a re-read loop gives up past the budget (setting the error word) or once another workgroup has failed
 __device__ __forceinline__ bool ts_giveup(uint64_t t0, unsigned it, int* err, long budget) {
@@ -1208,12 +1212,17 @@ __global__ void sweep_setup_kernel(SweepCall c, SweepCall* dst, const float* zt,
                                    long nzero, f32x4* s1, long ns1, f32x4* s2, long ns2) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *dst = c;
-  if (i < n) zw[i] = zt[i];
-  if (i < nzero) zero[i] = 0u;
-  // sentinel hand-offs: every ring slot of the sweep (grid-stride over the two ranges, 16 B per store)
+  // every range is grid-stride: the grid is capped (sweep_setup_grid), so B*nz may exceed the thread count
+  const long st = (long)gridDim.x * blockDim.x;
+  // a caller's NaN is stored canonical, so a NaN payload can never be the hand-off sentinel (TS_SENT) in the ring
+  for (long j = i; j < n; j += st) {
+    const float v = zt[j];
+    zw[j] = (v != v) ? __builtin_bit_cast(float, 0x7FC00000u) : v;
+  }
+  for (long j = i; j < nzero; j += st) zero[j] = 0u;
+  // sentinel hand-offs: every ring slot of the sweep (16 B per store)
   const float sv = __builtin_bit_cast(float, 0x7FC0DEADu);
   const f32x4 s4 = {sv, sv, sv, sv};
-  const long st = (long)gridDim.x * blockDim.x;
   for (long j = i; j < ns1; j += st) s1[j] = s4;
   for (long j = i; j < ns2; j += st) s2[j] = s4;
 }

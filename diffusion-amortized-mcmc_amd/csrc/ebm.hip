@@ -788,6 +788,16 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
 
 extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* stream);
 
+// the chain count from which engine 0 picks the MFMA engine: DAMC_EBM_MFMA_MIN_B read once per process (default
+// 2048); damc.langevin reads it through this entry point, so Python and the library never disagree
+extern "C" int damc_ebm_mfma_min_chains(void) {
+  static const int v = [] {
+    const char* e = getenv("DAMC_EBM_MFMA_MIN_B");
+    return e ? atoi(e) : 2048;
+  }();
+  return v;
+}
+
 // engine: 0 = by batch size (MFMA from DAMC_EBM_MFMA_MIN_B chains up), 1 = register-resident VALU, 2 = MFMA
 static int prior_langevin_impl(const damc_ebm_t* e, float* z, int B, int n_steps, double step, int with_noise,
                                const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
@@ -798,10 +808,7 @@ static int prior_langevin_impl(const damc_ebm_t* e, float* z, int B, int n_steps
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 2 * (size_t)n_steps, s));
   if (n_steps == 0) return 0;
   const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
-  static const int mfma_min_b = [] {
-    const char* v = getenv("DAMC_EBM_MFMA_MIN_B");
-    return v ? atoi(v) : 2048;
-  }();
+  const int mfma_min_b = damc_ebm_mfma_min_chains();
   if (engine == 2 && !ebm_mfma_ok(e->nz, e->nh)) return DAMC_ERR_UNSUPPORTED;
   if (ebm_mfma_ok(e->nz, e->nh) && (engine == 2 || (engine == 0 && B >= mfma_min_b))) {
     EbArgs a{};

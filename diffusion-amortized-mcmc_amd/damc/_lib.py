@@ -139,6 +139,7 @@ _SIGS = {
                                           _P, _P, _SZ, _P]),
     "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _P]),
     "damc_prior_langevin_engine": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _I, _P]),
+    "damc_ebm_mfma_min_chains": (_I, []),
     "damc_ebm_energy_grad": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P]),
     "damc_z_update": (_I, [_P, _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P]),
     "damc_philox_normal": (_I, [_P, _I, _I, _I, _U64, _U64, _U64, ctypes.c_uint32, _P]),

@@ -118,16 +118,16 @@ class EncoderPlan:
         k, cout, cin = conv.kernel_size[0], conv.out_channels, conv.in_channels
         w = _dev(conv.weight, dev)
         nb = int(L.damc_conv2d_x3_bytes(cout, cin, k)) if _lib.current_engine() == _lib.ENGINE_LIMB else 0
-        key = (str(dev), nb)
-        hit = self._wcache.get(i)
-        if hit is None or hit[0] != key:
-            buf = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else \
-                torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
-            hit = self._wcache[i] = (key, buf)
-        buf = hit[1]
+        # one buffer per (layer, thread, stream), like the workspace: a call on another stream or thread may still
+        # be reading this one's packed weights
+        cache = self._wcache.get(i)
+        if cache is None:
+            cache = self._wcache[i] = _lib.WorkspaceCache()
+        buf = cache.get(dev, nb if nb else 4 * k * k * cin * cout, ("encw", i, nb))
         if nb:
             check(L.damc_pack_conv2d_x3(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d x3")
             return None, buf, w
+        buf = buf[:4 * k * k * cin * cout].view(torch.float32)
         check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d")
         return buf, None, w
 

@@ -92,10 +92,9 @@ PRIOR_ENGINES = {"auto": 0, "valu": 1, "mfma": 2}
 
 
 def mfma_min_chains():
-    """Chain count from which "auto" picks the MFMA prior engine (the library reads the same variable)."""
-    import os
-
-    return int(os.environ.get("DAMC_EBM_MFMA_MIN_B", "2048"))
+    """Chain count from which "auto" picks the MFMA prior engine: the library's own threshold
+    (DAMC_EBM_MFMA_MIN_B read once per process), so Python and a C caller of engine 0 always agree."""
+    return int(_lib.lib().damc_ebm_mfma_min_chains())
 
 
 def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, step_offset=0, chain_base=0,

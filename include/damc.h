@@ -163,7 +163,12 @@ int damc_prior_langevin(const damc_ebm_t* ebm, float* z, int batch, int n_steps,
                         float* diag, void* stream);
 /* the same with the engine chosen per call: 0 = by batch size (the default above: the 16-chain MFMA tile kernel
  * from DAMC_EBM_MFMA_MIN_B = 2048 chains up, where the FC layers are real GEMMs), 1 = register-resident VALU
- * (one chain per workgroup), 2 = MFMA (nz % 16 == 0, nz and nh <= 256, else DAMC_ERR_UNSUPPORTED) */
+ * (one chain per workgroup), 2 = MFMA (nz % 16 == 0, nz and nh <= 256, else DAMC_ERR_UNSUPPORTED).
+ * Engine 0 is keyed on THIS call's batch.  The two engines sum in different orders, so a sharded caller that needs
+ * its shards' union bitwise equal to the unsharded block resolves the engine itself from the global chain count
+ * (>= damc_ebm_mfma_min_chains() -> 2, else 1) and passes 1 or 2, as damc.langevin does. */
+/* the threshold engine 0 uses: DAMC_EBM_MFMA_MIN_B, read once per process (default 2048) */
+int damc_ebm_mfma_min_chains(void);
 int damc_prior_langevin_engine(const damc_ebm_t* ebm, float* z, int batch, int n_steps, double step, int with_noise,
                                const float* noise, uint64_t seed, uint64_t step_offset, uint64_t chain_base,
                                float* diag, int engine, void* stream);

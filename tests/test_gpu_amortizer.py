@@ -146,10 +146,11 @@ def _wide_q(gpu_device, n_interval):
     return Q.to(gpu_device).eval()
 
 
-@pytest.mark.parametrize("B", [1, 37, 128, 300])
+@pytest.mark.parametrize("B", [1, 37, 128, 300, 600])
 def test_team_sweep_matches_launch_chain(am, gpu_device, monkeypatch, B):
     """The one-launch team sweep (default) against the per-block launch chain (DAMC_SWEEP_TEAM=0) at full CIFAR
-    width: B=300 gives teams 2-3 row tiles, B=37 a ragged last tile, B=1 one active team.  The two differ only in
+    width: B=300 gives teams 2-3 row tiles, B=37 a ragged last tile, B=1 one active team, B=600 puts B*nz past
+    the setup kernel's capped thread count (z rows past thread 65536 must still be copied).  The two differ only in
     the order of the K sum of the skip blocks, so eps of step 1 agrees to rel-L2 1e-6 and of step 2 to 1e-5; a
     10-step sweep amplifies fp32 rounding far beyond that, so the end point is judged
     against the fp64 oracle on the same injected noise: the team's distance within 3x the chain's (+1e-6)."""
@@ -181,6 +182,10 @@ def test_team_sweep_matches_launch_chain(am, gpu_device, monkeypatch, B):
     assert rel_l2(eps_t[0], eps_c[0]) <= 1e-6
     assert rel_l2(eps_t[1], eps_c[1]) <= 1e-5
     assert e_t <= 3 * e_c + 1e-6
+    tail = slice(min(B, 512), B)  # rows whose z lies past the setup grid's first 65536 threads
+    if B > 512:
+        assert rel_l2(zt_t[tail], z64[tail]) <= 3 * rel_l2(zt_c[tail], z64[tail]) + 1e-6
+        assert rel_l2(zt_c[tail], z64[tail]) <= 1e-2  # garbage rows would sit at ~1
 
 
 def test_team_sweep_is_deterministic(am, gpu_device):
