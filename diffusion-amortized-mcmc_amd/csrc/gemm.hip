@@ -821,10 +821,15 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
 // write groups are contiguous.  Double-buffered: 2 x 384 rows x 192 B = 147,456 B, one workgroup per CU.
 constexpr int X3_BM = 256, X3_BN = 128, X3_BK = 32, X3_ROWB = 192;
 __device__ __forceinline__ int x3_swz(int row) { return (row >> 1) & 3; }
+// F32A (variant bit 2097152): the A operand staged as fp32, one 128-B row of 8 16-B chunks per K tile, physical chunk
+// = logical chunk ^ f32a_swz(row & 15).  A lane of a 16x16x32 fragment read (row lane & 15, octet q = lane >> 4)
+// takes logical chunks 2q and 2q + 1 in two ds_read_b128; with u = (r >> 1) & 7 and the bit-1 flip on rows 4-11
+// (the rows the b128 lane groups pair with the other octet) every 16-lane group hits 16 distinct 4-bank groups.
+constexpr int X3_F32A = 2097152, X3A_ROWB = 128;
+__device__ __forceinline__ int f32a_swz(int r) { return ((r >> 1) & 7) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
 constexpr int X3_FLUSH = 8;  // K tiles per MFMA accumulation block (power of two)
 static_assert(X3_FLUSH * 32 == X3_NEGK, "sign blocks are accumulation blocks");
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
-constexpr int X3_AJ = X3_BM * X3_CHUNKS / 512, X3_BJ = X3_BN * X3_CHUNKS / 512;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -863,7 +868,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool WIDE = (V & 524288) != 0;
   static_assert(!(WIDE && P16), "one layout variant at a time");
   constexpr int BM = WIDE ? 128 : X3_BM, BN = WIDE ? 256 : X3_BN;
-  constexpr int AJ = BM * X3_CHUNKS / 512, BJ = BN * X3_CHUNKS / 512;
+  // X3_F32A: A staged as fp32 (4 B per element instead of 6 B of limbs) and split into its RNE limbs in registers after
+  // the fragment read, the same split as the producing epilogue's, so the MFMA operands and results are bitwise the
+  // limb path's; waves 8 along M x 1 along N (each 32 x 128), so every A element is split by one wave only
+  constexpr bool F32A = (V & X3_F32A) != 0;
+  static_assert(!F32A || (OM != O_WGRAD && M16 && (V & 4) && (V & 256) && !WIDE && !P16 &&
+                          !(V & (8 | 16 | 32 | 64 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 131072))),
+                "F32A: the default 16x16-tile LDS-DMA path only");
+  constexpr int AROWB = F32A ? X3A_ROWB : X3_ROWB, ESZ = F32A ? 4 : 6;
+  constexpr int AJ = BM * (F32A ? 8 : X3_CHUNKS) / 512, BJ = BN * X3_CHUNKS / 512;
+  constexpr int BUFB = BM * AROWB + BN * X3_ROWB;  // one LDS buffer (A image, then B image)
   constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * X3_ROWB];
   const int tid = threadIdx.x;
@@ -932,7 +946,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int hwq = p.Hq * p.Wq;
   const int nimg = (p.M + hwq - 1) / hwq;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.A3, (short)0, (OM == O_WGRAD) ? Cg * p.K * 6 : nimg * p.Hin * Win * Cg * 6, 0x00020000);
+      F32A ? (void*)p.A : (void*)p.A3, (short)0, (OM == O_WGRAD) ? Cg * p.K * 6 : nimg * p.Hin * Win * Cg * ESZ,
+      0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)Bg, (short)0, p.N * p.K * 6, 0x00020000);
 
@@ -943,7 +958,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
 #pragma unroll
   for (int j = 0; j < AJ; ++j) {
     // P16: 16-deep K stages, rows of 6 chunks in global order (the first X3P_AJ entries are used)
-    const int nch = P16 ? 6 : X3_CHUNKS;
+    const int nch = F32A ? 8 : P16 ? 6 : X3_CHUNKS;
     const int id = tid + 512 * j, row = id / nch, ch = id - row * nch;
     const int m = m0 + row;
     unsigned msk = 0;
@@ -971,7 +986,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
             msk |= 1u << (ky * kw + kx);
     }
     const int q = (ch / 3) ^ x3_swz(row), limb = ch - (ch / 3) * 3;  // logical octet of physical chunk ch
-    abase[j] = P16 ? base * 6 + ch * 16 : base * 6 + q * 48 + limb * 16;
+    abase[j] = F32A ? base * 4 + ((id & 7) ^ f32a_swz(row & 15)) * 16
+                    : P16 ? base * 6 + ch * 16 : base * 6 + q * 48 + limb * 16;
     amask[j] = msk;
     alds[j] = row * X3_ROWB + ch * 16;
   }
@@ -993,7 +1009,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   }
   unsigned aoff[AJ];
   auto set_tap = [&]() {
-    const int toff = (tky * Win + tkx) * Cg * 6;
+    const int toff = (tky * Win + tkx) * Cg * ESZ;
 #pragma unroll
     for (int j = 0; j < AJ; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
   };
@@ -1052,7 +1068,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   typedef __attribute__((address_space(3))) void* lds_t;
   const int wbase = (tid & ~63) * 16;
   auto dma_ab = [&](int k0, int buf) {
-    unsigned char* base = smem + buf * (BM + BN) * X3_ROWB + wbase;
+    unsigned char* base = smem + buf * BUFB + wbase;
     if constexpr (OM == O_WGRAD) {
       // the K tile is 32 samples of ONE pixel (wg_bp % 32 == 0): a chunk is live when its shifted pixel
       // lies inside the grid
@@ -1089,12 +1105,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     } else {
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * ESZ, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j)
       if (!(V & 32768) || k0 == kbeg)  // 32768: timing probe (wrong results), no B DMA after the first tile
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * X3_ROWB + 512 * 16 * j), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * AROWB + 512 * 16 * j), 16,
                                                (V & 4096) ? ((tid * 16 + 8192 * j) & 0xFFFF) : (int)boff[j],
                                                (V & 4096) ? 0 : k0 * 6, 0, 0);
     if constexpr (OM != O_WGRAD && !CMAJ) {
@@ -1188,7 +1204,79 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
   };
-  if constexpr (P16) {
+  if constexpr (F32A) {
+    // ---- fp32 A image (X3A_ROWB rows, f32a_swz), limb B image; wave w owns rows 32 w .. 32 w + 31 and all 128 columns:
+    // acc16[2 a + (t >> 2)][t & 3] is A tile a (16 rows) x B tile t (16 columns).  Per K tile: 4 ds_read_b128 of fp32 A,
+    // its RNE split (split3_octet, the epilogue's), then per B tile 3 limb reads (one tile ahead) and 12 MFMAs.
+    if (nk > 0) dma_ab(kbeg, 0);
+    __syncthreads();
+    const int fs = f32a_swz(lrow);
+    const int ca0 = ((2 * loct) ^ fs) * 16, ca1 = ((2 * loct + 1) ^ fs) * 16;
+    const int arow = (wave * 32 + lrow) * X3A_ROWB, brow = BM * X3A_ROWB + lrow * X3_ROWB + oct16;
+    bf16x8 fa[2][3], fb[2][3];
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* base = smem + (kt & 1) * BUFB;
+      if (kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+      f32x4 av[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        av[a][0] = *reinterpret_cast<const f32x4*>(base + arow + a * 16 * X3A_ROWB + ca0);
+        av[a][1] = *reinterpret_cast<const f32x4*>(base + arow + a * 16 * X3A_ROWB + ca1);
+      }
+      auto rd_b = [&](int t, int slot) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) fb[slot][l] = *reinterpret_cast<const bf16x8*>(base + brow + t * 16 * X3_ROWB + l * 16);
+      };
+      rd_b(0, 0);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const float v[8] = {av[a][0].x, av[a][0].y, av[a][0].z, av[a][0].w,
+                            av[a][1].x, av[a][1].y, av[a][1].z, av[a][1].w};
+        split3_octet(v, fa[a][0], fa[a][1], fa[a][2]);
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        if (t + 1 < 8) rd_b(t + 1, (t + 1) & 1);
+        const int sl = t & 1;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          f32x4 c = acc16[2 * a + (t >> 2)][t & 3];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][2], fb[sl][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fb[sl][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fb[sl][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][1], c, 0, 0, 0);
+          acc16[2 * a + (t >> 2)][t & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][0], c, 0, 0, 0);
+        }
+      }
+      __syncthreads();
+      if (((kt + 1) & (FLUSH - 1)) != 0) continue;
+      if constexpr (KREG) {
+        // the register slab layout of the 4 x 2 wave grid (x3_ksplit_reduce_tile_kernel): A tile a of this wave is row
+        // tile (w & 1) * 2 + a of wave row w >> 1, B tile t is column tile t & 3 of wave column t >> 2
+        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        const int ntile = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+        const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw) * ntile * (BM * BN)), (short)0,
+            p.kbpw * ntile * (BM * BN) * 4, 0x00020000);
+        const int soff = ((kt / FLUSH) * ntile + tm * ntn + tn) * (BM * BN * 4);
+        const int voff = ((wave >> 1) * 2 * 1024 + ((wave & 1) * 2) * 4 * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int a = i >> 1, wnp = i & 1;
+            acc16[i][j] *= sg;
+            if (m0 + wave * 32 + a * 16 < p.M)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl, voff,
+                                                     soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, 0);
+            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      } else {
+        flush16(kt);
+      }
+    }
+  } else if constexpr (P16) {
     // ---- 16-deep K stages: stage s (16 k) of the A and B tiles is 384 rows x 96 B (three limbs of two octets, global
     // order, conflict-free for every fragment pattern below without a swizzle), slot s & 3 of a 4-slot ring; the DMA
     // of stage s + 3 is issued at the start of stage s, so three stages are in flight across each raw barrier and a
@@ -1655,7 +1743,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   float* tile = reinterpret_cast<float*>(smem);
   long* rowtab = reinterpret_cast<long*>(smem + BM * TS * 4);
   if (tid < BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
-  if (M16) {
+  if (F32A) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wave * 32 + (i >> 1) * 16 + 4 * (lane >> 4) + r) * TS + ((i & 1) * 4 + j) * 16 + (lane & 15)] =
+              acc16[i][j][r];
+  } else if (M16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -21,6 +21,7 @@ from conftest import rel_l2
 pytestmark = pytest.mark.gpu
 
 GEN = {  # name: (constructor, nz, ngf, image size)
+    "cifar10": ("_netG_cifar10", 128, 128, 32),
     "svhn": ("_netG_svhn", 100, 64, 32),
     "celeba64": ("_netG_celeba64", 100, 128, 64),
     "celebaHQ": ("_netG_celebaHQ", 128, 128, 256),
@@ -59,12 +60,45 @@ def _kink_rows(L64, z, rel=1e-6):
     return kink
 
 
-def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0, kink=None):
+def _kink_flip_bound(L64, P64, z0, x, sigma, step, rows, rel=1e-6):
+    """Per kink sample: how far its one-step z can legitimately sit from the fp64 one.  A hidden unit within
+    rel x its layer's RMS of the LeakyReLU kink may take the other derivative (1 vs 0.2) in any fp32 evaluation;
+    for each such unit the fp64 step is recomputed with that unit's mask flipped (its activation negated, which
+    flips the backward's sign test only), and the row's bound is the sum over its units of
+    |z_flipped - z64| / |z64| (a triangle bound over any subset of flips)."""
+    from oracle import damc_oracle as orc
+
+    z0, x = z0.double(), x.double()
+    hs_all = orc.generator_forward(L64, z0)
+    rms = [h.pow(2).mean().sqrt() for h in hs_all[:-1]]
+    c = 0.5 * step * step
+    out = np.zeros(z0.shape[0])
+    for r in np.nonzero(rows)[0]:
+        zr, xr = z0[r:r + 1], x[r:r + 1]
+        hs = orc.generator_forward(L64, zr)
+        xh = hs[-1]
+        delta = ((xh - xr) / (sigma * sigma)) * orc._act_grad_from_out(xh, L64[-1]["act"])
+        g0 = orc.generator_vjp(L64, hs, delta)
+        zref = zr - c * (g0 + zr + orc.ebm_energy_grad(P64, zr)[1])
+        tot = 0.0
+        for li, h in enumerate(hs[:-1]):
+            for idx in torch.nonzero(h.abs() < rel * rms[li]):
+                h2 = h.clone()
+                v = h2[tuple(idx)]
+                h2[tuple(idx)] = -v if v != 0 else -1e-30
+                g2 = orc.generator_vjp(L64, hs[:li] + [h2] + hs[li + 1:], delta)
+                tot += float((c * (g2 - g0)).norm() / zref.norm())
+        out[r] = tot
+    return out
+
+
+def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0, kink=None, kink_bound=None):
     """Distance to fp64 against the fp32 reference arithmetic's.  per_row: per-sample relative errors, judged by
     their median and 90th percentile, and every row that is not a kink sample by the largest fp32-reference row
     error: a sample with a hidden pre-activation within fp32 rounding of the LeakyReLU kink can take the other
     derivative (1 vs 0.2) under any summation order (the SVHN B=64 batch's sample 54 has a first-layer unit at
-    1.2e-8), an ill-conditioned row that is only bounded (< 5e-2)."""
+    1.2e-8).  A kink row is held to the non-kink bound plus the effect of flipping its kink units' derivatives,
+    computed in fp64 (_kink_flip_bound), with 1.5x slack for second-order terms between flips."""
     if not per_row:
         e_hip, e_32 = rel_l2(got, ref64), rel_l2(ref32, ref64)
         print("%s: |hip-fp64| %.2e  |fp32 reference arithmetic-fp64| %.2e" % (what, e_hip, e_32))
@@ -77,14 +111,25 @@ def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0, kink=None)
           % (what, q(eh, .5), q(eh, .9), eh.max(), eh.argmax(), q(e3, .5), q(e3, .9), e3.max()))
     assert q(eh, .5) <= factor * q(e3, .5) + floor, what
     assert q(eh, .9) <= factor * q(e3, .9) + floor, what
-    assert eh.max() < 5e-2, what
-    if kink is not None and (~kink).any():
-        print("%s: %d kink sample(s); the other rows' max |hip-fp64| %.2e vs the fp32 reference's %.2e"
-              % (what, int(kink.sum()), eh[~kink].max(), e3[~kink].max()))
-        assert eh[~kink].max() <= factor * e3[~kink].max() + floor, what
+    if kink is None:  # no kink analysis (the whole-batch gradient below): the ill-conditioned rows are only bounded
+        assert eh.max() < 5e-2, what
+        return
+    if not kink.any():
+        assert eh.max() <= factor * e3.max() + floor, what
+        return
+    assert (~kink).any(), what
+    print("%s: %d kink sample(s); the other rows' max |hip-fp64| %.2e vs the fp32 reference's %.2e"
+          % (what, int(kink.sum()), eh[~kink].max(), e3[~kink].max()))
+    base = factor * e3[~kink].max() + floor
+    assert eh[~kink].max() <= base, what
+    for r in np.nonzero(kink)[0]:
+        print("%s: kink row %d |hip-fp64| %.2e  fp32 reference %.2e  flip bound %.2e"
+              % (what, r, eh[r], e3[r], kink_bound[r]))
+        assert eh[r] <= base + 1.5 * kink_bound[r], (what, r)
 
 
 @pytest.mark.parametrize("name,B,steps,noise,sigma", [
+    ("cifar10", 128, 1, False, 0.1), ("cifar10", 128, 10, False, 0.1),
     ("svhn", 64, 1, False, 0.1), ("svhn", 64, 30, True, 0.1),
     ("celeba64", 32, 1, False, 0.1), ("celeba64", 32, 10, False, 0.1), ("celeba64", 256, 1, False, 0.1),
     ("celebaHQ", 8, 1, False, 1.0)])
@@ -105,13 +150,35 @@ def test_full_width_posterior_vs_fp64(gpu_device, name, B, steps, noise, sigma):
                                  noise=None if xi is None else xi.double()).numpy()
     # one step: per sample (a kink sample is bounded, not compared); several steps: the whole batch, whose rel-L2
     # both implementations grow chaotically
+    kink = _kink_rows(L64, zc) if steps == 1 else None
+    kb = _kink_flip_bound(L64, P64, zc, xc, sigma, 0.1, kink) if steps == 1 else None
     _check("%s B=%d %d step(s) z" % (name, B, steps), z.cpu().numpy(), r32, r64, 1e-7 if steps == 1 else 1e-6,
-           per_row=steps == 1, kink=_kink_rows(L64, zc) if steps == 1 else None)
+           per_row=steps == 1, kink=kink, kink_bound=kb)
     if steps == 10:  # eval path: reconstruction MSE of the 10-step no-noise posterior (eval_gen_recon.py:184-194)
         mse = ((lv.generator_forward(z, G) - x) ** 2).mean(dim=(1, 2, 3)).cpu().numpy()
         m32 = ((orc.generator_sample(L32, torch.from_numpy(r32)) - xc) ** 2).mean(dim=(1, 2, 3)).numpy()
         m64 = ((orc.generator_sample(L64, torch.from_numpy(r64)) - xc.double()) ** 2).mean(dim=(1, 2, 3)).numpy()
         _check("%s B=%d recon MSE" % (name, B), mse, m32, m64, 1e-7)
+
+
+def test_cifar_prior_60_steps_vs_fp64(gpu_device):
+    """BASELINE headline's prior chain: 60 noisy steps (step 0.4, injected noise) on 2B = 256 chains of _netE(nz=128)
+    (MCMC.py:27-46, train_gen_recon.py:207-209), whole batch against fp64, accuracy-relative."""
+    from damc import langevin as lv
+    from damc import synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
+    z0 = torch.from_numpy(synth.normal_f32(13, 0, (256, 128)))
+    xi = torch.from_numpy(np.random.default_rng(60).standard_normal((60, 256, 128)).astype(np.float32))
+    z = z0.to(gpu_device)
+    lv.prior_langevin(z, E, 60, 0.4, True, noise=xi.to(gpu_device))
+    r32 = orc.prior_langevin(orc.ebm_params(E), z0, 60, 0.4, noise=xi).numpy()
+    r64 = orc.prior_langevin(orc.ebm_params(E, torch.float64), z0.double(), 60, 0.4, noise=xi.double()).numpy()
+    _check("cifar prior 2B=256 60 steps z", z.cpu().numpy(), r32, r64, 1e-7)
+    _check("cifar prior 2B=256 60 steps z (per chain)", z.cpu().numpy(), r32, r64, 1e-7, per_row=True,
+           kink=np.zeros(256, dtype=bool))
 
 
 def test_celebaHQ_b64_likelihood_gradient_vs_fp64(gpu_device):

@@ -254,7 +254,7 @@ int main(int argc, char** argv) {
   }
   // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only,
   // 4096 = DMA from one L2-hot 64 KB window
-  V vars[] = {{"v261", run_x3<261, 1>}, {"wide", run_x3<261 | 524288, 1>}};
+  V vars[] = {{"v261", run_x3<261, 1>}, {"f32a", run_x3<261 | X3_F32A, 1>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
