@@ -185,7 +185,9 @@ def test_team_sweep_matches_launch_chain(am, gpu_device, monkeypatch, B):
     tail = slice(min(B, 512), B)  # rows whose z lies past the setup grid's first 65536 threads
     if B > 512:
         assert rel_l2(zt_t[tail], z64[tail]) <= 3 * rel_l2(zt_c[tail], z64[tail]) + 1e-6
-        assert rel_l2(zt_c[tail], z64[tail]) <= 1e-2  # garbage rows would sit at ~1
+        # the tail rows as close to fp64 as the head rows (a 10-step sweep sits ~4e-2 from fp64 in fp32 either way;
+        # uninitialised rows would sit at ~1)
+        assert rel_l2(zt_c[tail], z64[tail]) <= 3 * rel_l2(zt_c[:512], z64[:512])
 
 
 def test_team_sweep_is_deterministic(am, gpu_device):
