@@ -117,11 +117,13 @@ def _check(what, got, ref32, ref64, floor, per_row=False, factor=3.0, kink=None,
     if not kink.any():
         assert eh.max() <= factor * e3.max() + floor, what
         return
-    assert (~kink).any(), what
-    print("%s: %d kink sample(s); the other rows' max |hip-fp64| %.2e vs the fp32 reference's %.2e"
-          % (what, int(kink.sum()), eh[~kink].max(), e3[~kink].max()))
-    base = factor * e3[~kink].max() + floor
-    assert eh[~kink].max() <= base, what
+    if (~kink).any():
+        print("%s: %d kink sample(s); the other rows' max |hip-fp64| %.2e vs the fp32 reference's %.2e"
+              % (what, int(kink.sum()), eh[~kink].max(), e3[~kink].max()))
+        base = factor * e3[~kink].max() + floor
+        assert eh[~kink].max() <= base, what
+    else:  # every sample has a near-kink unit (CelebA-HQ's 5.8M hidden units per sample): the median row's bound
+        base = factor * q(e3, .5) + floor
     for r in np.nonzero(kink)[0]:
         print("%s: kink row %d |hip-fp64| %.2e  fp32 reference %.2e  flip bound %.2e"
               % (what, r, eh[r], e3[r], kink_bound[r]))
