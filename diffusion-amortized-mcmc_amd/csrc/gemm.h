@@ -92,7 +92,10 @@ inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
 // the same for a weight operand whose rows are K long, with the values of the odd X3_NEGK-blocks of each row
 // negated (exact); the GEMM launches that read it set GemmArgs::b_negblk
-constexpr int X3_NEGK = 256;
+#ifndef DAMC_X3_NEGK
+#define DAMC_X3_NEGK 256  // k per sign block = per MFMA accumulation block (gemm.hip X3_FLUSH = X3_NEGK / 32)
+#endif
+constexpr int X3_NEGK = DAMC_X3_NEGK;
 int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s);
 // the same reordered for the channel-major K walk: a row's K = taps * Cg values [tap][c] are stored
 // [c / sw][tap][c % sw] (sw channels per slice), sign blocks counted in that order

@@ -827,7 +827,7 @@ __device__ __forceinline__ int x3_swz(int row) { return (row >> 1) & 3; }
 // (the rows the b128 lane groups pair with the other octet) every 16-lane group hits 16 distinct 4-bank groups.
 constexpr int X3_F32A = 2097152, X3A_ROWB = 128;
 __device__ __forceinline__ int f32a_swz(int r) { return ((r >> 1) & 7) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
-constexpr int X3_FLUSH = 8;  // K tiles per MFMA accumulation block (power of two)
+constexpr int X3_FLUSH = X3_NEGK / 32;  // K tiles per MFMA accumulation block (power of two)
 static_assert(X3_FLUSH * 32 == X3_NEGK, "sign blocks are accumulation blocks");
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1206,54 +1206,127 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   };
   if constexpr (F32A) {
     // ---- fp32 A image (X3A_ROWB rows, f32a_swz), limb B image; wave w owns rows 32 w .. 32 w + 31 and all 128 columns:
-    // acc16[2 a + (t >> 2)][t & 3] is A tile a (16 rows) x B tile t (16 columns).  Per K tile: 4 ds_read_b128 of fp32 A,
-    // its RNE split (split3_octet, the epilogue's), then per B tile 3 limb reads (one tile ahead) and 12 MFMAs.
-    if (nk > 0) dma_ab(kbeg, 0);
-    __syncthreads();
+    // acc16[2 a + (t >> 2)][t & 3] is A tile a (16 rows) x B tile t (16 columns).  A runs one tile ahead of B: during
+    // tile kt's MFMAs (limb fragments of A(kt) in registers, B(kt) read from LDS one 16-column tile ahead) each wave
+    // reads its fp32 rows of A(kt + 1) (4 ds_read_b128) and splits them into the next tile's limbs (split3_octet, the
+    // producing epilogue's RNE split), so the split's VALU runs in the MFMA gaps.  LDS-DMA: B(kt + 1) and A(kt + 2)
+    // are issued at the start of tile kt into the buffers tile kt - 1 finished with; the end-of-tile barrier lands
+    // them.  Double-buffered: 2 x (256 x 128 + 128 x 192) B.
+    auto dma_a = [&](int buf) {
+      unsigned char* dst = smem + buf * BUFB + wbase;
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(dst + 512 * 16 * j), 16, (int)aoff[j], ci0 * ESZ, 0, 0);
+      ci0 += X3_BK;
+      if (ci0 == Cg) {
+        ci0 = 0;
+        ++tap;
+        if (++tkx == kw) {
+          tkx = 0;
+          ++tky;
+        }
+        set_tap();
+      }
+    };
+    auto dma_b = [&](int k0, int buf) {
+      unsigned char* dst = smem + buf * BUFB + BM * X3A_ROWB + wbase;
+#pragma unroll
+      for (int j = 0; j < BJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(dst + 512 * 16 * j), 16, (int)boff[j], k0 * 6, 0, 0);
+    };
     const int fs = f32a_swz(lrow);
     const int ca0 = ((2 * loct) ^ fs) * 16, ca1 = ((2 * loct + 1) ^ fs) * 16;
     const int arow = (wave * 32 + lrow) * X3A_ROWB, brow = BM * X3A_ROWB + lrow * X3_ROWB + oct16;
-    bf16x8 fa[2][3], fb[2][3];
-    for (int kt = 0; kt < nk; ++kt) {
-      const unsigned char* base = smem + (kt & 1) * BUFB;
-      if (kt + 1 < nk) dma_ab(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
-      f32x4 av[2][2];
+    auto rd_a = [&](const unsigned char* buf, f32x4 (&av)[2][2]) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        av[a][0] = *reinterpret_cast<const f32x4*>(base + arow + a * 16 * X3A_ROWB + ca0);
-        av[a][1] = *reinterpret_cast<const f32x4*>(base + arow + a * 16 * X3A_ROWB + ca1);
+        av[a][0] = *reinterpret_cast<const f32x4*>(buf + arow + a * 16 * X3A_ROWB + ca0);
+        av[a][1] = *reinterpret_cast<const f32x4*>(buf + arow + a * 16 * X3A_ROWB + ca1);
       }
+    };
+    // RNE limb split of elements e, e + 1 of A tile a (split3_octet's arithmetic, element by element)
+    auto split2 = [&](const f32x4 (&av)[2][2], bf16x8 (&f)[2][3], int a, int e) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const float v = av[a][(e + d) >> 2][(e + d) & 3];
+        const __bf16 b0 = (__bf16)v;
+        const float r1 = v - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        const float r2 = r1 - (float)b1;
+        f[a][0][e + d] = b0;
+        f[a][1][e + d] = b1;
+        f[a][2][e + d] = (__bf16)r2;
+      }
+    };
+    auto rd_split = [&](const unsigned char* buf, bf16x8 (&f)[2][3]) {
+      f32x4 av[2][2];
+      rd_a(buf, av);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) split2(av, f, a, e);
+    };
+    bf16x8 fx[2][3], fy[2][3], fb[2][3];
+    if (nk > 0) {
+      dma_a(0);
+      dma_b(kbeg, 0);
+    }
+    if (nk > 1) dma_a(1);
+    __syncthreads();
+    rd_split(smem, fx);
+    constexpr int SG_MFMA = 0x8, SG_VALU = 0x2, SG_DS_RD = 0x100;
+    auto tile = [&](int kt, bf16x8 (&fc)[2][3], bf16x8 (&fn)[2][3]) {
+      const unsigned char* base = smem + (kt & 1) * BUFB;
+      if (kt + 1 < nk) dma_b(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+      if (kt + 2 < nk) dma_a(kt & 1);
+      // A(kt + 1): read and split unconditionally (past the last tile it is stale, in-bounds LDS, never used); two
+      // elements per B tile, in that tile's MFMA gaps
+      f32x4 av[2][2];
+      rd_a(smem + ((kt + 1) & 1) * BUFB, av);
       auto rd_b = [&](int t, int slot) {
 #pragma unroll
         for (int l = 0; l < 3; ++l) fb[slot][l] = *reinterpret_cast<const bf16x8*>(base + brow + t * 16 * X3_ROWB + l * 16);
       };
       rd_b(0, 0);
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const float v[8] = {av[a][0].x, av[a][0].y, av[a][0].z, av[a][0].w,
-                            av[a][1].x, av[a][1].y, av[a][1].z, av[a][1].w};
-        split3_octet(v, fa[a][0], fa[a][1], fa[a][2]);
-      }
-#pragma unroll
       for (int t = 0; t < 8; ++t) {
         if (t + 1 < 8) rd_b(t + 1, (t + 1) & 1);
         const int sl = t & 1;
+        split2(av, fn, t >> 2, (t & 3) * 2);
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           f32x4 c = acc16[2 * a + (t >> 2)][t & 3];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][2], fb[sl][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fb[sl][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fb[sl][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][1], c, 0, 0, 0);
-          acc16[2 * a + (t >> 2)][t & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fb[sl][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][2], fb[sl][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][1], fb[sl][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][0], fb[sl][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][1], fb[sl][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][0], fb[sl][1], c, 0, 0, 0);
+          acc16[2 * a + (t >> 2)][t & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[a][0], fb[sl][0], c, 0, 0, 0);
         }
       }
+      // schedule: the 4 A reads and B tiles 0 and 1 (6 reads) first, then per B tile t its 12 MFMAs with the split's
+      // VALU in their gaps, then B tile t + 2's reads (into the slot tile t's MFMAs just released)
+      __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 10, 0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+#pragma unroll
+        for (int m = 0; m < 12; ++m) {
+          __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(SG_VALU, 1, 0);
+        }
+        if (t + 2 < 8) __builtin_amdgcn_sched_group_barrier(SG_DS_RD, 3, 0);
+      }
+      // the next tile's limbs are complete before the barrier: otherwise the compiler sinks the split into the next
+      // tile, where it runs ahead of the first MFMAs instead of in this tile's gaps
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int l = 0; l < 3; ++l) asm volatile("" : "+v"(fn[a][l]));
       __syncthreads();
-      if (((kt + 1) & (FLUSH - 1)) != 0) continue;
+      if (((kt + 1) & (FLUSH - 1)) != 0) return;
       if constexpr (KREG) {
-        // the register slab layout of the 4 x 2 wave grid (x3_ksplit_reduce_tile_kernel): A tile a of this wave is row
-        // tile (w & 1) * 2 + a of wave row w >> 1, B tile t is column tile t & 3 of wave column t >> 2
+        // the register slab layout of the 4 x 2 wave grid (x3_ksplit_reduce_tile_kernel): A tile a of this wave is
+        // row tile (w & 1) * 2 + a of wave row w >> 1, B tile t is column tile t & 3 of wave column t >> 2
         const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
         const int ntile = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
         const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
@@ -1275,6 +1348,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       } else {
         flush16(kt);
       }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {  // two tiles per trip: the limb sets trade roles without register moves
+      tile(kt, fx, fy);
+      if (kt + 1 < nk) tile(kt + 1, fy, fx);
     }
   } else if constexpr (P16) {
     // ---- 16-deep K stages: stage s (16 k) of the A and B tiles is 384 rows x 96 B (three limbs of two octets, global
