@@ -564,7 +564,12 @@ __device__ __forceinline__ void ts_ready(f32x4 (&x)[N], int kps, const __amdgpu_
   } while (__any(any_sent(x)));
 }
 
-__global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
+// NT: threads per workgroup.  The flag protocols (sent 0 / 1) need the poll wave (threads 256..319) and the flag
+// lane (TS_PUB): 384.  The data-driven hand-off (sent 2, the default) has neither, so it runs 4 waves, one per SIMD,
+// which lifts the register cap from 256 to 512 per lane: at 384 threads the kernel spilled 38 VGPRs to scratch (152 B
+// per lane) once the sentinel re-read paths were added, +17 % sweep time (round 4 A/B).
+template <int NT>
+__global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   __shared__ int sflag;
   __shared__ uint64_t trs[3];                    // tools only: this stage's stamps
@@ -588,7 +593,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
   const int ld0 = emb_ld(a.b[0].kpa);
 
   if (a.n <= TS_TAB_STEPS)
-    for (int i = tid; i < 8 * a.n; i += TS_THREADS) tabs[i] = a.tab[i];
+    for (int i = tid; i < 8 * a.n; i += NT) tabs[i] = a.tab[i];
   // ---- the owned weight tiles into LDS, fragment order: (half, wave, k-group, lane) -> f32x4
   if (tid == 0) {
     int off = 0;
@@ -612,7 +617,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
         const int ng = kps >> 6;  // k-groups per wave
         const int units = 4 * ng * 64;
         f32x4* d4 = reinterpret_cast<f32x4*>(dst + (h ? 16 * b.kpa : 0));
-        for (int u = tid; u < units; u += TS_THREADS) {
+        for (int u = tid; u < units; u += NT) {
           const int l = u & 63, g = (u >> 6) % ng, w = (u >> 6) / ng;
           const int mm = l & 15, qq = l >> 4;
           const int k = w * (kps >> 2) + 16 * g + 4 * qq;
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       const int nt = ts_tiles(b, T, slot, &tn0);
       // tools only: the poll wave keeps its stamps in LDS (a global store in front of its poll would delay it);
       // the publishing lane writes them out after the flag
-      const bool tr = a.trace != nullptr && tid == 256;
+      const bool tr = a.trace != nullptr && tid == (NT > 256 ? 256 : 0);
       if (nt == 0) {  // nothing to compute: publish at once (this slot's earlier stores are drained)
         if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
@@ -787,7 +792,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
                   if (kk < nz) embs[m * ld0 + 2 * half + kk] = zv4[g][e];
                 }
             }
-            for (int c = 2 * half + nz + tid; c < b.kpa; c += TS_THREADS)
+            for (int c = 2 * half + nz + tid; c < b.kpa; c += NT)
 #pragma unroll
               for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
             __syncthreads();
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(TS_THREADS) void sweep_team_kernel(TsArgs a) {
       if (!a.sent && !(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.trace && tid == TS_PUB) {
+      if (a.trace && tid == (NT > 256 ? TS_PUB : 0)) {
         uint64_t* tg = a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4;
         tg[0] = trs[0];
         tg[1] = trs[1];
@@ -1529,7 +1534,9 @@ int team_slots() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     cached[dev] = (cus % 8 == 0 && cus >= 8) ? std::min(cus / 8, TS_MAXT) : -1;
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<TS_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TS_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)TS_LDS_MAX);
   }
   return std::max(cached[dev], 0);
@@ -1599,7 +1606,11 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
     std::lock_guard<std::mutex> lk(mu);
     if (ok_sm[dev] != sm) {
       int per = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel, TS_THREADS, sm) != hipSuccess || per < 1)
+      int per2 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel<TS_THREADS>, TS_THREADS, sm) !=
+              hipSuccess || per < 1 ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, sweep_team_kernel<256>, 256, sm) != hipSuccess ||
+          per2 < 1)
         return DAMC_ERR_UNSUPPORTED;
       ok_sm[dev] = sm;
     }
@@ -1688,7 +1699,10 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
     DAMC_CHECK(hipMalloc(&a.trace, tbytes));
     DAMC_CHECK(hipMemsetAsync(a.trace, 0, tbytes, s));
   }
-  hipLaunchKernelGGL(sweep_team_kernel, dim3(P), dim3(TS_THREADS), smem, s, a);
+  if (a.sent == 2)
+    hipLaunchKernelGGL(sweep_team_kernel<256>, dim3(P), dim3(256), smem, s, a);
+  else
+    hipLaunchKernelGGL(sweep_team_kernel<TS_THREADS>, dim3(P), dim3(TS_THREADS), smem, s, a);
   DAMC_LAUNCH_CHECK();
   if (trace) {  // tools/sweep_trace.py reads the dump: P, n, G, then the stamps
     std::vector<uint64_t> h((size_t)P * 7 * n * 4);

@@ -399,6 +399,13 @@ struct EbArgs {
   const float* noise;  // injected: PRIOR (n_steps, B, nz), POSTERIOR (B, nz)
   uint64_t seed, step_offset, chain_base;
   float* diag;         // PRIOR: (n_steps, 2) {sum E, |z|^2/2};  POSTERIOR: (4) {sum E, -, |z|^2/2, mean grad}
+  // POSTERIOR with nslab > 1: glik is the sum of nslab split-K slabs (slab k at slabs + k * slab_stride), added in
+  // slab_sum4_kernel's fixed order (16 groups of every 16th slab, then the groups in order), so the fused sum is
+  // bitwise the separate kernel's
+  const float* slabs;
+  int nslab;
+  long slab_stride;
+  unsigned short* z3;  // POSTERIOR: the new z also as x3 limbs [B][nz/8][3][8] (the limb-engine first layer's A), or null
 };
 
 __device__ __forceinline__ float block_sum1024(float v, float* red) {
@@ -426,6 +433,24 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
   __shared__ float part2[EB_WAVES][64 * EB_K2];
   __shared__ float part1[EB_WAVES][64 * EB_K1];
   __shared__ float red[EB_WAVES];
+  __shared__ float gpart[16][64 * EB_K1];  // POSTERIOR: the 16 slab-group sums of glik
+
+  // ---- POSTERIOR: the likelihood gradient's split-K slabs, summed as slab_sum4_kernel does (its loads are in flight
+  // while the weights load; the barrier below publishes the group sums)
+  if (MODE == EB_POSTERIOR && a.nslab > 1) {
+    const int c = tid & (64 * EB_K1 - 1), gp = tid / (64 * EB_K1);
+#pragma unroll
+    for (int h = 0; h < 16 / (EB_THREADS / (64 * EB_K1)); ++h) {
+      const int g = gp + (EB_THREADS / (64 * EB_K1)) * h;
+      float acc = 0.f;
+      if (c < nz) {
+        const float* src = a.slabs + (long)chain * nz + c;
+#pragma unroll 16
+        for (int k = g; k < a.nslab; k += 16) acc += src[(long)k * a.slab_stride];
+      }
+      gpart[g][c] = acc;
+    }
+  }
 
   // ---- weights -> registers (once per launch); column-coalesced rows
   float w2[EB_RW][EB_K2], w1[EB_RW][EB_K1];
@@ -548,13 +573,33 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
       if (MODE == EB_GRAD) {
         a.grad[gi] = gz;
       } else {
-        float g = (MODE == EB_POSTERIOR) ? a.glik[gi] + gz : gz;
+        float gl = 0.f;
+        if (MODE == EB_POSTERIOR) {
+          if (a.nslab > 1) {
+            gl = gpart[0][tid];
+#pragma unroll
+            for (int j = 1; j < 16; ++j) gl += gpart[j][tid];
+          } else {
+            gl = a.glik[gi];
+          }
+        }
+        float g = (MODE == EB_POSTERIOR) ? gl + gz : gz;
         g += zv;
         zsq = zv * zv;
         gsum = g;
         float zn = sub_rn(zv, mul_rn(a.c1, g));
         if (a.with_noise) zn = add_rn(zn, mul_rn(a.step, xs[tid]));
         zs[tid] = zn;
+        if (MODE == EB_POSTERIOR && a.z3) {  // RNE limbs (gemm.hip split3_octet's arithmetic), x3 octet layout
+          const __bf16 b0 = (__bf16)zn;
+          const float r1 = zn - (float)b0;
+          const __bf16 b1 = (__bf16)r1;
+          const __bf16 b2 = (__bf16)(r1 - (float)b1);
+          __bf16* o = reinterpret_cast<__bf16*>(a.z3) + ((long)chain * (nz >> 3) + (tid >> 3)) * 24 + (tid & 7);
+          o[0] = b0;
+          o[8] = b1;
+          o[16] = b2;
+        }
       }
     }
     if (want_e) {  // uniform branch
@@ -749,9 +794,14 @@ bool ebm_shape_ok(int R, int nz, int nh) {
 }  // namespace
 
 // host helpers used by generator.hip
+// the register-resident update kernel runs (and can sum split-K slabs and write z's limbs itself) for this EBM
+bool damc_posterior_update_fusable(const damc_ebm_t* e, int nz) { return e && e->nz == nz && ebm_reg_ok(nz, e->nh); }
+
 int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
                                  int nz, double step, int with_noise, const float* noise, uint64_t seed,
-                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s) {
+                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s,
+                                 unsigned short* z3, bool* wrote_z3) {
+  if (wrote_z3) *wrote_z3 = false;
   damc_ebm_t ev{};
   int use_ebm = 0;
   if (e) {
@@ -760,11 +810,16 @@ int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* sla
     if (ev.nz != nz) return DAMC_ERR_ARG;
   }
   const float c1 = (float)(0.5 * step * step);  // float32(0.5 * s * s), the reference's scalar
-  if (use_ebm && nslab == 1 && ebm_reg_ok(nz, ev.nh)) {
+  if (use_ebm && ebm_reg_ok(nz, ev.nh)) {
     EbArgs a{};
     a.e = ev;
     a.z = z;
     a.glik = slabs;
+    a.slabs = slabs;
+    a.nslab = nslab;
+    a.slab_stride = slab_stride;
+    a.z3 = (z3 && nz % 8 == 0) ? z3 : nullptr;
+    if (wrote_z3) *wrote_z3 = a.z3 != nullptr;
     a.B = B;
     a.c1 = c1;
     a.step = (float)step;

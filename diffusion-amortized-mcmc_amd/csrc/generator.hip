@@ -19,7 +19,9 @@ using damc::GemmArgs;
 
 int damc_launch_posterior_update(const damc_ebm_t* e, float* z, const float* slabs, int nslab, long slab_stride, int B,
                                  int nz, double step, int with_noise, const float* noise, uint64_t seed,
-                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s);
+                                 uint64_t step_idx, uint64_t chain_base, float* diag, hipStream_t s,
+                                 unsigned short* z3 = nullptr, bool* wrote_z3 = nullptr);
+bool damc_posterior_update_fusable(const damc_ebm_t* e, int nz);
 
 namespace {
 
@@ -1494,8 +1496,10 @@ double conv_flops(const damc_layer_t& L, int B) {
   return 2.0 * B * (double)L.hout * L.wout * L.cout * L.cin * taps;
 }
 
-// forward of layers [0, n-1) into ws.h; returns 0 on success
-int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& ws, hipStream_t s) {
+// forward of layers [0, n-1) into ws.h; returns 0 on success.  z3_ready: ws.z3 already holds z's limbs (the previous
+// posterior update wrote them)
+int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& ws, hipStream_t s,
+                   bool z3_ready = false) {
   for (int i = 0; i + 1 < g->n_layers; ++i) {
     const damc_layer_t& L = g->layers[i];
     GemmArgs a;
@@ -1510,7 +1514,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       // z . W on the limb engine: z -> limbs, 1x1 "convolution" against the x3 copy of the dgrad
       // packing [(oy,ox,co)][ci]; the epilogue writes the next layer's limbs too
       const int N = L.hout * L.wout * L.cout;
-      {
+      if (!z3_ready) {
         ProfScope ps("split_x3", 0.0, s);
         if ((rc = damc::launch_split_x3(z, (long)B * L.cin, ws.z3, s))) return rc;
       }
@@ -2171,16 +2175,29 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   hipStream_t s = as_stream(stream);
   if (diag) DAMC_CHECK(hipMemsetAsync(diag, 0, sizeof(float) * 4 * (size_t)n_steps, s));
   const float inv_s2 = (float)(1.0 / (sigma * sigma));
+  // the register-resident update kernel sums the first layer's split-K slabs itself (slab_sum4's order) and writes
+  // z's limbs for the next step's first layer; DAMC_POST_FUSE=0 (read per call) keeps the separate kernels
+  const char* pf = getenv("DAMC_POST_FUSE");
+  const bool fuse = !(pf && pf[0] == '0');
+  const bool z3_use = x3_proj(g->layers[0]) && ws.z3;
+  bool z3_ready = false;
   for (int i = 0; i < n_steps; ++i) {
     float* dg = diag ? diag + 4 * i : nullptr;
-    if ((rc = forward_hidden(g, z, B, ws, s))) return rc;
+    if ((rc = forward_hidden(g, z, B, ws, s, z3_ready))) return rc;
     if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s))) return rc;
     if ((rc = backward(g, B, ws, s))) return rc;
     const float* nz_i = noise ? noise + (size_t)i * B * g->nz : nullptr;
-    if ((rc = slab_sum(ws.slabs, ws.nslab, (long)B * g->nz, ws.glik, s))) return rc;
-    rc = damc_launch_posterior_update(ebm, z, ws.glik, 1, (long)B * g->nz, B, g->nz, step, with_noise, nz_i, seed,
-                                      step_offset + i, chain_base, dg, s);
+    const long n = (long)B * g->nz;
+    // fused only where slab_sum takes its slab_sum4 order (the order the update kernel reproduces)
+    const bool f = fuse && damc_posterior_update_fusable(ebm, g->nz) && (n & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(ws.slabs) | reinterpret_cast<uintptr_t>(ws.glik)) & 15) == 0;
+    if (!f && (rc = slab_sum(ws.slabs, ws.nslab, n, ws.glik, s))) return rc;
+    bool wrote = false;
+    rc = damc_launch_posterior_update(ebm, z, f ? ws.slabs : ws.glik, f ? ws.nslab : 1, n, B, g->nz, step,
+                                      with_noise, nz_i, seed, step_offset + i, chain_base, dg, s,
+                                      (f && z3_use) ? ws.z3 : nullptr, &wrote);
     if (rc) return rc;
+    z3_ready = wrote;
   }
   return 0;
 }

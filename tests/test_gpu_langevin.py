@@ -381,3 +381,20 @@ def test_lds_staged_output_projection_is_bitwise_the_direct_kernel(lv, gpu_devic
         out[mode] = z.cpu()
     assert torch.isfinite(out["1"]).all()
     assert torch.equal(out["0"], out["1"])
+
+
+@pytest.mark.parametrize("B", [16, 37])
+def test_fused_posterior_update_is_bitwise(lv, gpu_device, monkeypatch, B):
+    """The posterior update kernel sums the first layer's split-K slabs itself (slab_sum4's fixed order) and writes z's
+    limbs for the next step's first layer: 3 noisy steps bitwise equal to the separate slab-sum and limb-split
+    kernels (DAMC_POST_FUSE=0)."""
+    G, E, x, z0 = _cifar_full(gpu_device, B)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_POST_FUSE", mode)
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
+        torch.cuda.synchronize()
+        out[mode] = z.cpu()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
