@@ -41,7 +41,10 @@ constexpr int CH_THREADS = 64 * CH_WAVES;
 constexpr int TM = 16;           // rows per workgroup
 constexpr int TC = 8;            // output columns per workgroup (x 2 products)
 constexpr int KG = 16 * CH_WAVES;  // K padding granule: one 16-deep k-group per wave
-constexpr int CH_CHUNK = 8;      // k-groups whose loads a lane keeps in flight at once
+#ifndef DAMC_CH_CHUNK
+#define DAMC_CH_CHUNK 8
+#endif
+constexpr int CH_CHUNK = DAMC_CH_CHUNK;  // k-groups whose loads a lane keeps in flight at once
 constexpr int EMB_G = 8;         // in0: 16-deep k-groups of z (nz <= 128)
 
 // per-call values read by the last block (device memory in the workspace, written before each sweep so a cached
@@ -85,6 +88,14 @@ __host__ __device__ inline int emb_ld(int kp) { return kp + 8; }  // in0 LDS ima
 // k-groups, then their sum: half the dependent-MFMA latency of one chain on the stage's critical path (chain_kernel, the team
 // kernel and its rescue all use this function)
 __device__ __forceinline__ f32x4 emb_zb(const f32x4 (&zv4)[EMB_G], const f32x4 (&bv)[EMB_G]) {
+#ifdef DAMC_EMB_ONE_CHAIN  // A/B only (round 4 sweep attribution): round 2's single chain
+  f32x4 a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv4[g][e], bv[g][e], a1, 0, 0, 0);
+  return a1;
+#endif
   f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int g = 0; g < EMB_G; g += 2)

@@ -704,6 +704,8 @@ int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_en
 }
 }  // namespace
 
+extern "C" int damc_x3_sign_block(void) { return damc::X3_NEGK; }
+
 extern "C" size_t damc_conv2d_x3_bytes(int cout, int cin, int k) {
   if (cout <= 0 || cin <= 0 || k <= 0 || !damc::conv_kmajor_ok(cin) || cout % 8 != 0 || k * k > 32) return 0;
   return (size_t)cout * k * k * cin * 6;

@@ -67,6 +67,9 @@ struct GemmArgs {
   // limb engine: B3 holds -B on the odd blocks of X3_NEGK consecutive k of every row (launch_split_x3_negblk),
   // and the kernel subtracts those blocks' sums (the MFMA's truncation bias then alternates sign; gemm.hip)
   int b_negblk = 0;
+  // limb engine: the A operand is the fp32 tensor A (NHWC), staged as fp32 and split into limbs in registers
+  // (gemm_x3_kernel variant X3_F32A: 4 B per gathered element instead of 6 B of limbs); A3 unused
+  int a_f32 = 0;
   // limb engine, O_PHASE / O_DENSE: split-K over ksplit slices of k_per_z (a multiple of X3_NEGK) when the grid
   // would under-fill the chip; the slices' fp32 tiles go to kslab [zdim * ksplit][M][N] and a fixed-order reduce
   // applies the epilogue.  kslab = scratch the caller owns (kslab_floats of it); null: never split
@@ -93,7 +96,7 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
 // the same for a weight operand whose rows are K long, with the values of the odd X3_NEGK-blocks of each row
 // negated (exact); the GEMM launches that read it set GemmArgs::b_negblk
 #ifndef DAMC_X3_NEGK
-#define DAMC_X3_NEGK 256  // k per sign block = per MFMA accumulation block (gemm.hip X3_FLUSH = X3_NEGK / 32)
+#define DAMC_X3_NEGK 512  // k per sign block = per MFMA accumulation block (gemm.hip X3_FLUSH = X3_NEGK / 32)
 #endif
 constexpr int X3_NEGK = DAMC_X3_NEGK;
 int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s);

@@ -2063,7 +2063,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       // sign blocks per workgroup: the most (a power of two dividing ks) that still leaves >= 256 workgroups, so one
       // round covers the chip (the default 16x16-tile path only); DAMC_X3_KSPLIT_BPW (read per call) pins it
       int bpw = 1;
-      if (V == DAMC_X3_VARIANT && (V & 1) && !(V & (2048 | 65536 | 131072 | 262144))) {
+      if ((V & ~X3_F32A) == DAMC_X3_VARIANT && (V & 1) && !(V & (2048 | 65536 | 131072 | 262144))) {
         const char* eb = getenv("DAMC_X3_KSPLIT_BPW");
         if (eb) {
           bpw = std::max(1, atoi(eb));
@@ -2082,7 +2082,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       if (!a.kslab_reg) bpw = 1;
       a.kbpw = bpw;
       a.k_per_z = a.K / ks * bpw;
-      if constexpr (V == DAMC_X3_VARIANT && OM != O_WGRAD && (V & 1) && (V & 4) &&
+      if constexpr ((V & ~X3_F32A) == DAMC_X3_VARIANT && OM != O_WGRAD && (V & 1) && (V & 4) &&
                     !(V & (32 | 2048 | 65536 | 131072 | 262144 | 524288))) {
         if (a.kslab_reg)
           hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | 1048576>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0,
@@ -2270,10 +2270,12 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
 // launch's gathered x3 tensor stays below 2^31 bytes
 static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
   const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
-  if (!a.A3 || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 || taps % a.kw != 0 || taps > 32)
+  if (!(a.a_f32 ? a.A != nullptr : a.A3 != nullptr) || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 ||
+      taps % a.kw != 0 || taps > 32)
     return DAMC_ERR_ARG;
   if ((om == O_PHASE) != (zdim == 4) || (om == O_DENSE && zdim != 1)) return DAMC_ERR_ARG;
-  if (((uintptr_t)a.A3 | (uintptr_t)a.B3 | (uintptr_t)a.C | (uintptr_t)a.C3 | (uintptr_t)a.mask) % 16 != 0)
+  if (((uintptr_t)a.A3 | (uintptr_t)a.A | (uintptr_t)a.B3 | (uintptr_t)a.C | (uintptr_t)a.C3 | (uintptr_t)a.mask) % 16 !=
+      0)
     return DAMC_ERR_ARG;
   if (!a.C && !a.C3) return DAMC_ERR_ARG;
   if (epi == EPI_MASK && !a.mask && !a.mask_sgn) return DAMC_ERR_ARG;
@@ -2297,7 +2299,8 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   for (long b0 = 0; b0 < nimg; b0 += per) {
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
-    c.A3 = a.A3 + b0 * img * 3;
+    if (a.A3) c.A3 = a.A3 + b0 * img * 3;
+    if (a.a_f32) c.A = a.A + b0 * img;
     if (a.C) c.C = a.C + b0 * cimg;
     if (a.C3) c.C3 = a.C3 + b0 * cimg * 3;
     if (a.sgn) c.sgn = a.sgn + b0 * cimg / 8;
@@ -2308,13 +2311,13 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // (bitwise the default layout: every output takes the same MFMA sequence; 46.6 -> 35.7 us for CIFAR's B = 128
     // first layer, tools/gemm_bench.hip).  DAMC_X3_WIDE=0 (read per call) keeps the default layout
     const char* ew = getenv("DAMC_X3_WIDE");
-    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128) {
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32) {
       if (!(ew && ew[0] == '0')) {
         launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
         continue;
       }
     }
-    if (ew && ew[0] == '2') {  // A/B only: every limb GEMM on the 128 x 256 layout (bitwise the default)
+    if (ew && ew[0] == '2' && !c.a_f32) {  // A/B only: every limb GEMM on the 128 x 256 layout (bitwise the default)
       if (epi == EPI_BIAS_ACT && om == O_PHASE) {
         launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
         continue;
@@ -2324,10 +2327,13 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
         continue;
       }
     }
-#define DAMC_X3(E_, O_)                \
-  if (epi == E_ && om == O_) {         \
-    launch_x3_t<E_, O_>(c, zdim, s);   \
-    continue;                          \
+#define DAMC_X3(E_, O_)                                                  \
+  if (epi == E_ && om == O_) {                                           \
+    if (c.a_f32)                                                         \
+      launch_x3_t<E_, O_, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s);        \
+    else                                                                 \
+      launch_x3_t<E_, O_>(c, zdim, s);                                   \
+    continue;                                                            \
   }
     DAMC_X3(EPI_BIAS_ACT, O_PHASE)
     DAMC_X3(EPI_MASK, O_DENSE)
@@ -2413,7 +2419,7 @@ int launch_gemm_group(const GemmArgs* a, int n, Epi epi, const char* prof_name, 
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return DAMC_ERR_ARG;
-  if (a.A3) {
+  if (a.A3 || (a.a_f32 && a.B3)) {
     if (am != A_CONV) return DAMC_ERR_ARG;
     ProfScope ps(prof_name, flops, s);
     return launch_gemm_x3(a, epi, om, zdim, s);

@@ -644,11 +644,14 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
 // fragments (12 registers) are loaded once, the unit's D fragment and sign bits are loaded one unit ahead, and the
 // unit's 16 x 384 B of limbs leave through a per-wave LDS image as whole 16-B chunks.  Output lane l holds channels
 // 16 i + 4 (l >> 4) + r of pixel l & 15, so the LReLU' nibble of the sign bits applies directly.
-template <int NC, int NG>
+// F32O (round 4): the gradient leaves as fp32 NHWC (4 B per element: the next dgrad stages its A operand as fp32,
+// gemm.hip X3_F32A) through a per-wave image of 272-B pixel rows (8 rows of a ds_write_b128 group on 8 distinct
+// 4-bank groups), 4 wave-instructions of 16-B stores per unit; the values are the limb form's before its split.
+template <int NC, int NG, bool F32O = false>
 __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix, int Hin, int Win,
                                                                       const float* __restrict__ wpk,
                                                                       const float* __restrict__ delta,
-                                                                      float mask_slope, unsigned short* __restrict__ h3,
+                                                                      float mask_slope, void* __restrict__ outp,
                                                                       const unsigned char* __restrict__ hbits,
                                                                       int probe = 0) {
   // probe (tools/smallc_bench.hip only, wrong results): 1 no delta / sign-bit loads, 2 no output stores
@@ -686,7 +689,8 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
   // sits in a branch (a store in a divergent branch made the compiler wait vmcnt(0) for it at every unit)
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)delta, (short)0, npix * NC * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)hbits, (short)0, npix * (Cin / 8), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)h3, (short)0, npix * 6 * Cin, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc(outp, (short)0, npix * (F32O ? 4 : 6) * Cin, 0x00020000);
   constexpr int OOB = 0x7FFFFFF0;
   // the unit's loads: D's column for this lane's pixel (k = 8 q .. 8 q + 7) and the pixel's 8 sign-bit bytes of this
   // wave's 64 channels
@@ -743,6 +747,27 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
     for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d1, c[t], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d0, c[t], 0, 0, 0);
+    if constexpr (F32O) {
+      constexpr int FROW = 272;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const unsigned nib = ((t < 2 ? m0w : m1w) >> (16 * (t & 1) + nsh)) & 15u;
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = c[t][r] * (((nib >> r) & 1u) ? 1.f : mask_slope);
+        *reinterpret_cast<f32x4*>(stg + m * FROW + (16 * t + 4 * q) * 4) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cidx = lane + 64 * j, px = cidx >> 4, w = cidx & 15;
+        const u4 v = *reinterpret_cast<const u4*>(stg + px * FROW + w * 16);
+        const bool ok = un * 16 + px < npix && !(probe & 2);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, ok ? ((un * 16 + px) * Cin + wave * 64) * 4 + w * 16 : OOB, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       // channels 64 w + 16 t + 4 q .. + 3: byte 2 t + (q >> 1) of the wave's 8, nibble q & 1
@@ -779,6 +804,7 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, u4{lo[0], lo[1], hi[0], hi[1]}), ro,
                                              ok ? (un * 16 + px) * 6 * Cin + wave * 384 + w * 16 : OOB, 0, 0);
     }
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
@@ -788,7 +814,7 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
 bool smallc_k3_mfma_ok(const damc_layer_t& L) { return L.cin == 128 || L.cin == 256; }
 
 int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta, float mask_slope,
-                                unsigned short* h3, const unsigned char* hbits, hipStream_t s) {
+                                unsigned short* h3, const unsigned char* hbits, hipStream_t s, float* out32 = nullptr) {
   const int npix = B * L.hin * L.win;
   const int units = (npix + 15) / 16;
   static const int gmax = [] {  // DAMC_SMALLC_DGRAD_GRID: A/B of the persistent grid size
@@ -798,8 +824,12 @@ int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta
   const int grid = std::max(1, std::min(units, gmax));
   const int ng = L.cin / 64;
 #define SDM(NC_, NG_)                                                                                              \
-  hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin, L.win, \
-                     L.w_fwd, delta, mask_slope, h3, hbits)
+  if (out32)                                                                                                       \
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, true>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin, \
+                       L.win, L.w_fwd, delta, mask_slope, (void*)out32, hbits);                                    \
+  else                                                                                                             \
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin,     \
+                       L.win, L.w_fwd, delta, mask_slope, (void*)h3, hbits)
   if (L.cout == 3 && ng == 4) SDM(3, 4);
   else if (L.cout == 3) SDM(3, 2);
   else if (ng == 4) SDM(1, 4);
@@ -1214,8 +1244,9 @@ bool smallc_k3(const damc_layer_t& L) {
 }
 
 
+// f32_out (with sign bits, limb engine): the MFMA kernel writes the fp32 gradient into h instead of limbs into h3
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
-                 unsigned short* h3, const unsigned char* hbits_in, hipStream_t s) {
+                 unsigned short* h3, const unsigned char* hbits_in, hipStream_t s, bool f32_out = false) {
   if (h3 && !smallc_x3_ok(L)) return DAMC_ERR_ARG;
   if (hbits_in && (!smallc_k3(L) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
   if (smallc_k3(L)) {
@@ -1223,6 +1254,9 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
     // the Langevin path (sign bits in, limbs out) on the limb engine; DAMC_SMALLC_DGRAD_MFMA=0 (read per call)
     // selects the VALU kernel below
     const char* mf = getenv("DAMC_SMALLC_DGRAD_MFMA");
+    if (f32_out && hbits_in && smallc_k3_mfma_ok(L) && (double)B * L.hin * L.win * 6 * L.cin < 2147483647.0)
+      return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, nullptr, hbits_in, s, h);
+    if (f32_out) return DAMC_ERR_ARG;
     if (h3 && hbits_in && smallc_k3_mfma_ok(L) && (double)B * L.hin * L.win * 6 * L.cin < 2147483647.0 &&
         !(mf && mf[0] == '0'))
       return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, h3, hbits_in, s);
@@ -1498,8 +1532,10 @@ double conv_flops(const damc_layer_t& L, int B) {
 
 // forward of layers [0, n-1) into ws.h; returns 0 on success.  z3_ready: ws.z3 already holds z's limbs (the previous
 // posterior update wrote them)
+// f32a: limb-engine convolutions gather their input as fp32 (gemm.hip X3_F32A), so every activation is stored fp32
+// and no limb copy is written
 int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& ws, hipStream_t s,
-                   bool z3_ready = false) {
+                   bool z3_ready = false, bool f32a = false) {
   for (int i = 0; i + 1 < g->n_layers; ++i) {
     const damc_layer_t& L = g->layers[i];
     GemmArgs a;
@@ -1529,11 +1565,11 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.K = L.cin;
       a.k_per_z = a.K;
       if (g->n_layers > 1 && x3_fwd(g->layers[1])) {
-        a.C3 = ws.h3[0];
+        if (!f32a) a.C3 = ws.h3[0];
         wrote_x3 = true;
       }
       if (hbits(g, 0)) a.sgn = ws.hb[0];
-      if (!h_f32(g, 0)) a.C = nullptr;
+      if (!h_f32(g, 0) && !f32a) a.C = nullptr;
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
                              2.0 * B * (double)N * L.cin, s);
     } else if (L.kind == DAMC_LAYER_PROJ && damc::conv_kmajor_ok(L.cin)) {
@@ -1585,15 +1621,18 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.Hout = L.hout;
       a.Wout = L.wout;
       if (x3_fwd(L)) {
-        a.A3 = ws.h3[i - 1];
+        if (f32a)
+          a.a_f32 = 1;  // A = ws.h[i - 1] as fp32
+        else
+          a.A3 = ws.h3[i - 1];
         a.B3 = x3_of(L.w_fwd, up2_floats(L));
         a.b_negblk = 1;
         if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {  // the next layer's operand
-          a.C3 = ws.h3[i];
+          if (!f32a) a.C3 = ws.h3[i];
           wrote_x3 = true;
         }
         if (hbits(g, i)) a.sgn = ws.hb[i];
-        if (!h_f32(g, i)) a.C = nullptr;
+        if (!h_f32(g, i) && !f32a) a.C = nullptr;
         a.kslab = ws.kslab;  // split-K when the batch leaves the grid under-filled
         a.kslab_floats = ws.kslab_floats;
       }
@@ -1650,8 +1689,11 @@ int forward_final(const damc_generator_t* g, int B, const float* z, const float*
 // input gradient of layer i >= 1 from d (the gradient w.r.t. its pre-activation), masked with the
 // activation derivative of layer i-1: the result (the pre-activation gradient of layer i-1) overwrites
 // ws.h[i-1] and/or, when only a limb-engine dgrad reads it, ws.h3[i-1] (*x3_only = true)
+// f32a: the gradients limb-engine dgrads read are stored fp32 (d_f32: the incoming d is fp32 even where a limb copy
+// would have been read); *f32_out reports the form written
 int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const float* d, bool* x3_only,
-                hipStream_t s) {
+                hipStream_t s, bool f32a = false, bool d_f32 = false, bool* f32_out = nullptr) {
+  if (f32_out) *f32_out = false;
   {
     const damc_layer_t& L = g->layers[i];
     const damc_layer_t& P = g->layers[i - 1];
@@ -1659,9 +1701,11 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
     int rc;
     bool x3_out = false;  // the gradient went straight into its x3 copy
     if (L.kind == DAMC_LAYER_SMALLC) {
-      x3_out = x3_bwd(P) && smallc_x3_ok(L);
+      const bool fo = f32a && x3_bwd(P) && hbits(g, i - 1) && smallc_k3(L) && smallc_k3_mfma_ok(L);
+      x3_out = !fo && x3_bwd(P) && smallc_x3_ok(L);
       rc = smallc_dgrad(L, out, B, d, P.act, P.slope, x3_out ? ws.h3[i - 1] : nullptr,
-                        hbits(g, i - 1) ? ws.hb[i - 1] : nullptr, s);
+                        hbits(g, i - 1) ? ws.hb[i - 1] : nullptr, s, fo);
+      if (fo && f32_out) *f32_out = true;
     } else if (L.kind == DAMC_LAYER_UP2) {
       const bool x3 = x3_bwd(L);
       GemmArgs a;
@@ -1688,7 +1732,10 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
       a.mask_act = P.act;
       a.mask_slope = P.slope;
       if (x3) {
-        a.A3 = ws.h3[i];
+        if (d_f32)
+          a.a_f32 = 1;  // A = d as fp32
+        else
+          a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
         a.b_negblk = 1;
         a.kslab = ws.kslab;
@@ -1697,7 +1744,9 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
           a.mask_sgn = ws.hb[i - 1];
           a.mask = nullptr;
         }
-        if (x3_bwd(P)) {  // only the next dgrad reads this gradient: limbs only, the fp32 activation stays
+        if (x3_bwd(P) && f32a && hbits(g, i - 1)) {  // the next dgrad gathers this gradient as fp32
+          if (f32_out) *f32_out = true;
+        } else if (x3_bwd(P)) {  // only the next dgrad reads this gradient: limbs only, the fp32 activation stays
           a.C3 = ws.h3[i - 1];
           a.C = nullptr;
           x3_out = true;
@@ -1723,7 +1772,7 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
                              2.0 * B * (double)L.cin * L.cout, s);
     }
     if (rc) return rc;
-    if (x3_bwd(P) && !x3_out) {  // the next dgrad reads this gradient through the limb engine
+    if (x3_bwd(P) && !x3_out && !(f32_out && *f32_out)) {  // the next dgrad reads this gradient through the limb engine
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(out, act_floats(P, B), ws.h3[i - 1], s))) return rc;
     }
@@ -1762,14 +1811,16 @@ int dz_slabs(const damc_generator_t* g, int B, Workspace& ws, const float* d, hi
                            2.0 * B * (double)K * L0.cin, s);
 }
 
-// backward from ws.delta to the PROJ/first-layer split-K slabs
-int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s) {
+// backward from ws.delta to the PROJ/first-layer split-K slabs (f32a: see dgrad_layer)
+int backward(const damc_generator_t* g, int B, Workspace& ws, hipStream_t s, bool f32a = false) {
   const float* d = ws.delta;  // gradient w.r.t. the pre-activation of layer i (current)
+  bool d_f32 = false;
   for (int i = g->n_layers - 1; i >= 1; --i) {
-    bool x3_only = false;
-    int rc = dgrad_layer(g, B, ws, i, d, &x3_only, s);
+    bool x3_only = false, fo = false;
+    int rc = dgrad_layer(g, B, ws, i, d, &x3_only, s, f32a, d_f32, &fo);
     if (rc) return rc;
     d = ws.h[i - 1];
+    d_f32 = fo;
   }
   return dz_slabs(g, B, ws, d, s);
 }
@@ -2179,13 +2230,17 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   // z's limbs for the next step's first layer; DAMC_POST_FUSE=0 (read per call) keeps the separate kernels
   const char* pf = getenv("DAMC_POST_FUSE");
   const bool fuse = !(pf && pf[0] == '0');
+  // DAMC_X3_F32A (read per call): the limb-engine convolutions gather fp32 activations and gradients (gemm.hip
+  // X3_F32A), bitwise the limb-gathering form
+  const char* fa = getenv("DAMC_X3_F32A");
+  const bool f32a = fa && fa[0] == '1';
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;
   bool z3_ready = false;
   for (int i = 0; i < n_steps; ++i) {
     float* dg = diag ? diag + 4 * i : nullptr;
-    if ((rc = forward_hidden(g, z, B, ws, s, z3_ready))) return rc;
+    if ((rc = forward_hidden(g, z, B, ws, s, z3_ready, f32a))) return rc;
     if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s))) return rc;
-    if ((rc = backward(g, B, ws, s))) return rc;
+    if ((rc = backward(g, B, ws, s, f32a))) return rc;
     const float* nz_i = noise ? noise + (size_t)i * B * g->nz : nullptr;
     const long n = (long)B * g->nz;
     // fused only where slab_sum takes its slab_sum4 order (the order the update kernel reproduces)

@@ -246,6 +246,9 @@ typedef struct {
 } damc_encoder_t;
 /* bytes of the limb copy of a packed conv weight (0: the layer does not run on the limb engine) */
 size_t damc_conv2d_x3_bytes(int cout, int cin, int k);
+/* k per sign block of the limb engine's weight operands (odd blocks stored negated; = its MFMA accumulation block
+ * and its split-K granule): the build's DAMC_X3_NEGK, 512 by default */
+int damc_x3_sign_block(void);
 /* a Conv2d weight in its PyTorch layout (cout, cin, k, k), cin % 32 == 0 -> the limb engine's B operand of the
  * conv (damc_conv2d_x3_bytes bytes), in one pass */
 int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream);

@@ -337,7 +337,7 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
 
 @pytest.mark.parametrize("B", [4, 16])
 def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
-    """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one 256-k sign block per slice, reduced
+    """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block (damc_x3_sign_block() k) per slice, reduced
     in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
     width with DAMC_X3_KSPLIT=0 vs the default."""
     from damc import synth
@@ -394,6 +394,31 @@ def test_fused_posterior_update_is_bitwise(lv, gpu_device, monkeypatch, B):
         monkeypatch.setenv("DAMC_POST_FUSE", mode)
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
+        torch.cuda.synchronize()
+        out[mode] = z.cpu()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
+
+
+@pytest.mark.parametrize("name,B", [("cifar10", 16), ("cifar10", 128), ("svhn", 64), ("celeba64", 32)])
+def test_f32a_posterior_is_bitwise(lv, gpu_device, monkeypatch, name, B):
+    """DAMC_X3_F32A=1: the limb-engine convolutions gather fp32 activations / gradients and split them into limbs in
+    registers (gemm.hip X3_F32A), the output layer's dgrad writes fp32: 2 noisy posterior steps bitwise equal to the
+    limb-gathering path (B=16 runs split-K with register slabs, B=128 unsplit)."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    ctor, nz, ngf, hw = {"cifar10": ("_netG_cifar10", 128, 128, 32), "svhn": ("_netG_svhn", 100, 64, 32),
+                         "celeba64": ("_netG_celeba64", 100, 128, 64)}[name]
+    G = synth.load_into(getattr(dn, ctor)(nz=nz, ngf=ngf, nc=3), 0).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=nz), 10).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(11, 0, (B, 3, hw, hw))).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(12, 0, (B, nz))).to(gpu_device)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_X3_F32A", mode)
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=5)
         torch.cuda.synchronize()
         out[mode] = z.cpu()
     assert torch.isfinite(out["1"]).all()

@@ -155,7 +155,7 @@ def test_z_update_hook_vs_oracle(gpu_device):
 @pytest.mark.parametrize("cout,cin,k", [(16, 64, 4), (24, 32, 4), (40, 512, 4), (8, 32, 3), (16, 64, 1), (8, 32, 5)])
 def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     """damc_pack_conv2d_x3 (the encoder's per-call weight operand, Encoder_* convs, diffusion_net.py:227-372):
-    PyTorch (cout, cin, k, k) -> K-major [co][(ky, kx, ci)] with the odd 256-k blocks negated, as three RNE bf16
+    PyTorch (cout, cin, k, k) -> K-major [co][(ky, kx, ci)] with the odd sign blocks negated, as three RNE bf16
     limbs h = bf16(v), m = bf16(v - h), l = bf16(v - h - m) per 8-value octet; bit-exact against the same split in
     torch (k * k % 4 == 0 takes the tap-vectorised kernel, the rest the per-octet one)."""
     from damc import _lib
@@ -172,7 +172,8 @@ def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     torch.cuda.synchronize()
     K = k * k * cin
     v = w.permute(0, 2, 3, 1).reshape(cout, K)
-    sg = torch.where((torch.arange(K) // 256) % 2 == 1, -1.0, 1.0)
+    nk = int(L.damc_x3_sign_block())  # k per sign block
+    sg = torch.where((torch.arange(K) // nk) % 2 == 1, -1.0, 1.0)
     v = v * sg
     h = v.to(torch.bfloat16)
     r1 = v - h.float()

@@ -254,7 +254,7 @@ int main(int argc, char** argv) {
   }
   // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only,
   // 4096 = DMA from one L2-hot 64 KB window
-  V vars[] = {{"v261", run_x3<261, 1>}, {"f32a", run_x3<261 | X3_F32A, 1>}};
+  V vars[] = {{"v261", run_x3<261, 1>}, {"f32a", run_x3<261 | X3_F32A, 1>}, {"wide", run_x3<261 | 524288, 1>}};
   const int NV = sizeof(vars) / sizeof(vars[0]);
   // accuracy against an fp64 reference on sampled outputs (normalised by sum |a b|)
   {
@@ -308,6 +308,30 @@ int main(int argc, char** argv) {
         if (ms < best[si][v]) best[si][v] = ms;
       }
   CK(hipGetLastError());
+  // sustained load (the bench's regime: the chip lowers its clock under minutes of MFMA work, MI355X_MICROARCH.md
+  // DVFS give-back): per shape, variants alternate in blocks of 100 back-to-back launches, 6 blocks each after 100
+  // warm-up launches; mean of the variant's blocks
+  std::vector<std::vector<double>> sus(shapes.size(), std::vector<double>(NV, 0.0));
+  for (size_t si = 0; si < shapes.size(); ++si) {
+    for (int k = 0; k < 100; ++k) vars[0].fn(shapes[si], s);
+    for (int blk = 0; blk < 6; ++blk)
+      for (int v = 0; v < NV; ++v) {
+        CK(hipEventRecord(e0, s));
+        for (int k = 0; k < 100; ++k) vars[v].fn(shapes[si], s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        sus[si][v] += ms / 100 / 6;
+      }
+  }
+  printf("B=%d  sustained (6 x 100 launches, alternating) mean ms\n", B);
+  for (size_t si = 0; si < shapes.size(); ++si) {
+    printf("%-28s", shapes[si].name);
+    for (int v = 0; v < NV; ++v)
+      printf("  %s %.3f (%.1f)", vars[v].name, sus[si][v], shapes[si].flops / (sus[si][v] * 1e-3) / 1e12);
+    printf("\n");
+  }
   printf("B=%d  best-of-%d ms (TFLOP/s)\n", B, rounds);
   for (size_t si = 0; si < shapes.size(); ++si) {
     printf("%-28s", shapes[si].name);
