@@ -33,9 +33,10 @@ Q_NAMES = ["q_cifar10_s", "q_cifar10_small", "q_svhn_s", "q_celeba64_s", "q_cele
 # sqrt(1+e^-l) every step, so the reference's own fp32 result sits 3e-4 .. 8e-2 from an fp64 evaluation of the same
 # sweep (|reference - fp64|, per case).  Bound: 1.5x the largest |hip - reference| measured over the posterior and
 # prior sweeps of two rounds' GPU runs (profiles/r02/sweep_end_distances.txt, profiles/r03/sweep_end_distances.txt),
-# rounded up (q_cifar10_s / q_cifar10_full keep round 2's tighter 2e-2: measured 1.64e-2 / 1.67e-2).
+# rounded up (q_cifar10_s keeps round 2's tighter 2e-2: measured 1.64e-2).  q_cifar10_full: 1.5x round 4's largest
+# |hip - reference| over four GPU runs (8.0e-3; gpurun_out r4a/r4d/r4e logs).
 Q_END_TOL = {"q_cifar10_s": 2e-2, "q_cifar10_small": 1.35e-1, "q_svhn_s": 1.1e-3, "q_celeba64_s": 1.0e-1,
-             "q_celebaHQ_s": 9e-2, "q_mnist_s": 9e-2, "q_cifar10_full": 2e-2}
+             "q_celebaHQ_s": 9e-2, "q_mnist_s": 9e-2, "q_cifar10_full": 1.25e-2}
 
 
 def pytest_configure(config):
