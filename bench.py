@@ -34,6 +34,7 @@ import torch  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 (= f32 MFMA rate), MI355X_MICROARCH.md
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, no sparsity), MI355X_MICROARCH.md
+PEAK_CLOCK_GHZ = 2.4  # the engine clock the dense peaks are quoted at (MI355X_MICROARCH.md)
 LIMB_PRODUCTS = 6          # limb engine: 6 bf16 MFMA products per fp32 product (csrc/gemm.hip)
 B, NZ, NGF = 128, 128, 128
 POST_STEPS, PRIOR_STEPS = 30, 60
@@ -586,6 +587,16 @@ def main():
     torch.cuda.synchronize(device)
     L.damc_prof_enable(0)
     breakdown = query()
+    # the clock the dominant kernel's K loops hold, from in-kernel stamps (damc_clock_probe) over one more untimed
+    # block right behind the timed ones (MI355X_MICROARCH.md, DVFS give-back item 6)
+    clk = torch.zeros(4096 * 4, dtype=torch.int64, device=device)
+    L.damc_clock_probe(clk.data_ptr(), 4096)
+    one_block(lv, G, E, x, z0, p0, zbuf, pbuf, 3001, plan)
+    torch.cuda.synchronize(device)
+    L.damc_clock_probe(None, 0)
+    cs = clk.view(-1, 4).cpu().double()
+    ok = cs[:, 3] > cs[:, 1]
+    clock_ghz = float(((cs[ok, 2] - cs[ok, 0]) / (cs[ok, 3] - cs[ok, 1])).median()) * 0.1 if ok.any() else None
 
     t_max = max_over_ranks(elapsed)
     # the dominant class's mean launch time, max over ranks (a strong-scaling rank's per-rank batch)
@@ -667,6 +678,11 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
                 "traffic": traffic,
+                "clock_ghz": round(clock_ghz, 3) if clock_ghz else None,
+                "frac_at_clock": round(achieved / (peak * clock_ghz / PEAK_CLOCK_GHZ), 4) if clock_ghz else None,
+                "clock_basis": "median over the workgroups of one upconv_fwd launch of d(s_memtime) / "
+                               "d(s_memrealtime) x 100 MHz around the K loop, one untimed block after the timed ones; "
+                               "peak is quoted at %.1f GHz" % PEAK_CLOCK_GHZ,
                 "peak_basis": ("limb engine: fp32 FLOP at the bf16 dense MFMA peak %.0f / %d limb products "
                                "(executed bf16 MFMA %.0f TFLOP/s)" % (PEAK_BF16_TFLOPS, LIMB_PRODUCTS,
                                                                        achieved * LIMB_PRODUCTS)) if limb

@@ -70,6 +70,10 @@ struct GemmArgs {
   // limb engine: the A operand is the fp32 tensor A (NHWC), staged as fp32 and split into limbs in registers
   // (gemm_x3_kernel variant X3_F32A: 4 B per gathered element instead of 6 B of limbs); A3 unused
   int a_f32 = 0;
+  // clock probe (damc_clock_probe; diagnostics, off in timed work): thread 0 of each workgroup stores {s_memtime,
+  // s_memrealtime} before its K loop and after it, at clk[4 * (workgroup % clk_n)]
+  unsigned long long* clk = nullptr;
+  int clk_n = 0;
   // limb engine, O_PHASE / O_DENSE: split-K over ksplit slices of k_per_z (a multiple of X3_NEGK) when the grid
   // would under-fill the chip; the slices' fp32 tiles go to kslab [zdim * ksplit][M][N] and a fixed-order reduce
   // applies the epilogue.  kslab = scratch the caller owns (kslab_floats of it); null: never split

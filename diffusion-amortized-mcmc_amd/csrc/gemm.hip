@@ -884,6 +884,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = WIDE ? wave >> 2 : wave >> 1, wn = WIDE ? wave & 3 : wave & 1;
+  unsigned long long clk_t0 = 0, clk_r0 = 0;
+  if (p.clk && tid == 0) {
+    clk_t0 = __builtin_amdgcn_s_memtime();
+    clk_r0 = __builtin_amdgcn_s_memrealtime();
+  }
   constexpr bool RASTER = (V & 16) != 0 && OM != O_WGRAD;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntn = (p.N + BN - 1) / BN;
@@ -1793,6 +1798,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
     kloop(std::false_type{});
 
   }
+  if (p.clk && tid == 0) {  // the K loop's shader clocks over its 100 MHz ticks (damc_clock_probe)
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* c = p.clk + 4 * ((blockIdx.z * gridDim.x + blockIdx.x) % (unsigned)p.clk_n);
+    c[0] = clk_t0;
+    c[1] = clk_r0;
+    c[2] = t1;
+    c[3] = r1;
+  }
   if (KREG) return;  // every block already in its slab
   // the last partial block
   {
@@ -2268,6 +2281,10 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
 
 // limb-engine dispatch (A3 / B3 set, A_CONV geometry as the K-major engine); splits the batch so every
 // launch's gathered x3 tensor stays below 2^31 bytes
+// damc_clock_probe: the buffer O_PHASE limb-engine launches stamp (null: off)
+static unsigned long long* g_clk = nullptr;
+static int g_clk_n = 0;
+
 static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
   const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
   if (!(a.a_f32 ? a.A != nullptr : a.A3 != nullptr) || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 ||
@@ -2299,6 +2316,10 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   for (long b0 = 0; b0 < nimg; b0 += per) {
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
+    if (om == O_PHASE && g_clk) {
+      c.clk = g_clk;
+      c.clk_n = g_clk_n;
+    }
     if (a.A3) c.A3 = a.A3 + b0 * img * 3;
     if (a.a_f32) c.A = a.A + b0 * img;
     if (a.C) c.C = a.C + b0 * cimg;
@@ -2467,9 +2488,19 @@ int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const 
   return DAMC_ERR_UNSUPPORTED;
 }
 
+void set_clock_probe(unsigned long long* buf, int n) {
+  g_clk = (buf && n > 0) ? buf : nullptr;
+  g_clk_n = g_clk ? n : 0;
+}
+
 }  // namespace damc
 
 #ifndef DAMC_GEMM_NO_C_API
+extern "C" int damc_clock_probe(unsigned long long* buf, int n_slots) {
+  damc::set_clock_probe(buf, n_slots);
+  return 0;
+}
+
 extern "C" int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc,
                          int m, int n, int k, int act, float slope, void* stream) {
   damc::GemmArgs g;

@@ -249,6 +249,11 @@ size_t damc_conv2d_x3_bytes(int cout, int cin, int k);
 /* k per sign block of the limb engine's weight operands (odd blocks stored negated; = its MFMA accumulation block
  * and its split-K granule): the build's DAMC_X3_NEGK, 512 by default */
 int damc_x3_sign_block(void);
+/* diagnostics: while buf (n_slots * 4 uint64, device memory) is set, every k4 s2 ConvT forward on the limb engine
+ * stores, per workgroup w at buf[4 (w % n_slots)], {s_memtime, s_memrealtime} before and after its K loop: the
+ * clock the chip holds in that loop is d(memtime) / d(realtime) x 100 MHz.  buf = NULL switches it off.  Not
+ * thread-safe; keep it off in timed work (bench.py runs it on one extra block). */
+int damc_clock_probe(unsigned long long* buf, int n_slots);
 /* a Conv2d weight in its PyTorch layout (cout, cin, k, k), cin % 32 == 0 -> the limb engine's B operand of the
  * conv (damc_conv2d_x3_bytes bytes), in one pass */
 int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream);
