@@ -74,6 +74,13 @@ struct GemmArgs {
   // s_memrealtime} before its K loop and after it, at clk[4 * (workgroup % clk_n)]
   unsigned long long* clk = nullptr;
   int clk_n = 0;
+  // fused output-layer projection (O_PHASE, EPI_BIAS_ACT, N <= 256): after the epilogue, every output pixel's
+  // activated row h (N channels) is projected on the next layer's packed weights, proj_out[pixel][n] =
+  // sum_c h[c] proj_w[n][c] for n < proj_np (launch_proj_rows has the same arithmetic); proj_nostore: h itself
+  // (C) is not written (set by the launcher only where the projection ran in this kernel)
+  const float* proj_w = nullptr;
+  float* proj_out = nullptr;
+  int proj_np = 0, proj_ldw = 0, proj_nostore = 0;
   // limb engine, O_PHASE / O_DENSE: split-K over ksplit slices of k_per_z (a multiple of X3_NEGK) when the grid
   // would under-fill the chip; the slices' fp32 tiles go to kslab [zdim * ksplit][M][N] and a fixed-order reduce
   // applies the epilogue.  kslab = scratch the caller owns (kslab_floats of it); null: never split
@@ -87,6 +94,9 @@ struct GemmArgs {
   // [tile][wave][4 x 4 tiles][64 lanes] f32x4 (16-B stores straight from the accumulators; the reduce maps back)
   int kslab_reg = 0;
 };
+// the fused output-layer projection as a kernel of its own: P[pix][n] = sum_c h[pix][c] w[n][c] (c < C <= 256,
+// C % 16 == 0; n < np, np = 32 or 64; w rows ldw floats), bitwise the fused form (same MFMA sequence per row)
+int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, hipStream_t s);
 // slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
 long x3_ksplit_floats(int M, int N, int K, int zdim);
 

@@ -856,6 +856,67 @@ __device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf1
   }
 }
 
+// Output-layer projection of 16 rows of an LDS tile (row stride ts floats, C channels, C % 16 == 0) on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation): lane (row m = lane & 15, quarter q = lane >> 4) reads
+// the f32x4 run c = 16 g + 4 q .. + 3 of its row and of weight row n = 16 t + m, element e feeding MFMA step e (one k
+// bijection for both operands).  acc[t][r] = P[row r0 + 4 q + r][16 t + m].  gemm_x3_kernel's fused epilogue and
+// proj_rows_kernel share it, so the two forms are bitwise equal.
+template <int NT>
+__device__ __forceinline__ void proj16(const float* tile, int ts, int r0, int C, const float* w, int ldw,
+                                       f32x4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63, m = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < C / 16; ++g) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(tile + (r0 + m) * ts + 16 * g + 4 * q);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(w + (long)(16 * t + m) * ldw + 16 * g + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc[t], 0, 0, 0);
+    }
+  }
+}
+
+// the projection alone: 128 pixels per workgroup (8 waves x 16 rows) staged in LDS with gemm_x3_kernel's WIDE tile
+// stride, then proj16 (NT = np / 16)
+template <int NT>
+__global__ __launch_bounds__(512) void proj_rows_kernel(const float* __restrict__ h, long npix, int C,
+                                                        const float* __restrict__ w, int ldw, float* __restrict__ P) {
+  constexpr int TS = 256 + 4;
+  __shared__ __attribute__((aligned(16))) float tile[128 * TS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long p0 = (long)blockIdx.x * 128;
+  const int c4 = C / 4;
+  for (int i = tid; i < 128 * c4; i += 512) {
+    const int r = i / c4, c = (i - r * c4) * 4;
+    const long pix = p0 + r;
+    *reinterpret_cast<f32x4*>(tile + r * TS + c) =
+        pix < npix ? *reinterpret_cast<const f32x4*>(h + pix * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  f32x4 acc[NT];
+  proj16<NT>(tile, TS, wave * 16, C, w, ldw, acc);
+  const int m = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long pix = p0 + wave * 16 + 4 * q + r;
+      if (pix < npix) P[pix * (16 * NT) + 16 * t + m] = acc[t][r];
+    }
+}
+
+int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, hipStream_t s) {
+  if (C <= 0 || C > 256 || C % 16 || (np != 32 && np != 64) || npix <= 0) return DAMC_ERR_ARG;
+  const dim3 grid((unsigned)((npix + 127) / 128));
+  if (np == 32)
+    hipLaunchKernelGGL(proj_rows_kernel<2>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P);
+  else
+    hipLaunchKernelGGL(proj_rows_kernel<4>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
 __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool M16 = (V & 1) != 0;
@@ -1916,7 +1977,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       for (int e = 0; e < 8; ++e) bits |= (v[e] > 0.f ? 1u : 0u) << e;
       p.sgn[idx >> 3] = (unsigned char)bits;
     }
-    if (Cz) {
+    if (Cz && !p.proj_nostore) {
       *reinterpret_cast<f32x4*>(Cz + idx) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(Cz + idx + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
@@ -1927,6 +1988,34 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
       o[0] = h;
       o[1] = m;
       o[2] = l;
+    }
+    if (OM == O_PHASE && EPI == EPI_BIAS_ACT && WIDE && p.proj_out) {  // the activated row back into the tile
+      *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+  if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT && WIDE) {
+    // fused output-layer projection (GemmArgs::proj_out; the launcher sets it only when this tile holds every channel,
+    // n0 == 0 and N <= BN): 8 waves x 16 rows, proj16 as proj_rows_kernel, P indexed by the output pixel
+    if (p.proj_out) {
+      __syncthreads();
+      const int m = lane & 15, q = lane >> 4;
+      auto store = [&](auto NT_) {
+        constexpr int NT = decltype(NT_)::value;
+        f32x4 acc[NT];
+        proj16<NT>(tile, TS, wave * 16, p.N, p.proj_w, p.proj_ldw, acc);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long ro = rowtab[wave * 16 + 4 * q + r];
+            if (ro >= 0) p.proj_out[(ro / p.ldc) * (16 * NT) + 16 * t + m] = acc[t][r];
+          }
+      };
+      if (p.proj_np == 32)
+        store(std::integral_constant<int, 2>{});
+      else
+        store(std::integral_constant<int, 4>{});
     }
   }
 }
@@ -2073,6 +2162,12 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
       a.ksplit = ks;
+      a.proj_nostore = 0;  // the reduce writes C; the projection then runs as proj_rows_kernel over it
+      auto proj_after = [&]() {
+        if (OM == O_PHASE && a.proj_out)
+          (void)launch_proj_rows(a.C, (long)(a.M / (a.Hq * a.Wq)) * a.Hout * a.Wout, a.N, a.proj_w, a.proj_ldw,
+                                 a.proj_np, a.proj_out, s);
+      };
       // sign blocks per workgroup: the most (a power of two dividing ks) that still leaves >= 256 workgroups, so one
       // round covers the chip (the default 16x16-tile path only); DAMC_X3_KSPLIT_BPW (read per call) pins it
       int bpw = 1;
@@ -2110,11 +2205,13 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
         const long waves = (long)zdim * ntm * ntn * 128;
         hipLaunchKernelGGL((x3_ksplit_reduce_tile_kernel<EPI, OM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
                            a, zdim);
+        proj_after();
         return;
       }
       const long tot = (long)zdim * a.M * (a.N / 8);
       hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, OM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
                          zdim);
+      proj_after();
       return;
     }
   }
@@ -2319,6 +2416,15 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     if (om == O_PHASE && g_clk) {
       c.clk = g_clk;
       c.clk_n = g_clk_n;
+    }
+    if (a.proj_out) {  // the fused output-layer projection: the 128 x 256 layout, one N tile holding every channel
+      if (om != O_PHASE || epi != EPI_BIAS_ACT || a.N > 256 || a.N % 16 || !a.C || !a.proj_w ||
+          (a.proj_np != 32 && a.proj_np != 64))
+        return DAMC_ERR_ARG;
+      if (c.a_f32) return DAMC_ERR_UNSUPPORTED;  // the F32A loop has no 128 x 256 form
+      c.proj_out = a.proj_out + b0 * (long)a.Hout * a.Wout * a.proj_np;
+      launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+      continue;
     }
     if (a.A3) c.A3 = a.A3 + b0 * img * 3;
     if (a.a_f32) c.A = a.A + b0 * img;

@@ -1159,11 +1159,23 @@ bool smallc_twostage_ok(const damc_layer_t& L) {
   return L.cin % 8 == 0 && smallc_ntile(L) <= 2 && L.w_bwd != nullptr;
 }
 
+// the projection on proj16 (gemm.hip launch_proj_rows; the arithmetic of the fused ConvT epilogue) applies
+bool smallc_proj16_ok(const damc_layer_t& L) { return L.cin <= 256 && L.cin % 16 == 0 && smallc_ntile(L) <= 2; }
+
+// p_ready: Pbuf already holds the projections (the layer before ran them in its epilogue, GemmArgs::proj_out)
 int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta,
-                        float* xhat, float* sqerr, float* Pbuf, hipStream_t s) {
+                        float* xhat, float* sqerr, float* Pbuf, hipStream_t s, bool p_ready = false) {
   ProfScope ps("smallc_fwd", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
   const long npin = (long)B * L.hin * L.win;
   const int nt = smallc_ntile(L);
+  // DAMC_SMALLC_PROJ16=0 (read per call): the round-3 projection kernels below instead of proj16's
+  const char* p16 = getenv("DAMC_SMALLC_PROJ16");
+  const bool use16 = !(p16 && p16[0] == '0') && smallc_proj16_ok(L);
+  int rc = 0;
+  if (p_ready) {
+  } else if (use16) {
+    if ((rc = damc::launch_proj_rows(h, npin, L.cin, L.w_bwd, L.cin, 32 * nt, Pbuf, s))) return rc;
+  } else {
   const int g1 = (int)((npin + 127) / 128);
   // the LDS-staged kernel when Cin is whole 64-channel chunks (CIFAR B=128: 63.5 -> 51.3 us for projection + gather);
   // DAMC_SMALLC_PROJ_LDS=0 (read per call) selects the direct-load kernel
@@ -1190,6 +1202,7 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
     hipLaunchKernelGGL((smallc_proj_kernel<1>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
   else
     hipLaunchKernelGGL((smallc_proj_kernel<2>), dim3(g1), dim3(256), 0, s, h, npin, L.cin, L.w_bwd, Pbuf);
+  }
   const long npout = (long)B * L.hout * L.wout;
   const int g2 = (int)((npout + 255) / 256);
 #define SG(NC_, K_, S_)                                                                                             \
@@ -1205,8 +1218,10 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
 }
 
 int smallc_fwd(const damc_layer_t& L, const float* h, int B, const float* x, float inv_s2, float* delta, float* xhat,
-               float* sqerr, float* Pbuf, hipStream_t s) {
-  if (Pbuf && smallc_twostage_ok(L)) return smallc_fwd_twostage(L, h, B, x, inv_s2, delta, xhat, sqerr, Pbuf, s);
+               float* sqerr, float* Pbuf, hipStream_t s, bool p_ready = false) {
+  if (Pbuf && smallc_twostage_ok(L))
+    return smallc_fwd_twostage(L, h, B, x, inv_s2, delta, xhat, sqerr, Pbuf, s, p_ready);
+  if (p_ready) return DAMC_ERR_ARG;
   if (smallc_reg_ok(L)) {
     ProfScope ps("smallc_fwd", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / (L.stride * L.stride), s);
     if (L.cout == 3)
@@ -1534,8 +1549,9 @@ double conv_flops(const damc_layer_t& L, int B) {
 // posterior update wrote them)
 // f32a: limb-engine convolutions gather their input as fp32 (gemm.hip X3_F32A), so every activation is stored fp32
 // and no limb copy is written
+// proj: the last hidden layer's epilogue also runs the output layer's projection into ws.pbuf (proj_fusable)
 int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& ws, hipStream_t s,
-                   bool z3_ready = false, bool f32a = false) {
+                   bool z3_ready = false, bool f32a = false, bool proj = false) {
   for (int i = 0; i + 1 < g->n_layers; ++i) {
     const damc_layer_t& L = g->layers[i];
     GemmArgs a;
@@ -1635,6 +1651,15 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
         if (!h_f32(g, i) && !f32a) a.C = nullptr;
         a.kslab = ws.kslab;  // split-K when the batch leaves the grid under-filled
         a.kslab_floats = ws.kslab_floats;
+        if (proj && i + 2 == g->n_layers) {  // the output layer's per-tap projections (smallc_fwd_twostage's stage 1)
+          const damc_layer_t& F = g->layers[i + 1];
+          a.proj_w = F.w_bwd;
+          a.proj_ldw = F.cin;
+          a.proj_np = 32 * smallc_ntile(F);
+          a.proj_out = ws.pbuf;
+          a.proj_nostore = 1;  // the activation itself is read by nothing else in a posterior step
+          if (!a.C) a.C = ws.h[i];
+        }
       }
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
@@ -1647,15 +1672,26 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
   return 0;
 }
 
+// the output layer's projection can run in the epilogue of the ConvT before it (limb engine, k4 s2, every channel in
+// one 128 x 256 tile)
+bool proj_fusable(const damc_generator_t* g, const Workspace& ws) {
+  const int n = g->n_layers;
+  if (n < 3 || !ws.pbuf) return false;
+  const damc_layer_t& F = g->layers[n - 1];
+  const damc_layer_t& L = g->layers[n - 2];
+  return F.kind == DAMC_LAYER_SMALLC && smallc_twostage_ok(F) && smallc_proj16_ok(F) && L.kind == DAMC_LAYER_UP2 &&
+         x3_fwd(L) && L.cout == F.cin && F.w_bwd;
+}
+
 // final layer forward: delta (+ optional x_hat NCHW / row-major) and |x_hat-x|^2/(2s^2) into sqerr
 int forward_final(const damc_generator_t* g, int B, const float* z, const float* x, float inv_s2, Workspace& ws,
-                  float* xhat, float* sqerr, bool want_delta, hipStream_t s) {
+                  float* xhat, float* sqerr, bool want_delta, hipStream_t s, bool p_ready = false) {
   const int n = g->n_layers;
   const damc_layer_t& F = g->layers[n - 1];
   const float* hin = n >= 2 ? ws.h[n - 2] : z;
   if (F.kind == DAMC_LAYER_SMALLC)
     return smallc_fwd(F, hin, B, want_delta ? x : nullptr, inv_s2, want_delta ? ws.delta : nullptr, xhat, sqerr,
-                      ws.pbuf, s);
+                      ws.pbuf, s, p_ready);
   // LINEAR final layer
   GemmArgs a;
   a.A = hin;
@@ -2234,12 +2270,15 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   // X3_F32A), bitwise the limb-gathering form
   const char* fa = getenv("DAMC_X3_F32A");
   const bool f32a = fa && fa[0] == '1';
+  // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection
+  const char* sf = getenv("DAMC_SMALLC_FUSE");
+  const bool proj = !(sf && sf[0] == '0') && !f32a && proj_fusable(g, ws);
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;
   bool z3_ready = false;
   for (int i = 0; i < n_steps; ++i) {
     float* dg = diag ? diag + 4 * i : nullptr;
-    if ((rc = forward_hidden(g, z, B, ws, s, z3_ready, f32a))) return rc;
-    if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s))) return rc;
+    if ((rc = forward_hidden(g, z, B, ws, s, z3_ready, f32a, proj))) return rc;
+    if ((rc = forward_final(g, B, z, x, inv_s2, ws, nullptr, dg ? dg + 1 : nullptr, true, s, proj))) return rc;
     if ((rc = backward(g, B, ws, s, f32a))) return rc;
     const float* nz_i = noise ? noise + (size_t)i * B * g->nz : nullptr;
     const long n = (long)B * g->nz;

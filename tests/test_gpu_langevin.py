@@ -423,3 +423,20 @@ def test_f32a_posterior_is_bitwise(lv, gpu_device, monkeypatch, name, B):
         out[mode] = z.cpu()
     assert torch.isfinite(out["1"]).all()
     assert torch.equal(out["0"], out["1"])
+
+
+@pytest.mark.parametrize("B", [16, 128])
+def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B):
+    """The last ConvT's epilogue runs the output layer's per-tap projection (gemm.hip GemmArgs::proj_out, the 128 x 256
+    tile; B=16 splits K, so there the projection runs as proj_rows_kernel over the reduce's output): 2 noisy posterior
+    steps bitwise equal to the separate projection kernel (DAMC_SMALLC_FUSE=0), which shares proj16's arithmetic."""
+    G, E, x, z0 = _cifar_full(gpu_device, B)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_SMALLC_FUSE", mode)
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=9)
+        torch.cuda.synchronize()
+        out[mode] = z.cpu()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
