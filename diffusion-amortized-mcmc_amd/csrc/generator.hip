@@ -1664,7 +1664,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       rc = damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(L, B), s);
     }
     if (rc) return rc;
-    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1]) && !wrote_x3) {
+    if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1]) && !wrote_x3 && !f32a) {
       ProfScope ps("split_x3", 0.0, s);
       if ((rc = damc::launch_split_x3(ws.h[i], act_floats(L, B), ws.h3[i], s))) return rc;
     }
