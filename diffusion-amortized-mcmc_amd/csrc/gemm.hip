@@ -2125,6 +2125,80 @@ __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int 
   }
 }
 
+// Skinny limb GEMM for the first layer at per-rank batches (z . W, M = B <= 32 rows, K <= X3_NEGK: one sign block,
+// a 1 x 1 "convolution" of dense rows): 4 waves per workgroup, each 16 rows x 64 columns; the K tiles go from memory
+// straight into registers (two tiles' 30 loads of 16 B per lane in flight, no LDS staging, no barrier) -- the
+// 128 x 256 kernel streams its 50 MB of weight limbs through a two-deep LDS pipeline that left each workgroup
+// latency-bound at 4 K tiles.  Same fragments (octet q of the tile per lane quarter), the same six-product MFMA
+// sequence and the same block fold (fmaf(+1, acc, 0)), then gemm_x3_kernel's octet epilogue (x3_octet_epilogue):
+// every output is bitwise the 128 x 256 kernel's (tests/test_gpu_langevin.py).
+__global__ __launch_bounds__(256) void x3_skinny_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float st[4][16][64 + 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  const int n0 = (blockIdx.x * 4 + wave) * 64, r0 = blockIdx.y * 16;
+  if (n0 >= p.N) return;  // wave-uniform; the waves share no barrier
+  const int K8 = p.K >> 3, nk = p.K >> 5;
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A3, (short)0, p.M * p.K * 6, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B3, (short)0, p.N * p.K * 6, 0x00020000);
+  constexpr int OOB = 0x7FFFFFF0;
+  const int aoff = (r0 + m < p.M) ? ((r0 + m) * K8 + q) * 48 : OOB;
+  int boff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) boff[t] = (n0 + 16 * t + m < p.N) ? ((n0 + 16 * t + m) * K8 + q) * 48 : OOB;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int off, int kt, int l) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, off == OOB ? 0 : kt * 192 + l * 16, 0));
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    bf16x8 fa[2][3], fb[2][4][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) {
+        fa[u][l] = ld(ra, aoff, kt + u, l);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fb[u][t][l] = ld(rb, boff[t], kt + u, l);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (kt + u >= nk) break;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x4 c = acc[t];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[u][t][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[u][t][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[u][t][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[u][t][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[u][t][1], c, 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[u][t][0], c, 0, 0, 0);
+      }
+    }
+  }
+  // the block fold of gemm_x3_kernel's last partial block (tot = 0, sign block 0 positive), then the epilogue
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[wave][4 * q + r][16 * t + m] = __builtin_fmaf(1.f, acc[t][r], 0.f);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int id = lane + 64 * j, row = id >> 3, oct = id & 7;
+    const int mg = r0 + row, n = n0 + 8 * oct;
+    if (mg >= p.M || n >= p.N) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = st[wave][row][8 * oct + e];
+    x3_octet_epilogue<EPI_BIAS_ACT, O_DENSE>(p, mg, n, 0, 0, v);
+  }
+}
+
 // split-K plan of a limb-engine conv: an under-filled grid (see below; DAMC_X3_KSPLIT_WGS pins the bound) splits K
 // into its X3_NEGK sign blocks, one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
 // the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
@@ -2438,6 +2512,15 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // (bitwise the default layout: every output takes the same MFMA sequence; 46.6 -> 35.7 us for CIFAR's B = 128
     // first layer, tools/gemm_bench.hip).  DAMC_X3_WIDE=0 (read per call) keeps the default layout
     const char* ew = getenv("DAMC_X3_WIDE");
+    // the first layer at per-rank batches: the skinny kernel (bitwise the 128 x 256 layout); DAMC_X3_SKINNY=0 (read
+    // per call) keeps the tiled kernel
+    const char* esk = getenv("DAMC_X3_SKINNY");
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 32 && c.K <= X3_NEGK && c.Hin == 1 && c.Win == 1 &&
+        c.kw == 1 && c.Cg == c.K && c.A3 && !c.a_f32 && !c.proj_out && !(esk && esk[0] == '0')) {
+      hipLaunchKernelGGL(x3_skinny_kernel, dim3((unsigned)((c.N + 255) / 256), (unsigned)((c.M + 15) / 16)), dim3(256),
+                         0, s, c);
+      continue;
+    }
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32) {
       if (!(ew && ew[0] == '0')) {
         launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);

@@ -440,3 +440,19 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B):
         out[mode] = z.cpu()
     assert torch.isfinite(out["1"]).all()
     assert torch.equal(out["0"], out["1"])
+
+
+@pytest.mark.parametrize("B", [8, 16, 32])
+def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
+    """The first layer z . W at per-rank batches (B <= 32) runs on gemm.hip's x3_skinny_kernel (K tiles straight into
+    registers): 2 noisy posterior steps bitwise equal to the 128 x 256 tiled limb kernel (DAMC_X3_SKINNY=0)."""
+    G, E, x, z0 = _cifar_full(gpu_device, B)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_X3_SKINNY", mode)
+        z = z0.clone()
+        lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=13)
+        torch.cuda.synchronize()
+        out[mode] = z.cpu()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
