@@ -747,6 +747,57 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
   }
 }
 
+// The first layer's input gradient at per-rank batches (dz_slabs: M = B <= 32 dense rows as a 1 x 1 "convolution",
+// split-K slices of k_per_z, EPI_STORE into per-slice slabs): one workgroup per (slice, 128 columns), 4 waves of 32
+// columns, every fragment straight from memory into registers with 4 K tiles' loads in flight (the 128 x 128 kernel
+// walks a slice's 8 K tiles through a 2-3 deep LDS pipeline, latency-bound at this size).  The same 32x32x2 MFMA
+// sequence per output (k-quad q, then step s; lane half lk takes k = 8 q + 4 lk + s of each 32-deep tile) from zero
+// per slice, so every slab value is bitwise gemm_km_kernel's.
+__global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lrow = lane & 31, lk = lane >> 5;
+  const int z = blockIdx.x, n0 = blockIdx.y * 128 + wave * 32;
+  const int kbeg = z * p.k_per_z, kend = min(p.K, kbeg + p.k_per_z);
+  const int nk = kend > kbeg ? (kend - kbeg) / KM_BK : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.Cg * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.N * (int)p.ldb * 4, 0x00020000);
+  constexpr int OOB = 0x7FFFFFF0;
+  const int aoff = lrow < p.M ? (lrow * p.Cg + 4 * lk) * 4 : OOB;
+  const int boff = n0 + lrow < p.N ? ((n0 + lrow) * (int)p.ldb + 4 * lk) * 4 : OOB;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int kt = 0; kt < nk; kt += 4) {
+    f32x4 fa[4][4], fb[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool live = kt + u < nk;
+        const int k0 = (kbeg + (kt + u) * KM_BK + 8 * q) * 4;
+        fa[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 ra, live ? aoff : OOB, (live && aoff != OOB) ? k0 : 0, 0));
+        fb[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rb, live ? boff : OOB, (live && boff != OOB) ? k0 : 0, 0));
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kt + u >= nk) break;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][q][s2], fb[u][q][s2], acc, 0, 0, 0);
+    }
+  }
+  float* Cz = p.C + (long)z * p.c_zstride;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = (r & 3) + 8 * (r >> 2) + 4 * lk, n = n0 + lrow;
+    if (m < p.M && n < p.N) Cz[(long)m * p.ldc + n] = acc[r];
+  }
+}
+
 template <int EPI, int OM, int PIPE = DAMC_KM_PIPE, int DBG = 0>
 static void launch_km_t(const GemmArgs& a, int zdim, hipStream_t s) {
   const int ntm = (a.M + KM_BM - 1) / KM_BM, ntn = (a.N + BN - 1) / BN;
@@ -783,6 +834,14 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     c.C = a.C + b0 * cimg;
     if (a.mask) c.mask = a.mask + b0 * cimg;
     c.M = (int)(nb * hwq);
+    // dz_slabs at per-rank batches: km_skinny_kernel (bitwise gemm_km_kernel); DAMC_KM_SKINNY=0 (read per call) keeps
+    // the tiled kernel
+    const char* esk = getenv("DAMC_KM_SKINNY");
+    if (epi == EPI_STORE && om == O_DENSE && c.M <= 32 && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
+        c.kw == 1 && c.Cg == c.K && !(esk && esk[0] == '0')) {
+      hipLaunchKernelGGL(km_skinny_kernel, dim3((unsigned)zdim, (unsigned)((c.N + 127) / 128)), dim3(256), 0, s, c);
+      continue;
+    }
 #define DAMC_KM(E_, O_)                \
   if (epi == E_ && om == O_) {         \
     launch_km_t<E_, O_>(c, zdim, s);   \

@@ -444,12 +444,14 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B):
 
 @pytest.mark.parametrize("B", [8, 16, 32])
 def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
-    """The first layer z . W at per-rank batches (B <= 32) runs on gemm.hip's x3_skinny_kernel (K tiles straight into
-    registers): 2 noisy posterior steps bitwise equal to the 128 x 256 tiled limb kernel (DAMC_X3_SKINNY=0)."""
+    """The first layer at per-rank batches (B <= 32): z . W on gemm.hip's x3_skinny_kernel and its input gradient's
+    split-K slabs on km_skinny_kernel (fragments straight into registers): 2 noisy posterior steps bitwise equal to
+    the tiled kernels (DAMC_X3_SKINNY=0, DAMC_KM_SKINNY=0)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_X3_SKINNY", mode)
+        monkeypatch.setenv("DAMC_KM_SKINNY", mode)
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=13)
         torch.cuda.synchronize()
