@@ -885,6 +885,10 @@ __device__ __forceinline__ int x3_swz(int row) { return (row >> 1) & 3; }
 // takes logical chunks 2q and 2q + 1 in two ds_read_b128; with u = (r >> 1) & 7 and the bit-1 flip on rows 4-11
 // (the rows the b128 lane groups pair with the other octet) every 16-lane group hits 16 distinct 4-bank groups.
 constexpr int X3_F32A = 2097152, X3A_ROWB = 128;
+// X3_NARROW (variant bit 4194304): a 64 x 128 block tile, 8 waves 2 (M) x 4 (N) of 32 x 32 (2 x 2 MFMA tiles each),
+// 74 KB of LDS so two workgroups share a CU: a small-batch conv fills the chip without split-K slabs (every output
+// takes the default tile's MFMA sequence, so it is bitwise the default and the split forms)
+constexpr int X3_NARROW = 4194304;
 __device__ __forceinline__ int f32a_swz(int r) { return ((r >> 1) & 7) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
 constexpr int X3_FLUSH = X3_NEGK / 32;  // K tiles per MFMA accumulation block (power of two)
 static_assert(X3_FLUSH * 32 == X3_NEGK, "sign blocks are accumulation blocks");
@@ -977,7 +981,7 @@ int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, 
 }
 
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
-__global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
+__global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(GemmArgs p) {
   constexpr bool M16 = (V & 1) != 0;
   // 262144: 16-deep K stages in a 4-slot LDS ring (three stages in flight across raw barriers, counted vmcnt), each
   // MFMA taking two limb products over 16 k (P16 main loop below)
@@ -987,7 +991,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   // half-empty tile at M = 128 (the first layer, M = B) and half the A gather per K tile
   constexpr bool WIDE = (V & 524288) != 0;
   static_assert(!(WIDE && P16), "one layout variant at a time");
-  constexpr int BM = WIDE ? 128 : X3_BM, BN = WIDE ? 256 : X3_BN;
+  constexpr bool NARROW = (V & X3_NARROW) != 0;
+  static_assert(!NARROW || (!WIDE && !P16 && M16 && (V & 4) && !(V & (8 | 16 | 32 | 64 | 2048 | 1048576 | 2097152))),
+                "NARROW: the default LDS-DMA tap-major path, unsplit");
+  constexpr int BM = WIDE ? 128 : NARROW ? 64 : X3_BM, BN = WIDE ? 256 : X3_BN;
   // X3_F32A: A staged as fp32 (4 B per element instead of 6 B of limbs) and split into its RNE limbs in registers after
   // the fragment read, the same split as the producing epilogue's, so the MFMA operands and results are bitwise the
   // limb path's; waves 8 along M x 1 along N (each 32 x 128), so every A element is split by one wave only
@@ -996,14 +1003,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
                           !(V & (8 | 16 | 32 | 64 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 131072))),
                 "F32A: the default 16x16-tile LDS-DMA path only");
   constexpr int AROWB = F32A ? X3A_ROWB : X3_ROWB, ESZ = F32A ? 4 : 6;
-  constexpr int AJ = BM * (F32A ? 8 : X3_CHUNKS) / 512, BJ = BN * X3_CHUNKS / 512;
+  constexpr int AJ = (BM * (F32A ? 8 : X3_CHUNKS) + 511) / 512, BJ = BN * X3_CHUNKS / 512;  // NARROW: 1.5 -> 2
   constexpr int BUFB = BM * AROWB + BN * X3_ROWB;  // one LDS buffer (A image, then B image)
   constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * X3_ROWB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = WIDE ? wave >> 2 : wave >> 1, wn = WIDE ? wave & 3 : wave & 1;
+  const int wm = (WIDE || NARROW) ? wave >> 2 : wave >> 1, wn = (WIDE || NARROW) ? wave & 3 : wave & 1;
   unsigned long long clk_t0 = 0, clk_r0 = 0;
   if (p.clk && tid == 0) {
     clk_t0 = __builtin_amdgcn_s_memtime();
@@ -1329,7 +1336,70 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
   };
-  if constexpr (F32A) {
+  if constexpr (NARROW) {
+    // ---- 64 x 128 tile: A chunks 512 .. 767 are issued by waves 0-3 only (wave-uniform guard); per K tile each wave
+    // reads 2 A + 2 B tiles (12 ds_read_b128) and runs 24 MFMAs, smallest limb products first
+    auto dma_n = [&](int k0, int buf) {
+      unsigned char* base = smem + buf * BUFB + wbase;
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        if (512 * j + (tid & ~63) < BM * X3_CHUNKS)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+#pragma unroll
+      for (int j = 0; j < BJ; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * X3_ROWB + 512 * 16 * j), 16, (int)boff[j],
+                                                 k0 * 6, 0, 0);
+      ci0 += X3_BK;
+      if (ci0 == Cg) {
+        ci0 = 0;
+        ++tap;
+        if (++tkx == kw) {
+          tkx = 0;
+          ++tky;
+        }
+        set_tap();
+      }
+    };
+    if (nk > 0) dma_n(kbeg, 0);
+    __syncthreads();
+    const int afn = (wm * 32 + lrow) * X3_ROWB, bfn = (BM + wn * 32 + lrow) * X3_ROWB;
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* base = smem + (kt & 1) * BUFB;
+      if (kt + 1 < nk) dma_n(kbeg + (kt + 1) * X3_BK, (kt + 1) & 1);
+      bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+          fa[t][l] = *reinterpret_cast<const bf16x8*>(base + afn + t * 16 * X3_ROWB + oct16 + l * 16);
+          fb[t][l] = *reinterpret_cast<const bf16x8*>(base + bfn + t * 16 * X3_ROWB + oct16 + l * 16);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 c = acc16[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+        }
+      __syncthreads();
+      if (((kt + 1) & (FLUSH - 1)) == 0) {
+        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tot16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
+            acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
+  } else if constexpr (F32A) {
     // ---- fp32 A image (X3A_ROWB rows, f32a_swz), limb B image; wave w owns rows 32 w .. 32 w + 31 and all 128 columns:
     // acc16[2 a + (t >> 2)][t & 3] is A tile a (16 rows) x B tile t (16 columns).  A runs one tile ahead of B: during
     // tile kt's MFMAs (limb fragments of A(kt) in registers, B(kt) read from LDS one 16-column tile ahead) each wave
@@ -1931,10 +2001,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
   {
     const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
     if (M16) {
+      constexpr int MI = NARROW ? 2 : 4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < MI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc16[i][j][r] = __builtin_fmaf(sg, acc16[i][j][r], tot16[i][j][r]);
     } else {
@@ -1962,6 +2033,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x3_kernel(GemmArgs p) {
         for (int r = 0; r < 4; ++r)
           tile[(wave * 32 + (i >> 1) * 16 + 4 * (lane >> 4) + r) * TS + ((i & 1) * 4 + j) * 16 + (lane & 15)] =
               acc16[i][j][r];
+  } else if (NARROW) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 32 + j * 16 + (lane & 15)] = acc16[i][j][r];
   } else if (M16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -2291,6 +2370,20 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   GemmArgs a = a0;
   constexpr int BM = (V & 524288) ? 128 : X3_BM, BN = (V & 524288) ? 256 : X3_BN;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  if constexpr (V == DAMC_X3_VARIANT && OM != O_WGRAD) {
+    // an under-filled grid that the 64 x 128 tile fills (>= 256 workgroups): no split-K slabs; DAMC_X3_NARROW=0 (read
+    // per call) keeps split-K
+    const char* en = getenv("DAMC_X3_NARROW");
+    const long nnm = (a.M + 63) / 64;
+    if (a.kslab && !a.proj_out && !(en && en[0] == '0') && (long)ntm * ntn * zdim < 256 && nnm * ntn * zdim >= 256) {
+      a.ksplit = 1;
+      a.kbpw = 1;
+      a.kslab_reg = 0;
+      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | X3_NARROW>), dim3((unsigned)(nnm * ntn), 1, zdim), dim3(512), 0, s,
+                         a);
+      return;
+    }
+  }
   if (OM != O_WGRAD && a.kslab && !(V & 16)) {
     const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {

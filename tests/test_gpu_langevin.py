@@ -339,7 +339,8 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
 def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block (damc_x3_sign_block() k) per slice, reduced
     in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
-    width with DAMC_X3_KSPLIT=0 vs the default."""
+    width with DAMC_X3_KSPLIT=0 vs the default; and the 64 x 128 tile (gemm.hip X3_NARROW, which replaces split-K
+    where it fills the chip) against both."""
     from damc import synth
     from src import diffusion_net as dn
 
@@ -348,14 +349,16 @@ def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(gpu_device)
     z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, 128))).to(gpu_device)
     out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("DAMC_X3_KSPLIT", mode)
+    for mode, split, narrow in (("unsplit", "0", "0"), ("split", "1", "0"), ("narrow", "1", "1")):
+        monkeypatch.setenv("DAMC_X3_KSPLIT", split)
+        monkeypatch.setenv("DAMC_X3_NARROW", narrow)
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
         torch.cuda.synchronize()
         out[mode] = z.cpu()
-    assert torch.isfinite(out["1"]).all()
-    assert torch.equal(out["0"], out["1"])
+    assert torch.isfinite(out["split"]).all()
+    assert torch.equal(out["unsplit"], out["split"])
+    assert torch.equal(out["unsplit"], out["narrow"])
 
 
 @pytest.mark.parametrize("net,B", [("cifar10", 5), ("cifar10", 128), ("celeba64", 4)])
@@ -363,7 +366,8 @@ def test_lds_staged_output_projection_is_bitwise_the_direct_kernel(lv, gpu_devic
     """The output layer's projection stage staged through LDS (generator.hip smallc_proj_lds_kernel: same MFMA
     sequence, operands from LDS) gives the same bits as the direct-load kernel: 2 posterior steps at full width
     (CIFAR k3: one 32-column tile, ragged last wave at B=5; CelebA-64 k4 s2: two tiles) with
-    DAMC_SMALLC_PROJ_LDS=0 vs 1."""
+    DAMC_SMALLC_PROJ_LDS=0 vs 1 (with the round-4 proj16 kernel and the fused projection switched off, so these two
+    kernels are the ones compared)."""
     from damc import synth
     from src import diffusion_net as dn
 
@@ -373,6 +377,8 @@ def test_lds_staged_output_projection_is_bitwise_the_direct_kernel(lv, gpu_devic
     x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, hw, hw))).to(gpu_device)
     z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, nz))).to(gpu_device)
     out = {}
+    monkeypatch.setenv("DAMC_SMALLC_PROJ16", "0")
+    monkeypatch.setenv("DAMC_SMALLC_FUSE", "0")
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_SMALLC_PROJ_LDS", mode)
         z = z0.clone()
