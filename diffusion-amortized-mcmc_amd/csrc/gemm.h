@@ -121,6 +121,12 @@ int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned
 // slice-major with sign-alternating blocks when the default variant walks channel-major (DAMC_X3_VARIANT & 8),
 // else tap-major (launch_split_x3_negblk)
 int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s);
+// generator-layer packing through LDS tiles (fp32 + x3 in one pass; damc_pack_generator_layer); 1 = layout not
+// covered (the caller falls back to the element-wise packing + launch_split_x3_conv)
+int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned short* wf3, float* wb,
+                          unsigned short* wb3, hipStream_t s);
+int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf, float* wb, unsigned short* wb3,
+                           hipStream_t s);
 
 // a PyTorch Conv2d weight (cout, cin, k, k), cin % 8 == 0, straight to the limb B operand of the conv (the order
 // launch_split_x3_conv gives damc_pack_conv2d's K-major packing)

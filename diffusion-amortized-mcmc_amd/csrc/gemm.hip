@@ -2528,6 +2528,101 @@ int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* 
   return launch_split_x3_negblk(x, n, K, y, s);
 }
 
+// ---- generator-layer weight packing through LDS tiles (damc_pack_generator_layer's hot layouts): a ConvTranspose2d
+// weight W[ci][co][tap] (kk <= 16 taps) read in contiguous rows, written as whole octets of the packed matrix, with
+// its x3 copy (sign-alternating X3_NEGK blocks, split_x3_negblk_kernel's values) in the same pass -- the per-call
+// packing was scattered 4-byte stores plus a second read for the limb split.
+__device__ __forceinline__ void pack_store_octet(const float (&v)[8], long flat, int k, float* __restrict__ out,
+                                                 unsigned short* __restrict__ x3) {
+  f32x4* o = reinterpret_cast<f32x4*>(out + flat);
+  o[0] = f32x4{v[0], v[1], v[2], v[3]};
+  o[1] = f32x4{v[4], v[5], v[6], v[7]};
+  if (x3) {
+    const float sg = ((k / X3_NEGK) & 1) ? -1.f : 1.f;
+    const float u[8] = {sg * v[0], sg * v[1], sg * v[2], sg * v[3], sg * v[4], sg * v[5], sg * v[6], sg * v[7]};
+    bf16x8 h, m, l;
+    split3_octet(u, h, m, l);
+    bf16x8* y = reinterpret_cast<bf16x8*>(x3) + 3 * (flat / 8);
+    y[0] = h;
+    y[1] = m;
+    y[2] = l;
+  }
+}
+
+// out[ci][tap][co] = W[ci][co][tap]; x3 rows ci of K = kk * cout. Block: one ci, 128 output channels.
+constexpr int PK_ROW_CO = 128;
+__global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict__ w, int cout, int kk,
+                                                        float* __restrict__ out, unsigned short* __restrict__ x3) {
+  __shared__ float t[PK_ROW_CO * 17];
+  const int ci = blockIdx.y, co0 = blockIdx.x * PK_ROW_CO;
+  const int nco = min(PK_ROW_CO, cout - co0), nco8 = nco / 8, ld = kk + 1;
+  const float* src = w + ((long)ci * cout + co0) * kk;
+  for (int e = threadIdx.x; e < nco * kk; e += 256) t[(e / kk) * ld + e % kk] = src[e];
+  __syncthreads();
+  for (int o = threadIdx.x; o < kk * nco8; o += 256) {
+    const int tap = o / nco8, c8 = o - tap * nco8;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[(c8 * 8 + j) * ld + tap];
+    const int k = tap * cout + co0 + c8 * 8;
+    pack_store_octet(v, (long)ci * kk * cout + k, k, out, x3);
+  }
+}
+
+// out[seg][ci] with seg(co, tap) = the ConvT forward row order: UP2 ((phase * cout + co) * 4 + ty * 2 + tx, x3 rows
+// of 4 Cin per (phase, co)), PROJ (tap * cout + co, x3 rows of Cin). Block: 32 input x 8 output channels.
+__global__ void __launch_bounds__(256) pack_colT_kernel(const float* __restrict__ w, int cin, int cout, int kk, int up2,
+                                                        float* __restrict__ out, unsigned short* __restrict__ x3) {
+  __shared__ float t[32 * (8 * 16 + 1)];
+  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 8, rl = 8 * kk, ld = rl + 1;
+  for (int e = threadIdx.x; e < 32 * rl; e += 256) {
+    const int cl = e / rl, r = e - cl * rl;
+    t[cl * ld + r] = w[((long)(ci0 + cl) * cout + co0) * kk + r];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < rl * 4; o += 256) {
+    const int c8 = o & 3, r = o >> 2, col = r / kk, tap = r - col * kk, co = co0 + col;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[(c8 * 8 + j) * ld + r];
+    long seg;
+    int k = ci0 + c8 * 8;
+    if (up2) {  // ky = 3 - py - 2 ty (the stride-2 phase decomposition, generator.hip pack_up2_kernel)
+      const int ky = tap >> 2, kx = tap & 3, py = (3 - ky) & 1, px = (3 - kx) & 1;
+      const int tt = ((3 - ky - py) >> 1) * 2 + ((3 - kx - px) >> 1);
+      seg = ((long)(py * 2 + px) * cout + co) * 4 + tt;
+      k += tt * cin;
+    } else {
+      seg = (long)tap * cout + co;
+    }
+    pack_store_octet(v, seg * cin + ci0 + c8 * 8, k, out, x3);
+  }
+}
+
+static bool pack_tiled_ok(const void* a, const void* b, const void* c, const void* d) {
+  return (DAMC_X3_VARIANT & 8) == 0 &&  // the negblk limb order (launch_split_x3_conv)
+         (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)d) % 16) == 0;
+}
+
+// 1 = layout not covered (the caller packs element-wise)
+int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned short* wf3, float* wb,
+                          unsigned short* wb3, hipStream_t s) {
+  if (cin % KM_BK != 0 || cout % KM_BK != 0 || !pack_tiled_ok(wf, wf3, wb, wb3)) return 1;
+  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / 8), dim3(256), 0, s, w, cin, cout, 16, 1, wf, wf3);
+  hipLaunchKernelGGL(pack_rowT_kernel, dim3((cout + PK_ROW_CO - 1) / PK_ROW_CO, cin), dim3(256), 0, s, w, cout, 16,
+                     wb, wb3);
+  return (int)hipGetLastError();
+}
+
+int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf, float* wb, unsigned short* wb3,
+                           hipStream_t s) {
+  if (kk > 16 || cin % 32 != 0 || cout % 8 != 0 || !pack_tiled_ok(wf, wb, wb3, nullptr)) return 1;
+  hipLaunchKernelGGL(pack_rowT_kernel, dim3((cout + PK_ROW_CO - 1) / PK_ROW_CO, cin), dim3(256), 0, s, w, cout, kk,
+                     wf, (unsigned short*)nullptr);
+  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / 8), dim3(256), 0, s, w, cin, cout, kk, 0, wb, wb3);
+  return (int)hipGetLastError();
+}
+
 // a PyTorch Conv2d weight (cout, cin, k, k) straight to the limb engine's B operand of the conv, [co][(ky, kx, ci)]
 // with sign-alternating blocks (launch_split_x3_negblk of damc_pack_conv2d's K-major packing, in one pass)
 __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int cin, int k, unsigned short* __restrict__ y) {

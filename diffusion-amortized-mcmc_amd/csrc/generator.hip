@@ -2077,15 +2077,30 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
   hipStream_t s = as_stream(stream);
   const long n = (long)L->cin * L->cout * (L->kind == DAMC_LAYER_LINEAR ? 1 : (long)L->k * L->k);
   const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+  // LDS-tiled packing (fp32 + limbs in one pass) unless DAMC_PACK_TILED=0 (the element-wise A/B; bitwise the same)
+  const char* pt = getenv("DAMC_PACK_TILED");
+  const bool tiled = !(pt && pt[0] == '0');
   switch (L->kind) {
     case DAMC_LAYER_PROJ:
       if (!wb) return DAMC_ERR_ARG;
+      if (tiled) {
+        const int rc = damc::launch_pack_proj_tiled(
+            w, L->cin, L->cout, L->k * L->k, wf, wb,
+            x3_proj_cap(*L) ? reinterpret_cast<unsigned short*>(wb + n) : nullptr, s);
+        if (rc != 1) return rc;
+      }
       hipLaunchKernelGGL(pack_proj_kernel, grid, blk, 0, s, w, L->cin, L->cout, L->k, wf, wb);
       if (x3_proj_cap(*L))
         DAMC_CHECK((hipError_t)damc::launch_split_x3_negblk(wb, n, L->cin, reinterpret_cast<unsigned short*>(wb + n), s));
       break;
     case DAMC_LAYER_UP2:
       if (!wb || L->k != 4) return DAMC_ERR_ARG;
+      if (tiled) {
+        const int rc = damc::launch_pack_up2_tiled(
+            w, L->cin, L->cout, wf, x3_fwd_cap(*L) ? reinterpret_cast<unsigned short*>(wf + n) : nullptr, wb,
+            x3_bwd_cap(*L) ? reinterpret_cast<unsigned short*>(wb + n) : nullptr, s);
+        if (rc != 1) return rc;
+      }
       hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, (int)damc::conv_kmajor_ok(L->cin),
                          (int)damc::conv_kmajor_ok(L->cout), wf, wb);
       // x3 copies with sign-alternating K blocks (gemm.h GemmArgs::b_negblk): rows of 4 Cin (forward, per phase

@@ -181,3 +181,25 @@ def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     lo = (r1 - m.float()).to(torch.bfloat16)
     want = torch.stack([t.view(torch.int16).reshape(cout, K // 8, 8) for t in (h, m, lo)], dim=2).reshape(-1)
     assert torch.equal(out.cpu(), want)
+
+
+@pytest.mark.parametrize("cls,ngf", [("_netG_cifar10", 128), ("_netG_celebaHQ", 64), ("_netG_mnist", 64)])
+def test_tiled_weight_packing_is_bitwise_the_elementwise_packing(gpu_device, monkeypatch, cls, ngf):
+    """damc_pack_generator_layer's LDS-tiled path (fp32 + x3 limbs in one pass) writes exactly the bytes of the
+    element-wise packing + launch_split_x3_conv (DAMC_PACK_TILED=0) for every layer of the generators."""
+    from damc import plans, synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(getattr(dn, cls)(nz=128, ngf=ngf, nc=3), 3).to(gpu_device).eval()
+    plan = plans.generator_plan(G)
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DAMC_PACK_TILED", mode)
+        plan.refresh(gpu_device)
+        torch.cuda.synchronize()
+        got[mode] = [(wf.clone(), None if wb is None else wb.clone()) for wf, wb in plan.buffers]
+    for i, ((f0, b0), (f1, b1)) in enumerate(zip(got["0"], got["1"])):
+        assert torch.equal(f0, f1), f"layer {i} forward packing"
+        assert (b0 is None) == (b1 is None)
+        if b0 is not None:
+            assert torch.equal(b0, b1), f"layer {i} backward packing"
