@@ -42,7 +42,8 @@ constexpr int TM = 16;           // rows per workgroup
 constexpr int TC = 8;            // output columns per workgroup (x 2 products)
 constexpr int KG = 16 * CH_WAVES;  // K padding granule: one 16-deep k-group per wave
 #ifndef DAMC_CH_CHUNK
-#define DAMC_CH_CHUNK 8
+#define DAMC_CH_CHUNK 4  // 8 until round 4: with the sentinel re-read paths the team kernel at 8 ran 3.92 ms per B=128
+                         // sweep against 3.49 at 4 (same box, interleaved; profiles/r04/sweep_ab.txt)
 #endif
 constexpr int CH_CHUNK = DAMC_CH_CHUNK;  // k-groups whose loads a lane keeps in flight at once
 constexpr int EMB_G = 8;         // in0: 16-deep k-groups of z (nz <= 128)
@@ -592,6 +593,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
   const int er = tid >> 3, ec = tid & 7;
   const int T = a.T, team = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nz = a.nz, B = a.B, G = a.G;
+  const int sent = NT == 256 ? 2 : a.sent;  // compile-time in the 4-wave (data-driven) instantiation
   if (team >= G || slot >= T) return;  // no row tile for this team (its flags are never waited on)
   if (a.dbg & 4096) {  // tests only: report a failed wait at once
     if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -693,7 +695,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
       // the publishing lane writes them out after the flag
       const bool tr = a.trace != nullptr && tid == (NT > 256 ? 256 : 0);
       if (nt == 0) {  // nothing to compute: publish at once (this slot's earlier stores are drained)
-        if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == TS_PUB && sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
       const bool final_ = j == 6;
@@ -702,7 +704,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
       // in the same order (team_finish_kernel's rescue relies on it); it is normally known complete already (sb <
       // known); a slot that owned no tile of the stages since waits for it here
       const bool skip_early = b.kpb > 0;
-      if (skip_early && a.sent < 2 && !(7u * k + b.srcB < known)) {
+      if (skip_early && sent < 2 && !(7u * k + b.srcB < known)) {
         if (!ts_wait(teamflags, T, 7u * k + b.srcB + 1, a.err, a.budget, &sflag, a.diag)) return;
         known = 7u * k + b.srcB + 1;
       }
@@ -745,13 +747,13 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
           if (skip_early && !pre && cw)
             ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
-                           a.sent, a.err, a.budget);
+                           sent, a.err, a.budget);
           const int half = nz >> 1;
 
           // ---- wait for stage s - 1 of the team (once per stage)
           if (!waited) {
             if (tr) trs[0] = __builtin_amdgcn_s_memrealtime();
-            if (s > 0 && a.sent < 2 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
+            if (s > 0 && sent < 2 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
             if (tr) trs[1] = __builtin_amdgcn_s_memrealtime();
             known = s;
             waited = true;
@@ -765,7 +767,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               zv4[g] = (cw && xok && kk < nz && !(a.dbg & 64)) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4)
                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            if (a.sent && cw && __any(any_sent(zv4))) {  // z of this step not landed yet: re-read (bounded)
+            if (sent && cw && __any(any_sent(zv4))) {  // z of this step not landed yet: re-read (bounded)
               const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
               unsigned it = 0;
               do {
@@ -811,12 +813,12 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           } else if (cw && pre) {
             f32x4 xa[CH_CHUNK];
             ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
-            if (a.sent) ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
+            if (sent) ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
             ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
-            if (a.sent) ts_ready<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, a.err, a.budget);
+            if (sent) ts_ready<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, a.err, a.budget);
             ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw) {
-            ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg, a.sent, a.err,
+            ts_half<false>(acc, wl, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, nullptr, 0, a.dbg, sent, a.err,
                            a.budget);
           }
           if (cw) {
@@ -839,7 +841,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
             } else {  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
               const long zi = (long)erow * nz + ecol;
               float zv = ld_sc1_f(zk + zi);
-              if (a.sent && is_sent(zv)) {  // this thread's own store of the previous step, not landed yet
+              if (sent && is_sent(zv)) {  // this thread's own store of the previous step, not landed yet
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 unsigned it = 0;
                 do {
@@ -865,9 +867,9 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
         }
       }
       // publish: (drained-flag protocol) every storing wave drains first; one lane then stores the slot's flag
-      if (!a.sent && !(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!sent && !(a.dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == TS_PUB && a.sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == TS_PUB && sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == (NT > 256 ? TS_PUB : 0)) {
         uint64_t* tg = a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4;
         tg[0] = trs[0];

@@ -316,6 +316,205 @@ __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __rest
   }
 }
 
+// wave reduce-scatter of N per-lane values: halving exchanges (N/2 + N/4 + ... shuffles instead of 6 N), then a plain
+// butterfly over the lanes left sharing a channel; every lane returns the wave total of channel ch (fixed order)
+template <int N>
+__device__ __forceinline__ float wave_rsum(const float (&v)[N], int lane, int off, int& ch, int stop = 1) {
+  if constexpr (N == 1) {
+    float s = v[0];
+    for (; off >= stop; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+  } else {
+    constexpr int H = N / 2;
+    const bool hi = (lane & off) != 0;
+    float nv[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float keep = hi ? v[H + i] : v[i], send = hi ? v[i] : v[H + i];
+      nv[i] = keep + __shfl_xor(send, off);
+    }
+    ch = 2 * ch + (hi ? 1 : 0);
+    return wave_rsum<H>(nv, lane, off >> 1, ch, stop);
+  }
+}
+
+// The same layer in ONE pass when a sample's whole conv output for a group of G = 32 / P channels fits the registers of
+// a 1024-thread workgroup (P = ceil(H W / 1024) pixels per thread, 32 values each; launched at P = 1): grid
+// (B, C / G).  Each thread evaluates its pixels' channels with conv3_octet's arithmetic (same fmaf chain, so the same y), the workgroup sums them
+// per channel (wave reduce-scatter, then the 16 wave sums in a fixed order) for the mean, then sums (y - mean)^2 for the
+// variance (two passes over registers), and writes lrelu(IN(y)) as the next convolution's limbs.  The statistics pass,
+// the Welford partials, the merge kernel and the recomputing second pass all drop out.
+template <int CIN, int P>
+__global__ __launch_bounds__(1024) void conv3_in_fused_kernel(const float* __restrict__ x, int H, int W, int C,
+                                                              const float* __restrict__ w, const float* __restrict__ bias,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps, float slope,
+                                                              unsigned short* __restrict__ y3) {
+  constexpr int G = 32 / P;
+  extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][G] weights, [16][G] sums, [2][G] stats, window
+  float* wl = smf;
+  float* red = wl + 9 * CIN * G;
+  float* st = red + 16 * G;
+  float* win = st + 2 * G;
+  const int b = blockIdx.x, c0 = blockIdx.y * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HW = H * W;
+  for (int i = tid; i < 9 * CIN * G; i += 1024) wl[i] = w[(i / G) * C + c0 + i % G];
+  conv3_stage<CIN>(x, b, H, W, 0, H, win);
+  __syncthreads();
+  float y[P][G];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int p = tid + 1024 * j;
+    const bool ok = p < HW;
+    const int r = ok ? p / W : 0, xx = ok ? p - r * W : 0;
+    float xv[9 * CIN];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) xv[(ky * 3 + kx) * CIN + ci] = win[((r + ky) * (W + 2) + xx + kx) * CIN + ci];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9 * CIN; ++t) acc = fmaf(wl[t * G + g], xv[t], acc);
+      y[j][g] = ok ? acc + (bias ? bias[c0 + g] : 0.f) : 0.f;
+    }
+  }
+  // workgroup sum per channel into st[k * G + g]: wave totals, then the 16 waves in order
+  auto block_sum = [&](const float (&v)[G], int k) {
+    int ch = 0;
+    const float t = wave_rsum<G>(v, lane, 32, ch);
+    if ((lane & (64 / G - 1)) == 0) red[wave * G + ch] = t;
+    __syncthreads();
+    if (tid < G) {
+      float s = red[tid];
+#pragma unroll
+      for (int w2 = 1; w2 < 16; ++w2) s += red[w2 * G + tid];
+      st[k * G + tid] = s;
+    }
+    __syncthreads();
+  };
+  const float inv_n = 1.f / (float)HW;
+  float v[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    v[g] = y[0][g];
+#pragma unroll
+    for (int j = 1; j < P; ++j) v[g] += y[j][g];
+  }
+  block_sum(v, 0);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float mean = st[g] * inv_n;
+    v[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const float d = y[j][g] - mean;
+      v[g] = (tid + 1024 * j < HW) ? fmaf(d, d, v[g]) : v[g];
+    }
+  }
+  block_sum(v, 1);
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int p = tid + 1024 * j;
+    if (p >= HW) continue;
+#pragma unroll
+    for (int o = 0; o < G / 8; ++o) {
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // in_merge_kernel's scale / shift form
+        const int g = 8 * o + e;
+        const float mean = st[g] * inv_n;
+        const float scl = (1.f / sqrtf(st[G + g] * inv_n + eps)) * gamma[c0 + g];
+        const float u = fmaf(y[j][g], scl, beta[c0 + g] - mean * scl);
+        t[e] = u > 0.f ? u : u * slope;
+      }
+      damc::store_x3_octet(t, y3 + 3 * (((long)b * HW + p) * C + c0 + 8 * o));
+    }
+  }
+}
+
+// InstanceNorm + LeakyReLU of a stored conv output (NHWC fp32) to the next convolution's limbs in ONE kernel when a
+// sample has <= 256 pixels (the encoder's k4 s2 layers at 32x32 input): grid (B, C / 32), 256 threads = 64 pixel slots
+// x 4 channel octets, NIT = ceil(HW / 64) pixels per thread held in registers.  Sum, then sum of squared deviations
+// (two passes over registers; wave reduce-scatter + fixed-order wave sums), then in_merge_kernel's scale / shift and
+// in_apply_x3_kernel's normalise + LReLU + limb store.  Replaces in_stats + in_merge + in_apply_x3 (one read of the
+// activation instead of two, one launch instead of three).
+template <int NIT>
+__global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restrict__ y, int HW, int C,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float eps, float slope, unsigned short* __restrict__ y3) {
+  __shared__ float red[4][32];
+  __shared__ float st[2][32];
+  const int b = blockIdx.x, c0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pr = tid >> 2, q = tid & 3;
+  float v[NIT][8];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int p = pr + 64 * it;
+    if (p < HW) {
+      const float* src = y + ((long)b * HW + p) * C + c0 + 8 * q;
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src), a1 = *reinterpret_cast<const f32x4*>(src + 4);
+      v[it][0] = a0.x; v[it][1] = a0.y; v[it][2] = a0.z; v[it][3] = a0.w;
+      v[it][4] = a1.x; v[it][5] = a1.y; v[it][6] = a1.z; v[it][7] = a1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
+    }
+  }
+  // per-channel workgroup sum of t[e] (channel c0 + 8 q + e) into st[k]
+  auto block_sum = [&](const float (&t)[8], int k) {
+    int ch = 0;
+    const float w = wave_rsum<8>(t, lane, 32, ch, 4);  // lanes of one octet q differ in bits 2..5
+    if ((lane & 4) == 0) red[wave][8 * q + ch] = w;
+    __syncthreads();
+    if (tid < 32) st[k][tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    __syncthreads();
+  };
+  const float inv_n = 1.f / (float)HW;
+  float t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    t[e] = v[0][e];
+#pragma unroll
+    for (int it = 1; it < NIT; ++it) t[e] += v[it][e];
+  }
+  block_sum(t, 0);
+  float mean[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = st[0][8 * q + e] * inv_n;
+    t[e] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float d = v[it][e] - mean[e];
+      t[e] = (pr + 64 * it < HW) ? fmaf(d, d, t[e]) : t[e];
+    }
+  }
+  block_sum(t, 1);
+  float scl[8], shf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + 8 * q + e;
+    scl[e] = (1.f / sqrtf(st[1][8 * q + e] * inv_n + eps)) * gamma[c];
+    shf[e] = beta[c] - mean[e] * scl[e];
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int p = pr + 64 * it;
+    if (p >= HW) continue;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float u = fmaf(v[it][e], scl[e], shf[e]);
+      o[e] = u > 0.f ? u : u * slope;
+    }
+    damc::store_x3_octet(o, y3 + 3 * (((long)b * HW + p) * C + c0 + 8 * q));
+  }
+}
+
 // pixel splits of the statistics pass: <= 64 pixels per split (the Welford chain of a thread is serial),
 // merged with Chan's formula
 int in_splits(int hw) {
@@ -757,8 +956,22 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     if (sm > 65536) return DAMC_ERR_UNSUPPORTED;
     float* ssb = inws + (size_t)B * C * S * 3;
     ProfScope ps("enc_first", 2.0 * B * H * W * (double)C * 9 * L.cin * 2, s);
+    // one pass (conv3_in_fused_kernel) when a sample fits 1024 threads x <= 4 pixels; DAMC_ENC_FIRST_ONEPASS=0 (read
+    // per call) keeps the two recomputing passes
+    const char* op = getenv("DAMC_ENC_FIRST_ONEPASS");
+    const int P1 = (H * W + 1023) / 1024, G1 = P1 <= 1 ? 32 : (P1 <= 2 ? 16 : 8);
+    const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * G1 + 18 * G1) * sizeof(float);
+    // (P = 1 only: at 2 / 4 pixels per thread the kernel spills; CelebA-64 keeps the two passes)
+    const bool one = !(op && op[0] == '0') && P1 == 1 && C % G1 == 0 && sm1 <= 65536;
+#define DAMC_C1(CIN_, P_)                                                                                           \
+  if (one && L.cin == CIN_ && P1 == P_) {                                                                          \
+    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_, P_>), dim3(B, C / (32 / P_)), dim3(1024), sm1, s, x, H, W, C,     \
+                       L.w_packed, L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3);                           \
+  }
+    DAMC_C1(1, 1) DAMC_C1(3, 1) DAMC_C1(4, 1)
+#undef DAMC_C1
 #define DAMC_C3(CIN_)                                                                                               \
-  if (L.cin == CIN_) {                                                                                              \
+  if (!one && L.cin == CIN_) {                                                                                      \
     hipLaunchKernelGGL(conv3_stats_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,    \
                        inws);                                                                                       \
     hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
@@ -798,7 +1011,22 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     a3_ready = false;
     if (!L.in_gamma) continue;
     const int hw = sh.h[i + 1] * sh.w[i + 1];
-    if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
+    const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel form below
+    if (i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0')) {
+      ProfScope ps("instnorm", 0.0, s);
+      const dim3 g(B, L.cout / 32);
+      if (hw <= 64)
+        hipLaunchKernelGGL(in_fused_x3_kernel<1>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
+                           L.slope, a3);
+      else if (hw <= 128)
+        hipLaunchKernelGGL(in_fused_x3_kernel<2>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
+                           L.slope, a3);
+      else
+        hipLaunchKernelGGL(in_fused_x3_kernel<4>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
+                           L.slope, a3);
+      DAMC_LAUNCH_CHECK();
+      a3_ready = true;
+    } else if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
       const int S = in_splits(hw), cg = (L.cout + 63) / 64;
       float* ssb = inws + (size_t)B * L.cout * S * 3;
       ProfScope ps("instnorm", 0.0, s);

@@ -2371,11 +2371,13 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   constexpr int BM = (V & 524288) ? 128 : X3_BM, BN = (V & 524288) ? 256 : X3_BN;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   if constexpr (V == DAMC_X3_VARIANT && OM != O_WGRAD) {
-    // an under-filled grid that the 64 x 128 tile fills (>= 256 workgroups): no split-K slabs; DAMC_X3_NARROW=0 (read
-    // per call) keeps split-K
+    // opt-in (DAMC_X3_NARROW=1, read per call): an under-filled grid that the 64 x 128 tile fills (>= 256 workgroups)
+    // runs unsplit on it instead of split-K.  Measured slower at the CIFAR B=16 per-rank step: 158.7 / 152.2 us for the
+    // L2 forward / L3 dgrad against 121 / 122 us for split-K + reduce (profiles/r04/b16_narrow_kernel_stats.csv): the
+    // 32 x 32 wave tile reads 2x the LDS fragments per MFMA and stages 1.5x the bytes per flop
     const char* en = getenv("DAMC_X3_NARROW");
     const long nnm = (a.M + 63) / 64;
-    if (a.kslab && !a.proj_out && !(en && en[0] == '0') && (long)ntm * ntn * zdim < 256 && nnm * ntn * zdim >= 256) {
+    if (a.kslab && !a.proj_out && en && en[0] == '1' && (long)ntm * ntn * zdim < 256 && nnm * ntn * zdim >= 256) {
       a.ksplit = 1;
       a.kbpw = 1;
       a.kslab_reg = 0;
@@ -2549,11 +2551,11 @@ __device__ __forceinline__ void pack_store_octet(const float (&v)[8], long flat,
   }
 }
 
-// out[ci][tap][co] = W[ci][co][tap]; x3 rows ci of K = kk * cout. Block: one ci, 128 output channels.
+// out[ci][tap][co] = W[ci][co][tap]; x3 rows ci of K = kk * cout. Block: one ci, 128 output channels (kk <= 64).
 constexpr int PK_ROW_CO = 128;
 __global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict__ w, int cout, int kk,
                                                         float* __restrict__ out, unsigned short* __restrict__ x3) {
-  __shared__ float t[PK_ROW_CO * 17];
+  __shared__ float t[PK_ROW_CO * 65];
   const int ci = blockIdx.y, co0 = blockIdx.x * PK_ROW_CO;
   const int nco = min(PK_ROW_CO, cout - co0), nco8 = nco / 8, ld = kk + 1;
   const float* src = w + ((long)ci * cout + co0) * kk;
@@ -2570,11 +2572,12 @@ __global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict_
 }
 
 // out[seg][ci] with seg(co, tap) = the ConvT forward row order: UP2 ((phase * cout + co) * 4 + ty * 2 + tx, x3 rows
-// of 4 Cin per (phase, co)), PROJ (tap * cout + co, x3 rows of Cin). Block: 32 input x 8 output channels.
+// of 4 Cin per (phase, co)), PROJ (tap * cout + co, x3 rows of Cin). Block: 32 input x 128 / kk output channels (each
+// input channel's run of 128 contiguous weights).
 __global__ void __launch_bounds__(256) pack_colT_kernel(const float* __restrict__ w, int cin, int cout, int kk, int up2,
                                                         float* __restrict__ out, unsigned short* __restrict__ x3) {
-  __shared__ float t[32 * (8 * 16 + 1)];
-  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 8, rl = 8 * kk, ld = rl + 1;
+  __shared__ float t[32 * 129];
+  const int cot = 128 / kk, ci0 = blockIdx.x * 32, co0 = blockIdx.y * cot, rl = 128, ld = rl + 1;
   for (int e = threadIdx.x; e < 32 * rl; e += 256) {
     const int cl = e / rl, r = e - cl * rl;
     t[cl * ld + r] = w[((long)(ci0 + cl) * cout + co0) * kk + r];
@@ -2616,10 +2619,12 @@ int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned
 
 int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf, float* wb, unsigned short* wb3,
                            hipStream_t s) {
-  if (kk > 16 || cin % 32 != 0 || cout % 8 != 0 || !pack_tiled_ok(wf, wb, wb3, nullptr)) return 1;
+  if (kk > 64 || 128 % kk != 0 || cin % 32 != 0 || cout % 8 != 0 || cout % (128 / kk) != 0 ||
+      !pack_tiled_ok(wf, wb, wb3, nullptr))
+    return 1;
   hipLaunchKernelGGL(pack_rowT_kernel, dim3((cout + PK_ROW_CO - 1) / PK_ROW_CO, cin), dim3(256), 0, s, w, cout, kk,
                      wf, (unsigned short*)nullptr);
-  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / 8), dim3(256), 0, s, w, cin, cout, kk, 0, wb, wb3);
+  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / (128 / kk)), dim3(256), 0, s, w, cin, cout, kk, 0, wb, wb3);
   return (int)hipGetLastError();
 }
 
@@ -2648,30 +2653,32 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
 // 48-B limb octets of each tap (the thread-per-output-octet kernel above reads 4 B at a 64-B stride, every line 16x)
 __global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, int cin, int k,
                                          unsigned short* __restrict__ y) {
-  const int cin8 = cin / 8, taps = k * k, K8 = taps * cin8;
+  // one thread per (co, 4-tap group, channel octet), octets fastest: 4x the threads of one per (co, octet) walking
+  // all its taps (CIFAR encoder: 4 launches 69 -> ~25 us per Q(x) call), same values and stores
+  const int cin8 = cin / 8, taps = k * k, K8 = taps * cin8, tq = taps / 4;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)cout * cin8) return;
-  const int co = (int)(i / cin8), c8 = (int)(i - (long)co * cin8);
+  if (i >= (long)cout * tq * cin8) return;
+  const int c8 = (int)(i % cin8);
+  const long r = i / cin8;
+  const int t0 = 4 * (int)(r % tq), co = (int)(r / tq);
   const f32x4* src = reinterpret_cast<const f32x4*>(w + ((long)co * cin + c8 * 8) * taps);
   bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * ((long)co * K8 + c8);
-  for (int t0 = 0; t0 < taps; t0 += 4) {
-    f32x4 q[8];
+  f32x4 q[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = src[(e * taps + t0) / 4];
+  for (int e = 0; e < 8; ++e) q[e] = src[(e * taps + t0) / 4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int kk = (t0 + t) * cin + c8 * 8;
-      const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
-      float v[8];
+  for (int t = 0; t < 4; ++t) {
+    const int kk = (t0 + t) * cin + c8 * 8;
+    const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
+    float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = sg * q[e][t];
-      bf16x8 h, m, l;
-      split3_octet(v, h, m, l);
-      bf16x8* d = o + 3L * (t0 + t) * cin8;
-      d[0] = h;
-      d[1] = m;
-      d[2] = l;
-    }
+    for (int e = 0; e < 8; ++e) v[e] = sg * q[e][t];
+    bf16x8 h, m, l;
+    split3_octet(v, h, m, l);
+    bf16x8* d = o + 3L * (t0 + t) * cin8;
+    d[0] = h;
+    d[1] = m;
+    d[2] = l;
   }
 }
 
@@ -2679,7 +2686,7 @@ int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short
   if ((DAMC_X3_VARIANT & 8) != 0) return DAMC_ERR_UNSUPPORTED;  // the channel-major walk needs the slice-major order
   if (cout <= 0 || cin % 8 != 0 || k <= 0 || (uintptr_t)y % 16 != 0) return DAMC_ERR_ARG;
   if ((k * k) % 4 == 0 && (uintptr_t)w % 16 == 0) {
-    const long nt = (long)cout * (cin / 8);
+    const long nt = (long)cout * (k * k / 4) * (cin / 8);
     hipLaunchKernelGGL(pack_conv_x3_taps_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, cout, cin, k,
                        y);
     return (int)hipGetLastError();

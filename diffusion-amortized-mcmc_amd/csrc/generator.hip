@@ -1657,7 +1657,9 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
           a.proj_ldw = F.cin;
           a.proj_np = 32 * smallc_ntile(F);
           a.proj_out = ws.pbuf;
-          a.proj_nostore = 1;  // the activation itself is read by nothing else in a posterior step
+          // the activation itself is not stored when its sign bits carry the output layer's dgrad mask (k3 output
+          // layers, hbits); a k4 s2 output layer's dgrad reads the fp32 activation's sign
+          a.proj_nostore = hbits(g, i) ? 1 : 0;
           if (!a.C) a.C = ws.h[i];
         }
       }

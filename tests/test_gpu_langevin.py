@@ -339,8 +339,8 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
 def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block (damc_x3_sign_block() k) per slice, reduced
     in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
-    width with DAMC_X3_KSPLIT=0 vs the default; and the 64 x 128 tile (gemm.hip X3_NARROW, which replaces split-K
-    where it fills the chip) against both."""
+    width with DAMC_X3_KSPLIT=0 vs the default; and the opt-in 64 x 128 tile (gemm.hip X3_NARROW, DAMC_X3_NARROW=1,
+    which replaces split-K where it fills the chip) against both."""
     from damc import synth
     from src import diffusion_net as dn
 

@@ -252,6 +252,81 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
   }
+  // "eq" mode: bitwise equality of the F32A kernel against the default, unsplit and split-K (register slabs), with the
+  // library's epilogue operands (sign-bit mask for the dgrads, sign-bit output for the forwards, limb copy of C)
+  if (argc > 2 && !strcmp(argv[2], "eq")) {
+    float* slab;
+    const long slabn = 1L << 28;
+    CK(hipMalloc(&slab, slabn * 4));
+    for (size_t si = 0; si < shapes.size(); ++si) {
+      const Shape& sh = shapes[si];
+      const GemmArgs& a0 = sh.a;
+      const size_t nout = sh.phase ? (size_t)B * a0.Hout * a0.Wout * a0.ldc : (size_t)a0.M * a0.ldc;
+      float* mk = rnd(nout, 99);
+      std::vector<float> hm = to_host(mk, nout);
+      std::vector<unsigned char> bits(nout / 8, 0);
+      for (size_t i = 0; i < nout; ++i)
+        if (hm[i] > 0.f) bits[i / 8] |= (unsigned char)(1u << (i % 8));
+      unsigned char* dbits;
+      CK(hipMalloc(&dbits, nout / 8));
+      CK(hipMemcpy(dbits, bits.data(), nout / 8, hipMemcpyHostToDevice));
+      std::vector<float> outs[4];
+      std::vector<unsigned char> sgns[4];
+      for (int v = 0; v < 4; ++v) {
+        const bool f32a = v & 1, split = v & 2;
+        GemmArgs a = a0;
+        float* c;
+        unsigned char* sg;
+        CK(hipMalloc(&c, nout * 4));
+        CK(hipMalloc(&sg, nout / 8));
+        CK(hipMemset(c, 0, nout * 4));
+        CK(hipMemset(sg, 0, nout / 8));
+        a.C = c;
+        a.A3 = sh.a3;
+        a.B3 = sh.b3n;
+        a.b_negblk = 1;
+        a.b_zstride = (long)a.N * a.K;
+        a.a_f32 = f32a;
+        if (split) {
+          a.kslab = slab;
+          a.kslab_floats = slabn;
+        }
+        if (sh.phase) {
+          a.sgn = sg;
+          if (f32a) launch_x3_t<EPI_BIAS_ACT, O_PHASE, 261 | X3_F32A>(a, 4, s);
+          else launch_x3_t<EPI_BIAS_ACT, O_PHASE, 261>(a, 4, s);
+        } else {
+          a.mask = nullptr;
+          a.mask_sgn = dbits;
+          if (f32a) launch_x3_t<EPI_MASK, O_DENSE, 261 | X3_F32A>(a, 1, s);
+          else launch_x3_t<EPI_MASK, O_DENSE, 261>(a, 1, s);
+        }
+        CK(hipStreamSynchronize(s));
+        outs[v] = to_host(c, nout);
+        sgns[v].resize(nout / 8);
+        CK(hipMemcpy(sgns[v].data(), sg, nout / 8, hipMemcpyDeviceToHost));
+        CK(hipFree(c));
+        CK(hipFree(sg));
+      }
+      printf("eq B=%d %-28s", B, sh.name);
+      const char* nm[4] = {"v261", "f32a", "v261 split", "f32a split"};
+      for (int v = 1; v < 4; ++v) {
+        size_t nd = 0, first = (size_t)-1;
+        for (size_t i = 0; i < nout; ++i)
+          if (memcmp(&outs[v][i], &outs[0][i], 4)) {
+            if (first == (size_t)-1) first = i;
+            ++nd;
+          }
+        printf("  [%s: %zu differ%s%s]", nm[v], nd, sh.phase && memcmp(sgns[v].data(), sgns[0].data(), nout / 8) ? ", sign bits differ" : "",
+               nd ? "" : "");
+        if (nd) printf(" (first %zu: %.9g vs %.9g)", first, outs[v][first], outs[0][first]);
+      }
+      printf("\n");
+      CK(hipFree(mk));
+      CK(hipFree(dbits));
+    }
+    return 0;
+  }
   // timing probes beside the default: 512 = no DMA after the first tile, 1024 = fragment reads of the first tile only,
   // 4096 = DMA from one L2-hot 64 KB window
   V vars[] = {{"v261", run_x3<261, 1>}, {"f32a", run_x3<261 | X3_F32A, 1>}, {"wide", run_x3<261 | 524288, 1>}};
