@@ -592,9 +592,9 @@ __global__ __launch_bounds__(EB_THREADS) void ebm_reg_kernel(EbArgs a) {
         zs[tid] = zn;
         if (MODE == EB_POSTERIOR && a.z3) {  // RNE limbs (gemm.hip split3_octet's arithmetic), x3 octet layout
           const __bf16 b0 = (__bf16)zn;
-          const float r1 = zn - (float)b0;
+          const float r1 = sub_rn(zn, (float)b0);
           const __bf16 b1 = (__bf16)r1;
-          const __bf16 b2 = (__bf16)(r1 - (float)b1);
+          const __bf16 b2 = (__bf16)(sub_rn(r1, (float)b1));
           __bf16* o = reinterpret_cast<__bf16*>(a.z3) + ((long)chain * (nz >> 3) + (tid >> 3)) * 24 + (tid & 7);
           o[0] = b0;
           o[8] = b1;

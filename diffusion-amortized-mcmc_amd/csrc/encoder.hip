@@ -351,14 +351,12 @@ __global__ __launch_bounds__(1024) void conv3_in_fused_kernel(const float* __res
                                                               const float* __restrict__ beta, float eps, float slope,
                                                               unsigned short* __restrict__ y3) {
   constexpr int G = 32 / P;
-  extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][G] weights, [16][G] sums, [2][G] stats, window
-  float* wl = smf;
-  float* red = wl + 9 * CIN * G;
+  extern __shared__ __attribute__((aligned(16))) float smf[];  // [16][G] sums, [2][G] stats, the window
+  float* red = smf;
   float* st = red + 16 * G;
   float* win = st + 2 * G;
   const int b = blockIdx.x, c0 = blockIdx.y * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int HW = H * W;
-  for (int i = tid; i < 9 * CIN * G; i += 1024) wl[i] = w[(i / G) * C + c0 + i % G];
   conv3_stage<CIN>(x, b, H, W, 0, H, win);
   __syncthreads();
   float y[P][G];
@@ -374,11 +372,14 @@ __global__ __launch_bounds__(1024) void conv3_in_fused_kernel(const float* __res
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci) xv[(ky * 3 + kx) * CIN + ci] = win[((r + ky) * (W + 2) + xx + kx) * CIN + ci];
+    // weights at workgroup-uniform addresses: scalar loads into SGPRs, v_fma with an SGPR operand (from LDS they were
+    // 864 broadcast reads per thread, the kernel's bound)
+    const float* wg = w + c0;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float acc = 0.f;
 #pragma unroll
-      for (int t = 0; t < 9 * CIN; ++t) acc = fmaf(wl[t * G + g], xv[t], acc);
+      for (int t = 0; t < 9 * CIN; ++t) acc = fmaf(wg[t * C + g], xv[t], acc);
       y[j][g] = ok ? acc + (bias ? bias[c0 + g] : 0.f) : 0.f;
     }
   }
@@ -960,7 +961,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     // per call) keeps the two recomputing passes
     const char* op = getenv("DAMC_ENC_FIRST_ONEPASS");
     const int P1 = (H * W + 1023) / 1024, G1 = P1 <= 1 ? 32 : (P1 <= 2 ? 16 : 8);
-    const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * G1 + 18 * G1) * sizeof(float);
+    const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + 18 * G1) * sizeof(float);
     // (P = 1 only: at 2 / 4 pixels per thread the kernel spills; CelebA-64 keeps the two passes)
     const bool one = !(op && op[0] == '0') && P1 == 1 && C % G1 == 0 && sm1 <= 65536;
 #define DAMC_C1(CIN_, P_)                                                                                           \

@@ -140,11 +140,11 @@ __device__ __forceinline__ void store_x3_octet(const float (&v)[8], unsigned sho
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const __bf16 b0 = (__bf16)v[e];
-    const float r1 = v[e] - (float)b0;
+    const float r1 = sub_rn(v[e], (float)b0);
     const __bf16 b1 = (__bf16)r1;
     h[e] = b0;
     m[e] = b1;
-    l[e] = (__bf16)(r1 - (float)b1);
+    l[e] = (__bf16)(sub_rn(r1, (float)b1));
   }
   bf16x8_t* o = reinterpret_cast<bf16x8_t*>(dst);
   o[0] = h;

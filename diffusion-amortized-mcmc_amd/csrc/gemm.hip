@@ -910,9 +910,9 @@ __device__ __forceinline__ void split3_octet(const float (&v)[8], bf16x8& h, bf1
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const __bf16 b0 = (__bf16)v[e];
-    const float r1 = v[e] - (float)b0;
+    const float r1 = sub_rn(v[e], (float)b0);
     const __bf16 b1 = (__bf16)r1;
-    const float r2 = r1 - (float)b1;
+    const float r2 = sub_rn(r1, (float)b1);
     h[e] = b0;
     m[e] = b1;
     l[e] = (__bf16)r2;
@@ -1445,9 +1445,9 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       for (int d = 0; d < 2; ++d) {
         const float v = av[a][(e + d) >> 2][(e + d) & 3];
         const __bf16 b0 = (__bf16)v;
-        const float r1 = v - (float)b0;
+        const float r1 = sub_rn(v, (float)b0);
         const __bf16 b1 = (__bf16)r1;
-        const float r2 = r1 - (float)b1;
+        const float r2 = sub_rn(r1, (float)b1);
         f[a][0][e + d] = b0;
         f[a][1][e + d] = b1;
         f[a][2][e + d] = (__bf16)r2;
@@ -1535,9 +1535,16 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
           for (int j = 0; j < 4; ++j) {
             const int a = i >> 1, wnp = i & 1;
             acc16[i][j] *= sg;
-            if (m0 + wave * 32 + a * 16 < p.M)
+            if (m0 + wave * 32 + a * 16 < p.M) {
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl, voff,
                                                      soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, 0);
+              // wait states before any VALU may rewrite the store's data VGPRs: the register allocator reuses them
+              // for the next tile's scaled copy at once, and without these nops 3 of every 16 slab tiles held the
+              // next tile's values (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt)
+              __builtin_amdgcn_sched_barrier(0);
+              asm volatile("s_nop 4");
+              __builtin_amdgcn_sched_barrier(0);
+            }
             acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
       } else {
@@ -2710,6 +2717,26 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
 static unsigned long long* g_clk = nullptr;
 static int g_clk_n = 0;
 
+// an at-most-128-row GEMM whose K holds >= 8 sign blocks (the encoder's last conv: M = B, N = nemb, K = 16 Cin): the
+// 64 x 128 tile split into its sign blocks (row-major slabs, x3_ksplit_reduce_kernel), 4x the workgroups of the
+// 128 x 256 layout's split (CIFAR B=128: 16 x 16 = 256 instead of 64); bitwise the same (one slab per sign block)
+template <int EPI>
+static void launch_x3_narrow_split(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int ks = a.K / X3_NEGK;
+  a.ksplit = ks;
+  a.kbpw = 1;
+  a.kslab_reg = 0;
+  a.k_per_z = X3_NEGK;
+  a.proj_nostore = 0;
+  const int ntm = (a.M + 63) / 64, ntn = (a.N + X3_BN - 1) / X3_BN;
+  hipLaunchKernelGGL((gemm_x3_kernel<EPI, O_DENSE, DAMC_X3_VARIANT | X3_NARROW>), dim3(ntm * ntn, 1, ks), dim3(512), 0, s,
+                     a);
+  const long tot = (long)a.M * (a.N / 8);
+  hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, O_DENSE>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
+                     1);
+}
+
 static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
   const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
   if (!(a.a_f32 ? a.A != nullptr : a.A3 != nullptr) || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 ||
@@ -2773,6 +2800,13 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
         c.kw == 1 && c.Cg == c.K && c.A3 && !c.a_f32 && !c.proj_out && !(esk && esk[0] == '0')) {
       hipLaunchKernelGGL(x3_skinny_kernel, dim3((unsigned)((c.N + 255) / 256), (unsigned)((c.M + 15) / 16)), dim3(256),
                          0, s, c);
+      continue;
+    }
+    const char* ens = getenv("DAMC_X3_NARROW_SPLIT");  // (read per call) 0: the 128 x 256 layout below
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32 && !c.proj_out && c.kslab &&
+        c.K % X3_NEGK == 0 && c.K / X3_NEGK >= 8 && c.N % 8 == 0 && (long)(c.K / X3_NEGK) * c.M * c.N <= c.kslab_floats &&
+        !(ens && ens[0] == '0')) {
+      launch_x3_narrow_split<EPI_BIAS_ACT>(c, s);
       continue;
     }
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32) {

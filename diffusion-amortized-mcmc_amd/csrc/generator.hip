@@ -482,9 +482,9 @@ __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, 
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
         const __bf16 b0 = (__bf16)hv[c];
-        const float r1 = hv[c] - (float)b0;
+        const float r1 = sub_rn(hv[c], (float)b0);
         const __bf16 b1 = (__bf16)r1;
-        const __bf16 b2 = (__bf16)(r1 - (float)b1);
+        const __bf16 b2 = (__bf16)(sub_rn(r1, (float)b1));
         lh[c] = __builtin_bit_cast(unsigned short, b0);
         lm[c] = __builtin_bit_cast(unsigned short, b1);
         ll[c] = __builtin_bit_cast(unsigned short, b2);
@@ -604,11 +604,11 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
         for (int e = 0; e < 2; ++e) {
           const float x = v[2 * c2 + e];
           const __bf16 b0 = (__bf16)x;
-          const float r1 = x - (float)b0;
+          const float r1 = sub_rn(x, (float)b0);
           const __bf16 b1 = (__bf16)r1;
           hh[e] = __builtin_bit_cast(unsigned short, b0);
           mm[e] = __builtin_bit_cast(unsigned short, b1);
-          lo[e] = __builtin_bit_cast(unsigned short, (__bf16)(r1 - (float)b1));
+          lo[e] = __builtin_bit_cast(unsigned short, (__bf16)(sub_rn(r1, (float)b1)));
         }
         lh[c2] = hh[0] | ((unsigned)hh[1] << 16);
         lm[c2] = mm[0] | ((unsigned)mm[1] << 16);
@@ -676,11 +676,11 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
       const int k = 8 * q + e, tp = k / NC, o = k - tp * NC;
       const float v = k < 9 * NC ? wpk[((long)tp * Cin + ch) * NC + o] : 0.f;
       const __bf16 b0 = (__bf16)v;
-      const float r1 = v - (float)b0;
+      const float r1 = sub_rn(v, (float)b0);
       const __bf16 b1 = (__bf16)r1;
       wa[t][0][e] = b0;
       wa[t][1][e] = b1;
-      wa[t][2][e] = (__bf16)(r1 - (float)b1);
+      wa[t][2][e] = (__bf16)(sub_rn(r1, (float)b1));
     }
   }
   const int hw = Hin * Win;
@@ -723,11 +723,11 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const __bf16 b0 = (__bf16)dv[e];
-      const float r1 = dv[e] - (float)b0;
+      const float r1 = sub_rn(dv[e], (float)b0);
       const __bf16 b1 = (__bf16)r1;
       d0[e] = b0;
       d1[e] = b1;
-      d2[e] = (__bf16)(r1 - (float)b1);
+      d2[e] = (__bf16)(sub_rn(r1, (float)b1));
     }
     const unsigned m0w = mw0, m1w = mw1;
     load_unit(un + gridDim.x);  // the next unit's loads land under this one's MFMAs and stores
@@ -777,11 +777,11 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
       for (int r = 0; r < 4; ++r) {
         const float v = c[t][r] * (((nib >> r) & 1u) ? 1.f : mask_slope);
         const __bf16 b0 = (__bf16)v;
-        const float r1 = v - (float)b0;
+        const float r1 = sub_rn(v, (float)b0);
         const __bf16 b1 = (__bf16)r1;
         lh[r] = __builtin_bit_cast(unsigned short, b0);
         lm[r] = __builtin_bit_cast(unsigned short, b1);
-        ll[r] = __builtin_bit_cast(unsigned short, (__bf16)(r1 - (float)b1));
+        ll[r] = __builtin_bit_cast(unsigned short, (__bf16)(sub_rn(r1, (float)b1)));
       }
       // image [16 pixels][8 octets x 48 B]: this lane's 4 channels at octet 2 t + (q >> 1), half q & 1
       typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -1016,11 +1016,11 @@ __global__ __launch_bounds__(256) void smallc_proj_x3_kernel(const float* __rest
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const __bf16 b0 = (__bf16)v[e];
-      const float r1 = v[e] - (float)b0;
+      const float r1 = sub_rn(v[e], (float)b0);
       const __bf16 b1 = (__bf16)r1;
       hb[e] = b0;
       mb[e] = b1;
-      lb[e] = (__bf16)(r1 - (float)b1);
+      lb[e] = (__bf16)(sub_rn(r1, (float)b1));
     }
     wfr[t][ks][0][l] = hb;
     wfr[t][ks][1][l] = mb;
@@ -1058,11 +1058,11 @@ __global__ __launch_bounds__(256) void smallc_proj_x3_kernel(const float* __rest
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const __bf16 b0 = (__bf16)v[e];
-        const float r1 = v[e] - (float)b0;
+        const float r1 = sub_rn(v[e], (float)b0);
         const __bf16 b1 = (__bf16)r1;
         a[i][0][e] = b0;
         a[i][1][e] = b1;
-        a[i][2][e] = (__bf16)(r1 - (float)b1);
+        a[i][2][e] = (__bf16)(sub_rn(r1, (float)b1));
       }
     }
     if (ks + 2 < KS) gload(ks + 2);  // lands under this and the next step's MFMAs
@@ -2283,11 +2283,13 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   // z's limbs for the next step's first layer; DAMC_POST_FUSE=0 (read per call) keeps the separate kernels
   const char* pf = getenv("DAMC_POST_FUSE");
   const bool fuse = !(pf && pf[0] == '0');
-  // DAMC_X3_F32A (read per call): the limb-engine convolutions gather fp32 activations and gradients (gemm.hip
-  // X3_F32A), bitwise the limb-gathering form
+  // the limb-engine convolutions gather fp32 activations and gradients (gemm.hip X3_F32A), bitwise the limb-gathering
+  // form; DAMC_X3_F32A=0 (read per call) gathers limbs (CIFAR B=128 bench 51.1K -> 56.1K z-steps/s, B=16 per-rank
+  // step 0.625 -> 0.478 ms; profiles/r04/bench_f32a_ab.txt, step_f32a_ab.txt)
   const char* fa = getenv("DAMC_X3_F32A");
-  const bool f32a = fa && fa[0] == '1';
-  // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection
+  const bool f32a = !(fa && fa[0] == '0');
+  // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection (on the
+  // limb-gathering path only, DAMC_X3_F32A=0: the F32A tile has no 128 x 256 form)
   const char* sf = getenv("DAMC_SMALLC_FUSE");
   const bool proj = !(sf && sf[0] == '0') && !f32a && proj_fusable(g, ws);
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;

@@ -58,11 +58,11 @@ __global__ __launch_bounds__(256) void transpose_x3_kernel(const float* __restri
       for (int e = 0; e < 8; ++e) {  // RNE limb split, as the engine's own split (gemm.hip split3_octet)
         const float v = tile[cl][oct * 8 + e];
         const __bf16 b0 = (__bf16)v;
-        const float r1 = v - (float)b0;
+        const float r1 = sub_rn(v, (float)b0);
         const __bf16 b1 = (__bf16)r1;
         h[e] = b0;
         m[e] = b1;
-        l[e] = (__bf16)(r1 - (float)b1);
+        l[e] = (__bf16)(sub_rn(r1, (float)b1));
       }
       wg_bf16x8* o = reinterpret_cast<wg_bf16x8*>(dst + (((long)c * P + pq) * Bp + nb * 32 + oct * 8) * 3);
       o[0] = h;

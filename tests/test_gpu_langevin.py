@@ -339,8 +339,9 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
 def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block (damc_x3_sign_block() k) per slice, reduced
     in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
-    width with DAMC_X3_KSPLIT=0 vs the default; and the opt-in 64 x 128 tile (gemm.hip X3_NARROW, DAMC_X3_NARROW=1,
-    which replaces split-K where it fills the chip) against both."""
+    width with DAMC_X3_KSPLIT=0 vs the default (F32A, register slabs); and the opt-in 64 x 128 tile on the
+    limb-gathering path (gemm.hip X3_NARROW, DAMC_X3_NARROW=1 with DAMC_X3_F32A=0, which replaces split-K where it
+    fills the chip) against both."""
     from damc import synth
     from src import diffusion_net as dn
 
@@ -352,6 +353,7 @@ def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     for mode, split, narrow in (("unsplit", "0", "0"), ("split", "1", "0"), ("narrow", "1", "1")):
         monkeypatch.setenv("DAMC_X3_KSPLIT", split)
         monkeypatch.setenv("DAMC_X3_NARROW", narrow)
+        monkeypatch.setenv("DAMC_X3_F32A", "0" if narrow == "1" else "1")  # the 64 x 128 tile gathers limbs
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
         torch.cuda.synchronize()
@@ -435,8 +437,10 @@ def test_f32a_posterior_is_bitwise(lv, gpu_device, monkeypatch, name, B):
 def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B):
     """The last ConvT's epilogue runs the output layer's per-tap projection (gemm.hip GemmArgs::proj_out, the 128 x 256
     tile; B=16 splits K, so there the projection runs as proj_rows_kernel over the reduce's output): 2 noisy posterior
-    steps bitwise equal to the separate projection kernel (DAMC_SMALLC_FUSE=0), which shares proj16's arithmetic."""
+    steps bitwise equal to the separate projection kernel (DAMC_SMALLC_FUSE=0), which shares proj16's arithmetic.  The
+    fusion runs on the limb-gathering path (DAMC_X3_F32A=0)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
+    monkeypatch.setenv("DAMC_X3_F32A", "0")
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_SMALLC_FUSE", mode)

@@ -270,10 +270,14 @@ int main(int argc, char** argv) {
       unsigned char* dbits;
       CK(hipMalloc(&dbits, nout / 8));
       CK(hipMemcpy(dbits, bits.data(), nout / 8, hipMemcpyHostToDevice));
-      std::vector<float> outs[4];
-      std::vector<unsigned char> sgns[4];
-      for (int v = 0; v < 4; ++v) {
-        const bool f32a = v & 1, split = v & 2;
+      std::vector<float> outs[6];
+      std::vector<unsigned char> sgns[6];
+      for (int v = 0; v < 6; ++v) {
+        const bool f32a = (v & 1) || v >= 4, split = (v & 2) || v >= 4;
+        unsetenv("DAMC_X3_KSPLIT_BPW");
+        unsetenv("DAMC_X3_KSLAB_REG");
+        if (v == 4) setenv("DAMC_X3_KSPLIT_BPW", "1", 1);
+        if (v == 5) setenv("DAMC_X3_KSLAB_REG", "0", 1);
         GemmArgs a = a0;
         float* c;
         unsigned char* sg;
@@ -309,8 +313,8 @@ int main(int argc, char** argv) {
         CK(hipFree(sg));
       }
       printf("eq B=%d %-28s", B, sh.name);
-      const char* nm[4] = {"v261", "f32a", "v261 split", "f32a split"};
-      for (int v = 1; v < 4; ++v) {
+      const char* nm[6] = {"v261", "f32a", "v261 split", "f32a split", "f32a split bpw1", "f32a split rowmajor"};
+      for (int v = 1; v < 6; ++v) {
         size_t nd = 0, first = (size_t)-1;
         for (size_t i = 0; i < nout; ++i)
           if (memcmp(&outs[v][i], &outs[0][i], 4)) {
@@ -320,6 +324,18 @@ int main(int argc, char** argv) {
         printf("  [%s: %zu differ%s%s]", nm[v], nd, sh.phase && memcmp(sgns[v].data(), sgns[0].data(), nout / 8) ? ", sign bits differ" : "",
                nd ? "" : "");
         if (nd) printf(" (first %zu: %.9g vs %.9g)", first, outs[v][first], outs[0][first]);
+        if (nd && v == 3 && !sh.phase) {  // dgrad (O_DENSE, row = m): differing count per (wave_d, ij) of the 256x128 tile
+          std::vector<int> h(8 * 16, 0);
+          for (size_t i = 0; i < nout; ++i)
+            if (memcmp(&outs[v][i], &outs[0][i], 4)) {
+              const int m = (int)(i / a0.ldc) % 256, n = (int)(i % a0.ldc) % 128;
+              h[((m / 64) * 2 + n / 64) * 16 + ((m % 64) / 16) * 4 + (n % 64) / 16]++;
+            }
+          printf("\n   per (wave_d, ij):");
+          for (int k = 0; k < 128; ++k)
+            if (h[k]) printf(" %d/%d:%d", k / 16, k % 16, h[k]);
+          printf("\n");
+        }
       }
       printf("\n");
       CK(hipFree(mk));
