@@ -146,8 +146,10 @@ def cpu_baseline(budget_s=12.0, full=False):
         orc.posterior_langevin(L, P, z0, x, npost, SIGMA, S_POST, noise=torch.randn(npost, B, NZ))
         orc.prior_langevin(P, zp0, nprior, S_PRIOR, noise=torch.randn(nprior, 2 * B, NZ))
 
-    for _ in range(3 if full else 1):
+    for i in range(3 if full else 1):
         call()
+        if full:  # progress for a supervisor that reads silence as a hang
+            print("cpu baseline: warm-up call %d done" % (i + 1), file=sys.stderr, flush=True)
     ts = []
     t0 = time.perf_counter()
     while True:
@@ -155,6 +157,8 @@ def cpu_baseline(budget_s=12.0, full=False):
         call()
         ts.append(time.perf_counter() - t1)
         el = time.perf_counter() - t0
+        if full:
+            print("cpu baseline: timed call %d %.1f s" % (len(ts), ts[-1]), file=sys.stderr, flush=True)
         if (full and len(ts) >= 5) or (not full and ((el > budget_s and len(ts) >= 5) or len(ts) >= 200)):
             break
     torch.set_num_threads(prev_threads)

@@ -338,102 +338,112 @@ __device__ __forceinline__ float wave_rsum(const float (&v)[N], int lane, int of
   }
 }
 
-// The same layer in ONE pass when a sample's whole conv output for a group of G = 32 / P channels fits the registers of
-// a 1024-thread workgroup (P = ceil(H W / 1024) pixels per thread, 32 values each; launched at P = 1): grid
-// (B, C / G).  Each thread evaluates its pixels' channels with conv3_octet's arithmetic (same fmaf chain, so the same y), the workgroup sums them
-// per channel (wave reduce-scatter, then the 16 wave sums in a fixed order) for the mean, then sums (y - mean)^2 for the
-// variance (two passes over registers), and writes lrelu(IN(y)) as the next convolution's limbs.  The statistics pass,
-// the Welford partials, the merge kernel and the recomputing second pass all drop out.
-template <int CIN, int P>
-__global__ __launch_bounds__(1024) void conv3_in_fused_kernel(const float* __restrict__ x, int H, int W, int C,
+// The same layer in ONE pass when a sample has at most 1024 pixels (32 x 32: CIFAR-10, SVHN) and W % 4 == 0:
+// grid (B, C / 16), 512 threads = 2 channel octets (one per group of 4 waves, so weights are wave-uniform) x 256
+// 4-pixel row runs (1024 threads capped the kernel at 128 VGPRs and it spilled).  Each thread evaluates its 4 pixels x 8 channels with conv3_octet's arithmetic (same fmaf chain,
+// so the same y; each weight read once per 4 pixels, each window value once per run), the workgroup sums them per
+// channel (wave reduce-scatter, then the channel's 4 wave sums in a fixed order) for the mean, then sums
+// (y - mean)^2 for the variance (two passes over registers), and writes lrelu(IN(y)) as the next convolution's limbs.
+// The statistics pass, the Welford partials, the merge kernel and the recomputing second pass all drop out.
+template <int CIN>
+__global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __restrict__ x, int H, int W, int C,
                                                               const float* __restrict__ w, const float* __restrict__ bias,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps, float slope,
                                                               unsigned short* __restrict__ y3) {
-  constexpr int G = 32 / P;
-  extern __shared__ __attribute__((aligned(16))) float smf[];  // [16][G] sums, [2][G] stats, the window
-  float* red = smf;
-  float* st = red + 16 * G;
-  float* win = st + 2 * G;
-  const int b = blockIdx.x, c0 = blockIdx.y * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int HW = H * W;
+  extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][16] weights, [8][8] sums, [2][16], window
+  float* wl = smf;
+  float* red = wl + 9 * CIN * 16;
+  float* st = red + 8 * 8;
+  float* win = st + 32;
+  const int b = blockIdx.x, c0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HW = H * W, cg = wave >> 2, run = tid & 255;  // channels c0 + 8 cg .. + 7; pixels 4 run .. + 3
+  for (int i = tid; i < 9 * CIN * 16; i += 512) wl[i] = w[(i >> 4) * C + c0 + (i & 15)];
   conv3_stage<CIN>(x, b, H, W, 0, H, win);
   __syncthreads();
-  float y[P][G];
+  const int p0 = 4 * run, r = p0 / W, x0 = p0 - r * W;
+  const bool ok = p0 < HW;
+  float y[4][8];
+  {
+    float acc[4][8];
 #pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const int p = tid + 1024 * j;
-    const bool ok = p < HW;
-    const int r = ok ? p / W : 0, xx = ok ? p - r * W : 0;
-    float xv[9 * CIN];
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+#pragma unroll 1
+    for (int ky = 0; ky < 3; ++ky) {  // rolled: unrolled, the compiler hoisted every window and weight load and spilled
+      float xr[CIN][6];  // the window row's 6 columns x0 - 1 .. x0 + 4 (padded coordinates x0 .. x0 + 5)
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) xr[ci][c] = ok ? win[((r + ky) * (W + 2) + x0 + c) * CIN + ci] : 0.f;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) xv[(ky * 3 + kx) * CIN + ci] = win[((r + ky) * (W + 2) + xx + kx) * CIN + ci];
-    // weights at workgroup-uniform addresses: scalar loads into SGPRs, v_fma with an SGPR operand (from LDS they were
-    // 864 broadcast reads per thread, the kernel's bound)
-    const float* wg = w + c0;
+        for (int ci = 0; ci < CIN; ++ci) {
+          const int t = (ky * 3 + kx) * CIN + ci;  // conv3_octet's tap order
+          const f32x4 w0 = *reinterpret_cast<const f32x4*>(wl + t * 16 + 8 * cg);
+          const f32x4 w1 = *reinterpret_cast<const f32x4*>(wl + t * 16 + 8 * cg + 4);
+          const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float acc = 0.f;
+          for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int t = 0; t < 9 * CIN; ++t) acc = fmaf(wg[t * C + g], xv[t], acc);
-      y[j][g] = ok ? acc + (bias ? bias[c0 + g] : 0.f) : 0.f;
+            for (int e = 0; e < 8; ++e) acc[k][e] = fmaf(wv[e], xr[ci][k + kx], acc[k][e]);
+        }
     }
-  }
-  // workgroup sum per channel into st[k * G + g]: wave totals, then the 16 waves in order
-  auto block_sum = [&](const float (&v)[G], int k) {
-    int ch = 0;
-    const float t = wave_rsum<G>(v, lane, 32, ch);
-    if ((lane & (64 / G - 1)) == 0) red[wave * G + ch] = t;
-    __syncthreads();
-    if (tid < G) {
-      float s = red[tid];
 #pragma unroll
-      for (int w2 = 1; w2 < 16; ++w2) s += red[w2 * G + tid];
-      st[k * G + tid] = s;
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[k][e] = ok ? acc[k][e] + (bias ? bias[c0 + 8 * cg + e] : 0.f) : 0.f;
+  }
+  // per-channel workgroup sum of v[e] (channel c0 + 8 cg + e) into st[k * 16 + ...]
+  auto block_sum = [&](const float (&v)[8], int k) {
+    int ch = 0;
+    const float t = wave_rsum<8>(v, lane, 32, ch);
+    if ((lane & 7) == 0) red[wave * 8 + ch] = t;
+    __syncthreads();
+    if (tid < 16) {
+      const int g = tid >> 3, e = tid & 7;  // channel 8 g + e: waves 4 g .. 4 g + 3
+      st[k * 16 + tid] = ((red[(4 * g) * 8 + e] + red[(4 * g + 1) * 8 + e]) + red[(4 * g + 2) * 8 + e]) +
+                         red[(4 * g + 3) * 8 + e];
     }
     __syncthreads();
   };
   const float inv_n = 1.f / (float)HW;
-  float v[G];
+  float v[8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    v[g] = y[0][g];
-#pragma unroll
-    for (int j = 1; j < P; ++j) v[g] += y[j][g];
-  }
+  for (int e = 0; e < 8; ++e) v[e] = ((y[0][e] + y[1][e]) + y[2][e]) + y[3][e];
   block_sum(v, 0);
+  float mean[8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float mean = st[g] * inv_n;
-    v[g] = 0.f;
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = st[8 * cg + e] * inv_n;
+    float q = 0.f;
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const float d = y[j][g] - mean;
-      v[g] = (tid + 1024 * j < HW) ? fmaf(d, d, v[g]) : v[g];
+    for (int k = 0; k < 4; ++k) {
+      const float d = y[k][e] - mean[e];
+      q = ok ? fmaf(d, d, q) : q;
     }
+    v[e] = q;
   }
   block_sum(v, 1);
+  if (!ok) return;
+  float scl[8], shf[8];
 #pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const int p = tid + 1024 * j;
-    if (p >= HW) continue;
+  for (int e = 0; e < 8; ++e) {  // in_merge_kernel's scale / shift form
+    const int c = c0 + 8 * cg + e;
+    scl[e] = (1.f / sqrtf(st[16 + 8 * cg + e] * inv_n + eps)) * gamma[c];
+    shf[e] = beta[c] - mean[e] * scl[e];
+  }
 #pragma unroll
-    for (int o = 0; o < G / 8; ++o) {
-      float t[8];
+  for (int k = 0; k < 4; ++k) {
+    float t[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {  // in_merge_kernel's scale / shift form
-        const int g = 8 * o + e;
-        const float mean = st[g] * inv_n;
-        const float scl = (1.f / sqrtf(st[G + g] * inv_n + eps)) * gamma[c0 + g];
-        const float u = fmaf(y[j][g], scl, beta[c0 + g] - mean * scl);
-        t[e] = u > 0.f ? u : u * slope;
-      }
-      damc::store_x3_octet(t, y3 + 3 * (((long)b * HW + p) * C + c0 + 8 * o));
+    for (int e = 0; e < 8; ++e) {
+      const float u = fmaf(y[k][e], scl[e], shf[e]);
+      t[e] = u > 0.f ? u : u * slope;
     }
+    damc::store_x3_octet(t, y3 + 3 * (((long)b * HW + p0 + k) * C + c0 + 8 * cg));
   }
 }
 
@@ -960,16 +970,15 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     // one pass (conv3_in_fused_kernel) when a sample fits 1024 threads x <= 4 pixels; DAMC_ENC_FIRST_ONEPASS=0 (read
     // per call) keeps the two recomputing passes
     const char* op = getenv("DAMC_ENC_FIRST_ONEPASS");
-    const int P1 = (H * W + 1023) / 1024, G1 = P1 <= 1 ? 32 : (P1 <= 2 ? 16 : 8);
-    const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + 18 * G1) * sizeof(float);
-    // (P = 1 only: at 2 / 4 pixels per thread the kernel spills; CelebA-64 keeps the two passes)
-    const bool one = !(op && op[0] == '0') && P1 == 1 && C % G1 == 0 && sm1 <= 65536;
-#define DAMC_C1(CIN_, P_)                                                                                           \
-  if (one && L.cin == CIN_ && P1 == P_) {                                                                          \
-    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_, P_>), dim3(B, C / (32 / P_)), dim3(1024), sm1, s, x, H, W, C,     \
-                       L.w_packed, L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3);                           \
+    const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * 16 + 8 * 8 + 32) * sizeof(float);
+    // (a sample of at most 1024 pixels; CelebA-64 and larger keep the two passes)
+    const bool one = !(op && op[0] == '0') && H * W <= 1024 && W % 4 == 0 && C % 16 == 0 && sm1 <= 65536;
+#define DAMC_C1(CIN_)                                                                                               \
+  if (one && L.cin == CIN_) {                                                                                       \
+    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(B, C / 16), dim3(512), sm1, s, x, H, W, C, L.w_packed,     \
+                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3);                                       \
   }
-    DAMC_C1(1, 1) DAMC_C1(3, 1) DAMC_C1(4, 1)
+    DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
 #undef DAMC_C1
 #define DAMC_C3(CIN_)                                                                                               \
   if (!one && L.cin == CIN_) {                                                                                      \

@@ -81,6 +81,9 @@ struct GemmArgs {
   const float* proj_w = nullptr;
   float* proj_out = nullptr;
   int proj_np = 0, proj_ldw = 0, proj_nostore = 0;
+  // one chain per 128-channel chunk (gemm.hip PROJ_CHUNK), chunk j into proj_out + j * proj_pstride (floats; the whole
+  // batch's npix * proj_np); the gather adds the partials in order
+  long proj_pstride = 0;
   // limb engine, O_PHASE / O_DENSE: split-K over ksplit slices of k_per_z (a multiple of X3_NEGK) when the grid
   // would under-fill the chip; the slices' fp32 tiles go to kslab [zdim * ksplit][M][N] and a fixed-order reduce
   // applies the epilogue.  kslab = scratch the caller owns (kslab_floats of it); null: never split
@@ -95,8 +98,11 @@ struct GemmArgs {
   int kslab_reg = 0;
 };
 // the fused output-layer projection as a kernel of its own: P[pix][n] = sum_c h[pix][c] w[n][c] (c < C <= 256,
-// C % 16 == 0; n < np, np = 32 or 64; w rows ldw floats), bitwise the fused form (same MFMA sequence per row)
-int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, hipStream_t s);
+// C % 16 == 0; n < np, np = 32 or 64; w rows ldw floats), bitwise the fused form (same MFMA sequence per row); for
+// C > 128 the two 128-channel chunks' sums go to P and P + pstride
+constexpr int PROJ_CHUNK = 128;  // channels per output-layer projection chain (one F32A N tile)
+int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, long pstride,
+                     hipStream_t s);
 // slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
 long x3_ksplit_floats(int M, int N, int K, int zdim);
 

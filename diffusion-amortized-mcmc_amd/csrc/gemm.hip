@@ -942,10 +942,13 @@ __device__ __forceinline__ void proj16(const float* tile, int ts, int r0, int C,
 }
 
 // the projection alone: 128 pixels per workgroup (8 waves x 16 rows) staged in LDS with gemm_x3_kernel's WIDE tile
-// stride, then proj16 (NT = np / 16)
+// stride, then proj16 (NT = np / 16) per 128-channel chunk (PROJ_CHUNK): chunk j's chain goes to partial buffer j
+// (P + j npix np), and the gather adds the partials in order -- the chunking of the F32A tile's fused projection, whose
+// workgroups each hold one 128-channel N tile
 template <int NT>
 __global__ __launch_bounds__(512) void proj_rows_kernel(const float* __restrict__ h, long npix, int C,
-                                                        const float* __restrict__ w, int ldw, float* __restrict__ P) {
+                                                        const float* __restrict__ w, int ldw, float* __restrict__ P,
+                                                        long pstride) {
   constexpr int TS = 256 + 4;
   __shared__ __attribute__((aligned(16))) float tile[128 * TS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -958,25 +961,30 @@ __global__ __launch_bounds__(512) void proj_rows_kernel(const float* __restrict_
         pix < npix ? *reinterpret_cast<const f32x4*>(h + pix * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  f32x4 acc[NT];
-  proj16<NT>(tile, TS, wave * 16, C, w, ldw, acc);
   const int m = lane & 15, q = lane >> 4;
+  for (int c0 = 0; c0 < C; c0 += PROJ_CHUNK) {  // one chain per 128-channel chunk, into its own partial buffer
+    f32x4 acc[NT];
+    proj16<NT>(tile + c0, TS, wave * 16, min(PROJ_CHUNK, C - c0), w + c0, ldw, acc);
+    float* Pc = P + (c0 / PROJ_CHUNK) * pstride;
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long pix = p0 + wave * 16 + 4 * q + r;
-      if (pix < npix) P[pix * (16 * NT) + 16 * t + m] = acc[t][r];
-    }
+      for (int r = 0; r < 4; ++r) {
+        const long pix = p0 + wave * 16 + 4 * q + r;
+        if (pix < npix) Pc[pix * (16 * NT) + 16 * t + m] = acc[t][r];
+      }
+  }
 }
 
-int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, hipStream_t s) {
+int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, long pstride,
+                     hipStream_t s) {
   if (C <= 0 || C > 256 || C % 16 || (np != 32 && np != 64) || npix <= 0) return DAMC_ERR_ARG;
+  if (C > PROJ_CHUNK && pstride < npix * np) return DAMC_ERR_ARG;
   const dim3 grid((unsigned)((npix + 127) / 128));
   if (np == 32)
-    hipLaunchKernelGGL(proj_rows_kernel<2>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P);
+    hipLaunchKernelGGL(proj_rows_kernel<2>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P, pstride);
   else
-    hipLaunchKernelGGL(proj_rows_kernel<4>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P);
+    hipLaunchKernelGGL(proj_rows_kernel<4>, grid, dim3(512), 0, s, h, npix, C, w, ldw, P, pstride);
   return (int)hipGetLastError();
 }
 
@@ -2134,28 +2142,40 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       o[1] = m;
       o[2] = l;
     }
-    if (OM == O_PHASE && EPI == EPI_BIAS_ACT && WIDE && p.proj_out) {  // the activated row back into the tile
+    if (OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A) && p.proj_out) {  // the activated row back into the tile
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
   }
-  if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT && WIDE) {
-    // fused output-layer projection (GemmArgs::proj_out; the launcher sets it only when this tile holds every channel,
-    // n0 == 0 and N <= BN): 8 waves x 16 rows, proj16 as proj_rows_kernel, P indexed by the output pixel
+  if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A)) {
+    // fused output-layer projection (GemmArgs::proj_out), proj16 as proj_rows_kernel, P indexed by the output pixel,
+    // one chain per 128-channel chunk into partial buffer chunk (proj_rows_kernel's chunking).  WIDE: the tile holds
+    // every channel (n0 == 0, N <= 256), 8 waves x 16 rows, all chunks.  F32A: the tile holds channels n0 .. n0 + 127
+    // = chunk n0 / 128, 8 waves x 32 rows (two 16-row groups each)
     if (p.proj_out) {
       __syncthreads();
       const int m = lane & 15, q = lane >> 4;
       auto store = [&](auto NT_) {
         constexpr int NT = decltype(NT_)::value;
-        f32x4 acc[NT];
-        proj16<NT>(tile, TS, wave * 16, p.N, p.proj_w, p.proj_ldw, acc);
+        constexpr int RG = F32A ? 2 : 1;
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+        for (int g = 0; g < RG; ++g) {
+          const int r0 = F32A ? wave * 32 + g * 16 : wave * 16;
+          for (int c0 = 0; c0 < (F32A ? BN : p.N); c0 += PROJ_CHUNK) {
+            const int cc = F32A ? n0 : c0;  // global channel of the chunk's first column
+            if (cc >= p.N) break;
+            f32x4 acc[NT];
+            proj16<NT>(tile + c0, TS, r0, min(PROJ_CHUNK, p.N - cc), p.proj_w + cc, p.proj_ldw, acc);
+            float* Pc = p.proj_out + (cc / PROJ_CHUNK) * p.proj_pstride;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const long ro = rowtab[wave * 16 + 4 * q + r];
-            if (ro >= 0) p.proj_out[(ro / p.ldc) * (16 * NT) + 16 * t + m] = acc[t][r];
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const long ro = rowtab[r0 + 4 * q + r];
+                if (ro >= 0) Pc[(ro / p.ldc) * (16 * NT) + 16 * t + m] = acc[t][r];
+              }
           }
+        }
       };
       if (p.proj_np == 32)
         store(std::integral_constant<int, 2>{});
@@ -2401,7 +2421,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       auto proj_after = [&]() {
         if (OM == O_PHASE && a.proj_out)
           (void)launch_proj_rows(a.C, (long)(a.M / (a.Hq * a.Wq)) * a.Hout * a.Wout, a.N, a.proj_w, a.proj_ldw,
-                                 a.proj_np, a.proj_out, s);
+                                 a.proj_np, a.proj_out, a.proj_pstride, s);
       };
       // sign blocks per workgroup: the most (a power of two dividing ks) that still leaves >= 256 workgroups, so one
       // round covers the chip (the default 16x16-tile path only); DAMC_X3_KSPLIT_BPW (read per call) pins it
@@ -2772,15 +2792,6 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       c.clk = g_clk;
       c.clk_n = g_clk_n;
     }
-    if (a.proj_out) {  // the fused output-layer projection: the 128 x 256 layout, one N tile holding every channel
-      if (om != O_PHASE || epi != EPI_BIAS_ACT || a.N > 256 || a.N % 16 || !a.C || !a.proj_w ||
-          (a.proj_np != 32 && a.proj_np != 64))
-        return DAMC_ERR_ARG;
-      if (c.a_f32) return DAMC_ERR_UNSUPPORTED;  // the F32A loop has no 128 x 256 form
-      c.proj_out = a.proj_out + b0 * (long)a.Hout * a.Wout * a.proj_np;
-      launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
-      continue;
-    }
     if (a.A3) c.A3 = a.A3 + b0 * img * 3;
     if (a.a_f32) c.A = a.A + b0 * img;
     if (a.C) c.C = a.C + b0 * cimg;
@@ -2789,6 +2800,19 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     if (a.mask_sgn) c.mask_sgn = a.mask_sgn + b0 * cimg / 8;
     if (a.mask) c.mask = a.mask + b0 * cimg;
     c.M = (int)(nb * hwq);
+    if (a.proj_out) {  // the fused output-layer projection (GemmArgs::proj_out, 128-channel chunks)
+      if (om != O_PHASE || epi != EPI_BIAS_ACT || a.N > 256 || a.N % 16 || !a.C || !a.proj_w ||
+          (a.proj_np != 32 && a.proj_np != 64) || (a.N > PROJ_CHUNK && a.proj_pstride <= 0))
+        return DAMC_ERR_ARG;
+      c.proj_out = a.proj_out + b0 * (long)a.Hout * a.Wout * a.proj_np;
+      if (c.a_f32) {  // the F32A tile: each 128-channel N tile projects its chunk
+        if (a.N > PROJ_CHUNK && a.N % PROJ_CHUNK) return DAMC_ERR_UNSUPPORTED;
+        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s);
+      } else {  // the 128 x 256 layout: one N tile holding every channel
+        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+      }
+      continue;
+    }
     // at most 128 rows (the first layer, M = B <= 128): the 128 x 256 block layout, no half-empty 256-row tile
     // (bitwise the default layout: every output takes the same MFMA sequence; 46.6 -> 35.7 us for CIFAR's B = 128
     // first layer, tools/gemm_bench.hip).  DAMC_X3_WIDE=0 (read per call) keeps the default layout

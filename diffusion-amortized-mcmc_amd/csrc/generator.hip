@@ -417,18 +417,16 @@ __global__ __launch_bounds__(256) void smallc_fwd_s2_kernel(const float* __restr
   }
 }
 
-// UNI (Cin == 64 CH: one pixel per wave): the pixel index is made wave-uniform, so the K*K*NC delta gathers of a
-// pixel become scalar loads (s_load, scalar cache) instead of 64-lane vector loads of one address each
-template <int NC, int K, int S, int CH, bool UNI = false>
+template <int NC, int K, int S, int CH>
 __global__ __launch_bounds__(256) void smallc_dgrad_reg_kernel(float* h, int B, int Hin, int Win, int Cin, int pad,
                                                                int Hout, int Wout, const float* __restrict__ wpk,
                                                                const float* __restrict__ delta, int mask_act,
                                                                float mask_slope, unsigned short* __restrict__ h3) {
   typedef typename VecT<CH>::T V;
-  const int G = UNI ? 64 : Cin / CH, P = 64 / G;
+  const int G = Cin / CH, P = 64 / G;
   const int lane = threadIdx.x & 63;
-  const int wave = UNI ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (int)(threadIdx.x >> 6);
-  const int g = UNI ? lane : lane % G, sub = UNI ? 0 : lane / G;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane % G, sub = lane / G;
   const int ci0 = g * CH;
   float w[K * K][CH][NC];
 #pragma unroll
@@ -847,12 +845,6 @@ bool smallc_reg_ok(const damc_layer_t& L) {
   return G <= 64 && (64 % G) == 0;
 }
 
-// DAMC_SMALLC_UNI=1 (read per call): the k4 s2 dgrad at Cin 128 with wave-uniform pixels (opt-in until measured)
-inline bool uni_dgrad() {
-  const char* e = getenv("DAMC_SMALLC_UNI");
-  return e && e[0] == '1';
-}
-
 // dispatch of a register-resident instantiation (caller checked smallc_reg_ok)
 template <int NC>
 bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, float* h_out, int B, const float* x,
@@ -876,9 +868,6 @@ bool smallc_reg_dispatch(bool fwd, const damc_layer_t& L, const float* h_in, flo
   } else {
     if (L.k == 3)
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 3, 1, 4>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
-                         L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
-    else if (G == 64 && uni_dgrad())
-      hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2, true>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
                          L.win, L.cin, L.pad, L.hout, L.wout, L.w_fwd, delta_in, mask_act, mask_slope, h3);
     else
       hipLaunchKernelGGL((smallc_dgrad_reg_kernel<NC, 4, 2, 2>), dim3(grid), dim3(256), 0, s, h_out, B, L.hin,
@@ -1097,8 +1086,8 @@ __global__ __launch_bounds__(256) void smallc_proj_x3_kernel(const float* __rest
 // Stage 2: out[b,oy,ox,co] = bias + sum over the valid taps of P[input pixel][tap*NC + co], then tanh,
 // x_hat (NCHW) and the residual delta = (x_hat - x)/s^2 * (1 - x_hat^2) (NHWC).  One thread per output pixel.
 template <int NC, int K, int S>
-__global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restrict__ P, int ldp, int B, int Hin,
-                                                            int Win, int pad, int Hout, int Wout,
+__global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restrict__ P, const float* __restrict__ P1,
+                                                            int ldp, int B, int Hin, int Win, int pad, int Hout, int Wout,
                                                             const float* __restrict__ bias, const float* x,
                                                             float inv_s2, float* delta, float* xhat,
                                                             float* sqerr_sum) {
@@ -1125,9 +1114,9 @@ __global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restr
         if (tx < 0 || (S == 2 && (tx & 1))) continue;
         const int ix = tx / S;
         if (ix >= Win) continue;
-        const float* pp = P + (((long)b * Hin + iy) * Win + ix) * ldp + (ky * K + kx) * NC;
+        const long po = (((long)b * Hin + iy) * Win + ix) * ldp + (ky * K + kx) * NC;
 #pragma unroll
-        for (int o = 0; o < NC; ++o) acc[o] += pp[o];
+        for (int o = 0; o < NC; ++o) acc[o] += P1 ? P[po + o] + P1[po + o] : P[po + o];  // chunk partials in order
       }
     }
 #pragma unroll
@@ -1174,7 +1163,7 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   int rc = 0;
   if (p_ready) {
   } else if (use16) {
-    if ((rc = damc::launch_proj_rows(h, npin, L.cin, L.w_bwd, L.cin, 32 * nt, Pbuf, s))) return rc;
+    if ((rc = damc::launch_proj_rows(h, npin, L.cin, L.w_bwd, L.cin, 32 * nt, Pbuf, npin * 32 * nt, s))) return rc;
   } else {
   const int g1 = (int)((npin + 127) / 128);
   // the LDS-staged kernel when Cin is whole 64-channel chunks (CIFAR B=128: 63.5 -> 51.3 us for projection + gather);
@@ -1205,9 +1194,11 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   }
   const long npout = (long)B * L.hout * L.wout;
   const int g2 = (int)((npout + 255) / 256);
+  // the proj16 forms (proj_rows_kernel and the fused epilogues) leave one partial per 128-channel chunk
+  const float* P1 = ((p_ready || use16) && L.cin > damc::PROJ_CHUNK) ? Pbuf + npin * 32 * nt : nullptr;
 #define SG(NC_, K_, S_)                                                                                             \
-  hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2), dim3(256), 0, s, Pbuf, nt * 32, B, L.hin, L.win, \
-                     L.pad, L.hout, L.wout, L.bias, x, inv_s2, delta, xhat, sqerr)
+  hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2), dim3(256), 0, s, Pbuf, P1, nt * 32, B, L.hin,     \
+                     L.win, L.pad, L.hout, L.wout, L.bias, x, inv_s2, delta, xhat, sqerr)
   if (L.cout == 3) {
     if (L.k == 3) SG(3, 3, 1); else SG(3, 4, 2);
   } else {
@@ -1513,7 +1504,10 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   const int S = (g->n_layers == 1) ? 1 : proj_slices(K0);
   float* sl = take((long)S * B * g->nz);
   float* gl = take((long)B * g->nz);
-  float* pb = (F.kind == DAMC_LAYER_SMALLC) ? take((long)B * F.hin * F.win * smallc_ntile(F) * 32) : nullptr;
+  // the output layer's per-tap projections, one buffer per 128-channel chunk of its input (proj16's partials)
+  float* pb = (F.kind == DAMC_LAYER_SMALLC)
+                  ? take((long)B * F.hin * F.win * smallc_ntile(F) * 32 * ((F.cin + damc::PROJ_CHUNK - 1) / damc::PROJ_CHUNK))
+                  : nullptr;
   unsigned short* z3 =
       x3_proj_cap(L0) ? reinterpret_cast<unsigned short*>(take((long)B * g->nz * 3 / 2 + 4)) : nullptr;
   // split-K slabs: the largest any UP2 forward / input gradient of this batch uses (damc::x3_ksplit)
@@ -1657,6 +1651,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
           a.proj_ldw = F.cin;
           a.proj_np = 32 * smallc_ntile(F);
           a.proj_out = ws.pbuf;
+          a.proj_pstride = (long)B * F.hin * F.win * a.proj_np;
           // the activation itself is not stored when its sign bits carry the output layer's dgrad mask (k3 output
           // layers, hbits); a k4 s2 output layer's dgrad reads the fp32 activation's sign
           a.proj_nostore = hbits(g, i) ? 1 : 0;
@@ -1682,7 +1677,7 @@ bool proj_fusable(const damc_generator_t* g, const Workspace& ws) {
   const damc_layer_t& F = g->layers[n - 1];
   const damc_layer_t& L = g->layers[n - 2];
   return F.kind == DAMC_LAYER_SMALLC && smallc_twostage_ok(F) && smallc_proj16_ok(F) && L.kind == DAMC_LAYER_UP2 &&
-         x3_fwd(L) && L.cout == F.cin && F.w_bwd;
+         x3_fwd(L) && L.cout == F.cin && F.w_bwd && (F.cin <= damc::PROJ_CHUNK || F.cin % damc::PROJ_CHUNK == 0);
 }
 
 // final layer forward: delta (+ optional x_hat NCHW / row-major) and |x_hat-x|^2/(2s^2) into sqerr
@@ -2291,7 +2286,7 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection (on the
   // limb-gathering path only, DAMC_X3_F32A=0: the F32A tile has no 128 x 256 form)
   const char* sf = getenv("DAMC_SMALLC_FUSE");
-  const bool proj = !(sf && sf[0] == '0') && !f32a && proj_fusable(g, ws);
+  const bool proj = !(sf && sf[0] == '0') && proj_fusable(g, ws);
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;
   bool z3_ready = false;
   for (int i = 0; i < n_steps; ++i) {

@@ -433,14 +433,15 @@ def test_f32a_posterior_is_bitwise(lv, gpu_device, monkeypatch, name, B):
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [16, 128])
-def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B):
-    """The last ConvT's epilogue runs the output layer's per-tap projection (gemm.hip GemmArgs::proj_out, the 128 x 256
-    tile; B=16 splits K, so there the projection runs as proj_rows_kernel over the reduce's output): 2 noisy posterior
-    steps bitwise equal to the separate projection kernel (DAMC_SMALLC_FUSE=0), which shares proj16's arithmetic.  The
-    fusion runs on the limb-gathering path (DAMC_X3_F32A=0)."""
+@pytest.mark.parametrize("B,f32a", [(16, "1"), (128, "1"), (16, "0"), (128, "0")])
+def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B, f32a):
+    """The last ConvT's epilogue runs the output layer's per-tap projection (gemm.hip GemmArgs::proj_out; B=16
+    splits K, so there the projection runs as proj_rows_kernel over the reduce's output): 2 noisy posterior steps
+    bitwise equal to the separate projection kernel (DAMC_SMALLC_FUSE=0), which shares proj16's arithmetic and its
+    128-channel chunks.  Both tiles: the F32A kernel (each 128-channel N tile projects its chunk) and the
+    limb-gathering 128 x 256 layout (DAMC_X3_F32A=0, every channel in one tile)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
-    monkeypatch.setenv("DAMC_X3_F32A", "0")
+    monkeypatch.setenv("DAMC_X3_F32A", f32a)
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_SMALLC_FUSE", mode)
