@@ -1140,6 +1140,70 @@ __global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restr
   }
 }
 
+// The k3 s1 gather through LDS: a workgroup takes R output rows of one sample, stages the R + 2 input rows' projection
+// rows (9 NC taps each, the two chunk partials already added in order) with coalesced loads, then gathers from LDS with
+// smallc_gather_kernel's arithmetic (same tap order, same adds), so the result is bitwise that kernel's.  The
+// direct gather issued 27 (x 2 partials) scattered 4-B loads per output pixel: 36 us at CIFAR B=128.
+template <int NC>
+__global__ __launch_bounds__(256) void smallc_gather_lds_kernel(const float* __restrict__ P, const float* __restrict__ P1,
+                                                                int ldp, int H, int W, int R,
+                                                                const float* __restrict__ bias, const float* x,
+                                                                float inv_s2, float* delta, float* xhat,
+                                                                float* sqerr_sum) {
+  constexpr int T = 9 * NC;
+  extern __shared__ float pr[];  // [(R + 2) rows][W][T]
+  __shared__ float red[4];
+  const int b = blockIdx.x, r0 = blockIdx.y * R, rows = min(R, H - r0);
+  const int n = (rows + 2) * W * T;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int rr = i / (W * T), rem = i - rr * (W * T), px = rem / T, t = rem - px * T;
+    const int iy = r0 - 1 + rr;
+    if (iy < 0 || iy >= H) continue;
+    const long po = (((long)b * H + iy) * W + px) * ldp + t;
+    pr[i] = P1 ? P[po] + P1[po] : P[po];
+  }
+  __syncthreads();
+  float sq = 0.f;
+  for (int p = threadIdx.x; p < rows * W; p += 256) {
+    const int oy = r0 + p / W, ox = p - (p / W) * W;
+    float acc[NC];
+#pragma unroll
+    for (int o = 0; o < NC; ++o) acc[o] = bias ? bias[o] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy + 1 - ky;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox + 1 - kx;
+        if (ix < 0 || ix >= W) continue;
+        const float* q = pr + ((iy - r0 + 1) * W + ix) * T + (ky * 3 + kx) * NC;
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[o] += q[o];
+      }
+    }
+    const long pix = ((long)b * H + oy) * W + ox;
+#pragma unroll
+    for (int o = 0; o < NC; ++o) {
+      const float t = tanhf(acc[o]);
+      const long nchw = (((long)b * NC + o) * H + oy) * W + ox;
+      if (xhat) xhat[nchw] = t;
+      if (delta) {
+        const float rd = t - x[nchw];
+        delta[pix * NC + o] = rd * inv_s2 * (1.f - t * t);
+        sq += rd * rd;
+      }
+    }
+  }
+  if (sqerr_sum) {
+    sq = wave_sum(sq);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
 int smallc_ntile(const damc_layer_t& L) { return (L.k * L.k * L.cout + 31) / 32; }
 
 bool smallc_twostage_ok(const damc_layer_t& L) {
@@ -1196,6 +1260,24 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   const int g2 = (int)((npout + 255) / 256);
   // the proj16 forms (proj_rows_kernel and the fused epilogues) leave one partial per 128-channel chunk
   const float* P1 = ((p_ready || use16) && L.cin > damc::PROJ_CHUNK) ? Pbuf + npin * 32 * nt : nullptr;
+  // k3 s1 p1, the same grid in and out: the LDS-staged gather (bitwise); DAMC_SMALLC_GATHER_LDS=0 (read per call)
+  // keeps the direct one
+  const char* gl = getenv("DAMC_SMALLC_GATHER_LDS");
+  // rows per workgroup: at most what 60 KB of LDS holds (with the 2 halo rows), spread evenly over the strips
+  const int gRmax = L.wout > 0 ? std::min(L.hout, 15360 / (L.wout * 9 * L.cout) - 2) : 0;
+  const int gR = gRmax > 0 ? (L.hout + (L.hout + gRmax - 1) / gRmax - 1) / ((L.hout + gRmax - 1) / gRmax) : 0;
+  if (!(gl && gl[0] == '0') && L.k == 3 && L.stride == 1 && L.pad == 1 && L.hin == L.hout && L.win == L.wout &&
+      gR >= 4) {
+    const size_t sm = (size_t)(gR + 2) * L.wout * 9 * L.cout * sizeof(float);
+    const dim3 g(B, (L.hout + gR - 1) / gR);
+    if (L.cout == 3)
+      hipLaunchKernelGGL(smallc_gather_lds_kernel<3>, g, dim3(256), sm, s, Pbuf, P1, nt * 32, L.hout, L.wout, gR,
+                         L.bias, x, inv_s2, delta, xhat, sqerr);
+    else
+      hipLaunchKernelGGL(smallc_gather_lds_kernel<1>, g, dim3(256), sm, s, Pbuf, P1, nt * 32, L.hout, L.wout, gR,
+                         L.bias, x, inv_s2, delta, xhat, sqerr);
+    return (int)hipGetLastError();
+  }
 #define SG(NC_, K_, S_)                                                                                             \
   hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2), dim3(256), 0, s, Pbuf, P1, nt * 32, B, L.hin,     \
                      L.win, L.pad, L.hout, L.wout, L.bias, x, inv_s2, delta, xhat, sqerr)
