@@ -1266,8 +1266,10 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   // rows per workgroup: at most what 60 KB of LDS holds (with the 2 halo rows), spread evenly over the strips
   const int gRmax = L.wout > 0 ? std::min(L.hout, 15360 / (L.wout * 9 * L.cout) - 2) : 0;
   const int gR = gRmax > 0 ? (L.hout + (L.hout + gRmax - 1) / gRmax - 1) / ((L.hout + gRmax - 1) / gRmax) : 0;
+  // (only where the strips fill the chip: at CIFAR B=16, 48 workgroups, it measured 10 us slower than the direct
+  // gather; at B=128, 384 workgroups, 13 us faster; profiles/r04/gather_lds_ab.txt)
   if (!(gl && gl[0] == '0') && L.k == 3 && L.stride == 1 && L.pad == 1 && L.hin == L.hout && L.win == L.wout &&
-      gR >= 4) {
+      gR >= 4 && (long)B * ((L.hout + gR - 1) / gR) >= 256) {
     const size_t sm = (size_t)(gR + 2) * L.wout * 9 * L.cout * sizeof(float);
     const dim3 g(B, (L.hout + gR - 1) / gR);
     if (L.cout == 3)

@@ -471,11 +471,12 @@ def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [5, 128])
+@pytest.mark.parametrize("B", [100, 128])
 def test_lds_staged_gather_is_bitwise_the_direct_gather(lv, gpu_device, monkeypatch, B):
     """The k3 s1 output layer's gather (delta, x_hat from the per-tap projections and their two 128-channel partials)
     staged through LDS per strip of rows (generator.hip smallc_gather_lds_kernel): 2 noisy posterior steps bitwise
-    equal to the direct per-pixel gather (DAMC_SMALLC_GATHER_LDS=0); ragged batch B=5 and the full B=128."""
+    equal to the direct per-pixel gather (DAMC_SMALLC_GATHER_LDS=0), at batches whose strips fill the chip (the
+    LDS form runs from 256 workgroups: B=100 and the full B=128)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
     out = {}
     for mode in ("0", "1"):
