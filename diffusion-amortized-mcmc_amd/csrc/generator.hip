@@ -645,7 +645,10 @@ __global__ __launch_bounds__(256) void smallc_dgrad_k3_kernel(float* __restrict_
 // F32O (round 4): the gradient leaves as fp32 NHWC (4 B per element: the next dgrad stages its A operand as fp32,
 // gemm.hip X3_F32A) through a per-wave image of 272-B pixel rows (8 rows of a ds_write_b128 group on 8 distinct
 // 4-bank groups), 4 wave-instructions of 16-B stores per unit; the values are the limb form's before its split.
-template <int NC, int NG, bool F32O = false>
+// KT x KT taps at stride ST (round 4: also the k4 s2 p1 output layer of the 64x64 / 256x256 generators, whose K =
+// 16 NC = 48 runs as two 32-deep k steps per limb product, both in one accumulation chain; pixel y's window is
+// delta rows ST y - 1 .. ST y - 1 + KT - 1)
+template <int NC, int NG, bool F32O = false, int KT = 3, int ST = 1>
 __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix, int Hin, int Win,
                                                                       const float* __restrict__ wpk,
                                                                       const float* __restrict__ delta,
@@ -653,7 +656,9 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
                                                                       const unsigned char* __restrict__ hbits,
                                                                       int probe = 0) {
   // probe (tools/smallc_bench.hip only, wrong results): 1 no delta / sign-bit loads, 2 no output stores
-  static_assert(9 * NC <= 32, "the 3x3 window of NC channels fills one 32-deep k tile");
+  constexpr int KK = KT * KT * NC, KS = (KK + 31) / 32;  // k values of a pixel's window, 32-deep k steps
+  static_assert(KS <= 2, "at most two k steps");
+  const int Hout = ST * Hin, Wout = ST * Win;
   typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
   constexpr int Cin = 64 * NG;
   // per-wave output image, pixel rows padded 384 -> 392 B (98 dwords): the 16 lanes of a ds_write_b64 group (16
@@ -665,34 +670,37 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
   const int q = lane >> 4, m = lane & 15;
   unsigned char* const stg = stg_all[wave];
   // this wave's W^T limb fragments: tile t = channels 64 w + 16 t + m (rows), k = 8 q .. 8 q + 7
-  bf16x8_t wa[4][3];
+  bf16x8_t wa[KS][4][3];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int ch = 64 * wave + 16 * t + m;
+  for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * q + e, tp = k / NC, o = k - tp * NC;
-      const float v = k < 9 * NC ? wpk[((long)tp * Cin + ch) * NC + o] : 0.f;
-      const __bf16 b0 = (__bf16)v;
-      const float r1 = sub_rn(v, (float)b0);
-      const __bf16 b1 = (__bf16)r1;
-      wa[t][0][e] = b0;
-      wa[t][1][e] = b1;
-      wa[t][2][e] = (__bf16)(sub_rn(r1, (float)b1));
+    for (int t = 0; t < 4; ++t) {
+      const int ch = 64 * wave + 16 * t + m;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 32 * ks + 8 * q + e, tp = k / NC, o = k - tp * NC;
+        const float v = k < KK ? wpk[((long)tp * Cin + ch) * NC + o] : 0.f;
+        const __bf16 b0 = (__bf16)v;
+        const float r1 = sub_rn(v, (float)b0);
+        const __bf16 b1 = (__bf16)r1;
+        wa[ks][t][0][e] = b0;
+        wa[ks][t][1][e] = b1;
+        wa[ks][t][2][e] = (__bf16)(sub_rn(r1, (float)b1));
+      }
     }
-  }
   const int hw = Hin * Win;
   const int units = (npix + 15) >> 4;
   // every global access is a buffer access whose out-of-range offset reads zero / drops the store, so no load or store
   // sits in a branch (a store in a divergent branch made the compiler wait vmcnt(0) for it at every unit)
-  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)delta, (short)0, npix * NC * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)delta, (short)0, npix * ST * ST * NC * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)hbits, (short)0, npix * (Cin / 8), 0x00020000);
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc(outp, (short)0, npix * (F32O ? 4 : 6) * Cin, 0x00020000);
   constexpr int OOB = 0x7FFFFFF0;
   // the unit's loads: D's column for this lane's pixel (k = 8 q .. 8 q + 7) and the pixel's 8 sign-bit bytes of this
   // wave's 64 channels
-  float dv[8];
+  float dv[KS][8];
   unsigned mw0 = 0u, mw1 = 0u;
   auto load_unit = [&](int un) {
     const int pix = un * 16 + m;
@@ -700,13 +708,15 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
     const int b = live ? pix / hw : 0, rem = live ? pix - b * hw : 0;
     const int y = rem / Win, x = rem - y * Win;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * q + e, tp = k / NC, o = k - tp * NC;
-      const int yy = y + tp / 3 - 1, xx = x + tp % 3 - 1;
-      const bool ok = live && k < 9 * NC && (unsigned)yy < (unsigned)Hin && (unsigned)xx < (unsigned)Win;
-      dv[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            rd, ok ? ((((b * Hin + yy) * Win + xx) * NC + o) * 4) : OOB, 0, 0));
-    }
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 32 * ks + 8 * q + e, tp = k / NC, o = k - tp * NC;
+        const int yy = ST * y + tp / KT - 1, xx = ST * x + tp % KT - 1;
+        const bool ok = live && k < KK && (unsigned)yy < (unsigned)Hout && (unsigned)xx < (unsigned)Wout;
+        dv[ks][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rd, ok ? ((((b * Hout + yy) * Wout + xx) * NC + o) * 4) : OOB, 0, 0));
+      }
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
     const u2 t = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rb, live ? pix * (Cin / 8) + 8 * wave : OOB,
                                                                              0, 0));
@@ -717,34 +727,49 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
   load_unit(un);
   const int nsh = 8 * (q >> 1) + 4 * (q & 1);
   for (; un < units; un += gridDim.x) {
-    bf16x8_t d0, d1, d2;
+    bf16x8_t d0[KS], d1[KS], d2[KS];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const __bf16 b0 = (__bf16)dv[e];
-      const float r1 = sub_rn(dv[e], (float)b0);
-      const __bf16 b1 = (__bf16)r1;
-      d0[e] = b0;
-      d1[e] = b1;
-      d2[e] = (__bf16)(sub_rn(r1, (float)b1));
-    }
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const __bf16 b0 = (__bf16)dv[ks][e];
+        const float r1 = sub_rn(dv[ks][e], (float)b0);
+        const __bf16 b1 = (__bf16)r1;
+        d0[ks][e] = b0;
+        d1[ks][e] = b1;
+        d2[ks][e] = (__bf16)(sub_rn(r1, (float)b1));
+      }
     const unsigned m0w = mw0, m1w = mw1;
     load_unit(un + gridDim.x);  // the next unit's loads land under this one's MFMAs and stores
     f32x4 c[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) c[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // the four tiles' six-MFMA chains interleaved (independent accumulators), smallest limb products first
+    // the four tiles' six-MFMA chains interleaved (independent accumulators), smallest limb products first, each
+    // limb product over the k steps in order
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][2], d0, c[t], 0, 0, 0);
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][1], d1, c[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][2], d0[ks], c[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d2, c[t], 0, 0, 0);
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][1], d0, c[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][1], d1[ks], c[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d1, c[t], 0, 0, 0);
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], d0, c[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][0], d2[ks], c[t], 0, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][1], d0[ks], c[t], 0, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][0], d1[ks], c[t], 0, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][t][0], d0[ks], c[t], 0, 0, 0);
     if constexpr (F32O) {
       constexpr int FROW = 272;
 #pragma unroll
@@ -810,6 +835,8 @@ __global__ __launch_bounds__(64 * NG) void smallc_dgrad_k3_mfma_kernel(int npix,
 
 // the limb-engine form applies to the Langevin path's output layer: sign bits in, limbs out, Cin = 128 or 256
 bool smallc_k3_mfma_ok(const damc_layer_t& L) { return L.cin == 128 || L.cin == 256; }
+// ... and to the k4 s2 p1 output layer (round 4), Cin = 64, 128 or 256 (the caller checks the layer's geometry)
+bool smallc_s2_mfma_cin(const damc_layer_t& L) { return L.cin == 64 || L.cin == 128 || L.cin == 256; }
 
 int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta, float mask_slope,
                                 unsigned short* h3, const unsigned char* hbits, hipStream_t s, float* out32 = nullptr) {
@@ -821,17 +848,26 @@ int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta
   }();
   const int grid = std::max(1, std::min(units, gmax));
   const int ng = L.cin / 64;
-#define SDM(NC_, NG_)                                                                                              \
+#define SDM(NC_, NG_, KT_, ST_)                                                                                    \
   if (out32)                                                                                                       \
-    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, true>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin, \
-                       L.win, L.w_fwd, delta, mask_slope, (void*)out32, hbits);                                    \
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, true, KT_, ST_>), dim3(grid), dim3(64 * NG_), 0, s,    \
+                       npix, L.hin, L.win, L.w_fwd, delta, mask_slope, (void*)out32, hbits);                       \
   else                                                                                                             \
-    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_>), dim3(grid), dim3(64 * NG_), 0, s, npix, L.hin,     \
-                       L.win, L.w_fwd, delta, mask_slope, (void*)h3, hbits)
-  if (L.cout == 3 && ng == 4) SDM(3, 4);
-  else if (L.cout == 3) SDM(3, 2);
-  else if (ng == 4) SDM(1, 4);
-  else SDM(1, 2);
+    hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, false, KT_, ST_>), dim3(grid), dim3(64 * NG_), 0, s,   \
+                       npix, L.hin, L.win, L.w_fwd, delta, mask_slope, (void*)h3, hbits)
+  if (L.k == 4) {
+    if (L.cout == 3 && ng == 4) SDM(3, 4, 4, 2);
+    else if (L.cout == 3 && ng == 2) SDM(3, 2, 4, 2);
+    else if (L.cout == 3) SDM(3, 1, 4, 2);
+    else if (ng == 4) SDM(1, 4, 4, 2);
+    else if (ng == 2) SDM(1, 2, 4, 2);
+    else SDM(1, 1, 4, 2);
+  } else {
+    if (L.cout == 3 && ng == 4) SDM(3, 4, 3, 1);
+    else if (L.cout == 3) SDM(3, 2, 3, 1);
+    else if (ng == 4) SDM(1, 4, 3, 1);
+    else SDM(1, 2, 3, 1);
+  }
 #undef SDM
   return (int)hipGetLastError();
 }
@@ -1334,11 +1370,25 @@ bool smallc_k3(const damc_layer_t& L) {
 }
 
 
+// k4 s2 p1 output layer with the limb-engine dgrad (round 4): the layer before it writes sign bits for it
+// (DAMC_SMALLC_S2_MFMA=0, read per call: the register-resident VALU dgrad with the fp32 activation as mask)
+bool smallc_s2_mfma(const damc_layer_t& L) {
+  const char* e = getenv("DAMC_SMALLC_S2_MFMA");
+  return L.kind == DAMC_LAYER_SMALLC && L.k == 4 && L.stride == 2 && L.pad == 1 && L.hout == 2 * L.hin &&
+         L.wout == 2 * L.win && (L.cout == 1 || L.cout == 3) && smallc_s2_mfma_cin(L) && !(e && e[0] == '0');
+}
+
 // f32_out (with sign bits, limb engine): the MFMA kernel writes the fp32 gradient into h instead of limbs into h3
 int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int mask_act, float mask_slope,
                  unsigned short* h3, const unsigned char* hbits_in, hipStream_t s, bool f32_out = false) {
   if (h3 && !smallc_x3_ok(L)) return DAMC_ERR_ARG;
-  if (hbits_in && (!smallc_k3(L) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
+  if (hbits_in && (!(smallc_k3(L) || smallc_s2_mfma(L)) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
+  if (smallc_s2_mfma(L) && hbits_in) {  // sign bits in, limbs or fp32 out, on the limb engine
+    ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / 4, s);
+    if ((double)B * L.hin * L.win * 6 * L.cin >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
+    const bool fp32 = f32_out || !h3;  // the fp32 gradient into h (in place of the activation) when no limbs are asked
+    return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, fp32 ? nullptr : h3, hbits_in, s, fp32 ? h : nullptr);
+  }
   if (smallc_k3(L)) {
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
     // the Langevin path (sign bits in, limbs out) on the limb engine; DAMC_SMALLC_DGRAD_MFMA=0 (read per call)
@@ -1531,7 +1581,7 @@ bool hbits_cap(const damc_generator_t* g, int j) {
   const damc_layer_t& L = g->layers[j];
   const damc_layer_t& N = g->layers[j + 1];
   const bool prod = (j == 0) ? x3_proj_cap(L) : x3_fwd_cap(L);
-  return prod && L.act == DAMC_ACT_LRELU && (x3_bwd_cap(N) || smallc_k3(N));
+  return prod && L.act == DAMC_ACT_LRELU && (x3_bwd_cap(N) || smallc_k3(N) || smallc_s2_mfma(N));
 }
 bool hbits(const damc_generator_t* g, int j) { return limb(g->layers[0]) && hbits_cap(g, j); }
 // the fp32 activation j is stored unless sign bits carry the mask and the next layer's forward gathers
@@ -1818,7 +1868,8 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
     int rc;
     bool x3_out = false;  // the gradient went straight into its x3 copy
     if (L.kind == DAMC_LAYER_SMALLC) {
-      const bool fo = f32a && x3_bwd(P) && hbits(g, i - 1) && smallc_k3(L) && smallc_k3_mfma_ok(L);
+      const bool fo = f32a && x3_bwd(P) && hbits(g, i - 1) &&
+                      ((smallc_k3(L) && smallc_k3_mfma_ok(L)) || smallc_s2_mfma(L));
       x3_out = !fo && x3_bwd(P) && smallc_x3_ok(L);
       rc = smallc_dgrad(L, out, B, d, P.act, P.slope, x3_out ? ws.h3[i - 1] : nullptr,
                         hbits(g, i - 1) ? ws.hb[i - 1] : nullptr, s, fo);
