@@ -2709,9 +2709,60 @@ __global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, 
   }
 }
 
+// the same packing through LDS, one workgroup per (co, chunk of CC input channels): the chunk's CC * k * k floats are
+// one contiguous run of the PyTorch layout (read as f32x4, every lane a different 16 B), transposed in LDS to
+// (tap, channel), and each tap's CC / 8 limb octets are CC * 6 contiguous bytes of the output; every byte is read and
+// written once, in full lines (the tap-group kernel above reads each 64-B line from 4 waves far apart)
+template <int CC>
+__global__ __launch_bounds__(256) void pack_conv_x3_lds_kernel(const float* __restrict__ w, int cin, int taps,
+                                                               unsigned short* __restrict__ y) {
+  extern __shared__ float pk_t[];  // [CC][taps + 1]
+  const int co = blockIdx.y, cc0 = blockIdx.x * CC, tp1 = taps + 1, n4 = CC * taps / 4;
+  const f32x4* src = reinterpret_cast<const f32x4*>(w + ((long)co * cin + cc0) * taps);
+  for (int q = threadIdx.x; q < n4; q += 256) {
+    const f32x4 v = src[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * q + e, ci = f / taps;
+      pk_t[ci * tp1 + (f - ci * taps)] = v[e];
+    }
+  }
+  __syncthreads();
+  const int oc = CC / 8, cin8 = cin / 8;
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3L * ((long)co * taps * cin8 + cc0 / 8);
+  for (int q = threadIdx.x; q < taps * oc; q += 256) {
+    const int tap = q / oc, c8 = q - tap * oc;
+    const float sg = (((tap * cin + cc0 + c8 * 8) / X3_NEGK) & 1) ? -1.f : 1.f;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = sg * pk_t[(c8 * 8 + e) * tp1 + tap];
+    bf16x8 h, m, l;
+    split3_octet(v, h, m, l);
+    bf16x8* d = o + 3L * ((long)tap * cin8 + c8);
+    d[0] = h;
+    d[1] = m;
+    d[2] = l;
+  }
+}
+
 int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s) {
   if ((DAMC_X3_VARIANT & 8) != 0) return DAMC_ERR_UNSUPPORTED;  // the channel-major walk needs the slice-major order
   if (cout <= 0 || cin % 8 != 0 || k <= 0 || (uintptr_t)y % 16 != 0) return DAMC_ERR_ARG;
+  static const bool lds = [] {  // DAMC_PACK_CONV_LDS=0: the tap-group kernel below (A/B)
+    const char* e = getenv("DAMC_PACK_CONV_LDS");
+    return !(e && e[0] == '0');
+  }();
+  const int taps = k * k;
+  if (lds && taps <= 32 && (uintptr_t)w % 16 == 0 && (cin % 128 == 0 || cin == 64)) {
+    if (cin % 128 == 0) {
+      const size_t sm = (size_t)128 * (taps + 1) * sizeof(float);
+      hipLaunchKernelGGL(pack_conv_x3_lds_kernel<128>, dim3(cin / 128, cout), dim3(256), sm, s, w, cin, taps, y);
+    } else {
+      const size_t sm = (size_t)64 * (taps + 1) * sizeof(float);
+      hipLaunchKernelGGL(pack_conv_x3_lds_kernel<64>, dim3(1, cout), dim3(256), sm, s, w, cin, taps, y);
+    }
+    return (int)hipGetLastError();
+  }
   if ((k * k) % 4 == 0 && (uintptr_t)w % 16 == 0) {
     const long nt = (long)cout * (k * k / 4) * (cin / 8);
     hipLaunchKernelGGL(pack_conv_x3_taps_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, cout, cin, k,

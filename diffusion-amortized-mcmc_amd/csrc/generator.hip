@@ -842,9 +842,11 @@ int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta
                                 unsigned short* h3, const unsigned char* hbits, hipStream_t s, float* out32 = nullptr) {
   const int npix = B * L.hin * L.win;
   const int units = (npix + 15) / 16;
-  static const int gmax = [] {  // DAMC_SMALLC_DGRAD_GRID: A/B of the persistent grid size
+  // persistent grid: 1024 workgroups (CelebA-HQ B=64 step 8.03 / 8.06 -> 7.77 / 7.89 ms against 512, CIFAR B=128 within
+  // noise; profiles/r04/smallc_dgrad_grid_ab.txt); DAMC_SMALLC_DGRAD_GRID pins it (A/B)
+  static const int gmax = [] {
     const char* e = getenv("DAMC_SMALLC_DGRAD_GRID");
-    return e ? atoi(e) : 512;
+    return e ? atoi(e) : 1024;
   }();
   const int grid = std::max(1, std::min(units, gmax));
   const int ng = L.cin / 64;
@@ -1240,6 +1242,76 @@ __global__ __launch_bounds__(256) void smallc_gather_lds_kernel(const float* __r
   }
 }
 
+// The k4 s2 p1 gather through LDS (round 4): a workgroup takes an R x CW tile of output pixels (R, CW even) of one
+// sample; the R/2 + 2 x CW/2 + 2 input pixels its taps reach have their 16 NC projection values staged in LDS (the
+// chunk partials already added in order), then smallc_gather_kernel's loops and adds run over LDS: bitwise that kernel.
+template <int NC>
+__global__ __launch_bounds__(256) void smallc_gather_s2_lds_kernel(const float* __restrict__ P,
+                                                                   const float* __restrict__ P1, int ldp, int Hin,
+                                                                   int Win, int R, int CW,
+                                                                   const float* __restrict__ bias, const float* x,
+                                                                   float inv_s2, float* delta, float* xhat,
+                                                                   float* sqerr_sum) {
+  constexpr int T = 16 * NC;
+  extern __shared__ float pr[];  // [R/2 + 2][CW/2 + 2][T]
+  __shared__ float red[4];
+  const int Hout = 2 * Hin, Wout = 2 * Win;
+  const int b = blockIdx.z, oy0 = blockIdx.y * R, ox0 = blockIdx.x * CW;
+  const int IR = R / 2 + 2, IC = CW / 2 + 2, iy0 = oy0 / 2 - 1, ix0 = ox0 / 2 - 1;
+  for (int i = threadIdx.x; i < IR * IC * T; i += 256) {
+    const int rc = i / T, t = i - rc * T, r = rc / IC, c = rc - r * IC;
+    const int iy = iy0 + r, ix = ix0 + c;
+    if (iy < 0 || iy >= Hin || ix < 0 || ix >= Win) continue;
+    const long po = (((long)b * Hin + iy) * Win + ix) * ldp + t;
+    pr[i] = P1 ? P[po] + P1[po] : P[po];
+  }
+  __syncthreads();
+  float sq = 0.f;
+  for (int p = threadIdx.x; p < R * CW; p += 256) {
+    const int oy = oy0 + p / CW, ox = ox0 + p % CW;
+    if (oy >= Hout || ox >= Wout) continue;
+    float acc[NC];
+#pragma unroll
+    for (int o = 0; o < NC; ++o) acc[o] = bias ? bias[o] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky) {
+      const int ty = oy + 1 - ky;
+      if (ty < 0 || (ty & 1)) continue;
+      const int iy = ty / 2;
+      if (iy >= Hin) continue;
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) {
+        const int tx = ox + 1 - kx;
+        if (tx < 0 || (tx & 1)) continue;
+        const int ix = tx / 2;
+        if (ix >= Win) continue;
+        const float* q = pr + ((iy - iy0) * IC + (ix - ix0)) * T + (ky * 4 + kx) * NC;
+#pragma unroll
+        for (int o = 0; o < NC; ++o) acc[o] += q[o];
+      }
+    }
+    const long pix = ((long)b * Hout + oy) * Wout + ox;
+#pragma unroll
+    for (int o = 0; o < NC; ++o) {
+      const float t = tanhf(acc[o]);
+      const long nchw = (((long)b * NC + o) * Hout + oy) * Wout + ox;
+      if (xhat) xhat[nchw] = t;
+      if (delta) {
+        const float rd = t - x[nchw];
+        delta[pix * NC + o] = rd * inv_s2 * (1.f - t * t);
+        sq += rd * rd;
+      }
+    }
+  }
+  if (sqerr_sum) {
+    sq = wave_sum(sq);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+  }
+}
+
 int smallc_ntile(const damc_layer_t& L) { return (L.k * L.k * L.cout + 31) / 32; }
 
 bool smallc_twostage_ok(const damc_layer_t& L) {
@@ -1313,6 +1385,20 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
                          L.bias, x, inv_s2, delta, xhat, sqerr);
     else
       hipLaunchKernelGGL(smallc_gather_lds_kernel<1>, g, dim3(256), sm, s, Pbuf, P1, nt * 32, L.hout, L.wout, gR,
+                         L.bias, x, inv_s2, delta, xhat, sqerr);
+    return (int)hipGetLastError();
+  }
+  // k4 s2 p1: the LDS-staged gather over 16 x 32 output tiles (bitwise), where the tiles fill the chip
+  if (!(gl && gl[0] == '0') && L.k == 4 && L.stride == 2 && L.pad == 1 && L.hout == 2 * L.hin &&
+      L.wout == 2 * L.win && (long)B * ((L.hout + 15) / 16) * ((L.wout + 31) / 32) >= 256) {
+    const int R2 = 16, CW2 = 32;
+    const size_t sm = (size_t)(R2 / 2 + 2) * (CW2 / 2 + 2) * 16 * L.cout * sizeof(float);
+    const dim3 g((L.wout + CW2 - 1) / CW2, (L.hout + R2 - 1) / R2, B);
+    if (L.cout == 3)
+      hipLaunchKernelGGL(smallc_gather_s2_lds_kernel<3>, g, dim3(256), sm, s, Pbuf, P1, nt * 32, L.hin, L.win, R2, CW2,
+                         L.bias, x, inv_s2, delta, xhat, sqerr);
+    else
+      hipLaunchKernelGGL(smallc_gather_s2_lds_kernel<1>, g, dim3(256), sm, s, Pbuf, P1, nt * 32, L.hin, L.win, R2, CW2,
                          L.bias, x, inv_s2, delta, xhat, sqerr);
     return (int)hipGetLastError();
   }

@@ -471,13 +471,20 @@ def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [100, 128])
-def test_lds_staged_gather_is_bitwise_the_direct_gather(lv, gpu_device, monkeypatch, B):
-    """The k3 s1 output layer's gather (delta, x_hat from the per-tap projections and their two 128-channel partials)
-    staged through LDS per strip of rows (generator.hip smallc_gather_lds_kernel): 2 noisy posterior steps bitwise
-    equal to the direct per-pixel gather (DAMC_SMALLC_GATHER_LDS=0), at batches whose strips fill the chip (the
-    LDS form runs from 256 workgroups: B=100 and the full B=128)."""
-    G, E, x, z0 = _cifar_full(gpu_device, B)
+@pytest.mark.parametrize("net,B", [("cifar10", 100), ("cifar10", 128), ("celeba64", 32)])
+def test_lds_staged_gather_is_bitwise_the_direct_gather(lv, gpu_device, monkeypatch, net, B):
+    """The output layer's gather (delta, x_hat from the per-tap projections and their 128-channel partials)
+    staged through LDS (generator.hip smallc_gather_lds_kernel for k3 s1 row strips, smallc_gather_s2_lds_kernel for
+    k4 s2 16 x 32 tiles): 2 noisy posterior steps bitwise equal to the direct per-pixel gather
+    (DAMC_SMALLC_GATHER_LDS=0), at batches whose tiles fill the chip (the LDS forms run from 256 workgroups)."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    nz, hw = (128, 32) if net == "cifar10" else (100, 64)
+    G = synth.load_into(getattr(dn, "_netG_" + net)(nz=nz, ngf=128, nc=3), 0).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=nz), 10).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, hw, hw))).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, nz))).to(gpu_device)
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DAMC_SMALLC_GATHER_LDS", mode)

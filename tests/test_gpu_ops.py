@@ -152,12 +152,14 @@ def test_z_update_hook_vs_oracle(gpu_device):
     assert torch.equal(z.cpu(), (z0 - torch.tensor(c1) * (g + z0)) + torch.tensor(np.float32(s)) * xi_k)
 
 
-@pytest.mark.parametrize("cout,cin,k", [(16, 64, 4), (24, 32, 4), (40, 512, 4), (8, 32, 3), (16, 64, 1), (8, 32, 5)])
+@pytest.mark.parametrize("cout,cin,k", [(16, 64, 4), (24, 32, 4), (40, 512, 4), (8, 32, 3), (16, 64, 1), (8, 32, 5),
+                                         (8, 128, 4), (16, 256, 3), (8, 64, 5), (4, 512, 3), (8, 96, 4)])
 def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     """damc_pack_conv2d_x3 (the encoder's per-call weight operand, Encoder_* convs, diffusion_net.py:227-372):
     PyTorch (cout, cin, k, k) -> K-major [co][(ky, kx, ci)] with the odd sign blocks negated, as three RNE bf16
     limbs h = bf16(v), m = bf16(v - h), l = bf16(v - h - m) per 8-value octet; bit-exact against the same split in
-    torch (k * k % 4 == 0 takes the tap-vectorised kernel, the rest the per-octet one)."""
+    torch (cin % 128 == 0 or cin == 64 takes the LDS-transposing kernel, other k * k % 4 == 0 the tap-vectorised one,
+    the rest the per-octet one)."""
     from damc import _lib
     from damc._lib import ptr
 
