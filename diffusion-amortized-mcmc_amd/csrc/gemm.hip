@@ -2753,7 +2753,7 @@ int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short
     return !(e && e[0] == '0');
   }();
   const int taps = k * k;
-  if (lds && taps <= 32 && (uintptr_t)w % 16 == 0 && (cin % 128 == 0 || cin == 64)) {
+  if (lds && taps <= 32 && cout <= 65535 && (uintptr_t)w % 16 == 0 && (cin % 128 == 0 || cin == 64)) {
     if (cin % 128 == 0) {
       const size_t sm = (size_t)128 * (taps + 1) * sizeof(float);
       hipLaunchKernelGGL(pack_conv_x3_lds_kernel<128>, dim3(cin / 128, cout), dim3(256), sm, s, w, cin, taps, y);
