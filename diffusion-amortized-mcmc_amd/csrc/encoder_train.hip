@@ -291,7 +291,8 @@ int backward_up(const float* x, const float* dy, const float* w, int B, int hin,
     if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
     a.A3 = t.dy3;
     a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
-    a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy
+    a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy (up_view(...)'s forward sign block: generator.hip up2_negk_fwd)
+    a.negk = x3_conv_negk((long)ho * wo, cin, 4 * cout, 4);
   }
   return launch_gemm(a, A_CONV, EPI_BIAS_ACT, O_PHASE, 4, "enc_dgrad", 2.0 * M * cout * cin * 16, s);
 }

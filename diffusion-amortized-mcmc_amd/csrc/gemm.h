@@ -1,5 +1,6 @@
 // gemm.h — host interface of the fp32 MFMA implicit-GEMM engine (gemm.hip).
 #pragma once
+#include <cstdlib>
 #include "common.h"
 
 namespace damc {
@@ -25,6 +26,13 @@ enum OMode { O_DENSE = 0, O_PHASE = 1, O_WGRAD = 2 };
 //                   shift); C advanced by z * c_zstride (EPI_STORE only)
 //   b_kmajor      : B is stored transposed, Bt[n*ldb + k] (k contiguous).  Only the K-major convolution
 //                   engine reads this layout: A_CONV with conv_kmajor_ok(Cg), no split-K.
+// default k per sign block of the limb engine (GemmArgs::negk; the encoder, the weight gradients and every layer
+// whose generator.hip up2_negk rule does not pick 1024)
+#ifndef DAMC_X3_NEGK
+#define DAMC_X3_NEGK 512
+#endif
+constexpr int X3_NEGK = DAMC_X3_NEGK;
+
 struct GemmArgs {
   const float* A = nullptr;
   long lda = 0;
@@ -64,9 +72,15 @@ struct GemmArgs {
   // EPI_GATE: v + bias[n], then sigmoid on the columns n < gate_cols (a ConcatSquash block's hyper gate and
   // hyper bias computed by one GEMM, diffusion_net.py:441-443)
   int gate_cols = 0;
-  // limb engine: B3 holds -B on the odd blocks of X3_NEGK consecutive k of every row (launch_split_x3_negblk),
+  // limb engine: B3 holds -B on the odd blocks of negk consecutive k of every row (launch_split_x3_negblk),
   // and the kernel subtracts those blocks' sums (the MFMA's truncation bias then alternates sign; gemm.hip)
   int b_negblk = 0;
+  // limb engine: k per sign block = per MFMA accumulation block = per split-K slab (a power of two >= 32); the
+  // packer of B3 and every launch reading it use the same value (generator.hip up2_negk: 512 or 1024 per layer)
+  int negk = X3_NEGK;
+  // x3_skinny_kernel: the B operand as fp32 rows [N][K] (k contiguous), split into the B3 limbs in registers (the RNE
+  // split of the packer: bitwise the B3 operand, 2/3 of its bytes); null: B3 is read
+  const float* b32k = nullptr;
   // limb engine: the A operand is the fp32 tensor A (NHWC), staged as fp32 and split into limbs in registers
   // (gemm_x3_kernel variant X3_F32A: 4 B per gathered element instead of 6 B of limbs); A3 unused
   int a_f32 = 0;
@@ -97,6 +111,22 @@ struct GemmArgs {
   // [tile][wave][4 x 4 tiles][64 lanes] f32x4 (16-B stores straight from the accumulators; the reduce maps back)
   int kslab_reg = 0;
 };
+// k per sign block of a limb-engine conv weight (GemmArgs::negk), from the conv's shape alone (never the batch, so a
+// batch split over ranks runs the blocks, slabs and sums of the whole batch): 1024 where, at the headline's 8-way
+// per-rank batch of 16 samples, 512-k blocks would leave >= 512 split-K slices of the 256 x 128 tiles (two blocks per
+// workgroup), so the 1024-k block halves the slabs and still fills the chip (CIFAR-10 ngf=128 B=16 step 0.487 ->
+// 0.452 ms, CelebA-HQ B=8 1.244 -> 1.229 ms); 512 elsewhere, where the finer split is what fills the chip (SVHN B=64
+// 0.279 ms at 512 vs 0.374 at 1024, CelebA-64 B=32 0.421 vs 0.525; profiles/r05/negk_ab.txt).  Both lengths keep
+// the limb engine's error below the fp32-MFMA engine's.  DAMC_X3_NEGK_RULE=512 / 1024 (read per
+// call; the packing and the launches of one call read it alike) pins it for A/B.
+inline int x3_conv_negk(long m_per_sample, int N, int K, int zdim) {
+  const char* e = getenv("DAMC_X3_NEGK_RULE");
+  if (e && e[0] == '5') return 512;
+  if (K % 1024 != 0) return 512;
+  if (e && e[0] == '1') return 1024;
+  const long tiles16 = ((16 * m_per_sample + 255) / 256) * ((N + 127) / 128) * zdim;
+  return tiles16 * K >= (1L << 18) ? 1024 : 512;
+}
 // the fused output-layer projection as a kernel of its own: P[pix][n] = sum_c h[pix][c] w[n][c] (c < C <= 256,
 // C % 16 == 0; n < np, np = 32 or 64; w rows ldw floats), bitwise the fused form (same MFMA sequence per row); for
 // C > 128 the two 128-channel chunks' sums go to P and P + pstride
@@ -104,7 +134,7 @@ constexpr int PROJ_CHUNK = 128;  // channels per output-layer projection chain (
 int launch_proj_rows(const float* h, long npix, int C, const float* w, int ldw, int np, float* P, long pstride,
                      hipStream_t s);
 // slab floats a limb-engine conv of this shape uses when split (0: it runs unsplit); workspace sizing
-long x3_ksplit_floats(int M, int N, int K, int zdim);
+long x3_ksplit_floats(int M, int N, int K, int zdim, int negk = X3_NEGK);
 
 // The K-major convolution engine (a K tile never straddles a filter tap) applies when the gathered
 // channel count is a multiple of its K tile; weight packers pick the B layout with this predicate.
@@ -115,22 +145,19 @@ inline bool conv_kmajor_ok(int Cg) { return Cg > 0 && Cg % KM_BK == 0; }
 int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s);
 // the same for a weight operand whose rows are K long, with the values of the odd X3_NEGK-blocks of each row
 // negated (exact); the GEMM launches that read it set GemmArgs::b_negblk
-#ifndef DAMC_X3_NEGK
-#define DAMC_X3_NEGK 512  // k per sign block = per MFMA accumulation block (gemm.hip X3_FLUSH = X3_NEGK / 32)
-#endif
-constexpr int X3_NEGK = DAMC_X3_NEGK;
-int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s);
+int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s, int negk = X3_NEGK);
 // the same reordered for the channel-major K walk: a row's K = taps * Cg values [tap][c] are stored
 // [c / sw][tap][c % sw] (sw channels per slice), sign blocks counted in that order
-int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s);
+int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s,
+                         int negk = X3_NEGK);
 // the x3 copy of a conv weight (rows of K = taps * Cg) in the order the library's limb-engine kernels walk K:
 // slice-major with sign-alternating blocks when the default variant walks channel-major (DAMC_X3_VARIANT & 8),
 // else tap-major (launch_split_x3_negblk)
-int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s);
+int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk = X3_NEGK);
 // generator-layer packing through LDS tiles (fp32 + x3 in one pass; damc_pack_generator_layer); 1 = layout not
 // covered (the caller falls back to the element-wise packing + launch_split_x3_conv)
 int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned short* wf3, float* wb,
-                          unsigned short* wb3, hipStream_t s);
+                          unsigned short* wb3, hipStream_t s, int negk_f = X3_NEGK, int negk_b = X3_NEGK);
 int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf, float* wb, unsigned short* wb3,
                            hipStream_t s);
 

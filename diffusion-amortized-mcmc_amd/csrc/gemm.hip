@@ -777,10 +777,11 @@ __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
         const bool live = kt + u < nk;
         const int k0 = (kbeg + (kt + u) * KM_BK + 8 * q) * 4;
         fa[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 ra, live ? aoff : OOB, (live && aoff != OOB) ? k0 : 0, 0));
+                                                 ra, live ? aoff : OOB, live ? k0 : 0, 0));
         fb[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 rb, live ? boff : OOB, (live && boff != OOB) ? k0 : 0, 0));
+                                                 rb, live ? boff : OOB, live ? k0 : 0, 0));
       }
+    __builtin_amdgcn_sched_barrier(0);  // every load of the batch issued before the first MFMA waits on one
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (kt + u >= nk) break;
@@ -890,8 +891,7 @@ constexpr int X3_F32A = 2097152, X3A_ROWB = 128;
 // takes the default tile's MFMA sequence, so it is bitwise the default and the split forms)
 constexpr int X3_NARROW = 4194304;
 __device__ __forceinline__ int f32a_swz(int r) { return ((r >> 1) & 7) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
-constexpr int X3_FLUSH = X3_NEGK / 32;  // K tiles per MFMA accumulation block (power of two)
-static_assert(X3_FLUSH * 32 == X3_NEGK, "sign blocks are accumulation blocks");
+static_assert(X3_NEGK % 32 == 0 && (X3_NEGK & (X3_NEGK - 1)) == 0, "sign blocks are whole K tiles, a power of two");
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1013,7 +1013,9 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   constexpr int AROWB = F32A ? X3A_ROWB : X3_ROWB, ESZ = F32A ? 4 : 6;
   constexpr int AJ = (BM * (F32A ? 8 : X3_CHUNKS) + 511) / 512, BJ = BN * X3_CHUNKS / 512;  // NARROW: 1.5 -> 2
   constexpr int BUFB = BM * AROWB + BN * X3_ROWB;  // one LDS buffer (A image, then B image)
-  constexpr int FLUSH = (V & 64) ? 4 * X3_FLUSH : X3_FLUSH;  // 64: A/B of the block length (no b_negblk)
+  // K tiles per MFMA accumulation block = the GEMM's sign block (GemmArgs::negk, a power of two >= 32); 64: A/B of
+  // the block length (no b_negblk)
+  const int FLOG = __builtin_ctz((unsigned)p.negk >> 5) + ((V & 64) ? 2 : 0), FLUSH = 1 << FLOG;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * X3_ROWB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1296,10 +1298,10 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
     }
   };
 
-  // Blocked accumulation: the MFMA chain runs over X3_FLUSH K tiles, then adds into tot (a second fp32 sum
+  // Blocked accumulation: the MFMA chain runs over FLUSH K tiles, then adds into tot (a second fp32 sum
   // over the blocks, round-to-nearest VALU adds) and restarts from zero.  Rounding error of one output then
-  // grows with sqrt(K/32 * X3_FLUSH) + K/32/sqrt(X3_FLUSH) instead of K/32: ~3x less at K = 16384
-  // (tools/diag_hq.py), for 64 VGPRs and 64 v_add_f32 per X3_FLUSH tiles.
+  // grows with sqrt(K/32 * FLUSH) + K/32/sqrt(FLUSH) instead of K/32: ~3x less at K = 16384
+  // (tools/diag_hq.py), for 64 VGPRs and 64 v_add_f32 per FLUSH tiles.
   // Sign alternation (b_negblk): v_mfma_f32_16x16x32_bf16 aligns its 32 products and the accumulator before
   // one rounding and drops the low bits toward -inf, a bias of -0.19 x 2^-24 max|term| per instruction on
   // random operands that flips sign when the operands are negated (tools/mfma_bias.hip).  A bias that keeps
@@ -1334,7 +1336,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
   auto flush16 = [&](int ktd) {  // block flush after the MFMAs of K tile ktd
-    const float sg = (p.b_negblk && (((ktd + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+    const float sg = (p.b_negblk && (((ktd + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1396,7 +1398,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
         }
       __syncthreads();
       if (((kt + 1) & (FLUSH - 1)) == 0) {
-        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        const float sg = (p.b_negblk && (((kt + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1530,12 +1532,12 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       if constexpr (KREG) {
         // the register slab layout of the 4 x 2 wave grid (x3_ksplit_reduce_tile_kernel): A tile a of this wave is
         // row tile (w & 1) * 2 + a of wave row w >> 1, B tile t is column tile t & 3 of wave column t >> 2
-        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        const float sg = (p.b_negblk && (((kt + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
         const int ntile = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
         const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw) * ntile * (BM * BN)), (short)0,
             p.kbpw * ntile * (BM * BN) * 4, 0x00020000);
-        const int soff = ((kt / FLUSH) * ntile + tm * ntn + tn) * (BM * BN * 4);
+        const int soff = ((kt >> FLOG) * ntile + tm * ntn + tn) * (BM * BN * 4);
         const int voff = ((wave >> 1) * 2 * 1024 + ((wave & 1) * 2) * 4 * 64 + lane) * 16;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1548,7 +1550,9 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
                                                      soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, 0);
               // wait states before any VALU may rewrite the store's data VGPRs: the register allocator reuses them
               // for the next tile's scaled copy at once, and without these nops 3 of every 16 slab tiles held the
-              // next tile's values (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt)
+              // next tile's values (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt).  Observed with ROCm 7.2.0's
+              // clang 22 (roc-7.2.0 26014); the cause (a missed VMEM-store-data hazard) is not pinned, so
+              // test_f32a_posterior_is_bitwise (B=16, register slabs) is the required gate for any toolchain change
               __builtin_amdgcn_sched_barrier(0);
               asm volatile("s_nop 4");
               __builtin_amdgcn_sched_barrier(0);
@@ -1947,12 +1951,12 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
         // split-K: every sign block's signed sum straight from the accumulators into its own slab, in the register
         // layout (one 16-B store per lane and tile: 1 KB per wave-instruction); x3_ksplit_reduce_kernel maps back
         // buffer stores: one VGPR of offset (wave, lane), the rest scalar, so the 256 accumulator VGPRs do not spill
-        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        const float sg = (p.b_negblk && (((kt + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
         const int ntile = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
         const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(p.kslab + ((long)zph * p.ksplit + zsl * p.kbpw) * ntile * (BM * BN)), (short)0,
             p.kbpw * ntile * (BM * BN) * 4, 0x00020000);
-        const int soff = ((kt / FLUSH) * ntile + tm * ntn + tn) * (BM * BN * 4);
+        const int soff = ((kt >> FLOG) * ntile + tm * ntn + tn) * (BM * BN * 4);
         const int voff = (wave * 1024 + lane) * 16;
         const bool live = m0 + wm * 64 < p.M;  // a wave whose 64 rows are all past M stores nothing (the reduce skips them)
 #pragma unroll
@@ -1966,7 +1970,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
             acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
       } else if (!(V & 32) && ((kt + 1) & (FLUSH - 1)) == 0) {
-        const float sg = (p.b_negblk && (((kt + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+        const float sg = (p.b_negblk && (((kt + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
         if (M16) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -2014,7 +2018,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   if (KREG) return;  // every block already in its slab
   // the last partial block
   {
-    const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) / FLUSH) & 1)) ? -1.f : 1.f;
+    const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
     if (M16) {
       constexpr int MI = NARROW ? 2 : 4;
 #pragma unroll
@@ -2227,6 +2231,79 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_tile_kernel(GemmArgs p, 
   x3_octet_epilogue<EPI, OM>(p, m, n, py, px, o);
 }
 
+// the split-K reduce of a ConvT forward whose epilogue also runs the output layer's projection (GemmArgs::proj_out,
+// register slab layout): one workgroup per (phase, 256 x 128 tile, 128-row half).  Wave w sums the 8 16x16 tiles of
+// rows 16 w .. + 15 (x3_ksplit_reduce_tile_kernel's per-lane order) into an LDS tile, the octet epilogue writes the
+// sign bits (and C unless proj_nostore) and leaves the activated rows in the tile, and wave w projects its 16 rows
+// with proj16 into the chunk's partial buffer -- the F32A tile's fused epilogue on the same sums, so the result is
+// bitwise the unsplit kernel's, without the fp32 activation's write and re-read by proj_rows_kernel
+template <int NT>
+__global__ __launch_bounds__(512) void x3_ksplit_reduce_proj_kernel(GemmArgs p, int zdim) {
+  constexpr int TS = X3_BN + 4;
+  __shared__ __attribute__((aligned(16))) float tile[128 * TS];
+  __shared__ long rowtab[128];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ntm = (p.M + X3_BM - 1) / X3_BM, ntn = (p.N + X3_BN - 1) / X3_BN;
+  const long ntile = (long)ntm * ntn;
+  const int half = blockIdx.x & 1;
+  const long tl = blockIdx.x >> 1;
+  const int tile_i = (int)(tl % ntile), ph = (int)(tl / ntile);
+  if (ph >= zdim) return;  // workgroup-uniform
+  const int tm = tile_i / ntn, tn = tile_i - tm * ntn;
+  const int py = ph >> 1, px = ph & 1;
+  const int r16 = half * 128 + 16 * w;  // this wave's 16 rows within the 256-row tile
+  const int wm = r16 >> 6, ti = (r16 & 63) >> 4;
+  const long sstride = ntile * (X3_BM * X3_BN / 4);
+  const f32x4* src = reinterpret_cast<const f32x4*>(p.kslab) + (long)ph * p.ksplit * sstride + (long)tile_i * 8 * 16 * 64;
+  f32x4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (tm * X3_BM + r16 < p.M) {  // wave-uniform
+    for (int sl = 0; sl < p.ksplit; ++sl) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // u = (wave_n, j): columns 64 (u >> 2) + 16 (u & 3)
+        const int wv = wm * 2 + (u >> 2), ij = ti * 4 + (u & 3);
+        v[u] += src[(long)sl * sstride + ((long)wv * 16 + ij) * 64 + lane];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[(16 * w + 4 * (lane >> 4) + r) * TS + 16 * u + (lane & 15)] = v[u][r];
+  if (tid < 128) {
+    const int m = tm * X3_BM + half * 128 + tid;
+    rowtab[tid] = m < p.M ? gemm_row_offset<O_PHASE>(p, m, py, px) : -1;
+  }
+  __syncthreads();
+  GemmArgs q = p;
+  if (p.proj_nostore) q.C = nullptr;
+  for (int o = tid; o < 128 * 16; o += 512) {
+    const int row = o >> 4, oc = (o & 15) * 8;
+    const int m = tm * X3_BM + half * 128 + row, n = tn * X3_BN + oc;
+    if (m >= p.M || n >= p.N) continue;
+    float e8[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) e8[c] = tile[row * TS + oc + c];
+    x3_octet_epilogue<EPI_BIAS_ACT, O_PHASE>(q, m, n, py, px, e8);
+    *reinterpret_cast<f32x4*>(tile + row * TS + oc) = f32x4{e8[0], e8[1], e8[2], e8[3]};
+    *reinterpret_cast<f32x4*>(tile + row * TS + oc + 4) = f32x4{e8[4], e8[5], e8[6], e8[7]};
+  }
+  __syncthreads();
+  const int cc = tn * X3_BN;
+  f32x4 acc[NT];
+  proj16<NT>(tile, TS, 16 * w, min(PROJ_CHUNK, p.N - cc), p.proj_w + cc, p.proj_ldw, acc);
+  float* Pc = p.proj_out + (cc / PROJ_CHUNK) * p.proj_pstride;
+  const int mm = lane & 15, qq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long ro = rowtab[16 * w + 4 * qq + r];
+      if (ro >= 0) Pc[(ro / p.ldc) * (16 * NT) + 16 * t + mm] = acc[t][r];
+    }
+}
+
 template <int EPI, int OM>
 __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2290,51 +2367,89 @@ __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int 
   }
 }
 
-// Skinny limb GEMM for the first layer at per-rank batches (z . W, M = B <= 32 rows, K <= X3_NEGK: one sign block,
+// Skinny limb GEMM for the first layer at per-rank batches (z . W, M = B <= 32 rows, K <= negk: one sign block,
 // a 1 x 1 "convolution" of dense rows): 4 waves per workgroup, each 16 rows x 64 columns; the K tiles go from memory
 // straight into registers (two tiles' 30 loads of 16 B per lane in flight, no LDS staging, no barrier) -- the
 // 128 x 256 kernel streams its 50 MB of weight limbs through a two-deep LDS pipeline that left each workgroup
 // latency-bound at 4 K tiles.  Same fragments (octet q of the tile per lane quarter), the same six-product MFMA
 // sequence and the same block fold (fmaf(+1, acc, 0)), then gemm_x3_kernel's octet epilogue (x3_octet_epilogue):
 // every output is bitwise the 128 x 256 kernel's (tests/test_gpu_langevin.py).
+// Round 5: each wave takes 16 rows x 16 NTW columns (NTW = 1: 4x the waves of the 64-column form, so a CU holds 16
+// waves and keeps 4 K tiles' loads in flight per lane -- the 64-column wave serialised its loads at 86 VGPRs), and
+// F32B reads the weights as fp32 rows split in registers with the packer's RNE split (2/3 of the limb bytes).  The
+// MFMA sequence per output is unchanged, so every output is still bitwise the 128 x 256 kernel's.
+template <bool F32B, int NTW>
 __global__ __launch_bounds__(256) void x3_skinny_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) float st[4][16][64 + 4];
+  constexpr int WC = 16 * NTW, KU = 4;  // columns per wave, K tiles per batch of loads
+  __shared__ __attribute__((aligned(16))) float st[4][16][WC + 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, q = lane >> 4;
-  const int n0 = (blockIdx.x * 4 + wave) * 64, r0 = blockIdx.y * 16;
+  const int n0 = (blockIdx.x * 4 + wave) * WC, r0 = blockIdx.y * 16;
   if (n0 >= p.N) return;  // wave-uniform; the waves share no barrier
   const int K8 = p.K >> 3, nk = p.K >> 5;
-  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A3, (short)0, p.M * p.K * 6, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.B3, (short)0, p.N * p.K * 6, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = F32B ? __builtin_amdgcn_make_buffer_rsrc((void*)p.b32k, (short)0, p.N * p.K * 4, 0x00020000)
+                                        : __builtin_amdgcn_make_buffer_rsrc((void*)p.B3, (short)0, p.N * p.K * 6, 0x00020000);
   constexpr int OOB = 0x7FFFFFF0;
   const int aoff = (r0 + m < p.M) ? ((r0 + m) * K8 + q) * 48 : OOB;
-  int boff[4];
+  int boff[NTW];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) boff[t] = (n0 + 16 * t + m < p.N) ? ((n0 + 16 * t + m) * K8 + q) * 48 : OOB;
-  f32x4 acc[4];
+  for (int t = 0; t < NTW; ++t)
+    boff[t] = (n0 + 16 * t + m < p.N) ? (F32B ? ((n0 + 16 * t + m) * p.K + 8 * q) * 4 : ((n0 + 16 * t + m) * K8 + q) * 48)
+                                      : OOB;
+  f32x4 acc[NTW];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int off, int kt, int l) {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, off == OOB ? 0 : kt * 192 + l * 16, 0));
+    // the sgpr offset must be wave-uniform (a per-lane soffset made the compiler wrap every load in a waterfall loop);
+    // an out-of-range lane's voffset (OOB) alone takes the load out of range
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, kt * 192 + l * 16, 0));
   };
-  for (int kt = 0; kt < nk; kt += 2) {
-    bf16x8 fa[2][3], fb[2][4][3];
+  for (int kt = 0; kt < nk; kt += KU) {
+    bf16x8 fa[KU][3], fb[KU][NTW][3];
+    if constexpr (F32B) {
+      // 8 fp32 of row n per lane and K tile (two 16-B loads), split as the packer splits (K <= negk: sign block 0)
+      f32x4 fv[KU][NTW][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < KU; ++u) {
+        const bool live = kt + u < nk;
 #pragma unroll
-      for (int l = 0; l < 3; ++l) {
-        fa[u][l] = ld(ra, aoff, kt + u, l);
+        for (int l = 0; l < 3; ++l) fa[u][l] = ld(ra, live ? aoff : OOB, kt + u, l);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) fb[u][t][l] = ld(rb, boff[t], kt + u, l);
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            fv[u][t][h] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, live ? boff[t] : OOB, (kt + u) * 128 + h * 16, 0));
       }
+      __builtin_amdgcn_sched_barrier(0);  // every load of the batch issued before the split waits on one
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < KU; ++u)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const float v[8] = {fv[u][t][0][0], fv[u][t][0][1], fv[u][t][0][2], fv[u][t][0][3],
+                              fv[u][t][1][0], fv[u][t][1][1], fv[u][t][1][2], fv[u][t][1][3]};
+          split3_octet(v, fb[u][t][0], fb[u][t][1], fb[u][t][2]);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const bool live = kt + u < nk;
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+          fa[u][l] = ld(ra, live ? aoff : OOB, kt + u, l);
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) fb[u][t][l] = ld(rb, live ? boff[t] : OOB, kt + u, l);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load of the batch issued before the first MFMA waits on one
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
       if (kt + u >= nk) break;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < NTW; ++t) {
         f32x4 c = acc[t];
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[u][t][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[u][t][1], c, 0, 0, 0);
@@ -2347,16 +2462,17 @@ __global__ __launch_bounds__(256) void x3_skinny_kernel(GemmArgs p) {
   }
   // the block fold of gemm_x3_kernel's last partial block (tot = 0, sign block 0 positive), then the epilogue
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < NTW; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[wave][4 * q + r][16 * t + m] = __builtin_fmaf(1.f, acc[t][r], 0.f);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  constexpr int NOCT = 16 * WC / 8;  // (row, octet) items of the wave's tile
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int id = lane + 64 * j, row = id >> 3, oct = id & 7;
+  for (int j = 0; j < (NOCT + 63) / 64; ++j) {
+    const int id = lane + 64 * j, row = id / (WC / 8), oct = id % (WC / 8);
     const int mg = r0 + row, n = n0 + 8 * oct;
-    if (mg >= p.M || n >= p.N) continue;
+    if (id >= NOCT || mg >= p.M || n >= p.N) continue;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = st[wave][row][8 * oct + e];
@@ -2365,10 +2481,10 @@ __global__ __launch_bounds__(256) void x3_skinny_kernel(GemmArgs p) {
 }
 
 // split-K plan of a limb-engine conv: an under-filled grid (see below; DAMC_X3_KSPLIT_WGS pins the bound) splits K
-// into its X3_NEGK sign blocks, one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
+// into its negk sign blocks (GemmArgs::negk), one per slice.  A slice's tile is then exactly the unsplit kernel's block sum (sign applied), and the reduce adds
 // the blocks in the kernel's order with the kernel's single rounding per block: the split result is bitwise the
 // unsplit one, so a batch split over ranks (or calls) still reproduces the one-call chains bit for bit
-int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn) {
+int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn, int negk = X3_NEGK) {
   // DAMC_X3_KSPLIT=0 disables; DAMC_X3_KSPLIT_WGS: the grid size below which a conv splits (A/B)
   const char* ev = getenv("DAMC_X3_KSPLIT");  // per call: tests compare both paths in one process
   const bool on = !(ev && ev[0] == '0');
@@ -2377,23 +2493,23 @@ int x3_ksplit(int M, int N, int K, int zdim, int bm, int bn) {
     return e ? atol(e) : -1L;
   }();
   const long wgs = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * zdim;
-  if (!on || K % X3_NEGK != 0 || K / X3_NEGK < 2) return 1;
-  const int ks = K / X3_NEGK;
+  if (!on || K % negk != 0 || K / negk < 2) return 1;
+  const int ks = K / negk;
   // default: below 128 workgroups always; below 256 (half the chip idle) when K has at most 16 sign blocks, since
   // the slab bytes grow with K (CIFAR B=16/32 per-rank steps -2.6 / -1.5 %, B=64's K=8192 dgrad stays unsplit)
   const bool split = below >= 0 ? wgs < below : (wgs < 128 || (wgs < 256 && ks <= 16));
   return split ? ks : 1;
 }
 
-long x3_ksplit_floats(int M, int N, int K, int zdim) {  // either block layout (gemm_x3_kernel, V & 524288)
-  const int ks = std::max(x3_ksplit(M, N, K, zdim, X3_BM, X3_BN), x3_ksplit(M, N, K, zdim, 128, 256));
+long x3_ksplit_floats(int M, int N, int K, int zdim, int negk) {  // either block layout (gemm_x3_kernel, V & 524288)
+  const int ks = std::max(x3_ksplit(M, N, K, zdim, X3_BM, X3_BN, negk), x3_ksplit(M, N, K, zdim, 128, 256, negk));
   // the register slab layout covers whole 256 x 128 tiles
   const long padded = (long)((M + X3_BM - 1) / X3_BM) * X3_BM * ((N + X3_BN - 1) / X3_BN) * X3_BN;
   return ks > 1 ? (long)zdim * ks * std::max((long)M * N, padded) : 0;
 }
 
 template <int EPI, int OM, int V = DAMC_X3_VARIANT>
-static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
+static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   GemmArgs a = a0;
   constexpr int BM = (V & 524288) ? 128 : X3_BM, BN = (V & 524288) ? 256 : X3_BN;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
@@ -2410,18 +2526,20 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       a.kslab_reg = 0;
       hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | X3_NARROW>), dim3((unsigned)(nnm * ntn), 1, zdim), dim3(512), 0, s,
                          a);
-      return;
+      return 0;
     }
   }
   if (OM != O_WGRAD && a.kslab && !(V & 16)) {
-    const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN);
+    const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN, a.negk);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
       a.ksplit = ks;
+      const int nostore0 = a.proj_nostore;  // the caller's: honoured where the reduce runs the projection itself
       a.proj_nostore = 0;  // the reduce writes C; the projection then runs as proj_rows_kernel over it
       auto proj_after = [&]() {
         if (OM == O_PHASE && a.proj_out)
-          (void)launch_proj_rows(a.C, (long)(a.M / (a.Hq * a.Wq)) * a.Hout * a.Wout, a.N, a.proj_w, a.proj_ldw,
-                                 a.proj_np, a.proj_out, a.proj_pstride, s);
+          return launch_proj_rows(a.C, (long)(a.M / (a.Hq * a.Wq)) * a.Hout * a.Wout, a.N, a.proj_w, a.proj_ldw,
+                                  a.proj_np, a.proj_out, a.proj_pstride, s);
+        return 0;
       };
       // sign blocks per workgroup: the most (a power of two dividing ks) that still leaves >= 256 workgroups, so one
       // round covers the chip (the default 16x16-tile path only); DAMC_X3_KSPLIT_BPW (read per call) pins it
@@ -2457,17 +2575,29 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
         hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
       }
       if (a.kslab_reg) {  // one wave per 16x16 tile, four per workgroup
+        // a ConvT forward with the fused output-layer projection: the reduce runs the projection too (bitwise the
+        // reduce + proj_rows_kernel); DAMC_REDUCE_PROJ=0 (read per call) keeps the two kernels
+        const char* erp = getenv("DAMC_REDUCE_PROJ");
+        if (OM == O_PHASE && EPI == EPI_BIAS_ACT && a.proj_out && a.N % 16 == 0 && a.N <= 256 &&
+            (a.N <= PROJ_CHUNK || a.N % PROJ_CHUNK == 0) && (a.proj_np == 32 || a.proj_np == 64) &&
+            !(erp && erp[0] == '0')) {
+          a.proj_nostore = nostore0;
+          const unsigned nwg = (unsigned)(zdim * ntm * ntn * 2);
+          if (a.proj_np == 32)
+            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<2>), dim3(nwg), dim3(512), 0, s, a, zdim);
+          else
+            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<4>), dim3(nwg), dim3(512), 0, s, a, zdim);
+          return (int)hipGetLastError();
+        }
         const long waves = (long)zdim * ntm * ntn * 128;
         hipLaunchKernelGGL((x3_ksplit_reduce_tile_kernel<EPI, OM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
                            a, zdim);
-        proj_after();
-        return;
+        return proj_after();
       }
       const long tot = (long)zdim * a.M * (a.N / 8);
       hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, OM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
                          zdim);
-      proj_after();
-      return;
+      return proj_after();
     }
   }
   a.ksplit = 1;
@@ -2477,6 +2607,7 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim), dim3(512), 0, s, a);
+  return 0;
 }
 
 // fp32 [rows][C] -> x3 [rows][C/8][3][8]; one thread per channel octet
@@ -2494,12 +2625,13 @@ __global__ void split_x3_kernel(const float* __restrict__ x, long n8, unsigned s
   o[2] = l;
 }
 
-// rows of K values; octets in odd X3_NEGK-blocks of a row negated
-__global__ void split_x3_negblk_kernel(const float* __restrict__ x, long n8, int K8, unsigned short* __restrict__ y) {
+// rows of K values; octets in odd negk-blocks of a row negated
+__global__ void split_x3_negblk_kernel(const float* __restrict__ x, long n8, int K8, unsigned short* __restrict__ y,
+                                       int negk) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n8) return;
   const long k8 = i % K8;
-  const float sg = ((k8 * 8 / X3_NEGK) & 1) ? -1.f : 1.f;
+  const float sg = ((k8 * 8 / negk) & 1) ? -1.f : 1.f;
   const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
   const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
   const float v[8] = {sg * v0.x, sg * v0.y, sg * v0.z, sg * v0.w, sg * v1.x, sg * v1.y, sg * v1.z, sg * v1.w};
@@ -2511,25 +2643,25 @@ __global__ void split_x3_negblk_kernel(const float* __restrict__ x, long n8, int
   o[2] = l;
 }
 
-int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s) {
+int launch_split_x3_negblk(const float* x, long n, int K, unsigned short* y, hipStream_t s, int negk) {
   if (K <= 0 || K % 8 != 0 || n % K != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0) return DAMC_ERR_ARG;
   const long n8 = n / 8;
   if (n8 == 0) return 0;
-  hipLaunchKernelGGL(split_x3_negblk_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, y);
+  hipLaunchKernelGGL(split_x3_negblk_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, y, negk);
   return (int)hipGetLastError();
 }
 
 // weight rows of K = taps * Cg values in tap-major order [tap][c] -> x3 in slice-major order
-// [c / 32][tap][c % 32] (the channel-major K walk, V & 8), odd X3_NEGK-blocks of the new order negated
+// [c / 32][tap][c % 32] (the channel-major K walk, V & 8), odd negk-blocks of the new order negated
 __global__ void split_x3_cmaj_kernel(const float* __restrict__ x, long n8, int K8, int Cg8, int taps, int sw8,
-                                     unsigned short* __restrict__ y) {
+                                     unsigned short* __restrict__ y, int negk) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // source octet
   if (i >= n8) return;
   const long row = i / K8;
   const int k8 = (int)(i - row * K8);
   const int tp = k8 / Cg8, c8 = k8 - tp * Cg8;  // octet c8 of tap tp
   const int d8 = (c8 / sw8) * taps * sw8 + tp * sw8 + c8 % sw8;  // destination octet within the row
-  const float sg = ((d8 * 8 / X3_NEGK) & 1) ? -1.f : 1.f;
+  const float sg = ((d8 * 8 / negk) & 1) ? -1.f : 1.f;
   const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
   const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
   const float v[8] = {sg * v0.x, sg * v0.y, sg * v0.z, sg * v0.w, sg * v1.x, sg * v1.y, sg * v1.z, sg * v1.w};
@@ -2541,33 +2673,33 @@ __global__ void split_x3_cmaj_kernel(const float* __restrict__ x, long n8, int K
   o[2] = l;
 }
 
-int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s) {
+int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned short* y, hipStream_t s, int negk) {
   if (K <= 0 || Cg <= 0 || sw <= 0 || sw % 8 != 0 || Cg % sw != 0 || K % Cg != 0 || n % K != 0 ||
       ((uintptr_t)x | (uintptr_t)y) % 16 != 0)
     return DAMC_ERR_ARG;
   const long n8 = n / 8;
   if (n8 == 0) return 0;
   hipLaunchKernelGGL(split_x3_cmaj_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, Cg / 8,
-                     K / Cg, sw / 8, y);
+                     K / Cg, sw / 8, y, negk);
   return (int)hipGetLastError();
 }
 
-int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s) {
-  if ((DAMC_X3_VARIANT & 8) != 0 && Cg % 32 == 0) return launch_split_x3_cmaj(x, n, K, Cg, 32, y, s);
-  return launch_split_x3_negblk(x, n, K, y, s);
+int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk) {
+  if ((DAMC_X3_VARIANT & 8) != 0 && Cg % 32 == 0) return launch_split_x3_cmaj(x, n, K, Cg, 32, y, s, negk);
+  return launch_split_x3_negblk(x, n, K, y, s, negk);
 }
 
 // ---- generator-layer weight packing through LDS tiles (damc_pack_generator_layer's hot layouts): a ConvTranspose2d
 // weight W[ci][co][tap] (kk <= 16 taps) read in contiguous rows, written as whole octets of the packed matrix, with
-// its x3 copy (sign-alternating X3_NEGK blocks, split_x3_negblk_kernel's values) in the same pass -- the per-call
+// its x3 copy (sign-alternating negk blocks, split_x3_negblk_kernel's values) in the same pass -- the per-call
 // packing was scattered 4-byte stores plus a second read for the limb split.
 __device__ __forceinline__ void pack_store_octet(const float (&v)[8], long flat, int k, float* __restrict__ out,
-                                                 unsigned short* __restrict__ x3) {
+                                                 unsigned short* __restrict__ x3, int negk) {
   f32x4* o = reinterpret_cast<f32x4*>(out + flat);
   o[0] = f32x4{v[0], v[1], v[2], v[3]};
   o[1] = f32x4{v[4], v[5], v[6], v[7]};
   if (x3) {
-    const float sg = ((k / X3_NEGK) & 1) ? -1.f : 1.f;
+    const float sg = ((k / negk) & 1) ? -1.f : 1.f;
     const float u[8] = {sg * v[0], sg * v[1], sg * v[2], sg * v[3], sg * v[4], sg * v[5], sg * v[6], sg * v[7]};
     bf16x8 h, m, l;
     split3_octet(u, h, m, l);
@@ -2581,7 +2713,8 @@ __device__ __forceinline__ void pack_store_octet(const float (&v)[8], long flat,
 // out[ci][tap][co] = W[ci][co][tap]; x3 rows ci of K = kk * cout. Block: one ci, 128 output channels (kk <= 64).
 constexpr int PK_ROW_CO = 128;
 __global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict__ w, int cout, int kk,
-                                                        float* __restrict__ out, unsigned short* __restrict__ x3) {
+                                                        float* __restrict__ out, unsigned short* __restrict__ x3,
+                                                        int negk) {
   __shared__ float t[PK_ROW_CO * 65];
   const int ci = blockIdx.y, co0 = blockIdx.x * PK_ROW_CO;
   const int nco = min(PK_ROW_CO, cout - co0), nco8 = nco / 8, ld = kk + 1;
@@ -2594,7 +2727,7 @@ __global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = t[(c8 * 8 + j) * ld + tap];
     const int k = tap * cout + co0 + c8 * 8;
-    pack_store_octet(v, (long)ci * kk * cout + k, k, out, x3);
+    pack_store_octet(v, (long)ci * kk * cout + k, k, out, x3, negk);
   }
 }
 
@@ -2602,7 +2735,8 @@ __global__ void __launch_bounds__(256) pack_rowT_kernel(const float* __restrict_
 // of 4 Cin per (phase, co)), PROJ (tap * cout + co, x3 rows of Cin). Block: 32 input x 128 / kk output channels (each
 // input channel's run of 128 contiguous weights).
 __global__ void __launch_bounds__(256) pack_colT_kernel(const float* __restrict__ w, int cin, int cout, int kk, int up2,
-                                                        float* __restrict__ out, unsigned short* __restrict__ x3) {
+                                                        float* __restrict__ out, unsigned short* __restrict__ x3,
+                                                        int negk) {
   __shared__ float t[32 * 129];
   const int cot = 128 / kk, ci0 = blockIdx.x * 32, co0 = blockIdx.y * cot, rl = 128, ld = rl + 1;
   for (int e = threadIdx.x; e < 32 * rl; e += 256) {
@@ -2625,7 +2759,7 @@ __global__ void __launch_bounds__(256) pack_colT_kernel(const float* __restrict_
     } else {
       seg = (long)tap * cout + co;
     }
-    pack_store_octet(v, seg * cin + ci0 + c8 * 8, k, out, x3);
+    pack_store_octet(v, seg * cin + ci0 + c8 * 8, k, out, x3, negk);
   }
 }
 
@@ -2636,11 +2770,11 @@ static bool pack_tiled_ok(const void* a, const void* b, const void* c, const voi
 
 // 1 = layout not covered (the caller packs element-wise)
 int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned short* wf3, float* wb,
-                          unsigned short* wb3, hipStream_t s) {
+                          unsigned short* wb3, hipStream_t s, int negk_f, int negk_b) {
   if (cin % KM_BK != 0 || cout % KM_BK != 0 || !pack_tiled_ok(wf, wf3, wb, wb3)) return 1;
-  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / 8), dim3(256), 0, s, w, cin, cout, 16, 1, wf, wf3);
+  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / 8), dim3(256), 0, s, w, cin, cout, 16, 1, wf, wf3, negk_f);
   hipLaunchKernelGGL(pack_rowT_kernel, dim3((cout + PK_ROW_CO - 1) / PK_ROW_CO, cin), dim3(256), 0, s, w, cout, 16,
-                     wb, wb3);
+                     wb, wb3, negk_b);
   return (int)hipGetLastError();
 }
 
@@ -2650,8 +2784,9 @@ int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf,
       !pack_tiled_ok(wf, wb, wb3, nullptr))
     return 1;
   hipLaunchKernelGGL(pack_rowT_kernel, dim3((cout + PK_ROW_CO - 1) / PK_ROW_CO, cin), dim3(256), 0, s, w, cout, kk,
-                     wf, (unsigned short*)nullptr);
-  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / (128 / kk)), dim3(256), 0, s, w, cin, cout, kk, 0, wb, wb3);
+                     wf, (unsigned short*)nullptr, X3_NEGK);
+  hipLaunchKernelGGL(pack_colT_kernel, dim3(cin / 32, cout / (128 / kk)), dim3(256), 0, s, w, cin, cout, kk, 0, wb, wb3,
+                     X3_NEGK);
   return (int)hipGetLastError();
 }
 
@@ -2794,11 +2929,11 @@ static int g_clk_n = 0;
 template <int EPI>
 static void launch_x3_narrow_split(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
-  const int ks = a.K / X3_NEGK;
+  const int ks = a.K / a.negk;
   a.ksplit = ks;
   a.kbpw = 1;
   a.kslab_reg = 0;
-  a.k_per_z = X3_NEGK;
+  a.k_per_z = a.negk;
   a.proj_nostore = 0;
   const int ntm = (a.M + 63) / 64, ntn = (a.N + X3_BN - 1) / X3_BN;
   hipLaunchKernelGGL((gemm_x3_kernel<EPI, O_DENSE, DAMC_X3_VARIANT | X3_NARROW>), dim3(ntm * ntn, 1, ks), dim3(512), 0, s,
@@ -2858,9 +2993,9 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       c.proj_out = a.proj_out + b0 * (long)a.Hout * a.Wout * a.proj_np;
       if (c.a_f32) {  // the F32A tile: each 128-channel N tile projects its chunk
         if (a.N > PROJ_CHUNK && a.N % PROJ_CHUNK) return DAMC_ERR_UNSUPPORTED;
-        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s);
+        if (const int rc_ = launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s)) return rc_;
       } else {  // the 128 x 256 layout: one N tile holding every channel
-        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        if (const int rc_ = launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s)) return rc_;
       }
       continue;
     }
@@ -2871,42 +3006,47 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // the first layer at per-rank batches: the skinny kernel (bitwise the 128 x 256 layout); DAMC_X3_SKINNY=0 (read
     // per call) keeps the tiled kernel
     const char* esk = getenv("DAMC_X3_SKINNY");
-    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 32 && c.K <= X3_NEGK && c.Hin == 1 && c.Win == 1 &&
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 32 && c.K <= c.negk && c.Hin == 1 && c.Win == 1 &&
         c.kw == 1 && c.Cg == c.K && c.A3 && !c.a_f32 && !c.proj_out && !(esk && esk[0] == '0')) {
-      hipLaunchKernelGGL(x3_skinny_kernel, dim3((unsigned)((c.N + 255) / 256), (unsigned)((c.M + 15) / 16)), dim3(256),
-                         0, s, c);
+      // fp32 weights split in registers where the caller passes them (2/3 of the limb bytes; bitwise the same
+      // operands); DAMC_X3_SKINNY_F32B=0 (read per call) reads the limbs
+      const char* efb = getenv("DAMC_X3_SKINNY_F32B");
+      const dim3 gsk((unsigned)((c.N + 63) / 64), (unsigned)((c.M + 15) / 16));
+      if (c.b32k && (c.K % 32) == 0 && (uintptr_t)c.b32k % 16 == 0 && !(efb && efb[0] == '0'))
+        hipLaunchKernelGGL((x3_skinny_kernel<true, 1>), gsk, dim3(256), 0, s, c);
+      else
+        hipLaunchKernelGGL((x3_skinny_kernel<false, 1>), gsk, dim3(256), 0, s, c);
       continue;
     }
     const char* ens = getenv("DAMC_X3_NARROW_SPLIT");  // (read per call) 0: the 128 x 256 layout below
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32 && !c.proj_out && c.kslab &&
-        c.K % X3_NEGK == 0 && c.K / X3_NEGK >= 8 && c.N % 8 == 0 && (long)(c.K / X3_NEGK) * c.M * c.N <= c.kslab_floats &&
+        c.K % c.negk == 0 && c.K / c.negk >= 8 && c.N % 8 == 0 && (long)(c.K / c.negk) * c.M * c.N <= c.kslab_floats &&
         !(ens && ens[0] == '0')) {
       launch_x3_narrow_split<EPI_BIAS_ACT>(c, s);
       continue;
     }
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32) {
       if (!(ew && ew[0] == '0')) {
-        launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        if (const int rc_ = launch_x3_t<EPI_BIAS_ACT, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s)) return rc_;
         continue;
       }
     }
     if (ew && ew[0] == '2' && !c.a_f32) {  // A/B only: every limb GEMM on the 128 x 256 layout (bitwise the default)
       if (epi == EPI_BIAS_ACT && om == O_PHASE) {
-        launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        if (const int rc_ = launch_x3_t<EPI_BIAS_ACT, O_PHASE, DAMC_X3_VARIANT | 524288>(c, zdim, s)) return rc_;
         continue;
       }
       if (epi == EPI_MASK && om == O_DENSE) {
-        launch_x3_t<EPI_MASK, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s);
+        if (const int rc_ = launch_x3_t<EPI_MASK, O_DENSE, DAMC_X3_VARIANT | 524288>(c, zdim, s)) return rc_;
         continue;
       }
     }
-#define DAMC_X3(E_, O_)                                                  \
-  if (epi == E_ && om == O_) {                                           \
-    if (c.a_f32)                                                         \
-      launch_x3_t<E_, O_, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s);        \
-    else                                                                 \
-      launch_x3_t<E_, O_>(c, zdim, s);                                   \
-    continue;                                                            \
+#define DAMC_X3(E_, O_)                                                      \
+  if (epi == E_ && om == O_) {                                               \
+    const int rc_ = c.a_f32 ? launch_x3_t<E_, O_, DAMC_X3_VARIANT | X3_F32A>(c, zdim, s) \
+                            : launch_x3_t<E_, O_>(c, zdim, s);               \
+    if (rc_) return rc_;                                                     \
+    continue;                                                                \
   }
     DAMC_X3(EPI_BIAS_ACT, O_PHASE)
     DAMC_X3(EPI_MASK, O_DENSE)

@@ -840,38 +840,53 @@ bool smallc_s2_mfma_cin(const damc_layer_t& L) { return L.cin == 64 || L.cin == 
 
 int launch_smallc_dgrad_k3_mfma(const damc_layer_t& L, int B, const float* delta, float mask_slope,
                                 unsigned short* h3, const unsigned char* hbits, hipStream_t s, float* out32 = nullptr) {
-  const int npix = B * L.hin * L.win;
-  const int units = (npix + 15) / 16;
+  // the kernel addresses its operands through 32-bit buffer offsets: batches whose gradient image would reach 2^31
+  // bytes (CelebA-HQ from B = 342 with limbs out, CIFAR from B = 2731) run in per-sample-aligned chunks (pixels never
+  // interact across samples, so the chunking changes no result)
+  const long hw = (long)L.hin * L.win;
+  const long per_sample = hw * L.cin * (out32 ? 4 : 6);
+  if (per_sample >= 2147483647L - 16) return DAMC_ERR_UNSUPPORTED;
+  const int bc = (int)std::min<long>(B, (2147483647L - 16) / per_sample);
   // persistent grid: 1024 workgroups (CelebA-HQ B=64 step 8.03 / 8.06 -> 7.77 / 7.89 ms against 512, CIFAR B=128 within
   // noise; profiles/r04/smallc_dgrad_grid_ab.txt); DAMC_SMALLC_DGRAD_GRID pins it (A/B)
   static const int gmax = [] {
     const char* e = getenv("DAMC_SMALLC_DGRAD_GRID");
     return e ? atoi(e) : 1024;
   }();
-  const int grid = std::max(1, std::min(units, gmax));
   const int ng = L.cin / 64;
+  for (int b0 = 0; b0 < B; b0 += bc) {
+    const int npix = (int)(std::min(bc, B - b0) * hw);
+    const int units = (npix + 15) / 16;
+    const int grid = std::max(1, std::min(units, gmax));
+    const float* dl = delta + (long)b0 * L.hout * L.wout * L.cout;
+    const unsigned char* hb = hbits + (long)b0 * hw * (L.cin / 8);
+    float* o32 = out32 ? out32 + (long)b0 * hw * L.cin : nullptr;
+    unsigned short* o3 = h3 ? h3 + (long)b0 * hw * L.cin * 3 : nullptr;
 #define SDM(NC_, NG_, KT_, ST_)                                                                                    \
-  if (out32)                                                                                                       \
+  if (o32)                                                                                                         \
     hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, true, KT_, ST_>), dim3(grid), dim3(64 * NG_), 0, s,    \
-                       npix, L.hin, L.win, L.w_fwd, delta, mask_slope, (void*)out32, hbits);                       \
+                       npix, L.hin, L.win, L.w_fwd, dl, mask_slope, (void*)o32, hb);                                \
   else                                                                                                             \
     hipLaunchKernelGGL((smallc_dgrad_k3_mfma_kernel<NC_, NG_, false, KT_, ST_>), dim3(grid), dim3(64 * NG_), 0, s,   \
-                       npix, L.hin, L.win, L.w_fwd, delta, mask_slope, (void*)h3, hbits)
-  if (L.k == 4) {
-    if (L.cout == 3 && ng == 4) SDM(3, 4, 4, 2);
-    else if (L.cout == 3 && ng == 2) SDM(3, 2, 4, 2);
-    else if (L.cout == 3) SDM(3, 1, 4, 2);
-    else if (ng == 4) SDM(1, 4, 4, 2);
-    else if (ng == 2) SDM(1, 2, 4, 2);
-    else SDM(1, 1, 4, 2);
-  } else {
-    if (L.cout == 3 && ng == 4) SDM(3, 4, 3, 1);
-    else if (L.cout == 3) SDM(3, 2, 3, 1);
-    else if (ng == 4) SDM(1, 4, 3, 1);
-    else SDM(1, 2, 3, 1);
-  }
+                       npix, L.hin, L.win, L.w_fwd, dl, mask_slope, (void*)o3, hb)
+    if (L.k == 4) {
+      if (L.cout == 3 && ng == 4) SDM(3, 4, 4, 2);
+      else if (L.cout == 3 && ng == 2) SDM(3, 2, 4, 2);
+      else if (L.cout == 3) SDM(3, 1, 4, 2);
+      else if (ng == 4) SDM(1, 4, 4, 2);
+      else if (ng == 2) SDM(1, 2, 4, 2);
+      else SDM(1, 1, 4, 2);
+    } else {
+      if (L.cout == 3 && ng == 4) SDM(3, 4, 3, 1);
+      else if (L.cout == 3) SDM(3, 2, 3, 1);
+      else if (ng == 4) SDM(1, 4, 3, 1);
+      else SDM(1, 2, 3, 1);
+    }
 #undef SDM
-  return (int)hipGetLastError();
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 bool smallc_reg_ok(const damc_layer_t& L) {
@@ -1471,7 +1486,6 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
   if (hbits_in && (!(smallc_k3(L) || smallc_s2_mfma(L)) || mask_act != DAMC_ACT_LRELU)) return DAMC_ERR_ARG;
   if (smallc_s2_mfma(L) && hbits_in) {  // sign bits in, limbs or fp32 out, on the limb engine
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k / 4, s);
-    if ((double)B * L.hin * L.win * 6 * L.cin >= 2147483647.0) return DAMC_ERR_UNSUPPORTED;
     const bool fp32 = f32_out || !h3;  // the fp32 gradient into h (in place of the activation) when no limbs are asked
     return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, fp32 ? nullptr : h3, hbits_in, s, fp32 ? h : nullptr);
   }
@@ -1479,13 +1493,12 @@ int smallc_dgrad(const damc_layer_t& L, float* h, int B, const float* delta, int
     ProfScope ps("smallc_dgrad", 2.0 * B * L.hout * L.wout * L.cout * L.cin * L.k * L.k, s);
     // the Langevin path (sign bits in, limbs out) on the limb engine; DAMC_SMALLC_DGRAD_MFMA=0 (read per call)
     // selects the VALU kernel below
+    // (any batch: the MFMA kernel runs in batch chunks below 2^31 bytes)
     const char* mf = getenv("DAMC_SMALLC_DGRAD_MFMA");
-    if (f32_out && hbits_in && smallc_k3_mfma_ok(L) && (double)B * L.hin * L.win * 6 * L.cin < 2147483647.0)
-      return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, nullptr, hbits_in, s, h);
-    if (f32_out) return DAMC_ERR_ARG;
-    if (h3 && hbits_in && smallc_k3_mfma_ok(L) && (double)B * L.hin * L.win * 6 * L.cin < 2147483647.0 &&
-        !(mf && mf[0] == '0'))
-      return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, h3, hbits_in, s);
+    const bool use_mf = hbits_in && smallc_k3_mfma_ok(L) && !(mf && mf[0] == '0');
+    if (f32_out && use_mf) return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, nullptr, hbits_in, s, h);
+    if (f32_out) h3 = nullptr;  // the VALU kernel below writes the fp32 gradient into h when no limbs are asked
+    if (h3 && use_mf) return launch_smallc_dgrad_k3_mfma(L, B, delta, mask_slope, h3, hbits_in, s);
     // 8 rows per block with the next mask nibbles prefetched: 66.4 us vs 69.9 (4 rows, no prefetch) at the
     // CIFAR B=128 shape (tools/smallc_bench.hip; 16 rows leave CUs idle: 115 us); fewer rows per block when the
     // batch would leave fewer than 256 blocks (B=16: 60 us at 8 rows, 64 blocks).  Pixels are independent, so
@@ -1652,6 +1665,10 @@ bool x3_proj_cap(const damc_layer_t& L) {
 bool x3_proj(const damc_layer_t& L) { return limb(L) && x3_proj_cap(L); }
 bool x3_bwd(const damc_layer_t& L) { return limb(L) && x3_bwd_cap(L); }
 size_t up2_floats(const damc_layer_t& L) { return (size_t)L.cin * L.cout * 16; }
+// the sign block of a UP2 layer's forward (K = 4 Cin per phase) and input-gradient (K = 16 Cout) limb weights
+// (damc::x3_conv_negk: by shape, the same for the packing and every launch that reads it)
+int up2_negk_fwd(const damc_layer_t& L) { return damc::x3_conv_negk((long)L.hin * L.win, L.cout, 4 * L.cin, 4); }
+int up2_negk_bwd(const damc_layer_t& L) { return damc::x3_conv_negk((long)L.hin * L.win, L.cin, 16 * L.cout, 1); }
 // x3 copy of a packed weight matrix, stored behind its fp32 packing (n floats, 16-B aligned)
 const unsigned short* x3_of(const float* w, size_t n) { return reinterpret_cast<const unsigned short*>(w + n); }
 // activation j needs an x3 copy when layer j+1 consumes it in the forward pass, or layer j consumes its
@@ -1735,8 +1752,10 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   for (int i = 0; i < g->n_layers; ++i) {
     const damc_layer_t& L = g->layers[i];
     if (L.kind != DAMC_LAYER_UP2) continue;
-    if (x3_fwd_cap(L)) ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cout, 4 * L.cin, 4));
-    if (x3_bwd_cap(L)) ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cin, 16 * L.cout, 1));
+    if (x3_fwd_cap(L))
+      ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cout, 4 * L.cin, 4, up2_negk_fwd(L)));
+    if (x3_bwd_cap(L))
+      ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cin, 16 * L.cout, 1, up2_negk_bwd(L)));
   }
   float* ks = ksf ? take(ksf) : nullptr;
   if (w) {
@@ -1787,6 +1806,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.A = z;
       a.A3 = ws.z3;
       a.B3 = x3_of(L.w_bwd, (size_t)L.cin * N);
+      a.b32k = L.w_bwd;  // the same weights as fp32 rows (the skinny kernel splits them in registers)
       a.b_negblk = 1;
       a.Cg = L.cin;
       a.ldc = N;
@@ -1857,6 +1877,7 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
           a.A3 = ws.h3[i - 1];
         a.B3 = x3_of(L.w_fwd, up2_floats(L));
         a.b_negblk = 1;
+        a.negk = up2_negk_fwd(L);
         if (i + 1 < g->n_layers && x3_fwd(g->layers[i + 1])) {  // the next layer's operand
           if (!f32a) a.C3 = ws.h3[i];
           wrote_x3 = true;
@@ -1992,6 +2013,7 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
           a.A3 = ws.h3[i];
         a.B3 = x3_of(L.w_bwd, up2_floats(L));
         a.b_negblk = 1;
+        a.negk = up2_negk_bwd(L);
         a.kslab = ws.kslab;
         a.kslab_floats = ws.kslab_floats;
         if (hbits(g, i - 1)) {
@@ -2290,6 +2312,12 @@ extern "C" int damc_generator_layer_packed_sizes(const damc_layer_t* L, size_t* 
   return DAMC_ERR_ARG;
 }
 
+extern "C" int damc_x3_layer_sign_block(const damc_layer_t* L, int input_grad) {
+  if (!L) return 0;
+  if (input_grad) return x3_bwd_cap(*L) ? up2_negk_bwd(*L) : 0;
+  return x3_fwd_cap(*L) ? up2_negk_fwd(*L) : 0;
+}
+
 extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, float* wf, float* wb, void* stream) {
   if (!L || !w || !wf) return DAMC_ERR_ARG;
   hipStream_t s = as_stream(stream);
@@ -2316,7 +2344,8 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       if (tiled) {
         const int rc = damc::launch_pack_up2_tiled(
             w, L->cin, L->cout, wf, x3_fwd_cap(*L) ? reinterpret_cast<unsigned short*>(wf + n) : nullptr, wb,
-            x3_bwd_cap(*L) ? reinterpret_cast<unsigned short*>(wb + n) : nullptr, s);
+            x3_bwd_cap(*L) ? reinterpret_cast<unsigned short*>(wb + n) : nullptr, s, up2_negk_fwd(*L),
+            up2_negk_bwd(*L));
         if (rc != 1) return rc;
       }
       hipLaunchKernelGGL(pack_up2_kernel, grid, blk, 0, s, w, L->cin, L->cout, (int)damc::conv_kmajor_ok(L->cin),
@@ -2325,9 +2354,11 @@ extern "C" int damc_pack_generator_layer(const damc_layer_t* L, const float* w, 
       // and output channel) and 16 Cout (input gradient, per input channel)
       // (in the K order the limb-engine kernels walk: damc::launch_split_x3_conv)
       if (x3_fwd_cap(*L))
-        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wf, n, 4 * L->cin, L->cin, reinterpret_cast<unsigned short*>(wf + n), s));
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wf, n, 4 * L->cin, L->cin, reinterpret_cast<unsigned short*>(wf + n), s,
+                                                          up2_negk_fwd(*L)));
       if (x3_bwd_cap(*L))
-        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wb, n, 16 * L->cout, L->cout, reinterpret_cast<unsigned short*>(wb + n), s));
+        DAMC_CHECK((hipError_t)damc::launch_split_x3_conv(wb, n, 16 * L->cout, L->cout, reinterpret_cast<unsigned short*>(wb + n), s,
+                                                          up2_negk_bwd(*L)));
       break;
     case DAMC_LAYER_SMALLC:
       if (wb) DAMC_CHECK(hipMemsetAsync(wb, 0, sizeof(float) * smallc_ntile(*L) * 32 * (size_t)L->cin, s));
@@ -2438,6 +2469,7 @@ extern "C" int damc_convT_fwd(const damc_layer_t* L, const float* in, int B, flo
     a.A3 = a3;
     a.B3 = x3_of(L->w_fwd, up2_floats(*L));
     a.b_negblk = 1;
+    a.negk = up2_negk_fwd(*L);
   }
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_PHASE, 4, "upconv_fwd", conv_flops(*L, B), s);
 }
@@ -2477,6 +2509,7 @@ extern "C" int damc_convT_dgrad(const damc_layer_t* L, const float* gout, int B,
     a.A3 = a3;
     a.B3 = x3_of(L->w_bwd, up2_floats(*L));
     a.b_negblk = 1;
+    a.negk = up2_negk_bwd(*L);
   }
   return damc::launch_gemm(a, damc::A_CONV, mask_pre ? damc::EPI_MASK : damc::EPI_STORE, damc::O_DENSE, 1,
                            "upconv_dgrad", conv_flops(*L, B), s);
@@ -2504,8 +2537,9 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   // step 0.625 -> 0.478 ms; profiles/r04/bench_f32a_ab.txt, step_f32a_ab.txt)
   const char* fa = getenv("DAMC_X3_F32A");
   const bool f32a = !(fa && fa[0] == '0');
-  // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection (on the
-  // limb-gathering path only, DAMC_X3_F32A=0: the F32A tile has no 128 x 256 form)
+  // DAMC_SMALLC_FUSE (read per call, default on): the last ConvT's epilogue runs the output layer's projection on both
+  // paths: the F32A tile projects its own 128-channel chunk per N tile (the gather adds the chunks' partials), the
+  // limb-gathering path (DAMC_X3_F32A=0) projects every channel in the 128 x 256 tile
   const char* sf = getenv("DAMC_SMALLC_FUSE");
   const bool proj = !(sf && sf[0] == '0') && proj_fusable(g, ws);
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;

@@ -159,6 +159,7 @@ _SIGS = {
     "damc_gemm": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
     "damc_conv2d_x3_bytes": (_SZ, [_I, _I, _I]),
     "damc_x3_sign_block": (_I, []),
+    "damc_x3_layer_sign_block": (_I, [ctypes.POINTER(Layer), _I]),
     "damc_clock_probe": (_I, [_P, _I]),
     "damc_pack_conv2d_x3": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),

@@ -247,8 +247,12 @@ typedef struct {
 /* bytes of the limb copy of a packed conv weight (0: the layer does not run on the limb engine) */
 size_t damc_conv2d_x3_bytes(int cout, int cin, int k);
 /* k per sign block of the limb engine's weight operands (odd blocks stored negated; = its MFMA accumulation block
- * and its split-K granule): the build's DAMC_X3_NEGK, 512 by default */
+ * and its split-K granule) for the encoder's convs (damc_pack_conv2d_x3): the build's DAMC_X3_NEGK, 512 by default */
 int damc_x3_sign_block(void);
+/* the sign block of a generator UP2 layer's limb weights (damc_pack_generator_layer), forward (input_grad = 0,
+ * K = 4 Cin) or input gradient (1, K = 16 Cout): 512 or 1024 by the layer's shape alone (gemm.h x3_conv_negk);
+ * 0 for a layer without limb weights */
+int damc_x3_layer_sign_block(const damc_layer_t* L, int input_grad);
 /* diagnostics: while buf (n_slots * 4 uint64, device memory) is set, every k4 s2 ConvT forward on the limb engine
  * stores, per workgroup w at buf[4 (w % n_slots)], {s_memtime, s_memrealtime} before and after its K loop: the
  * clock the chip holds in that loop is d(memtime) / d(realtime) x 100 MHz.  buf = NULL switches it off.  Not

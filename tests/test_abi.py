@@ -147,3 +147,40 @@ def test_adam_chunk_table_host_only():
     with pytest.raises(NotImplementedError):
         optim.Adam([p], amsgrad=True)
     assert sorted(optim.AdamW([p]).defaults) == sorted(torch.optim.AdamW([p]).defaults)
+
+
+def test_layer_sign_block_rule(monkeypatch):
+    """gemm.h x3_conv_negk, through damc_x3_layer_sign_block (host only): the generator's UP2 limb weights take 1024-k
+    sign blocks where 16 samples would already split 512-k blocks two per workgroup (every UP2 GEMM of the headline
+    _netG_cifar10 ngf=128), 512-k blocks where the finer split is what fills the chip (_netG_svhn ngf=64,
+    _netG_celeba64 ngf=128), by shape only; DAMC_X3_NEGK_RULE pins it."""
+    from damc import _lib
+
+    L = _lib.lib()
+
+    def up2(cin, cout, hin):
+        d = _lib.Layer()
+        d.kind, d.cin, d.cout, d.k, d.stride, d.pad = _lib.LAYER_UP2, cin, cout, 4, 2, 1
+        d.hin = d.win = hin
+        d.hout = d.wout = 2 * hin
+        return d
+
+    def blocks(layers):
+        return [(L.damc_x3_layer_sign_block(ctypes.byref(d), 0), L.damc_x3_layer_sign_block(ctypes.byref(d), 1))
+                for d in layers]
+
+    cifar = [up2(1024, 512, 8), up2(512, 256, 16)]
+    svhn = [up2(512, 256, 4), up2(256, 128, 8)]
+    celeba64 = [up2(1024, 512, 4), up2(512, 256, 8), up2(256, 128, 16)]
+    hq = [up2(2048, 1024, 4), up2(1024, 512, 8), up2(512, 512, 16), up2(512, 256, 32), up2(256, 128, 64)]
+    assert blocks(cifar) == [(1024, 1024)] * 2
+    assert blocks(svhn) == [(512, 512)] * 2
+    assert blocks(celeba64) == [(512, 512)] * 3
+    assert blocks(hq) == [(1024, 1024)] * 5
+    monkeypatch.setenv("DAMC_X3_NEGK_RULE", "512")
+    assert blocks(cifar) == [(512, 512)] * 2
+    monkeypatch.setenv("DAMC_X3_NEGK_RULE", "1024")
+    assert blocks(svhn) == [(1024, 1024)] * 2
+    d = _lib.Layer()
+    d.kind = _lib.LAYER_SMALLC
+    assert L.damc_x3_layer_sign_block(ctypes.byref(d), 0) == 0

@@ -163,6 +163,71 @@ def test_full_width_posterior_vs_fp64(gpu_device, name, B, steps, noise, sigma):
         _check("%s B=%d recon MSE" % (name, B), mse, m32, m64, 1e-7)
 
 
+@pytest.mark.timeout(900)
+def test_headline_posterior_30_noisy_steps_vs_fp64(gpu_device):
+    """The bench's own posterior leg (BASELINE config 3: CIFAR-10 _netG_cifar10 ngf=128, nz=128, B=128, 30 steps,
+    sigma 0.1, step 0.1; MCMC.py:48-74, train_gen_recon.py:203-205) with injected noise, the whole batch against
+    fp64, accuracy-relative like the 10-step case (both fp32 implementations drift chaotically from fp64 over 30
+    steps: the criterion is that the HIP arithmetic drifts no more than 3x the reference's own)."""
+    from damc import langevin as lv
+    from oracle import damc_oracle as orc
+
+    B, steps = 128, 30
+    G, E, x, z0 = _case("cifar10", B, gpu_device)
+    (L32, P32), (L64, P64) = _oracles(G, E)
+    xi = torch.from_numpy(np.random.default_rng(B + steps).standard_normal((steps, B, 128)).astype(np.float32))
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, E, steps, 0.1, 0.1, True, noise=xi.to(gpu_device))
+    zc, xc = z0.cpu(), x.cpu()
+    r32 = orc.posterior_langevin(L32, P32, zc, xc, steps, 0.1, 0.1, noise=xi).numpy()
+    r64 = orc.posterior_langevin(L64, P64, zc.double(), xc.double(), steps, 0.1, 0.1, noise=xi.double()).numpy()
+    _check("cifar10 B=128 30 noisy steps z", z.cpu().numpy(), r32, r64, 1e-6)
+    # per sample: the median and 90th percentile rows against the fp32 reference's (no per-row max: a sample whose
+    # trajectory crossed a LeakyReLU kink in either fp32 evaluation diverges chaotically in both)
+    _check("cifar10 B=128 30 noisy steps z (per chain)", z.cpu().numpy(), r32, r64, 1e-6, per_row=True)
+
+
+def test_headline_in_kernel_philox_equals_materialised_stream(gpu_device):
+    """The bench's posterior leg with the in-kernel Philox4x32-10 draw (CIFAR-10 ngf=128, B=128, 30 steps, with_noise)
+    is bitwise the same call fed damc_philox_normal's materialised posterior stream (same seed, steps 0..29, chains
+    0..127) as injected noise: the in-kernel noise the bench times is exactly the stream the statistical tests check
+    (test_philox_noise_statistics) and that the injected-noise parity tests stand in for."""
+    from damc import langevin as lv
+
+    B, steps, seed = 128, 30, 0x5EED1234
+    G, E, x, z0 = _case("cifar10", B, gpu_device)
+    za, zb = z0.clone(), z0.clone()
+    lv.posterior_langevin(za, x, G, E, steps, 0.1, 0.1, True, seed=seed)
+    xi = lv.philox_normal(steps, B, 128, seed, gpu_device)
+    lv.posterior_langevin(zb, x, G, E, steps, 0.1, 0.1, True, noise=xi)
+    torch.cuda.synchronize()
+    assert torch.isfinite(za).all() and not torch.equal(za, z0)
+    assert torch.equal(za, zb), float((za - zb).abs().max())
+    # and the sharded form (chain_base) draws the same stream: the upper half alone, keyed by its global index
+    zc = z0[64:].clone()
+    lv.posterior_langevin(zc, x[64:].contiguous(), G, E, steps, 0.1, 0.1, True, seed=seed, chain_base=64)
+    assert torch.equal(zc, za[64:])
+
+
+@pytest.mark.parametrize("name,B,part", [("cifar10", 2752, 128), ("celebaHQ", 344, 8)])
+def test_output_layer_dgrad_beyond_2gb_is_chunked(gpu_device, name, B, part):
+    """Batches whose output-layer input gradient reaches 2^31 bytes (CIFAR's k3 layer from B = 2731 with fp32 out,
+    CelebA-HQ's k4 s2 layer from B = 342 with limbs out) take a full posterior step: the limb-engine dgrad runs in
+    per-sample chunks, and the first and last chains are bitwise the same chains run as a small batch
+    (chain_base keys the noise by global index)."""
+    from damc import langevin as lv
+
+    G, E, x, z0 = _case(name, B, gpu_device)
+    sigma = 1.0 if name == "celebaHQ" else 0.1
+    za = z0.clone()
+    lv.posterior_langevin(za, x, G, E, 1, sigma, 0.1, True, seed=77)
+    assert torch.isfinite(za).all()
+    for s in (0, B - part):
+        zb = z0[s:s + part].clone()
+        lv.posterior_langevin(zb, x[s:s + part].contiguous(), G, E, 1, sigma, 0.1, True, seed=77, chain_base=s)
+        assert torch.equal(za[s:s + part], zb), (s, float((za[s:s + part] - zb).abs().max()))
+
+
 def test_cifar_prior_60_steps_vs_fp64(gpu_device):
     """BASELINE headline's prior chain: 60 noisy steps (step 0.4, injected noise) on 2B = 256 chains of _netE(nz=128)
     (MCMC.py:27-46, train_gen_recon.py:207-209), whole batch against fp64, accuracy-relative."""

@@ -350,7 +350,10 @@ def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
     x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(gpu_device)
     z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, 128))).to(gpu_device)
     out = {}
-    for mode, split, narrow in (("unsplit", "0", "0"), ("split", "1", "0"), ("narrow", "1", "1")):
+    for mode, split, narrow in (("unsplit", "0", "0"), ("split", "1", "0"), ("split2", "1", "0"), ("narrow", "1", "1")):
+        # split2: the reduce and the output-layer projection as two kernels (DAMC_REDUCE_PROJ=0) instead of the fused
+        # x3_ksplit_reduce_proj_kernel
+        monkeypatch.setenv("DAMC_REDUCE_PROJ", "0" if mode == "split2" else "1")
         monkeypatch.setenv("DAMC_X3_KSPLIT", split)
         monkeypatch.setenv("DAMC_X3_NARROW", narrow)
         monkeypatch.setenv("DAMC_X3_F32A", "0" if narrow == "1" else "1")  # the 64 x 128 tile gathers limbs
@@ -360,6 +363,7 @@ def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
         out[mode] = z.cpu()
     assert torch.isfinite(out["split"]).all()
     assert torch.equal(out["unsplit"], out["split"])
+    assert torch.equal(out["unsplit"], out["split2"])
     assert torch.equal(out["unsplit"], out["narrow"])
 
 
@@ -457,18 +461,21 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B, f32a
 def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     """The first layer at per-rank batches (B <= 32): z . W on gemm.hip's x3_skinny_kernel and its input gradient's
     split-K slabs on km_skinny_kernel (fragments straight into registers): 2 noisy posterior steps bitwise equal to
-    the tiled kernels (DAMC_X3_SKINNY=0, DAMC_KM_SKINNY=0)."""
+    the tiled kernels (DAMC_X3_SKINNY=0, DAMC_KM_SKINNY=0), with the skinny kernel reading the weights as fp32 rows
+    split in registers (round 5, default) and as the packed limbs (DAMC_X3_SKINNY_F32B=0)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
     out = {}
-    for mode in ("0", "1"):
+    for mode, f32b in (("0", "1"), ("1", "1"), ("1", "0")):
         monkeypatch.setenv("DAMC_X3_SKINNY", mode)
         monkeypatch.setenv("DAMC_KM_SKINNY", mode)
+        monkeypatch.setenv("DAMC_X3_SKINNY_F32B", f32b)
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=13)
         torch.cuda.synchronize()
-        out[mode] = z.cpu()
-    assert torch.isfinite(out["1"]).all()
-    assert torch.equal(out["0"], out["1"])
+        out[mode + f32b] = z.cpu()
+    assert torch.isfinite(out["11"]).all()
+    assert torch.equal(out["01"], out["11"])
+    assert torch.equal(out["01"], out["10"])
 
 
 @pytest.mark.parametrize("net,B", [("cifar10", 100), ("cifar10", 128), ("celeba64", 32)])

@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""One Q update on the HIP path (bench.py q_update_bench's step_hip: Q.calculate_loss(x, z, mask).mean().backward()
++ damc.optim's fused clip + AdamW; train_gen_recon.py:211-220) at the bench config (CIFAR-10 B=128, nif 64, nxemb 1024,
+ntemb 128), for rocprofv3 --kernel-trace --stats: 3 warm-up updates, then `calls` updates between two
+synchronisations (their kernels are the ones a trace window should take).  usage: python tools/q_update_trace.py
+[calls]"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(HERE, "diffusion-amortized-mcmc_amd"), HERE]
+import torch  # noqa: E402
+
+from damc import optim as dopt  # noqa: E402
+from damc import synth  # noqa: E402
+from src import diffusion_net as dn  # noqa: E402
+
+calls = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+B, NZ = 128, 128
+dev = torch.device("cuda:0")
+Q = dn._netQ_U(nc=3, nz=NZ, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=100, logsnr_min=-5.1,
+               logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A", dataset="cifar10")
+synth.load_into(Q, 20)
+Q.to(dev).train()
+opt = dopt.AdamW(Q.parameters(), weight_decay=1e-4, lr=2e-4, betas=(0.5, 0.999))
+x = torch.from_numpy(synth.uniform_f32(51, 0, (B, 3, 32, 32))).to(dev)
+z = torch.from_numpy(synth.normal_f32(52, 0, (B, NZ))).to(dev)
+mask = (torch.from_numpy(synth.uniform_f32(53, 0, (B, 1), 0.0, 1.0)) >= 0.2).float().to(dev)
+
+
+def step():
+    opt.zero_grad(set_to_none=True)
+    Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
+    opt.clip_and_step(100)
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+for _ in range(calls):
+    step()
+b.record()
+b.synchronize()
+print("Q update B=%d: %.3f ms per update" % (B, a.elapsed_time(b) / calls))
