@@ -345,18 +345,27 @@ __device__ __forceinline__ float wave_rsum(const float (&v)[N], int lane, int of
 // channel (wave reduce-scatter, then the channel's 4 wave sums in a fixed order) for the mean, then sums
 // (y - mean)^2 for the variance (two passes over registers), and writes lrelu(IN(y)) as the next convolution's limbs.
 // The statistics pass, the Welford partials, the merge kernel and the recomputing second pass all drop out.
+// 1-D grid: workgroup (b, C / 16 chunk) for the first nconv = B * C / 16, then the per-call limb packing of the
+// limb layers' weights (pk, pack_conv_x3_block) as extra workgroups of the same launch, so the two fill the chip
+// together (a separate packing launch, or one on a forked stream, costs its own ramp / the event hand-offs)
 template <int CIN>
 __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __restrict__ x, int H, int W, int C,
                                                               const float* __restrict__ w, const float* __restrict__ bias,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps, float slope,
-                                                              unsigned short* __restrict__ y3) {
+                                                              unsigned short* __restrict__ y3, int nconv,
+                                                              damc::PackConvList pk) {
   extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][16] weights, [8][8] sums, [2][16], window
+  if ((int)blockIdx.x >= nconv) {  // workgroup-uniform
+    damc::pack_conv_x3_block(pk, (int)blockIdx.x - nconv, threadIdx.x, 512, smf);
+    return;
+  }
   float* wl = smf;
   float* red = wl + 9 * CIN * 16;
   float* st = red + 8 * 8;
   float* win = st + 32;
-  const int b = blockIdx.x, c0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ncb = C / 16, b = blockIdx.x / ncb, c0 = (blockIdx.x - b * ncb) * 16, tid = threadIdx.x, lane = tid & 63,
+            wave = tid >> 6;
   const int HW = H * W, cg = wave >> 2, run = tid & 255;  // channels c0 + 8 cg .. + 7; pixels 4 run .. + 3
   for (int i = tid; i < 9 * CIN * 16; i += 512) wl[i] = w[(i >> 4) * C + c0 + (i & 15)];
   conv3_stage<CIN>(x, b, H, W, 0, H, win);
@@ -825,10 +834,13 @@ struct EncShapes {
   int h[DAMC_MAX_ENC_LAYERS + 1], w[DAMC_MAX_ENC_LAYERS + 1];
   size_t act_max = 0, slab_max = 0, in_max = 0;
   size_t a3_max = 0, w3_max = 0, ks_max = 0;  // limb engine: activation limbs, weight limbs, split-K slabs
+  size_t wsrc_off[DAMC_MAX_ENC_LAYERS] = {}, wsrc_bytes = 0;  // the limb operands packed from w_src (workspace)
   bool limb[DAMC_MAX_ENC_LAYERS] = {};
   bool first_fused = false;  // layer 0 as conv3_stats + conv3_apply_x3 (no stored conv output, no NHWC copy)
   int first_rows = 1, first_strips = 1;
 };
+size_t round256(size_t b) { return (b + 255) / 256 * 256; }
+
 bool enc_limb_layer(const damc_encoder_t* e, const damc_enc_layer_t& L) {
   return e->engine == DAMC_ENGINE_LIMB && damc::conv_kmajor_ok(L.cin) && L.cout % 8 == 0 && L.k * L.k <= 32;
 }
@@ -850,11 +862,17 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
     sh->w[i + 1] = wo;
     if (i + 1 < e->n_layers) sh->act_max = std::max(sh->act_max, (size_t)B * ho * wo * L.cout);
     sh->limb[i] = enc_limb_layer(e, L);
-    if (!L.w_packed && !(sh->limb[i] && L.w_x3)) return false;  // the engine's weight operand
+    if (!L.w_packed && !(sh->limb[i] && (L.w_x3 || L.w_src))) return false;  // the engine's weight operand
+    if (L.w_src && (!sh->limb[i] || L.w_x3 || (uintptr_t)L.w_src % 16 != 0)) return false;
     if (sh->limb[i]) {
       const long M = (long)B * ho * wo, K = (long)L.k * L.k * L.cin;
       sh->a3_max = std::max(sh->a3_max, (size_t)B * sh->h[i] * sh->w[i] * L.cin * 6);
-      if (!L.w_x3) sh->w3_max = std::max(sh->w3_max, (size_t)L.cout * K * 6);
+      if (L.w_src) {
+        sh->wsrc_off[i] = sh->wsrc_bytes;
+        sh->wsrc_bytes += round256((size_t)L.cout * K * 6);
+      } else if (!L.w_x3) {
+        sh->w3_max = std::max(sh->w3_max, (size_t)L.cout * K * 6);
+      }
       sh->ks_max = std::max(sh->ks_max, (size_t)damc::x3_ksplit_floats((int)M, L.cout, (int)K, 1));
     } else {
       sh->slab_max = std::max(sh->slab_max,
@@ -879,7 +897,6 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
   }
   return true;
 }
-size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
 // y (B, ho, wo, cout) NHWC = conv(x3 limbs of x) + bias on the limb engine
 int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_enc_layer_t& L, const void* w3, float* y,
@@ -931,7 +948,7 @@ extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B)
   if (!enc_shapes(e, B, &sh)) return 0;
   return 2 * round256(sh.act_max * 4) + round256(std::max<size_t>(sh.slab_max, 1) * 4) +
          round256(std::max<size_t>(sh.in_max, 1) * 4) + round256(sh.a3_max) + round256(sh.w3_max) +
-         round256(sh.ks_max * 4);
+         round256(sh.ks_max * 4) + sh.wsrc_bytes;
 }
 
 extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B, float* xemb, void* wsp, size_t wsb,
@@ -956,8 +973,30 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   unsigned short* a3 = reinterpret_cast<unsigned short*>(take(sh.a3_max));
   unsigned short* w3 = reinterpret_cast<unsigned short*>(take(sh.w3_max));
   float* kslab = reinterpret_cast<float*>(take(sh.ks_max * 4));
+  char* wsrc = sh.wsrc_bytes ? take(sh.wsrc_bytes) : nullptr;
   hipStream_t s = as_stream(stream);
   int rc;
+  // the w_src layers' limb operands, all in one launch: as extra workgroups of the one-pass first layer when it runs
+  // (conv3_in_fused_kernel), else on their own before it
+  damc::PackConvList pl{};
+  if (wsrc) {
+    for (int i = 0; i < n; ++i) {
+      const damc_enc_layer_t& L = e->layers[i];
+      if (!L.w_src) continue;
+      unsigned short* y = reinterpret_cast<unsigned short*>(wsrc + sh.wsrc_off[i]);
+      if (damc::pack_conv_x3_many_ok(L.w_src, L.cin, L.k)) {
+        pl.w[pl.n] = L.w_src;
+        pl.y[pl.n] = y;
+        pl.cin[pl.n] = L.cin;
+        pl.taps[pl.n] = L.k * L.k;
+        pl.blk0[++pl.n] = L.cout;
+      } else if ((rc = damc::launch_pack_conv_x3(L.w_src, L.cout, L.cin, L.k, y, s))) {
+        return rc;
+      }
+    }
+    if (pl.n && damc::pack_conv_x3_many_prep(pl)) return DAMC_ERR_UNSUPPORTED;
+  }
+  bool pl_done = pl.n == 0;
   bool a3_ready = false;  // a3 holds the limbs of the current layer's input (written by the previous layer's norm)
   int i0 = 0;
   if (sh.first_fused) {  // layer 0: conv3 + InstanceNorm + LeakyReLU straight to layer 1's limbs
@@ -973,10 +1012,17 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * 16 + 8 * 8 + 32) * sizeof(float);
     // (a sample of at most 1024 pixels; CelebA-64 and larger keep the two passes)
     const bool one = !(op && op[0] == '0') && H * W <= 1024 && W % 4 == 0 && C % 16 == 0 && sm1 <= 65536;
+    if (!one && !pl_done) {
+      if ((rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
+      pl_done = true;
+    }
+    const int nconv = B * (C / 16), npk = pl_done ? 0 : pl.blk0[pl.n];
+    const size_t smp = std::max(sm1, pl_done ? (size_t)0 : (size_t)pl.lds);
 #define DAMC_C1(CIN_)                                                                                               \
   if (one && L.cin == CIN_) {                                                                                       \
-    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(B, C / 16), dim3(512), sm1, s, x, H, W, C, L.w_packed,     \
-                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3);                                       \
+    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(nconv + npk), dim3(512), smp, s, x, H, W, C, L.w_packed,  \
+                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3, nconv, pl);                            \
+    pl_done = true;                                                                                                 \
   }
     DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
 #undef DAMC_C1
@@ -997,6 +1043,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   } else if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) {
     return rc;
   }
+  if (!pl_done && (rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
   for (int i = i0; i < n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
@@ -1005,7 +1052,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         const long na = (long)B * sh.h[i] * sh.w[i] * L.cin;
         if ((rc = damc::launch_split_x3(buf[i & 1], na, a3, s))) return rc;
       }
-      const void* wl = L.w_x3;
+      const void* wl = L.w_x3 ? L.w_x3 : L.w_src ? static_cast<const void*>(wsrc + sh.wsrc_off[i]) : nullptr;
       if (!wl) {  // the limb copy from the fp32 packing
         const int K = L.k * L.k * L.cin;
         if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;

@@ -238,6 +238,34 @@ def test_encoder_limb_engine_vs_fp32_engine_b128(gpu_device):
     _check("Encoder_cifar10 nif=64 B=128 xemb, fp32 engine", got32, e32, e64, 1e-7)
 
 
+@pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
+def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
+    """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch on a side stream that
+    overlaps the first conv.  Bitwise the per-layer damc_pack_conv2d_x3 operands (DAMC_ENC_WSRC=0), and a weight
+    rewritten in place through .data between calls (the reference's EMA update, train_gen_recon.py:258-261) is seen
+    by the next call."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    hw = GEN[name][3]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 2, (B, 3, hw, hw))).to(gpu_device)
+    monkeypatch.setenv("DAMC_ENC_WSRC", "1")
+    a = amortizer.encoder_forward(enc, x).cpu()
+    monkeypatch.setenv("DAMC_ENC_WSRC", "0")
+    b = amortizer.encoder_forward(enc, x).cpu()
+    assert torch.equal(a, b)
+    with torch.no_grad():
+        for m in enc.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.data.copy_(m.weight.data * 0.75)
+    b2 = amortizer.encoder_forward(enc, x).cpu()
+    monkeypatch.setenv("DAMC_ENC_WSRC", "1")
+    a2 = amortizer.encoder_forward(enc, x).cpu()
+    assert torch.equal(a2, b2)
+    assert not torch.equal(a2, a)
+
+
 def test_celebaHQ_q_sweep_vs_fp64(gpu_device):
     """CelebA-HQ Q(x) at its per-rank size (B=8 of 64): Encoder_celebaHQ(nif=64) + the 100-step 'large' reverse sweep
     (nxemb 1024, ntemb 128; train_gen_recon.py:360-380 defaults) with injected noise, vs the fp64 oracle."""
