@@ -353,8 +353,8 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
                                                               const float* __restrict__ w, const float* __restrict__ bias,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps, float slope,
-                                                              unsigned short* __restrict__ y3, int nconv,
-                                                              damc::PackConvList pk) {
+                                                              unsigned short* __restrict__ y3, float* __restrict__ y32,
+                                                              int nconv, damc::PackConvList pk) {
   extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][16] weights, [8][8] sums, [2][16], window
   if ((int)blockIdx.x >= nconv) {  // workgroup-uniform
     damc::pack_conv_x3_block(pk, (int)blockIdx.x - nconv, threadIdx.x, 512, smf);
@@ -452,7 +452,13 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
       const float u = fmaf(y[k][e], scl[e], shf[e]);
       t[e] = u > 0.f ? u : u * slope;
     }
-    damc::store_x3_octet(t, y3 + 3 * (((long)b * HW + p0 + k) * C + c0 + 8 * cg));
+    const long off = ((long)b * HW + p0 + k) * C + c0 + 8 * cg;
+    if (y32) {  // fp32 NHWC for an F32A next conv
+      *reinterpret_cast<f32x4*>(y32 + off) = f32x4{t[0], t[1], t[2], t[3]};
+      *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{t[4], t[5], t[6], t[7]};
+    } else {
+      damc::store_x3_octet(t, y3 + 3 * off);
+    }
   }
 }
 
@@ -463,9 +469,12 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
 // in_apply_x3_kernel's normalise + LReLU + limb store.  Replaces in_stats + in_merge + in_apply_x3 (one read of the
 // activation instead of two, one launch instead of three).
 template <int NIT>
-__global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restrict__ y, int HW, int C,
+// y32 != NULL: the result leaves as fp32 NHWC at y32 instead of limbs (the next conv stages it as fp32, gemm.hip
+// X3_F32A); y32 may be y itself (every thread writes only the elements it read, after both block sums)
+__global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW, int C,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                          float eps, float slope, unsigned short* __restrict__ y3) {
+                                                          float eps, float slope, unsigned short* __restrict__ y3,
+                                                          float* y32) {
   __shared__ float red[4][32];
   __shared__ float st[2][32];
   const int b = blockIdx.x, c0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -531,7 +540,13 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restric
       const float u = fmaf(v[it][e], scl[e], shf[e]);
       o[e] = u > 0.f ? u : u * slope;
     }
-    damc::store_x3_octet(o, y3 + 3 * (((long)b * HW + p) * C + c0 + 8 * q));
+    const long off = ((long)b * HW + p) * C + c0 + 8 * q;
+    if (y32) {
+      *reinterpret_cast<f32x4*>(y32 + off) = f32x4{o[0], o[1], o[2], o[3]};
+      *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    } else {
+      damc::store_x3_octet(o, y3 + 3 * off);
+    }
   }
 }
 
@@ -899,11 +914,18 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
 }
 
 // y (B, ho, wo, cout) NHWC = conv(x3 limbs of x) + bias on the limb engine
-int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_enc_layer_t& L, const void* w3, float* y,
-                float* kslab, size_t kslab_floats, hipStream_t s) {
+// af32 != NULL: the input as fp32 NHWC, staged as fp32 and split into limbs in registers (X3_F32A; bitwise the limb
+// input a3 = the RNE limbs of af32)
+int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int win, const damc_enc_layer_t& L,
+                const void* w3, float* y, float* kslab, size_t kslab_floats, hipStream_t s) {
   const int hout = (hin + 2 * L.pad - L.k) / L.stride + 1, wout = (win + 2 * L.pad - L.k) / L.stride + 1;
   damc::GemmArgs a;
-  a.A3 = a3;
+  if (af32) {
+    a.A = af32;
+    a.a_f32 = 1;
+  } else {
+    a.A3 = a3;
+  }
   a.Hin = hin;
   a.Win = win;
   a.Cg = L.cin;
@@ -998,6 +1020,15 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   }
   bool pl_done = pl.n == 0;
   bool a3_ready = false;  // a3 holds the limbs of the current layer's input (written by the previous layer's norm)
+  bool in32 = false;      // or the previous layer's norm left it as fp32 NHWC in buf[i & 1] for an F32A conv
+  // the k4 s2 p1 limb convs stage their input as fp32 (X3_F32A) where the norm before them can write fp32 (the
+  // one-pass kernels); DAMC_ENC_F32A=0 (read per call): limbs throughout
+  const char* fe = getenv("DAMC_ENC_F32A");
+  const bool f32a_on = !(fe && fe[0] == '0');
+  auto f32a_layer = [&](int i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    return f32a_on && i < n && sh.limb[i] && L.k == 4 && L.stride == 2 && L.pad == 1;
+  };
   int i0 = 0;
   if (sh.first_fused) {  // layer 0: conv3 + InstanceNorm + LeakyReLU straight to layer 1's limbs
     const damc_enc_layer_t& L = e->layers[0];
@@ -1017,11 +1048,12 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       pl_done = true;
     }
     const int nconv = B * (C / 16), npk = pl_done ? 0 : pl.blk0[pl.n];
+    float* y32 = (one && f32a_layer(1)) ? buf[1] : nullptr;
     const size_t smp = std::max(sm1, pl_done ? (size_t)0 : (size_t)pl.lds);
 #define DAMC_C1(CIN_)                                                                                               \
   if (one && L.cin == CIN_) {                                                                                       \
     hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(nconv + npk), dim3(512), smp, s, x, H, W, C, L.w_packed,  \
-                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3, nconv, pl);                            \
+                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3, y32, nconv, pl);                       \
     pl_done = true;                                                                                                 \
   }
     DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
@@ -1038,7 +1070,8 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     DAMC_C3(1) DAMC_C3(3) DAMC_C3(4)
 #undef DAMC_C3
     DAMC_LAUNCH_CHECK();
-    a3_ready = true;
+    in32 = y32 != nullptr;
+    a3_ready = !in32;
     i0 = 1;
   } else if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) {
     return rc;
@@ -1048,7 +1081,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
     if (sh.limb[i]) {
-      if (!a3_ready) {
+      if (!a3_ready && !in32) {
         const long na = (long)B * sh.h[i] * sh.w[i] * L.cin;
         if ((rc = damc::launch_split_x3(buf[i & 1], na, a3, s))) return rc;
       }
@@ -1058,7 +1091,8 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;
         wl = w3;
       }
-      if ((rc = enc_conv_x3(a3, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max, s))) return rc;
+      if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max, s)))
+        return rc;
     } else {
       const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
       if ((rc = damc_conv2d_nhwc(buf[i & 1], B, sh.h[i], sh.w[i], L.cin, L.w_packed, L.bias, L.cout, L.k, L.stride,
@@ -1066,23 +1100,26 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         return rc;
     }
     a3_ready = false;
+    in32 = false;
     if (!L.in_gamma) continue;
     const int hw = sh.h[i + 1] * sh.w[i + 1];
     const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel form below
     if (i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0')) {
       ProfScope ps("instnorm", 0.0, s);
       const dim3 g(B, L.cout / 32);
+      float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
       if (hw <= 64)
         hipLaunchKernelGGL(in_fused_x3_kernel<1>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32);
       else if (hw <= 128)
         hipLaunchKernelGGL(in_fused_x3_kernel<2>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32);
       else
         hipLaunchKernelGGL(in_fused_x3_kernel<4>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32);
       DAMC_LAUNCH_CHECK();
-      a3_ready = true;
+      in32 = y32 != nullptr;
+      a3_ready = !in32;
     } else if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
       const int S = in_splits(hw), cg = (L.cout + 63) / 64;
       float* ssb = inws + (size_t)B * L.cout * S * 3;

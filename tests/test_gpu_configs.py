@@ -238,6 +238,24 @@ def test_encoder_limb_engine_vs_fp32_engine_b128(gpu_device):
     _check("Encoder_cifar10 nif=64 B=128 xemb, fp32 engine", got32, e32, e64, 1e-7)
 
 
+@pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32), ("cifar10", 16)])
+def test_encoder_f32a_convs_are_bitwise(gpu_device, monkeypatch, name, B):
+    """The encoder's k4 s2 limb convs staging their input as fp32 (gemm.hip X3_F32A, the one-pass norms writing fp32
+    in place) against the limb inputs (DAMC_ENC_F32A=0): the in-register split is the producing epilogue's RNE split,
+    so xemb is bitwise the same."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    hw = GEN[name][3]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 3, (B, 3, hw, hw))).to(gpu_device)
+    monkeypatch.setenv("DAMC_ENC_F32A", "1")
+    a = amortizer.encoder_forward(enc, x).cpu()
+    monkeypatch.setenv("DAMC_ENC_F32A", "0")
+    b = amortizer.encoder_forward(enc, x).cpu()
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
 def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
     """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch on a side stream that
