@@ -471,10 +471,14 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
 template <int NIT>
 // y32 != NULL: the result leaves as fp32 NHWC at y32 instead of limbs (the next conv stages it as fp32, gemm.hip
 // X3_F32A); y32 may be y itself (every thread writes only the elements it read, after both block sums)
+// slab != NULL: y was not written; the conv's ks split-K slabs (register layout of the 256 x 128 limb tiles, as
+// x3_ksplit_reduce_tile_kernel reads them, sstride4 f32x4 per slab, ntn 128-channel tiles) are summed here in the
+// reduce's order from 0, then the conv bias added: the reduce + epilogue's arithmetic, so the values are bitwise C's
 __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW, int C,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           float eps, float slope, unsigned short* __restrict__ y3,
-                                                          float* y32) {
+                                                          float* y32, const float* __restrict__ slab, int ks, int ntn,
+                                                          long sstride4, const float* __restrict__ cbias) {
   __shared__ float red[4][32];
   __shared__ float st[2][32];
   const int b = blockIdx.x, c0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -483,7 +487,25 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int p = pr + 64 * it;
-    if (p < HW) {
+    if (p < HW && slab) {
+      const long m = (long)b * HW + p;
+      const int n = c0 + 8 * q, rm = (int)(m & 255), rn = n & 127;
+      const long tile = (m >> 8) * ntn + (n >> 7);
+      const int wv = (rm >> 6) * 2 + (rn >> 6), ij = ((rm & 63) >> 4) * 4 + ((rn & 63) >> 4);
+      const long base = ((tile * 8 + wv) * 16 + ij) * 64 + ((rm & 15) >> 2) * 16 + (rn & 15);  // f32x4 of element 0
+      const int r = rm & 3;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
+      for (int sl = 0; sl < ks; ++sl) {
+        const float* src = slab + ((long)sl * sstride4 + base) * 4 + r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] += src[4 * e];
+      }
+      if (cbias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] += cbias[n + e];
+      }
+    } else if (p < HW) {
       const float* src = y + ((long)b * HW + p) * C + c0 + 8 * q;
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(src), a1 = *reinterpret_cast<const f32x4*>(src + 4);
       v[it][0] = a0.x; v[it][1] = a0.y; v[it][2] = a0.z; v[it][3] = a0.w;
@@ -917,7 +939,7 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
 // af32 != NULL: the input as fp32 NHWC, staged as fp32 and split into limbs in registers (X3_F32A; bitwise the limb
 // input a3 = the RNE limbs of af32)
 int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int win, const damc_enc_layer_t& L,
-                const void* w3, float* y, float* kslab, size_t kslab_floats, hipStream_t s) {
+                const void* w3, float* y, float* kslab, size_t kslab_floats, int* defer, hipStream_t s) {
   const int hout = (hin + 2 * L.pad - L.k) / L.stride + 1, wout = (win + 2 * L.pad - L.k) / L.stride + 1;
   damc::GemmArgs a;
   if (af32) {
@@ -948,6 +970,7 @@ int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int
   a.act = DAMC_ACT_NONE;
   a.kslab = kslab;
   a.kslab_floats = (long)kslab_floats;
+  a.ksplit_deferred = defer;
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
                            2.0 * a.M * (double)L.cout * a.K, s);
 }
@@ -1077,9 +1100,15 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     return rc;
   }
   if (!pl_done && (rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
+  const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel norm below
+  const char* isl = getenv("DAMC_ENC_IN_SLABS");   // (read per call) 0: the split-K reduce kernel writes C first
   for (int i = i0; i < n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
+    const int hw = sh.h[i + 1] * sh.w[i + 1];
+    // the norm after this conv is the one-pass kernel; it then also sums the conv's split-K slabs itself
+    const bool in1 = L.in_gamma && i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0');
+    int ks_def = 0;
     if (sh.limb[i]) {
       if (!a3_ready && !in32) {
         const long na = (long)B * sh.h[i] * sh.w[i] * L.cin;
@@ -1091,7 +1120,8 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;
         wl = w3;
       }
-      if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max, s)))
+      if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max,
+                            (in1 && !(isl && isl[0] == '0')) ? &ks_def : nullptr, s)))
         return rc;
     } else {
       const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
@@ -1102,21 +1132,22 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     a3_ready = false;
     in32 = false;
     if (!L.in_gamma) continue;
-    const int hw = sh.h[i + 1] * sh.w[i + 1];
-    const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel form below
-    if (i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0')) {
+    if (in1) {
       ProfScope ps("instnorm", 0.0, s);
       const dim3 g(B, L.cout / 32);
       float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
+      const int ntn = (L.cout + 127) / 128;
+      const long sstride4 = (long)((B * hw + 255) / 256) * ntn * (256 * 128 / 4);
+      const float* sl = ks_def > 0 ? kslab : nullptr;
       if (hw <= 64)
         hipLaunchKernelGGL(in_fused_x3_kernel<1>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       else if (hw <= 128)
         hipLaunchKernelGGL(in_fused_x3_kernel<2>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       else
         hipLaunchKernelGGL(in_fused_x3_kernel<4>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       DAMC_LAUNCH_CHECK();
       in32 = y32 != nullptr;
       a3_ready = !in32;

@@ -70,6 +70,11 @@ struct GemmArgs {
   // limb engine: the A operand is the fp32 tensor A (NHWC), staged as fp32 and split into limbs in registers
   // (gemm_x3_kernel variant X3_F32A: 4 B per gathered element instead of 6 B of limbs); A3 unused
   int a_f32 = 0;
+  // host pointer (EPI_BIAS_ACT, O_DENSE, no C3 / sgn): when set and the launch splits K into register-layout slabs
+  // (kslab_reg), the reduce is skipped and the slab count is written here for a consumer that sums the slabs itself
+  // (the encoder's InstanceNorm; slab layout: gemm.hip x3_ksplit_reduce_tile_kernel); 0 = the launcher reduced or did
+  // not split, C holds the result
+  int* ksplit_deferred = nullptr;
   // clock probe (damc_clock_probe; diagnostics, off in timed work): thread 0 of each workgroup stores {s_memtime,
   // s_memrealtime} before its K loop and after it, at clk[4 * (workgroup % clk_n)]
   unsigned long long* clk = nullptr;

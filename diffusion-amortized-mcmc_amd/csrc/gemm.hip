@@ -2457,6 +2457,10 @@ static void launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
         hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
       }
       if (a.kslab_reg) {  // one wave per 16x16 tile, four per workgroup
+        if (EPI == EPI_BIAS_ACT && OM == O_DENSE && a.ksplit_deferred && !a.C3 && !a.sgn) {
+          *a.ksplit_deferred = ks;  // the consumer sums the slabs (GemmArgs::ksplit_deferred)
+          return;
+        }
         const long waves = (long)zdim * ntm * ntn * 128;
         hipLaunchKernelGGL((x3_ksplit_reduce_tile_kernel<EPI, OM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
                            a, zdim);
@@ -2835,9 +2839,11 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   const long per = (lim / 6 - 1) / img;
   if (per < 1) return DAMC_ERR_UNSUPPORTED;
   const long cimg = (om == O_PHASE) ? (long)a.Hout * a.Wout * a.ldc : hwq * a.ldc;
+  if (a.ksplit_deferred) *a.ksplit_deferred = 0;
   for (long b0 = 0; b0 < nimg; b0 += per) {
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
+    if (nimg > per) c.ksplit_deferred = nullptr;  // one launch's slabs only
     if (om == O_PHASE && g_clk) {
       c.clk = g_clk;
       c.clk_n = g_clk_n;

@@ -241,19 +241,23 @@ def test_encoder_limb_engine_vs_fp32_engine_b128(gpu_device):
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32), ("cifar10", 16)])
 def test_encoder_f32a_convs_are_bitwise(gpu_device, monkeypatch, name, B):
     """The encoder's k4 s2 limb convs staging their input as fp32 (gemm.hip X3_F32A, the one-pass norms writing fp32
-    in place) against the limb inputs (DAMC_ENC_F32A=0): the in-register split is the producing epilogue's RNE split,
-    so xemb is bitwise the same."""
+    in place) against the limb inputs (DAMC_ENC_F32A=0), and the one-pass norms summing the convs' split-K slabs
+    themselves (GemmArgs::ksplit_deferred) against the reduce kernel (DAMC_ENC_IN_SLABS=0): the in-register split is
+    the producing epilogue's RNE split and the slab sum the reduce's order, so xemb is bitwise the same."""
     from damc import amortizer, synth
     from src import diffusion_net as dn
 
     hw = GEN[name][3]
     enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
     x = torch.from_numpy(synth.uniform_f32(13, 3, (B, 3, hw, hw))).to(gpu_device)
-    monkeypatch.setenv("DAMC_ENC_F32A", "1")
-    a = amortizer.encoder_forward(enc, x).cpu()
-    monkeypatch.setenv("DAMC_ENC_F32A", "0")
-    b = amortizer.encoder_forward(enc, x).cpu()
-    assert torch.equal(a, b)
+    outs = {}
+    for f32a in "10":
+        for slabs in "10":  # DAMC_ENC_IN_SLABS: the one-pass norm sums the convs' split-K slabs itself
+            monkeypatch.setenv("DAMC_ENC_F32A", f32a)
+            monkeypatch.setenv("DAMC_ENC_IN_SLABS", slabs)
+            outs[f32a + slabs] = amortizer.encoder_forward(enc, x).cpu()
+    for k, v in outs.items():
+        assert torch.equal(v, outs["00"]), k
 
 
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
