@@ -1390,7 +1390,7 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
   }
   // k4 s2 p1: the LDS-staged gather over 16 x 32 output tiles (bitwise), where the tiles fill the chip
   if (!(gl && gl[0] == '0') && L.k == 4 && L.stride == 2 && L.pad == 1 && L.hout == 2 * L.hin &&
-      L.wout == 2 * L.win && (long)B * ((L.hout + 15) / 16) * ((L.wout + 31) / 32) >= 256) {
+      L.wout == 2 * L.win && B <= 65535 && (long)B * ((L.hout + 15) / 16) * ((L.wout + 31) / 32) >= 256) {
     const int R2 = 16, CW2 = 32;
     const size_t sm = (size_t)(R2 / 2 + 2) * (CW2 / 2 + 2) * 16 * L.cout * sizeof(float);
     const dim3 g((L.wout + CW2 - 1) / CW2, (L.hout + R2 - 1) / R2, B);
