@@ -993,7 +993,7 @@ extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B)
   if (!enc_shapes(e, B, &sh)) return 0;
   return 2 * round256(sh.act_max * 4) + round256(std::max<size_t>(sh.slab_max, 1) * 4) +
          round256(std::max<size_t>(sh.in_max, 1) * 4) + round256(sh.a3_max) + round256(sh.w3_max) +
-         round256(sh.ks_max * 4) + sh.wsrc_bytes;
+         round256(sh.ks_max * 4) + sh.wsrc_bytes + 256;  // + the packing's status word (DAMC_ENC_PACK_CHECK)
 }
 
 extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B, float* xemb, void* wsp, size_t wsb,
@@ -1019,8 +1019,15 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   unsigned short* w3 = reinterpret_cast<unsigned short*>(take(sh.w3_max));
   float* kslab = reinterpret_cast<float*>(take(sh.ks_max * 4));
   char* wsrc = sh.wsrc_bytes ? take(sh.wsrc_bytes) : nullptr;
+  int* pack_err = reinterpret_cast<int*>(take(256));
   hipStream_t s = as_stream(stream);
   int rc;
+  // DAMC_ENC_PACK_CHECK=1 (read per call; tests, never timed work): the packing workgroups report any workgroup outside
+  // their list in a status word the call zeroes first and reads back at its end (one host sync), returning
+  // DAMC_ERR_UNSUPPORTED if it was set
+  const char* pc = getenv("DAMC_ENC_PACK_CHECK");
+  const bool pack_check = pc && pc[0] == '1';
+  if (pack_check && (rc = (int)hipMemsetAsync(pack_err, 0, sizeof(int), s))) return rc;
   // the w_src layers' limb operands, all in one launch: as extra workgroups of the one-pass first layer when it runs
   // (conv3_in_fused_kernel), else on their own before it
   damc::PackConvList pl{};
@@ -1029,7 +1036,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       const damc_enc_layer_t& L = e->layers[i];
       if (!L.w_src) continue;
       unsigned short* y = reinterpret_cast<unsigned short*>(wsrc + sh.wsrc_off[i]);
-      if (damc::pack_conv_x3_many_ok(L.w_src, L.cin, L.k)) {
+      if (pl.n < 8 && damc::pack_conv_x3_many_ok(L.w_src, L.cin, L.k)) {
         pl.w[pl.n] = L.w_src;
         pl.y[pl.n] = y;
         pl.cin[pl.n] = L.cin;
@@ -1040,6 +1047,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       }
     }
     if (pl.n && damc::pack_conv_x3_many_prep(pl)) return DAMC_ERR_UNSUPPORTED;
+    pl.err = pack_check ? pack_err : nullptr;
   }
   bool pl_done = pl.n == 0;
   bool a3_ready = false;  // a3 holds the limbs of the current layer's input (written by the previous layer's norm)
@@ -1167,6 +1175,12 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
                                               stream))) {
       return rc;
     }
+  }
+  if (pack_check) {
+    int flag = 0;
+    if ((rc = (int)hipMemcpyAsync(&flag, pack_err, sizeof(int), hipMemcpyDeviceToHost, s))) return rc;
+    if ((rc = (int)hipStreamSynchronize(s))) return rc;
+    if (flag) return DAMC_ERR_UNSUPPORTED;
   }
   return 0;
 }

@@ -151,6 +151,8 @@ struct PackConvList {
   int cin[8], taps[8], cc[8], blk0[9];
   int ready;   // set by pack_conv_x3_many_prep (blk0 then holds workgroup offsets, not couts)
   int lds;     // dynamic LDS bytes per workgroup (prep)
+  int cout[8];  // (prep) each layer's output channels: the device-side bound of a workgroup's weight rows
+  int* err;     // optional device status word: a workgroup outside the list ORs 1 into it and writes nothing
 };
 bool pack_conv_x3_many_ok(const float* w, int cin, int k);
 // fills in cc and lds and turns blk0[i + 1] (layer i's cout on entry) into running workgroup offsets, once (ready);
@@ -186,11 +188,18 @@ __device__ __forceinline__ void store_x3_octet(const float (&v)[8], unsigned sho
 // CC * 6 contiguous bytes of the K-major output, odd sign blocks negated
 __device__ __forceinline__ void pack_conv_x3_block(const PackConvList& l, int blk, int tid, int nthr, float* pk_t) {
   typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  // bound (workgroup-uniform, before any access): the workgroup must name a weight row of the prepared list; one that
+  // does not (a grid larger than the list) writes nothing and flags the status word
+  const bool in_list = l.ready && l.n >= 1 && l.n <= 8 && blk >= 0 && blk < l.blk0[l.n];
   int li = 0;
-  while (li + 1 < l.n && blk >= l.blk0[li + 1]) ++li;
+  while (in_list && li + 1 < l.n && blk >= l.blk0[li + 1]) ++li;
   blk -= l.blk0[li];
-  const int CC = l.cc[li], cin = l.cin[li], taps = l.taps[li], nch = cin / CC;
-  const int co = blk / nch, cc0 = (blk - co * nch) * CC, tp1 = taps + 1, n4 = CC * taps / 4;
+  const int CC = l.cc[li], cin = l.cin[li], taps = l.taps[li], nch = CC > 0 ? cin / CC : 0;
+  const int co = nch > 0 ? blk / nch : 0, cc0 = (blk - co * nch) * CC, tp1 = taps + 1, n4 = CC * taps / 4;
+  if (!in_list || nch <= 0 || co >= l.cout[li] || cc0 + CC > cin) {
+    if (tid == 0 && l.err) atomicOr(l.err, 1);
+    return;
+  }
   const f32x4_t* src = reinterpret_cast<const f32x4_t*>(l.w[li] + ((long)co * cin + cc0) * taps);
   for (int q = tid; q < n4; q += nthr) {
     const f32x4_t v = src[q];

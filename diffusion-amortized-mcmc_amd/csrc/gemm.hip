@@ -2736,7 +2736,14 @@ int pack_conv_x3_many_prep(PackConvList& l) {
     l.cc[i] = l.cin[i] % 128 == 0 ? 128 : 64;
     sm = std::max(sm, (size_t)l.cc[i] * (l.taps[i] + 1) * sizeof(float));
   }
-  for (int i = 0; i < l.n; ++i) l.blk0[i + 1] = l.blk0[i] + l.blk0[i + 1] * (l.cin[i] / l.cc[i]);
+  for (int i = 0; i < l.n; ++i) {
+    l.cout[i] = l.blk0[i + 1];
+    l.blk0[i + 1] = l.blk0[i] + l.blk0[i + 1] * (l.cin[i] / l.cc[i]);
+  }
+  // the grid is exactly the work list: one workgroup per (layer, co, channel chunk), nothing more
+  long total = 0;
+  for (int i = 0; i < l.n; ++i) total += (long)l.cout[i] * (l.cin[i] / l.cc[i]);
+  if (total != l.blk0[l.n]) return 1;
   l.lds = (int)sm;
   l.ready = 1;
   return 0;

@@ -203,10 +203,14 @@ def test_celebaHQ_b64_likelihood_gradient_vs_fp64(gpu_device):
 
 
 @pytest.mark.parametrize("name,B", [("celeba64", 32), ("celebaHQ", 8)])
-def test_full_width_encoder_vs_fp64(gpu_device, name, B):
+def test_full_width_encoder_vs_fp64(gpu_device, monkeypatch, name, B):
     from damc import amortizer, synth
     from oracle import damc_oracle as orc
     from src import diffusion_net as dn
+
+    # the library's weight packing (w_src, extra workgroups of the first layer's launch on CelebA-64's two-pass path)
+    # reports any workgroup outside its list; the call then fails instead of returning xemb
+    monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
 
     hw = GEN[name][3]
     enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
@@ -262,8 +266,8 @@ def test_encoder_f32a_convs_are_bitwise(gpu_device, monkeypatch, name, B):
 
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
 def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
-    """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch on a side stream that
-    overlaps the first conv.  Bitwise the per-layer damc_pack_conv2d_x3 operands (DAMC_ENC_WSRC=0), and a weight
+    """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch (extra workgroups of the
+    first layer's launch, or a launch of its own before a two-pass first layer), under the packing's status word.  Bitwise the per-layer damc_pack_conv2d_x3 operands (DAMC_ENC_WSRC=0), and a weight
     rewritten in place through .data between calls (the reference's EMA update, train_gen_recon.py:258-261) is seen
     by the next call."""
     from damc import amortizer, synth
@@ -272,6 +276,7 @@ def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, nam
     hw = GEN[name][3]
     enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
     x = torch.from_numpy(synth.uniform_f32(13, 2, (B, 3, hw, hw))).to(gpu_device)
+    monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
     monkeypatch.setenv("DAMC_ENC_WSRC", "1")
     a = amortizer.encoder_forward(enc, x).cpu()
     monkeypatch.setenv("DAMC_ENC_WSRC", "0")
