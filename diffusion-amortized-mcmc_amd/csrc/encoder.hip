@@ -345,18 +345,27 @@ __device__ __forceinline__ float wave_rsum(const float (&v)[N], int lane, int of
 // channel (wave reduce-scatter, then the channel's 4 wave sums in a fixed order) for the mean, then sums
 // (y - mean)^2 for the variance (two passes over registers), and writes lrelu(IN(y)) as the next convolution's limbs.
 // The statistics pass, the Welford partials, the merge kernel and the recomputing second pass all drop out.
+// 1-D grid: workgroup (b, C / 16 chunk) for the first nconv = B * C / 16, then the per-call limb packing of the
+// limb layers' weights (pk, pack_conv_x3_block) as extra workgroups of the same launch, so the two fill the chip
+// together (a separate packing launch, or one on a forked stream, costs its own ramp / the event hand-offs)
 template <int CIN>
 __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __restrict__ x, int H, int W, int C,
                                                               const float* __restrict__ w, const float* __restrict__ bias,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps, float slope,
-                                                              unsigned short* __restrict__ y3) {
+                                                              unsigned short* __restrict__ y3, float* __restrict__ y32,
+                                                              int nconv, damc::PackConvList pk) {
   extern __shared__ __attribute__((aligned(16))) float smf[];  // [9 CIN][16] weights, [8][8] sums, [2][16], window
+  if ((int)blockIdx.x >= nconv) {  // workgroup-uniform
+    damc::pack_conv_x3_block(pk, (int)blockIdx.x - nconv, threadIdx.x, 512, smf);
+    return;
+  }
   float* wl = smf;
   float* red = wl + 9 * CIN * 16;
   float* st = red + 8 * 8;
   float* win = st + 32;
-  const int b = blockIdx.x, c0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ncb = C / 16, b = blockIdx.x / ncb, c0 = (blockIdx.x - b * ncb) * 16, tid = threadIdx.x, lane = tid & 63,
+            wave = tid >> 6;
   const int HW = H * W, cg = wave >> 2, run = tid & 255;  // channels c0 + 8 cg .. + 7; pixels 4 run .. + 3
   for (int i = tid; i < 9 * CIN * 16; i += 512) wl[i] = w[(i >> 4) * C + c0 + (i & 15)];
   conv3_stage<CIN>(x, b, H, W, 0, H, win);
@@ -443,7 +452,13 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
       const float u = fmaf(y[k][e], scl[e], shf[e]);
       t[e] = u > 0.f ? u : u * slope;
     }
-    damc::store_x3_octet(t, y3 + 3 * (((long)b * HW + p0 + k) * C + c0 + 8 * cg));
+    const long off = ((long)b * HW + p0 + k) * C + c0 + 8 * cg;
+    if (y32) {  // fp32 NHWC for an F32A next conv
+      *reinterpret_cast<f32x4*>(y32 + off) = f32x4{t[0], t[1], t[2], t[3]};
+      *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{t[4], t[5], t[6], t[7]};
+    } else {
+      damc::store_x3_octet(t, y3 + 3 * off);
+    }
   }
 }
 
@@ -454,9 +469,16 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
 // in_apply_x3_kernel's normalise + LReLU + limb store.  Replaces in_stats + in_merge + in_apply_x3 (one read of the
 // activation instead of two, one launch instead of three).
 template <int NIT>
-__global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restrict__ y, int HW, int C,
+// y32 != NULL: the result leaves as fp32 NHWC at y32 instead of limbs (the next conv stages it as fp32, gemm.hip
+// X3_F32A); y32 may be y itself (every thread writes only the elements it read, after both block sums)
+// slab != NULL: y was not written; the conv's ks split-K slabs (register layout of the 256 x 128 limb tiles, as
+// x3_ksplit_reduce_tile_kernel reads them, sstride4 f32x4 per slab, ntn 128-channel tiles) are summed here in the
+// reduce's order from 0, then the conv bias added: the reduce + epilogue's arithmetic, so the values are bitwise C's
+__global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW, int C,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                          float eps, float slope, unsigned short* __restrict__ y3) {
+                                                          float eps, float slope, unsigned short* __restrict__ y3,
+                                                          float* y32, const float* __restrict__ slab, int ks, int ntn,
+                                                          long sstride4, const float* __restrict__ cbias) {
   __shared__ float red[4][32];
   __shared__ float st[2][32];
   const int b = blockIdx.x, c0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -465,7 +487,25 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restric
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int p = pr + 64 * it;
-    if (p < HW) {
+    if (p < HW && slab) {
+      const long m = (long)b * HW + p;
+      const int n = c0 + 8 * q, rm = (int)(m & 255), rn = n & 127;
+      const long tile = (m >> 8) * ntn + (n >> 7);
+      const int wv = (rm >> 6) * 2 + (rn >> 6), ij = ((rm & 63) >> 4) * 4 + ((rn & 63) >> 4);
+      const long base = ((tile * 8 + wv) * 16 + ij) * 64 + ((rm & 15) >> 2) * 16 + (rn & 15);  // f32x4 of element 0
+      const int r = rm & 3;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
+      for (int sl = 0; sl < ks; ++sl) {
+        const float* src = slab + ((long)sl * sstride4 + base) * 4 + r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] += src[4 * e];
+      }
+      if (cbias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] += cbias[n + e];
+      }
+    } else if (p < HW) {
       const float* src = y + ((long)b * HW + p) * C + c0 + 8 * q;
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(src), a1 = *reinterpret_cast<const f32x4*>(src + 4);
       v[it][0] = a0.x; v[it][1] = a0.y; v[it][2] = a0.z; v[it][3] = a0.w;
@@ -522,7 +562,13 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* __restric
       const float u = fmaf(v[it][e], scl[e], shf[e]);
       o[e] = u > 0.f ? u : u * slope;
     }
-    damc::store_x3_octet(o, y3 + 3 * (((long)b * HW + p) * C + c0 + 8 * q));
+    const long off = ((long)b * HW + p) * C + c0 + 8 * q;
+    if (y32) {
+      *reinterpret_cast<f32x4*>(y32 + off) = f32x4{o[0], o[1], o[2], o[3]};
+      *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    } else {
+      damc::store_x3_octet(o, y3 + 3 * off);
+    }
   }
 }
 
@@ -825,10 +871,13 @@ struct EncShapes {
   int h[DAMC_MAX_ENC_LAYERS + 1], w[DAMC_MAX_ENC_LAYERS + 1];
   size_t act_max = 0, slab_max = 0, in_max = 0;
   size_t a3_max = 0, w3_max = 0, ks_max = 0;  // limb engine: activation limbs, weight limbs, split-K slabs
+  size_t wsrc_off[DAMC_MAX_ENC_LAYERS] = {}, wsrc_bytes = 0;  // the limb operands packed from w_src (workspace)
   bool limb[DAMC_MAX_ENC_LAYERS] = {};
   bool first_fused = false;  // layer 0 as conv3_stats + conv3_apply_x3 (no stored conv output, no NHWC copy)
   int first_rows = 1, first_strips = 1;
 };
+size_t round256(size_t b) { return (b + 255) / 256 * 256; }
+
 bool enc_limb_layer(const damc_encoder_t* e, const damc_enc_layer_t& L) {
   return e->engine == DAMC_ENGINE_LIMB && damc::conv_kmajor_ok(L.cin) && L.cout % 8 == 0 && L.k * L.k <= 32;
 }
@@ -850,11 +899,17 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
     sh->w[i + 1] = wo;
     if (i + 1 < e->n_layers) sh->act_max = std::max(sh->act_max, (size_t)B * ho * wo * L.cout);
     sh->limb[i] = enc_limb_layer(e, L);
-    if (!L.w_packed && !(sh->limb[i] && L.w_x3)) return false;  // the engine's weight operand
+    if (!L.w_packed && !(sh->limb[i] && (L.w_x3 || L.w_src))) return false;  // the engine's weight operand
+    if (L.w_src && (!sh->limb[i] || L.w_x3 || (uintptr_t)L.w_src % 16 != 0)) return false;
     if (sh->limb[i]) {
       const long M = (long)B * ho * wo, K = (long)L.k * L.k * L.cin;
       sh->a3_max = std::max(sh->a3_max, (size_t)B * sh->h[i] * sh->w[i] * L.cin * 6);
-      if (!L.w_x3) sh->w3_max = std::max(sh->w3_max, (size_t)L.cout * K * 6);
+      if (L.w_src) {
+        sh->wsrc_off[i] = sh->wsrc_bytes;
+        sh->wsrc_bytes += round256((size_t)L.cout * K * 6);
+      } else if (!L.w_x3) {
+        sh->w3_max = std::max(sh->w3_max, (size_t)L.cout * K * 6);
+      }
       sh->ks_max = std::max(sh->ks_max, (size_t)damc::x3_ksplit_floats((int)M, L.cout, (int)K, 1));
     } else {
       sh->slab_max = std::max(sh->slab_max,
@@ -879,14 +934,20 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
   }
   return true;
 }
-size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
 // y (B, ho, wo, cout) NHWC = conv(x3 limbs of x) + bias on the limb engine
-int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_enc_layer_t& L, const void* w3, float* y,
-                float* kslab, size_t kslab_floats, hipStream_t s) {
+// af32 != NULL: the input as fp32 NHWC, staged as fp32 and split into limbs in registers (X3_F32A; bitwise the limb
+// input a3 = the RNE limbs of af32)
+int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int win, const damc_enc_layer_t& L,
+                const void* w3, float* y, float* kslab, size_t kslab_floats, int* defer, hipStream_t s) {
   const int hout = (hin + 2 * L.pad - L.k) / L.stride + 1, wout = (win + 2 * L.pad - L.k) / L.stride + 1;
   damc::GemmArgs a;
-  a.A3 = a3;
+  if (af32) {
+    a.A = af32;
+    a.a_f32 = 1;
+  } else {
+    a.A3 = a3;
+  }
   a.Hin = hin;
   a.Win = win;
   a.Cg = L.cin;
@@ -909,6 +970,7 @@ int enc_conv_x3(const unsigned short* a3, int B, int hin, int win, const damc_en
   a.act = DAMC_ACT_NONE;
   a.kslab = kslab;
   a.kslab_floats = (long)kslab_floats;
+  a.ksplit_deferred = defer;
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
                            2.0 * a.M * (double)L.cout * a.K, s);
 }
@@ -931,7 +993,7 @@ extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B)
   if (!enc_shapes(e, B, &sh)) return 0;
   return 2 * round256(sh.act_max * 4) + round256(std::max<size_t>(sh.slab_max, 1) * 4) +
          round256(std::max<size_t>(sh.in_max, 1) * 4) + round256(sh.a3_max) + round256(sh.w3_max) +
-         round256(sh.ks_max * 4);
+         round256(sh.ks_max * 4) + sh.wsrc_bytes + 256;  // + the packing's status word (DAMC_ENC_PACK_CHECK)
 }
 
 extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B, float* xemb, void* wsp, size_t wsb,
@@ -956,9 +1018,48 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   unsigned short* a3 = reinterpret_cast<unsigned short*>(take(sh.a3_max));
   unsigned short* w3 = reinterpret_cast<unsigned short*>(take(sh.w3_max));
   float* kslab = reinterpret_cast<float*>(take(sh.ks_max * 4));
+  char* wsrc = sh.wsrc_bytes ? take(sh.wsrc_bytes) : nullptr;
+  int* pack_err = reinterpret_cast<int*>(take(256));
   hipStream_t s = as_stream(stream);
   int rc;
+  // DAMC_ENC_PACK_CHECK=1 (read per call; tests, never timed work): the packing workgroups report any workgroup outside
+  // their list in a status word the call zeroes first and reads back at its end (one host sync), returning
+  // DAMC_ERR_UNSUPPORTED if it was set
+  const char* pc = getenv("DAMC_ENC_PACK_CHECK");
+  const bool pack_check = pc && pc[0] == '1';
+  if (pack_check && (rc = (int)hipMemsetAsync(pack_err, 0, sizeof(int), s))) return rc;
+  // the w_src layers' limb operands, all in one launch: as extra workgroups of the one-pass first layer when it runs
+  // (conv3_in_fused_kernel), else on their own before it
+  damc::PackConvList pl{};
+  if (wsrc) {
+    for (int i = 0; i < n; ++i) {
+      const damc_enc_layer_t& L = e->layers[i];
+      if (!L.w_src) continue;
+      unsigned short* y = reinterpret_cast<unsigned short*>(wsrc + sh.wsrc_off[i]);
+      if (pl.n < 8 && damc::pack_conv_x3_many_ok(L.w_src, L.cin, L.k)) {
+        pl.w[pl.n] = L.w_src;
+        pl.y[pl.n] = y;
+        pl.cin[pl.n] = L.cin;
+        pl.taps[pl.n] = L.k * L.k;
+        pl.blk0[++pl.n] = L.cout;
+      } else if ((rc = damc::launch_pack_conv_x3(L.w_src, L.cout, L.cin, L.k, y, s))) {
+        return rc;
+      }
+    }
+    if (pl.n && damc::pack_conv_x3_many_prep(pl)) return DAMC_ERR_UNSUPPORTED;
+    pl.err = pack_check ? pack_err : nullptr;
+  }
+  bool pl_done = pl.n == 0;
   bool a3_ready = false;  // a3 holds the limbs of the current layer's input (written by the previous layer's norm)
+  bool in32 = false;      // or the previous layer's norm left it as fp32 NHWC in buf[i & 1] for an F32A conv
+  // the k4 s2 p1 limb convs stage their input as fp32 (X3_F32A) where the norm before them can write fp32 (the
+  // one-pass kernels); DAMC_ENC_F32A=0 (read per call): limbs throughout
+  const char* fe = getenv("DAMC_ENC_F32A");
+  const bool f32a_on = !(fe && fe[0] == '0');
+  auto f32a_layer = [&](int i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    return f32a_on && i < n && sh.limb[i] && L.k == 4 && L.stride == 2 && L.pad == 1;
+  };
   int i0 = 0;
   if (sh.first_fused) {  // layer 0: conv3 + InstanceNorm + LeakyReLU straight to layer 1's limbs
     const damc_enc_layer_t& L = e->layers[0];
@@ -973,10 +1074,18 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     const size_t sm1 = ((size_t)(H + 2) * (W + 2) * L.cin + (size_t)9 * L.cin * 16 + 8 * 8 + 32) * sizeof(float);
     // (a sample of at most 1024 pixels; CelebA-64 and larger keep the two passes)
     const bool one = !(op && op[0] == '0') && H * W <= 1024 && W % 4 == 0 && C % 16 == 0 && sm1 <= 65536;
+    if (!one && !pl_done) {
+      if ((rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
+      pl_done = true;
+    }
+    const int nconv = B * (C / 16), npk = pl_done ? 0 : pl.blk0[pl.n];
+    float* y32 = (one && f32a_layer(1)) ? buf[1] : nullptr;
+    const size_t smp = std::max(sm1, pl_done ? (size_t)0 : (size_t)pl.lds);
 #define DAMC_C1(CIN_)                                                                                               \
   if (one && L.cin == CIN_) {                                                                                       \
-    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(B, C / 16), dim3(512), sm1, s, x, H, W, C, L.w_packed,     \
-                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3);                                       \
+    hipLaunchKernelGGL((conv3_in_fused_kernel<CIN_>), dim3(nconv + npk), dim3(512), smp, s, x, H, W, C, L.w_packed,  \
+                       L.bias, L.in_gamma, L.in_beta, L.in_eps, L.slope, a3, y32, nconv, pl);                       \
+    pl_done = true;                                                                                                 \
   }
     DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
 #undef DAMC_C1
@@ -992,26 +1101,36 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     DAMC_C3(1) DAMC_C3(3) DAMC_C3(4)
 #undef DAMC_C3
     DAMC_LAUNCH_CHECK();
-    a3_ready = true;
+    in32 = y32 != nullptr;
+    a3_ready = !in32;
     i0 = 1;
   } else if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, buf[0], stream))) {
     return rc;
   }
+  if (!pl_done && (rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
+  const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel norm below
+  const char* isl = getenv("DAMC_ENC_IN_SLABS");   // (read per call) 0: the split-K reduce kernel writes C first
   for (int i = i0; i < n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
+    const int hw = sh.h[i + 1] * sh.w[i + 1];
+    // the norm after this conv is the one-pass kernel; it then also sums the conv's split-K slabs itself
+    const bool in1 = L.in_gamma && i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0');
+    int ks_def = 0;
     if (sh.limb[i]) {
-      if (!a3_ready) {
+      if (!a3_ready && !in32) {
         const long na = (long)B * sh.h[i] * sh.w[i] * L.cin;
         if ((rc = damc::launch_split_x3(buf[i & 1], na, a3, s))) return rc;
       }
-      const void* wl = L.w_x3;
+      const void* wl = L.w_x3 ? L.w_x3 : L.w_src ? static_cast<const void*>(wsrc + sh.wsrc_off[i]) : nullptr;
       if (!wl) {  // the limb copy from the fp32 packing
         const int K = L.k * L.k * L.cin;
         if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;
         wl = w3;
       }
-      if ((rc = enc_conv_x3(a3, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max, s))) return rc;
+      if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max,
+                            (in1 && !(isl && isl[0] == '0')) ? &ks_def : nullptr, s)))
+        return rc;
     } else {
       const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
       if ((rc = damc_conv2d_nhwc(buf[i & 1], B, sh.h[i], sh.w[i], L.cin, L.w_packed, L.bias, L.cout, L.k, L.stride,
@@ -1019,23 +1138,27 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         return rc;
     }
     a3_ready = false;
+    in32 = false;
     if (!L.in_gamma) continue;
-    const int hw = sh.h[i + 1] * sh.w[i + 1];
-    const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel form below
-    if (i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0')) {
+    if (in1) {
       ProfScope ps("instnorm", 0.0, s);
       const dim3 g(B, L.cout / 32);
+      float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
+      const int ntn = (L.cout + 127) / 128;
+      const long sstride4 = (long)((B * hw + 255) / 256) * ntn * (256 * 128 / 4);
+      const float* sl = ks_def > 0 ? kslab : nullptr;
       if (hw <= 64)
         hipLaunchKernelGGL(in_fused_x3_kernel<1>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       else if (hw <= 128)
         hipLaunchKernelGGL(in_fused_x3_kernel<2>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       else
         hipLaunchKernelGGL(in_fused_x3_kernel<4>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
       DAMC_LAUNCH_CHECK();
-      a3_ready = true;
+      in32 = y32 != nullptr;
+      a3_ready = !in32;
     } else if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
       const int S = in_splits(hw), cg = (L.cout + 63) / 64;
       float* ssb = inws + (size_t)B * L.cout * S * 3;
@@ -1052,6 +1175,12 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
                                               stream))) {
       return rc;
     }
+  }
+  if (pack_check) {
+    int flag = 0;
+    if ((rc = (int)hipMemcpyAsync(&flag, pack_err, sizeof(int), hipMemcpyDeviceToHost, s))) return rc;
+    if ((rc = (int)hipStreamSynchronize(s))) return rc;
+    if (flag) return DAMC_ERR_UNSUPPORTED;
   }
   return 0;
 }

@@ -84,6 +84,11 @@ struct GemmArgs {
   // limb engine: the A operand is the fp32 tensor A (NHWC), staged as fp32 and split into limbs in registers
   // (gemm_x3_kernel variant X3_F32A: 4 B per gathered element instead of 6 B of limbs); A3 unused
   int a_f32 = 0;
+  // host pointer (EPI_BIAS_ACT, O_DENSE, no C3 / sgn): when set and the launch splits K into register-layout slabs
+  // (kslab_reg), the reduce is skipped and the slab count is written here for a consumer that sums the slabs itself
+  // (the encoder's InstanceNorm; slab layout: gemm.hip x3_ksplit_reduce_tile_kernel); 0 = the launcher reduced or did
+  // not split, C holds the result
+  int* ksplit_deferred = nullptr;
   // clock probe (damc_clock_probe; diagnostics, off in timed work): thread 0 of each workgroup stores {s_memtime,
   // s_memrealtime} before its K loop and after it, at clk[4 * (workgroup % clk_n)]
   unsigned long long* clk = nullptr;
@@ -164,6 +169,24 @@ int launch_pack_proj_tiled(const float* w, int cin, int cout, int kk, float* wf,
 // a PyTorch Conv2d weight (cout, cin, k, k), cin % 8 == 0, straight to the limb B operand of the conv (the order
 // launch_split_x3_conv gives damc_pack_conv2d's K-major packing)
 int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s);
+// several Conv2d weights (PyTorch layout) to their limb B operands in one launch (the LDS-transposing kernel):
+// n <= 8 layers, each cin % 128 == 0 or cin == 64, k * k <= 32, w 16-B aligned; returns 1 (nothing launched) otherwise
+struct PackConvList {
+  int n;
+  const float* w[8];
+  unsigned short* y[8];
+  int cin[8], taps[8], cc[8], blk0[9];
+  int ready;   // set by pack_conv_x3_many_prep (blk0 then holds workgroup offsets, not couts)
+  int lds;     // dynamic LDS bytes per workgroup (prep)
+  int cout[8];  // (prep) each layer's output channels: the device-side bound of a workgroup's weight rows
+  int* err;     // optional device status word: a workgroup outside the list ORs 1 into it and writes nothing
+};
+bool pack_conv_x3_many_ok(const float* w, int cin, int k);
+// fills in cc and lds and turns blk0[i + 1] (layer i's cout on entry) into running workgroup offsets, once (ready);
+// nonzero when a layer is not covered or l was already prepared
+int pack_conv_x3_many_prep(PackConvList& l);
+// launches a list (prepared here unless ready)
+int launch_pack_conv_x3_many(PackConvList l, hipStream_t s);
 
 // the limb form of 8 consecutive fp32 values (the engine's RNE split: v = hi + mid + lo to 24 significand bits),
 // stored as one x3 octet [3][8] bf16 at dst (16-B aligned)
@@ -183,6 +206,47 @@ __device__ __forceinline__ void store_x3_octet(const float (&v)[8], unsigned sho
   o[0] = h;
   o[1] = m;
   o[2] = l;
+}
+
+// one workgroup (nthr threads, pk_t = CC * (taps + 1) floats of LDS) of the LDS-transposing conv weight packing
+// (gemm.hip pack_conv_x3_lds_kernel; also run by the encoder's first-layer kernel as extra workgroups): workgroup blk
+// of a prepared list = (layer, co, chunk of CC input channels).  The chunk's CC * k * k floats are one contiguous run
+// of the PyTorch layout (read as f32x4), transposed in LDS to (tap, channel); each tap's CC / 8 limb octets are
+// CC * 6 contiguous bytes of the K-major output, odd sign blocks negated
+__device__ __forceinline__ void pack_conv_x3_block(const PackConvList& l, int blk, int tid, int nthr, float* pk_t) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  // bound (workgroup-uniform, before any access): the workgroup must name a weight row of the prepared list; one that
+  // does not (a grid larger than the list) writes nothing and flags the status word
+  const bool in_list = l.ready && l.n >= 1 && l.n <= 8 && blk >= 0 && blk < l.blk0[l.n];
+  int li = 0;
+  while (in_list && li + 1 < l.n && blk >= l.blk0[li + 1]) ++li;
+  blk -= l.blk0[li];
+  const int CC = l.cc[li], cin = l.cin[li], taps = l.taps[li], nch = CC > 0 ? cin / CC : 0;
+  const int co = nch > 0 ? blk / nch : 0, cc0 = (blk - co * nch) * CC, tp1 = taps + 1, n4 = CC * taps / 4;
+  if (!in_list || nch <= 0 || co >= l.cout[li] || cc0 + CC > cin) {
+    if (tid == 0 && l.err) atomicOr(l.err, 1);
+    return;
+  }
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(l.w[li] + ((long)co * cin + cc0) * taps);
+  for (int q = tid; q < n4; q += nthr) {
+    const f32x4_t v = src[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * q + e, ci = f / taps;
+      pk_t[ci * tp1 + (f - ci * taps)] = v[e];
+    }
+  }
+  __syncthreads();
+  const int oc = CC / 8, cin8 = cin / 8;
+  unsigned short* o = l.y[li] + 24L * ((long)co * taps * cin8 + cc0 / 8);
+  for (int q = tid; q < taps * oc; q += nthr) {
+    const int tap = q / oc, c8 = q - tap * oc;
+    const float sg = (((tap * cin + cc0 + c8 * 8) / X3_NEGK) & 1) ? -1.f : 1.f;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = sg * pk_t[(c8 * 8 + e) * tp1 + tap];
+    store_x3_octet(v, o + 24L * ((long)tap * cin8 + c8));
+  }
 }
 
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices

@@ -2575,6 +2575,10 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
         hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0, s, a);
       }
       if (a.kslab_reg) {  // one wave per 16x16 tile, four per workgroup
+        if (EPI == EPI_BIAS_ACT && OM == O_DENSE && a.ksplit_deferred && !a.C3 && !a.sgn) {
+          *a.ksplit_deferred = ks;  // the consumer sums the slabs (GemmArgs::ksplit_deferred)
+          return 0;
+        }
         // a ConvT forward with the fused output-layer projection: the reduce runs the projection too (bitwise the
         // reduce + proj_rows_kernel); DAMC_REDUCE_PROJ=0 (read per call) keeps the two kernels
         const char* erp = getenv("DAMC_REDUCE_PROJ");
@@ -2844,40 +2848,46 @@ __global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, 
   }
 }
 
-// the same packing through LDS, one workgroup per (co, chunk of CC input channels): the chunk's CC * k * k floats are
-// one contiguous run of the PyTorch layout (read as f32x4, every lane a different 16 B), transposed in LDS to
-// (tap, channel), and each tap's CC / 8 limb octets are CC * 6 contiguous bytes of the output; every byte is read and
-// written once, in full lines (the tap-group kernel above reads each 64-B line from 4 waves far apart)
-template <int CC>
-__global__ __launch_bounds__(256) void pack_conv_x3_lds_kernel(const float* __restrict__ w, int cin, int taps,
-                                                               unsigned short* __restrict__ y) {
+// the same packing through LDS, one workgroup per (layer, co, chunk of CC input channels) (pack_conv_x3_block, gemm.h):
+// every byte is read and written once, in full lines (the tap-group kernel below reads each 64-B line from 4 waves
+// far apart).  Several layers share one launch (the encoder's per-call packing: one dispatch instead of one per layer)
+__global__ __launch_bounds__(256) void pack_conv_x3_lds_kernel(PackConvList l) {
   extern __shared__ float pk_t[];  // [CC][taps + 1]
-  const int co = blockIdx.y, cc0 = blockIdx.x * CC, tp1 = taps + 1, n4 = CC * taps / 4;
-  const f32x4* src = reinterpret_cast<const f32x4*>(w + ((long)co * cin + cc0) * taps);
-  for (int q = threadIdx.x; q < n4; q += 256) {
-    const f32x4 v = src[q];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int f = 4 * q + e, ci = f / taps;
-      pk_t[ci * tp1 + (f - ci * taps)] = v[e];
-    }
+  pack_conv_x3_block(l, blockIdx.x, threadIdx.x, 256, pk_t);
+}
+
+bool pack_conv_x3_many_ok(const float* w, int cin, int k) {
+  return (DAMC_X3_VARIANT & 8) == 0 && k > 0 && k * k <= 32 && (uintptr_t)w % 16 == 0 && (cin % 128 == 0 || cin == 64);
+}
+
+int pack_conv_x3_many_prep(PackConvList& l) {
+  if (l.ready || l.n < 1 || l.n > 8) return 1;
+  size_t sm = 0;
+  l.blk0[0] = 0;
+  for (int i = 0; i < l.n; ++i) {
+    if (l.taps[i] <= 0 || l.taps[i] > 32 || (uintptr_t)l.w[i] % 16 || (uintptr_t)l.y[i] % 16 ||
+        !(l.cin[i] % 128 == 0 || l.cin[i] == 64) || l.blk0[i + 1] <= 0)
+      return 1;
+    l.cc[i] = l.cin[i] % 128 == 0 ? 128 : 64;
+    sm = std::max(sm, (size_t)l.cc[i] * (l.taps[i] + 1) * sizeof(float));
   }
-  __syncthreads();
-  const int oc = CC / 8, cin8 = cin / 8;
-  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3L * ((long)co * taps * cin8 + cc0 / 8);
-  for (int q = threadIdx.x; q < taps * oc; q += 256) {
-    const int tap = q / oc, c8 = q - tap * oc;
-    const float sg = (((tap * cin + cc0 + c8 * 8) / X3_NEGK) & 1) ? -1.f : 1.f;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = sg * pk_t[(c8 * 8 + e) * tp1 + tap];
-    bf16x8 h, m, l;
-    split3_octet(v, h, m, l);
-    bf16x8* d = o + 3L * ((long)tap * cin8 + c8);
-    d[0] = h;
-    d[1] = m;
-    d[2] = l;
+  for (int i = 0; i < l.n; ++i) {
+    l.cout[i] = l.blk0[i + 1];
+    l.blk0[i + 1] = l.blk0[i] + l.blk0[i + 1] * (l.cin[i] / l.cc[i]);
   }
+  // the grid is exactly the work list: one workgroup per (layer, co, channel chunk), nothing more
+  long total = 0;
+  for (int i = 0; i < l.n; ++i) total += (long)l.cout[i] * (l.cin[i] / l.cc[i]);
+  if (total != l.blk0[l.n]) return 1;
+  l.lds = (int)sm;
+  l.ready = 1;
+  return 0;
+}
+
+int launch_pack_conv_x3_many(PackConvList l, hipStream_t s) {
+  if (!l.ready && pack_conv_x3_many_prep(l)) return 1;
+  hipLaunchKernelGGL(pack_conv_x3_lds_kernel, dim3((unsigned)l.blk0[l.n]), dim3(256), (size_t)l.lds, s, l);
+  return (int)hipGetLastError();
 }
 
 int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short* y, hipStream_t s) {
@@ -2888,15 +2898,15 @@ int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short
     return !(e && e[0] == '0');
   }();
   const int taps = k * k;
-  if (lds && taps <= 32 && cout <= 65535 && (uintptr_t)w % 16 == 0 && (cin % 128 == 0 || cin == 64)) {
-    if (cin % 128 == 0) {
-      const size_t sm = (size_t)128 * (taps + 1) * sizeof(float);
-      hipLaunchKernelGGL(pack_conv_x3_lds_kernel<128>, dim3(cin / 128, cout), dim3(256), sm, s, w, cin, taps, y);
-    } else {
-      const size_t sm = (size_t)64 * (taps + 1) * sizeof(float);
-      hipLaunchKernelGGL(pack_conv_x3_lds_kernel<64>, dim3(1, cout), dim3(256), sm, s, w, cin, taps, y);
-    }
-    return (int)hipGetLastError();
+  if (lds && pack_conv_x3_many_ok(w, cin, k)) {
+    PackConvList l{};
+    l.n = 1;
+    l.w[0] = w;
+    l.y[0] = y;
+    l.cin[0] = cin;
+    l.taps[0] = taps;
+    l.blk0[1] = cout;
+    return launch_pack_conv_x3_many(l, s);
   }
   if ((k * k) % 4 == 0 && (uintptr_t)w % 16 == 0) {
     const long nt = (long)cout * (k * k / 4) * (cin / 8);
@@ -2971,9 +2981,11 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
   const long per = (lim / 6 - 1) / img;
   if (per < 1) return DAMC_ERR_UNSUPPORTED;
   const long cimg = (om == O_PHASE) ? (long)a.Hout * a.Wout * a.ldc : hwq * a.ldc;
+  if (a.ksplit_deferred) *a.ksplit_deferred = 0;
   for (long b0 = 0; b0 < nimg; b0 += per) {
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
+    if (nimg > per) c.ksplit_deferred = nullptr;  // one launch's slabs only
     if (om == O_PHASE && g_clk) {
       c.clk = g_clk;
       c.clk_n = g_clk_n;

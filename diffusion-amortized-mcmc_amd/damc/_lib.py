@@ -90,7 +90,7 @@ class EncLayer(ctypes.Structure):  # damc_enc_layer_t
     _fields_ = [("cin", ctypes.c_int), ("cout", ctypes.c_int), ("k", ctypes.c_int), ("stride", ctypes.c_int),
                 ("pad", ctypes.c_int), ("w_packed", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("in_gamma", ctypes.c_void_p), ("in_beta", ctypes.c_void_p), ("in_eps", ctypes.c_float),
-                ("slope", ctypes.c_float), ("w_x3", ctypes.c_void_p)]
+                ("slope", ctypes.c_float), ("w_x3", ctypes.c_void_p), ("w_src", ctypes.c_void_p)]
 
 
 class Encoder(ctypes.Structure):  # damc_encoder_t

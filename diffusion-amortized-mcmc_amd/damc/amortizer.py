@@ -12,6 +12,7 @@ call on the host in fp32 with the reference's own op sequence and handed to the 
 """
 import ctypes
 import math
+import os
 import weakref
 
 import torch
@@ -113,11 +114,17 @@ class EncoderPlan:
         """The conv's weight operand, repacked per call from the live parameter: the nets train between calls,
         and the reference updates its EMA target Q_dummy through param.data.copy_ (train_gen_recon.py:258-261),
         which leaves the parameter's version counter unchanged, so no version-keyed cache could see it.  A layer on
-        the limb engine is one pass from the PyTorch layout straight to limbs (damc_pack_conv2d_x3); the first 3x3
-        conv keeps the fp32 packing.  Buffers are reused across calls."""
+        the limb engine hands the library its PyTorch weight (w_src): damc_q_encoder_fwd packs all of them as extra
+        workgroups of the first conv's launch (DAMC_ENC_WSRC=0: one damc_pack_conv2d_x3 launch per layer, before the
+        call); the first 3x3 conv keeps the fp32 packing.  Buffers are reused across
+        calls.  Returns (w_packed, w_x3, w_src, keep-alive)."""
         k, cout, cin = conv.kernel_size[0], conv.out_channels, conv.in_channels
         w = _dev(conv.weight, dev)
         nb = int(L.damc_conv2d_x3_bytes(cout, cin, k)) if _lib.current_engine() == _lib.ENGINE_LIMB else 0
+        if nb and os.environ.get("DAMC_ENC_WSRC", "1") != "0":
+            w = w.contiguous()
+            if w.data_ptr() % 16 == 0:
+                return None, None, w, w
         # one buffer per (layer, thread, stream), like the workspace: a call on another stream or thread may still
         # be reading this one's packed weights (ADVICE r3)
         cache = self._wcache.get(i)
@@ -126,10 +133,10 @@ class EncoderPlan:
         buf = cache.get(dev, nb if nb else 4 * k * k * cin * cout, ("encw", i, nb))
         if nb:
             check(L.damc_pack_conv2d_x3(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d x3")
-            return None, buf, w
+            return None, buf, None, w
         buf = buf[:4 * k * k * cin * cout].view(torch.float32)
         check(L.damc_pack_conv2d(ptr(w), cout, cin, k, ptr(buf), stream), "pack conv2d")
-        return buf, None, w
+        return buf, None, None, w
 
     def forward(self, x):
         """The whole encoder in one damc_q_encoder_fwd call (weights re-packed per call into reused buffers)."""
@@ -146,11 +153,11 @@ class EncoderPlan:
         for i, (conv, norm, slope) in enumerate(self.stages):
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             cout, cin = conv.out_channels, conv.in_channels
-            wp, w3, w = self._packed(i, conv, dev, L, stream)
+            wp, w3, wsrc, w = self._packed(i, conv, dev, L, stream)
             bias = _dev(conv.bias, dev) if conv.bias is not None else None
             e = d.layers[i]
             e.cin, e.cout, e.k, e.stride, e.pad = cin, cout, k, s, p
-            e.w_packed, e.bias, e.w_x3 = ptr(wp), ptr(bias), ptr(w3)
+            e.w_packed, e.bias, e.w_x3, e.w_src = ptr(wp), ptr(bias), ptr(w3), ptr(wsrc)
             keep += [bias, w]
             if norm is not None:
                 g, b = _dev(norm.weight, dev), _dev(norm.bias, dev)

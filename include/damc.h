@@ -229,7 +229,8 @@ int damc_nchw_to_nhwc(const float* x, int batch, int c, int hw, float* y, void* 
  * engine DAMC_ENGINE_LIMB: the convolutions whose input channel count is a multiple of 32 (every one but the
  * first 3x3 at the reference's nif) run on the limb engine (fp32-accurate, bf16 MFMA; see DAMC_ENGINE_*), the
  * input activation split into limbs per call; w_x3 = damc_pack_conv2d_x3 of the layer's weight (then w_packed
- * may be NULL for that layer), or NULL (the library splits w_packed into the workspace per call). */
+ * may be NULL for that layer), or w_src = the weight itself (packed by the library per call, see below), or neither
+ * (the library splits w_packed into the workspace per call). */
 #define DAMC_MAX_ENC_LAYERS 8
 typedef struct {
   int cin, cout, k, stride, pad;
@@ -238,6 +239,9 @@ typedef struct {
   const float *in_gamma, *in_beta; /* InstanceNorm2d affine (cout); NULL: no norm / activation after it */
   float in_eps, slope;
   const void* w_x3;               /* the limb B operand (damc_pack_conv2d_x3) or NULL                 */
+  const float* w_src;             /* or the PyTorch Conv2d weight (cout, cin, k, k) of a limb layer, 16-B aligned:
+                                     the library packs every such layer into the workspace per call, as extra
+                                     workgroups of the first layer's launch (w_x3 and w_packed then unused)   */
 } damc_enc_layer_t;
 typedef struct {
   int n_layers, nc, h, w;

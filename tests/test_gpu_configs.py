@@ -268,10 +268,14 @@ def test_celebaHQ_b64_likelihood_gradient_vs_fp64(gpu_device):
 
 
 @pytest.mark.parametrize("name,B", [("celeba64", 32), ("celebaHQ", 8)])
-def test_full_width_encoder_vs_fp64(gpu_device, name, B):
+def test_full_width_encoder_vs_fp64(gpu_device, monkeypatch, name, B):
     from damc import amortizer, synth
     from oracle import damc_oracle as orc
     from src import diffusion_net as dn
+
+    # the library's weight packing (w_src, extra workgroups of the first layer's launch on CelebA-64's two-pass path)
+    # reports any workgroup outside its list; the call then fails instead of returning xemb
+    monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
 
     hw = GEN[name][3]
     enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
@@ -301,6 +305,57 @@ def test_encoder_limb_engine_vs_fp32_engine_b128(gpu_device):
         e64 = orc.encoder_forward(enc.double(), x.cpu().double()).numpy()
     _check("Encoder_cifar10 nif=64 B=128 xemb, limb engine", got, e32, e64, 1e-7)
     _check("Encoder_cifar10 nif=64 B=128 xemb, fp32 engine", got32, e32, e64, 1e-7)
+
+
+@pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32), ("cifar10", 16)])
+def test_encoder_f32a_convs_are_bitwise(gpu_device, monkeypatch, name, B):
+    """The encoder's k4 s2 limb convs staging their input as fp32 (gemm.hip X3_F32A, the one-pass norms writing fp32
+    in place) against the limb inputs (DAMC_ENC_F32A=0), and the one-pass norms summing the convs' split-K slabs
+    themselves (GemmArgs::ksplit_deferred) against the reduce kernel (DAMC_ENC_IN_SLABS=0): the in-register split is
+    the producing epilogue's RNE split and the slab sum the reduce's order, so xemb is bitwise the same."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    hw = GEN[name][3]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 3, (B, 3, hw, hw))).to(gpu_device)
+    outs = {}
+    for f32a in "10":
+        for slabs in "10":  # DAMC_ENC_IN_SLABS: the one-pass norm sums the convs' split-K slabs itself
+            monkeypatch.setenv("DAMC_ENC_F32A", f32a)
+            monkeypatch.setenv("DAMC_ENC_IN_SLABS", slabs)
+            outs[f32a + slabs] = amortizer.encoder_forward(enc, x).cpu()
+    for k, v in outs.items():
+        assert torch.equal(v, outs["00"]), k
+
+
+@pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
+def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
+    """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch (extra workgroups of the
+    first layer's launch, or a launch of its own before a two-pass first layer), under the packing's status word.  Bitwise the per-layer damc_pack_conv2d_x3 operands (DAMC_ENC_WSRC=0), and a weight
+    rewritten in place through .data between calls (the reference's EMA update, train_gen_recon.py:258-261) is seen
+    by the next call."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    hw = GEN[name][3]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 2, (B, 3, hw, hw))).to(gpu_device)
+    monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
+    monkeypatch.setenv("DAMC_ENC_WSRC", "1")
+    a = amortizer.encoder_forward(enc, x).cpu()
+    monkeypatch.setenv("DAMC_ENC_WSRC", "0")
+    b = amortizer.encoder_forward(enc, x).cpu()
+    assert torch.equal(a, b)
+    with torch.no_grad():
+        for m in enc.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.data.copy_(m.weight.data * 0.75)
+    b2 = amortizer.encoder_forward(enc, x).cpu()
+    monkeypatch.setenv("DAMC_ENC_WSRC", "1")
+    a2 = amortizer.encoder_forward(enc, x).cpu()
+    assert torch.equal(a2, b2)
+    assert not torch.equal(a2, a)
 
 
 def test_celebaHQ_q_sweep_vs_fp64(gpu_device):
