@@ -299,6 +299,14 @@ __global__ void slab_bias_sum_kernel(const float* __restrict__ slabs, int S, int
 constexpr int kMaxSplit = 16;
 int gemm(const float* A, long lda, const float* Bm, long ldb, const float* bias, float* C, long ldc, int M, int N,
          int K, const char* name, hipStream_t s, float* slab = nullptr) {
+  // round 5: every product of this net is small (M = B rows or K = B): one launch of the 16 x 16-per-wave kernel
+  // instead of the tiled engine's 1-16 workgroups or its split-K slabs plus a reduce; DAMC_DN_SMALL_GEMM=0 (read per
+  // call) keeps the tiled engine
+  const char* esg = getenv("DAMC_DN_SMALL_GEMM");
+  if (!(esg && esg[0] == '0')) {
+    const int rc = launch_small_gemm(A, lda, Bm, ldb, bias, C, ldc, M, N, K, s);
+    if (rc != DAMC_ERR_UNSUPPORTED) return rc;
+  }
   GemmArgs a;
   a.A = A;
   a.lda = lda;

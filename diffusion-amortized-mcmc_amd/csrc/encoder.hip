@@ -988,6 +988,47 @@ extern "C" int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, voi
   return damc::launch_pack_conv_x3(w, cout, cin, k, static_cast<unsigned short*>(w_x3), as_stream(stream));
 }
 
+// one Conv2d + bias on the limb engine for the Q update's encoder forward (the training path keeps every conv output,
+// so it runs the convs one by one): k4 s2 p1 layers stage their fp32 NHWC input directly (X3_F32A), other shapes split
+// it into limbs in the workspace first; split-K slabs in the workspace where the output tiles would not fill the chip
+extern "C" size_t damc_conv2d_x3_workspace_bytes(int B, int hin, int win, int cin, int cout, int k, int stride,
+                                                 int pad) {
+  if (B <= 0 || hin <= 0 || win <= 0 || stride <= 0 || pad < 0 || !damc_conv2d_x3_bytes(cout, cin, k)) return 0;
+  const int hout = (hin + 2 * pad - k) / stride + 1, wout = (win + 2 * pad - k) / stride + 1;
+  if (hout <= 0 || wout <= 0) return 0;
+  const bool f32a = k == 4 && stride == 2 && pad == 1;
+  const size_t a3 = f32a ? 0 : round256((size_t)B * hin * win * cin * 6);
+  return a3 + round256((size_t)std::max<long>(damc::x3_ksplit_floats(B * hout * wout, cout, k * k * cin, 1), 1) * 4);
+}
+
+extern "C" int damc_conv2d_x3_nhwc(const float* x, int B, int hin, int win, int cin, const void* w_x3,
+                                   const float* bias, int cout, int k, int stride, int pad, float* y, void* wsp,
+                                   size_t wsb, void* stream) {
+  const size_t need = damc_conv2d_x3_workspace_bytes(B, hin, win, cin, cout, k, stride, pad);
+  if (!x || !w_x3 || !y || !need) return DAMC_ERR_ARG;
+  if (!wsp || wsb < need) return DAMC_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  damc_enc_layer_t L{};
+  L.cin = cin;
+  L.cout = cout;
+  L.k = k;
+  L.stride = stride;
+  L.pad = pad;
+  L.bias = bias;
+  const bool f32a = k == 4 && stride == 2 && pad == 1;
+  char* base = static_cast<char*>(wsp);
+  unsigned short* a3 = nullptr;
+  size_t off = 0;
+  if (!f32a) {
+    a3 = reinterpret_cast<unsigned short*>(base);
+    off = round256((size_t)B * hin * win * cin * 6);
+    const int rc = damc::launch_split_x3(x, (long)B * hin * win * cin, a3, s);
+    if (rc) return rc;
+  }
+  return enc_conv_x3(a3, f32a ? x : nullptr, B, hin, win, L, w_x3, y, reinterpret_cast<float*>(base + off),
+                     (wsb - off) / 4, nullptr, s);
+}
+
 extern "C" size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* e, int B) {
   EncShapes sh;
   if (!enc_shapes(e, B, &sh)) return 0;

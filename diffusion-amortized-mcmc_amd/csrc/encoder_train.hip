@@ -354,7 +354,11 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     a.N = KK;
     a.K = B;
     a.k_per_z = B;
-    if ((rc = launch_gemm(a, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_wgrad", 2.0 * cout * KK * B, s))) return rc;
+    // the small-GEMM kernel (one 16 x 16 tile per wave: 32K waves here instead of the tiled engine's 512 workgroups
+    // with K = B = 128 each), the tiled engine where it does not apply
+    rc = launch_small_gemm(a.A, a.lda, a.B, a.ldb, nullptr, a.C, a.ldc, a.M, a.N, a.K, s);
+    if (rc == DAMC_ERR_UNSUPPORTED) rc = launch_gemm(a, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_wgrad", 2.0 * cout * KK * B, s);
+    if (rc) return rc;
     const long n = (long)cout * KK;
     hipLaunchKernelGGL(permute_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)t.g,
                        cout, cin, k, dw);
@@ -372,7 +376,9 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
       d.N = KK;
       d.K = cout;
       d.k_per_z = cout;
-      if ((rc = launch_gemm(d, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_dgrad", 2.0 * B * KK * cout, s))) return rc;
+      rc = launch_small_gemm(d.A, d.lda, d.B, d.ldb, nullptr, d.C, d.ldc, d.M, d.N, d.K, s);
+      if (rc == DAMC_ERR_UNSUPPORTED) rc = launch_gemm(d, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_dgrad", 2.0 * B * KK * cout, s);
+      if (rc) return rc;
     }
     return (int)hipGetLastError();
   }

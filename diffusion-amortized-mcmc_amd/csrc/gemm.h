@@ -117,20 +117,32 @@ struct GemmArgs {
   int kslab_reg = 0;
 };
 // k per sign block of a limb-engine conv weight (GemmArgs::negk), from the conv's shape alone (never the batch, so a
-// batch split over ranks runs the blocks, slabs and sums of the whole batch): 1024 where, at the headline's 8-way
-// per-rank batch of 16 samples, 512-k blocks would leave >= 512 split-K slices of the 256 x 128 tiles (two blocks per
-// workgroup), so the 1024-k block halves the slabs and still fills the chip (CIFAR-10 ngf=128 B=16 step 0.487 ->
-// 0.452 ms, CelebA-HQ B=8 1.244 -> 1.229 ms); 512 elsewhere, where the finer split is what fills the chip (SVHN B=64
-// 0.279 ms at 512 vs 0.374 at 1024, CelebA-64 B=32 0.421 vs 0.525; profiles/r05/negk_ab.txt).  Both lengths keep
-// the limb engine's error below the fp32-MFMA engine's.  DAMC_X3_NEGK_RULE=512 / 1024 (read per
-// call; the packing and the launches of one call read it alike) pins it for A/B.
+// batch split over ranks runs the blocks, slabs and sums of the whole batch).  W16 = (256 x 128 output tiles of the
+// GEMM at 16 samples) x K measures how finely a 16-sample batch must split K to fill the chip:
+//   W16 >= 2^18: 1024 (512-k blocks would already leave two per workgroup, so the 1024-k block halves the slabs and
+//                still fills the chip: every UP2 GEMM of CIFAR-10 ngf=128 and CelebA-HQ);
+//   W16 >= 2^16: 512 (CelebA-64 ngf=128);
+//   below:       256 (SVHN ngf=64: its per-config batch of 64 fills the chip only with 256-k slices).
+// Measured (profiles/r05/negk_ab.txt, posterior step ms, 1024 / 512 / 256 where run): CIFAR B=16 0.452 / 0.487 /
+// 0.539, CelebA-HQ B=8 1.229 / 1.244 / 1.39, CelebA-64 B=32 0.525 / 0.421 / 0.476, B=256 - / 2.06 / 2.19, SVHN B=64
+// 0.374 / 0.279 / 0.248.  Every length keeps the limb engine's error at or below the fp32-MFMA engine's (DESIGN.md
+// section 4).  DAMC_X3_NEGK_RULE=256 / 512 / 1024 (read per call; the packing and the launches of one call read it
+// alike) pins it for A/B.
 inline int x3_conv_negk(long m_per_sample, int N, int K, int zdim) {
   const char* e = getenv("DAMC_X3_NEGK_RULE");
-  if (e && e[0] == '5') return 512;
-  if (K % 1024 != 0) return 512;
-  if (e && e[0] == '1') return 1024;
-  const long tiles16 = ((16 * m_per_sample + 255) / 256) * ((N + 127) / 128) * zdim;
-  return tiles16 * K >= (1L << 18) ? 1024 : 512;
+  int nk;
+  if (e && e[0] == '2') {
+    nk = 256;
+  } else if (e && e[0] == '5') {
+    nk = 512;
+  } else if (e && e[0] == '1') {
+    nk = 1024;
+  } else {
+    const long w16 = ((16 * m_per_sample + 255) / 256) * ((N + 127) / 128) * zdim * (long)K;
+    nk = w16 >= (1L << 18) ? 1024 : w16 >= (1L << 16) ? 512 : 256;
+  }
+  while (nk > 256 && K % nk != 0) nk >>= 1;
+  return nk;
 }
 // the fused output-layer projection as a kernel of its own: P[pix][n] = sum_c h[pix][c] w[n][c] (c < C <= 256,
 // C % 16 == 0; n < np, np = 32 or 64; w rows ldw floats), bitwise the fused form (same MFMA sequence per row); for
@@ -252,6 +264,11 @@ __device__ __forceinline__ void pack_conv_x3_block(const PackConvList& l, int bl
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);
 
+// small fp32 GEMMs in one launch (gemm.hip small_gemm_kernel): C = act(A . B + bias[n % bias_mod]) (bias_mod 0: n),
+// A (M x K, K % 4 == 0, lda % 4 == 0, 16-B aligned), B (K x N row-major); one 16 x 16 output tile per wave, exact
+// fp32 products, fp32 accumulation
+int launch_small_gemm(const float* A, long lda, const float* B, long ldb, const float* bias, float* C, long ldc, int M,
+                      int N, int K, hipStream_t s, int bias_mod = 0, int act = DAMC_ACT_NONE, float slope = 0.f);
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);
 

@@ -415,6 +415,68 @@ __global__ __launch_bounds__(256, OCC) void gemm_f32_group_kernel(GemmGroup g) {
 }
 
 // ================================================================================================
+// Small fp32 GEMMs (the Q update's denoiser: B = 128-row activations times weights, and the weight gradients with
+// K = B): C (M x N, ldc) = A (M x K row-major, lda) . B (K x N row-major, ldb) (+ bias[n]), exact fp32 products on
+// v_mfma_f32_16x16x4f32 with fp32 accumulation.  One 16 x 16 output tile per wave, the whole K in one chain, operands
+// straight from memory into registers (KU 16-k steps of loads in flight), so a 128 x 512 product is 256 waves in ONE
+// launch -- the tiled engine gave it 4 workgroups, or split K into slabs plus a reduce launch.  Lane (m, q) supplies
+// A[row m][k0 + 4 q + e] and B[k0 + 4 q + e][col m] to MFMA step e (proj16's k bijection).
+template <int KU>
+__global__ __launch_bounds__(256) void small_gemm_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
+                                                         long ldb, const float* __restrict__ bias, float* __restrict__ C,
+                                                         long ldc, int M, int N, int K, int bias_mod, int act,
+                                                         float slope) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntn = (N + 15) >> 4;
+  const long tile = (long)blockIdx.x * 4 + wave;
+  const int tm = (int)(tile / ntn), tn = (int)(tile - (long)tm * ntn);
+  if (tm * 16 >= M) return;  // wave-uniform
+  const int m = lane & 15, q = lane >> 4;
+  const int row = tm * 16 + m, col = tn * 16 + m;
+  const bool rok = row < M, cok = col < N;
+  const float* Ar = A + (long)(rok ? row : 0) * lda;
+  const float* Bc = B + (cok ? col : 0);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 16 * KU) {
+    f32x4 a[KU], b[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {  // K % 4 == 0: a lane's 4 k are all in range or all out; loads from clamped
+      const int k = k0 + 16 * u + 4 * q;  // (valid) addresses, then zeroed, so no load sits in a branch
+      const bool kin = k < K;
+      const int kk = kin ? k : 0;
+      a[u] = *reinterpret_cast<const f32x4*>(Ar + kk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[u][e] = Bc[(long)(kk + e) * ldb];
+      if (!(rok && kin)) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!(cok && kin)) b[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the KU steps' loads all in flight before the first MFMA waits
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][e], b[u][e], acc, 0, 0, 0);
+  }
+  if (!cok) return;
+  const float bv = bias ? bias[bias_mod > 0 ? col % bias_mod : col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = tm * 16 + 4 * q + r;
+    if (rr < M) C[(long)rr * ldc + col] = act_apply(acc[r] + bv, act, slope);
+  }
+}
+
+int launch_small_gemm(const float* A, long lda, const float* B, long ldb, const float* bias, float* C, long ldc, int M,
+                      int N, int K, hipStream_t s, int bias_mod, int act, float slope) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < N || ldc < N) return DAMC_ERR_ARG;
+  if (K % 4 != 0 || lda % 4 != 0 || (reinterpret_cast<uintptr_t>(A) & 15) != 0) return DAMC_ERR_UNSUPPORTED;  // f32x4 A
+  ProfScope ps("small_gemm", 2.0 * M * N * K, s);
+  const long tiles = (long)((M + 15) / 16) * ((N + 15) / 16);
+  hipLaunchKernelGGL(small_gemm_kernel<4>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, A, lda, B, ldb, bias, C,
+                     ldc, M, N, K, bias_mod, act, slope);
+  return (int)hipGetLastError();
+}
+
+// ================================================================================================
 // K-major convolution engine (A_CONV with Cg % 32 == 0, B packed [n][k]).
 //
 // Both operands are staged k-contiguous: a global float4 (4 consecutive channels of one pixel, or 4
@@ -2232,32 +2294,44 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_tile_kernel(GemmArgs p, 
 }
 
 // the split-K reduce of a ConvT forward whose epilogue also runs the output layer's projection (GemmArgs::proj_out,
-// register slab layout): one workgroup per (phase, 256 x 128 tile, 128-row half).  Wave w sums the 8 16x16 tiles of
-// rows 16 w .. + 15 (x3_ksplit_reduce_tile_kernel's per-lane order) into an LDS tile, the octet epilogue writes the
-// sign bits (and C unless proj_nostore) and leaves the activated rows in the tile, and wave w projects its 16 rows
-// with proj16 into the chunk's partial buffer -- the F32A tile's fused epilogue on the same sums, so the result is
-// bitwise the unsplit kernel's, without the fp32 activation's write and re-read by proj_rows_kernel
+// register slab layout): one workgroup of 4 waves per (phase, 256 x 128 tile, 64-row quarter).  Wave w sums the 8
+// 16x16 tiles of rows 16 w .. + 15 of the quarter (x3_ksplit_reduce_tile_kernel's per-lane order) into an LDS tile,
+// the octet epilogue writes the sign bits (and C unless proj_nostore) and leaves the activated rows in the tile, and
+// wave w projects its 16 rows with proj16 into the chunk's partial buffer -- the F32A tile's fused epilogue on the
+// same sums, so the result is bitwise the unsplit kernel's, without the fp32 activation's write and re-read by
+// proj_rows_kernel
 template <int NT>
-__global__ __launch_bounds__(512) void x3_ksplit_reduce_proj_kernel(GemmArgs p, int zdim) {
-  constexpr int TS = X3_BN + 4;
-  __shared__ __attribute__((aligned(16))) float tile[128 * TS];
-  __shared__ long rowtab[128];
+__global__ __launch_bounds__(256) void x3_ksplit_reduce_proj_kernel(GemmArgs p, int zdim) {
+  constexpr int TS = X3_BN + 4, RW = 64;
+  __shared__ __attribute__((aligned(16))) float tile[RW * TS];
+  __shared__ long rowtab[RW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ntm = (p.M + X3_BM - 1) / X3_BM, ntn = (p.N + X3_BN - 1) / X3_BN;
   const long ntile = (long)ntm * ntn;
-  const int half = blockIdx.x & 1;
-  const long tl = blockIdx.x >> 1;
+  const int qtr = blockIdx.x & 3;
+  const long tl = blockIdx.x >> 2;
   const int tile_i = (int)(tl % ntile), ph = (int)(tl / ntile);
   if (ph >= zdim) return;  // workgroup-uniform
   const int tm = tile_i / ntn, tn = tile_i - tm * ntn;
   const int py = ph >> 1, px = ph & 1;
-  const int r16 = half * 128 + 16 * w;  // this wave's 16 rows within the 256-row tile
+  const int r16 = qtr * RW + 16 * w;  // this wave's 16 rows within the 256-row tile
   const int wm = r16 >> 6, ti = (r16 & 63) >> 4;
   const long sstride = ntile * (X3_BM * X3_BN / 4);
   const f32x4* src = reinterpret_cast<const f32x4*>(p.kslab) + (long)ph * p.ksplit * sstride + (long)tile_i * 8 * 16 * 64;
   f32x4 v[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the chunk's projection weights (proj16's b operands: row 16 t + m, k = 16 g + 4 q .. + 3) into registers first,
+  // so their loads overlap the slab loads instead of chaining through proj16's k loop
+  const int cc = tn * X3_BN, cw = min(PROJ_CHUNK, p.N - cc);
+  const int mm = lane & 15, qq = lane >> 4;
+  f32x4 wb[PROJ_CHUNK / 16][NT];
+#pragma unroll
+  for (int g = 0; g < PROJ_CHUNK / 16; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      wb[g][t] = 16 * g < cw ? *reinterpret_cast<const f32x4*>(p.proj_w + cc + (long)(16 * t + mm) * p.proj_ldw + 16 * g + 4 * qq)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
   if (tm * X3_BM + r16 < p.M) {  // wave-uniform
     for (int sl = 0; sl < p.ksplit; ++sl) {
 #pragma unroll
@@ -2271,16 +2345,16 @@ __global__ __launch_bounds__(512) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
   for (int u = 0; u < 8; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tile[(16 * w + 4 * (lane >> 4) + r) * TS + 16 * u + (lane & 15)] = v[u][r];
-  if (tid < 128) {
-    const int m = tm * X3_BM + half * 128 + tid;
+  if (tid < RW) {
+    const int m = tm * X3_BM + qtr * RW + tid;
     rowtab[tid] = m < p.M ? gemm_row_offset<O_PHASE>(p, m, py, px) : -1;
   }
   __syncthreads();
   GemmArgs q = p;
   if (p.proj_nostore) q.C = nullptr;
-  for (int o = tid; o < 128 * 16; o += 512) {
+  for (int o = tid; o < RW * 16; o += 256) {
     const int row = o >> 4, oc = (o & 15) * 8;
-    const int m = tm * X3_BM + half * 128 + row, n = tn * X3_BN + oc;
+    const int m = tm * X3_BM + qtr * RW + row, n = tn * X3_BN + oc;
     if (m >= p.M || n >= p.N) continue;
     float e8[8];
 #pragma unroll
@@ -2290,11 +2364,20 @@ __global__ __launch_bounds__(512) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
     *reinterpret_cast<f32x4*>(tile + row * TS + oc + 4) = f32x4{e8[4], e8[5], e8[6], e8[7]};
   }
   __syncthreads();
-  const int cc = tn * X3_BN;
+  // proj16's arithmetic (same MFMA sequence per output) with the preloaded weights
   f32x4 acc[NT];
-  proj16<NT>(tile, TS, 16 * w, min(PROJ_CHUNK, p.N - cc), p.proj_w + cc, p.proj_ldw, acc);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < PROJ_CHUNK / 16; ++g) {
+    if (16 * g >= cw) break;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(tile + (16 * w + mm) * TS + 16 * g + 4 * qq);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], wb[g][t][e], acc[t], 0, 0, 0);
+  }
   float* Pc = p.proj_out + (cc / PROJ_CHUNK) * p.proj_pstride;
-  const int mm = lane & 15, qq = lane >> 4;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -2586,11 +2669,11 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
             (a.N <= PROJ_CHUNK || a.N % PROJ_CHUNK == 0) && (a.proj_np == 32 || a.proj_np == 64) &&
             !(erp && erp[0] == '0')) {
           a.proj_nostore = nostore0;
-          const unsigned nwg = (unsigned)(zdim * ntm * ntn * 2);
+          const unsigned nwg = (unsigned)(zdim * ntm * ntn * 4);
           if (a.proj_np == 32)
-            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<2>), dim3(nwg), dim3(512), 0, s, a, zdim);
+            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<2>), dim3(nwg), dim3(256), 0, s, a, zdim);
           else
-            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<4>), dim3(nwg), dim3(512), 0, s, a, zdim);
+            hipLaunchKernelGGL((x3_ksplit_reduce_proj_kernel<4>), dim3(nwg), dim3(256), 0, s, a, zdim);
           return (int)hipGetLastError();
         }
         const long waves = (long)zdim * ntm * ntn * 128;

@@ -1189,7 +1189,11 @@ __global__ __launch_bounds__(256) void smallc_gather_kernel(const float* __restr
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = sq;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(sqerr_sum, (red[0] + red[1] + red[2] + red[3]) * (0.5f * inv_s2));
+    if (threadIdx.x == 0) {
+      float t = red[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+      atomicAdd(sqerr_sum, t * (0.5f * inv_s2));
+    }
   }
 }
 
@@ -1417,8 +1421,12 @@ int smallc_fwd_twostage(const damc_layer_t& L, const float* h, int B, const floa
                          L.bias, x, inv_s2, delta, xhat, sqerr);
     return (int)hipGetLastError();
   }
+  // one wave per workgroup where 256-thread workgroups would leave CUs idle (CIFAR B=16: 256 workgroups of 64 instead
+  // of 64 of 256 -- a pixel's 54 scattered loads are latency-bound, so the CU count carries it); pixels are independent
+  const int tpb = g2 < 512 ? 64 : 256;
+  const int g2t = (int)((npout + tpb - 1) / tpb);
 #define SG(NC_, K_, S_)                                                                                             \
-  hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2), dim3(256), 0, s, Pbuf, P1, nt * 32, B, L.hin,     \
+  hipLaunchKernelGGL((smallc_gather_kernel<NC_, K_, S_>), dim3(g2t), dim3(tpb), 0, s, Pbuf, P1, nt * 32, B, L.hin,    \
                      L.win, L.pad, L.hout, L.wout, L.bias, x, inv_s2, delta, xhat, sqerr)
   if (L.cout == 3) {
     if (L.k == 3) SG(3, 3, 1); else SG(3, 4, 2);
@@ -1849,8 +1857,19 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
       a.N = N;
       a.K = L.cin;
       a.k_per_z = a.K;
-      rc = damc::launch_gemm(a, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
-                             2.0 * B * (double)N * L.cin, s);
+      // a first layer whose nz is no multiple of 32 (SVHN, CelebA-64: nz = 100): the small-GEMM kernel, one 16 x 16
+      // tile per wave (SVHN B=64: 2048 waves; the tiled engine ran 64 workgroups for 29 us); chosen by shape, never by
+      // batch, so sharded chains stay bitwise the whole batch's.  DAMC_PROJ_SMALL=0 (read per call): the tiled engine
+      const char* eps_ = getenv("DAMC_PROJ_SMALL");
+      rc = DAMC_ERR_UNSUPPORTED;
+      if (L.kind == DAMC_LAYER_PROJ && !(eps_ && eps_[0] == '0')) {
+        ProfScope ps("proj_fwd", 2.0 * B * (double)N * L.cin, s);
+        rc = damc::launch_small_gemm(a.A, a.lda, a.B, a.ldb, L.bias, a.C, a.ldc, B, N, L.cin, s, L.cout, L.act,
+                                     L.slope);
+      }
+      if (rc == DAMC_ERR_UNSUPPORTED)
+        rc = damc::launch_gemm(a, damc::A_DENSE, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "proj_fwd",
+                               2.0 * B * (double)N * L.cin, s);
     } else {  // UP2
       a.A = ws.h[i - 1];
       a.Hin = L.hin;

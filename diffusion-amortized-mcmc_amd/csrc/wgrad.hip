@@ -159,22 +159,76 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
   if (rl == 0 && c < C) out[(long)blockIdx.y * C + c] = red[cl];
 }
 
+// the same sums four channels per thread (C % 4 == 0, ld % 4 == 0, 16-B aligned): CL4 float4 lanes of 4 channels,
+// 256 / CL4 row lanes (16 at C = 64 instead of 4), so both passes keep many more loads in flight per thread-row
+__global__ __launch_bounds__(256) void colsum4_kernel(const float* __restrict__ X, long R, int C4, long ld4, int CL4,
+                                                      long rows_per, float* __restrict__ out) {
+  __shared__ f32x4 red[256];
+  const int RL = 256 / CL4;
+  const int cl = threadIdx.x % CL4, rl = threadIdx.x / CL4;
+  const int c4 = blockIdx.x * CL4 + cl;
+  const long r0 = (long)blockIdx.y * rows_per;
+  const long r1 = min(R, r0 + rows_per);
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < C4) {
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    for (long r = r0 + rl; r < r1; r += RL) sum += X4[r * ld4 + c4];
+  }
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (int h = RL / 2; h > 0; h >>= 1) {
+    if (rl < h) red[threadIdx.x] += red[threadIdx.x + h * CL4];
+    __syncthreads();
+  }
+  if (rl == 0 && c4 < C4) reinterpret_cast<f32x4*>(out)[(long)blockIdx.y * C4 + c4] = red[cl];
+}
+
 static int colsum_lanes(int C) {
   int cl = 1;
   while (cl < C && cl < 64) cl <<= 1;
   return cl;
 }
-// row blocks of the first pass: <= 16 rows per thread, at most 1024 blocks (the second pass sums them)
+// row blocks of the first pass: <= 16 rows per thread, at most 1024 blocks (the second pass sums them); a single
+// pass up to 8x that (a two-pass sum of a 128-row batch cost two launches for 32 loads per thread)
 static long colsum_blocks(long R, int C) {
   const long per = 16L * (256 / colsum_lanes(C));
-  return R <= per ? 1 : std::min<long>(1024, (R + per - 1) / per);
+  return R <= 8 * per ? 1 : std::min<long>(1024, (R + per - 1) / per);
+}
+// float4 form: 256 row blocks at most (32 float4 rows per thread per pass at R = 131072, C = 64), one pass up to 32
+// rows per thread
+static int colsum4_lanes(int C4) {
+  int cl = 1;
+  while (cl < C4 && cl < 64) cl <<= 1;
+  return cl;
+}
+static long colsum4_blocks(long R, int C) {
+  const long rl = 256 / colsum4_lanes(C / 4);
+  return R <= 32 * rl ? 1 : std::min<long>(256, (R + 32 * rl - 1) / (32 * rl));
 }
 
-size_t colsum_tmp_floats(long R, int C) { return (size_t)colsum_blocks(R, C) * C; }
+size_t colsum_tmp_floats(long R, int C) {
+  return (size_t)std::max(colsum_blocks(R, C), colsum4_blocks(R, C)) * C;
+}
 
 int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s) {
   if (!X || !out || R <= 0 || C <= 0 || ld < C) return DAMC_ERR_ARG;
   ProfScope ps("bias_grad", 0.0, s);
+  if (C % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out) |
+                                      reinterpret_cast<uintptr_t>(tmp)) & 15) == 0) {
+    const int C4 = C / 4, CL4 = colsum4_lanes(C4);
+    const long nrb = colsum4_blocks(R, C);
+    const unsigned gx = (unsigned)((C4 + CL4 - 1) / CL4);
+    if (nrb == 1) {
+      hipLaunchKernelGGL(colsum4_kernel, dim3(gx, 1), dim3(256), 0, s, X, R, C4, ld / 4, CL4, R, out);
+      return (int)hipGetLastError();
+    }
+    if (!tmp) return DAMC_ERR_ARG;
+    const long per = (R + nrb - 1) / nrb;
+    hipLaunchKernelGGL(colsum4_kernel, dim3(gx, (unsigned)nrb), dim3(256), 0, s, X, R, C4, ld / 4, CL4, per, tmp);
+    hipLaunchKernelGGL(colsum4_kernel, dim3(gx, 1), dim3(256), 0, s, (const float*)tmp, nrb, C4, (long)C4, CL4, nrb,
+                       out);
+    return (int)hipGetLastError();
+  }
   const int CL = colsum_lanes(C);
   const long nrb = colsum_blocks(R, C);
   const unsigned gx = (unsigned)((C + CL - 1) / CL);

@@ -142,6 +142,33 @@ class Adam(torch.optim.Optimizer):
             steps.append(st["step"])
         return ps, gs, ms, vs, steps
 
+    def _advance_steps(self, group, steps):
+        """+1 on the step counters of the parameters being updated, as torch's _multi_tensor_adam does, and their
+        common value (None when they differ).  Where every parameter of the group is updated and all counters agree,
+        the group's states share ONE step tensor (equal values, so torch's state_dict and load_state_dict see the
+        same counts), and the advance is one add instead of a foreach over ~100 CPU scalars plus a stack and a
+        compare (~0.6 ms of host time per Q update)."""
+        shared = steps[0]
+        if len(steps) == len(group["params"]) and all(t is shared for t in steps):
+            shared.add_(1.0)
+            return float(shared)
+        if len(steps) < len(group["params"]) or len({id(t) for t in steps}) < len(steps):
+            # a shared counter and only some parameters updated: each updated parameter gets its own counter first
+            i = 0
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                steps[i] = self.state[p]["step"] = steps[i].clone()
+                i += 1
+        torch._foreach_add_(steps, 1.0)
+        sv = torch.stack(steps)
+        if not bool((sv == sv[0]).all()):
+            return None
+        if len(steps) == len(group["params"]):  # all in step: share one counter from here on
+            for p in group["params"]:
+                self.state[p]["step"] = shared
+        return float(sv[0])
+
     @staticmethod
     def _hparams(group, step):
         beta1, beta2 = group["betas"]
@@ -176,12 +203,12 @@ class Adam(torch.optim.Optimizer):
             ps, gs, ms, vs, steps = collected[gi] if collected is not None else self._collect(group)
             if not ps:
                 continue
-            torch._foreach_add_(steps, 1.0)
-            sv = torch.stack(steps)
-            if bool((sv == sv[0]).all()):
-                self._launch(group, ps, gs, ms, vs, float(sv[0]), clip)
+            common = self._advance_steps(group, steps)
+            if common is not None:
+                self._launch(group, ps, gs, ms, vs, common, clip)
                 continue
             # parameters that joined the group at different steps: one launch per step value
+            sv = torch.stack(steps)
             for val in sorted(set(sv.tolist())):
                 idx = [i for i, x in enumerate(sv.tolist()) if x == val]
                 self._launch(group, [ps[i] for i in idx], [gs[i] for i in idx], [ms[i] for i in idx],

@@ -134,17 +134,30 @@ def _blocks_of(p):
     return list(p.in_layers) + list(p.mid_layers) + list(p.out_layers)
 
 
+_DN_PARAMS = weakref.WeakKeyDictionary()  # denoiser -> (entries, owning (module._parameters, name) per entry)
+
+
 def _denoiser_params(p):
-    """[(field, block index or None, parameter)] in a fixed order."""
+    """[(field, block index or None, parameter)] in a fixed order.  Cached per module (walking ~60 submodule
+    attributes costs ~0.1 ms of host time per call, twice per Q update); the cache is revalidated every call against
+    the owning modules' parameter dicts, so a parameter replaced by assignment is picked up."""
+    c = _DN_PARAMS.get(p)
+    if c is not None and all(d.get(k) is t for (d, k), (_, _, t) in zip(c[1], c[0])):
+        return c[0]
     t1, t2 = p.time_mlp[1], p.time_mlp[3]
     out = [("bmat", None, p.B), ("tw1", None, t1.weight), ("tb1", None, t1.bias), ("tw2", None, t2.weight),
            ("tb2", None, t2.bias)]
+    own = [(p._parameters, "B"), (t1._parameters, "weight"), (t1._parameters, "bias"), (t2._parameters, "weight"),
+           (t2._parameters, "bias")]
     for b, blk in enumerate(_blocks_of(p)):
         lc = blk._layer_ctx[1]
-        for key, t in zip(_BLOCK_KEYS, (blk._layer[0].weight, blk._layer[0].bias, blk._skip.weight, blk._skip.bias,
-                                        blk._hyper_gate.weight, blk._hyper_gate.bias, blk._hyper_bias.weight,
-                                        lc.weight, lc.bias)):
-            out.append((key, b, t))
+        mods = (blk._layer[0], blk._layer[0], blk._skip, blk._skip, blk._hyper_gate, blk._hyper_gate,
+                blk._hyper_bias, lc, lc)
+        names = ("weight", "bias", "weight", "bias", "weight", "bias", "weight", "weight", "bias")
+        for key, m, nm in zip(_BLOCK_KEYS, mods, names):
+            out.append((key, b, getattr(m, nm)))
+            own.append((m._parameters, nm))
+    _DN_PARAMS[p] = (out, own)
     return out
 
 
@@ -279,17 +292,27 @@ class _EncoderTrainFn(torch.autograd.Function):
         h = torch.empty(B, H, W, C, dtype=torch.float32, device=dev)
         check(L.damc_nchw_to_nhwc(ptr(x.detach().float().contiguous()), B, C, H * W, ptr(h), stream), "nchw_to_nhwc")
         saved = []
+        limb = _lib.current_engine() == _lib.ENGINE_LIMB
         for conv, norm, slope in stages:
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             cout, cin = conv.out_channels, conv.in_channels
-            wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
-            check(L.damc_pack_conv2d(ptr(conv.weight), cout, cin, k, ptr(wp), stream), "pack conv2d")
             Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
             y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
-            nsl = int(L.damc_conv2d_workspace_floats(B, H, W, cin, cout, k, s, p))
-            sl = torch.empty(nsl, dtype=torch.float32, device=dev) if nsl else None
-            check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(conv.bias), cout, k, s, p, ptr(y), ptr(sl),
-                                     nsl, stream), "conv2d")
+            nbx = int(L.damc_conv2d_x3_workspace_bytes(B, H, W, cin, cout, k, s, p)) if limb else 0
+            if nbx:  # the limb engine (fp32-accurate bf16 MFMA), as the Q(x) forward runs these convs (a10)
+                w3 = torch.empty(int(L.damc_conv2d_x3_bytes(cout, cin, k)) // 2, dtype=torch.int16, device=dev)
+                check(L.damc_pack_conv2d_x3(ptr(conv.weight.detach().contiguous()), cout, cin, k, ptr(w3), stream),
+                      "pack conv2d x3")
+                ws = torch.empty(nbx, dtype=torch.uint8, device=dev)
+                check(L.damc_conv2d_x3_nhwc(ptr(h), B, H, W, cin, ptr(w3), ptr(conv.bias), cout, k, s, p, ptr(y),
+                                            ptr(ws), nbx, stream), "conv2d x3")
+            else:
+                wp = torch.empty(k * k * cin * cout, dtype=torch.float32, device=dev)
+                check(L.damc_pack_conv2d(ptr(conv.weight), cout, cin, k, ptr(wp), stream), "pack conv2d")
+                nsl = int(L.damc_conv2d_workspace_floats(B, H, W, cin, cout, k, s, p))
+                sl = torch.empty(nsl, dtype=torch.float32, device=dev) if nsl else None
+                check(L.damc_conv2d_nhwc(ptr(h), B, H, W, cin, ptr(wp), ptr(conv.bias), cout, k, s, p, ptr(y),
+                                         ptr(sl), nsl, stream), "conv2d")
             stats, out = None, y
             if norm is not None:
                 out = torch.empty_like(y)

@@ -265,6 +265,13 @@ int damc_clock_probe(unsigned long long* buf, int n_slots);
 /* a Conv2d weight in its PyTorch layout (cout, cin, k, k), cin % 32 == 0 -> the limb engine's B operand of the
  * conv (damc_conv2d_x3_bytes bytes), in one pass */
 int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream);
+/* one Conv2d (+ bias) on the limb engine, NHWC fp32 in and out (the Q update's encoder forward, which keeps every conv
+ * output for its backward): w_x3 = damc_pack_conv2d_x3 of the weight; k4 s2 p1 convs stage x as fp32, other shapes
+ * split it into limbs in the workspace (damc_conv2d_x3_workspace_bytes; 0 = the shape has no limb-engine form) */
+size_t damc_conv2d_x3_workspace_bytes(int batch, int hin, int win, int cin, int cout, int k, int stride, int pad);
+int damc_conv2d_x3_nhwc(const float* x, int batch, int hin, int win, int cin, const void* w_x3, const float* bias,
+                        int cout, int k, int stride, int pad, float* y, void* workspace, size_t workspace_bytes,
+                        void* stream);
 size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* enc, int batch);
 int damc_q_encoder_fwd(const damc_encoder_t* enc, const float* x, int batch, float* xemb, void* workspace,
                        size_t workspace_bytes, void* stream);

@@ -152,8 +152,8 @@ def test_adam_chunk_table_host_only():
 def test_layer_sign_block_rule(monkeypatch):
     """gemm.h x3_conv_negk, through damc_x3_layer_sign_block (host only): the generator's UP2 limb weights take 1024-k
     sign blocks where 16 samples would already split 512-k blocks two per workgroup (every UP2 GEMM of the headline
-    _netG_cifar10 ngf=128), 512-k blocks where the finer split is what fills the chip (_netG_svhn ngf=64,
-    _netG_celeba64 ngf=128), by shape only; DAMC_X3_NEGK_RULE pins it."""
+    _netG_cifar10 ngf=128 and of _netG_celebaHQ), 512 for _netG_celeba64 ngf=128 and 256 for _netG_svhn ngf=64,
+    whose batches fill the chip only with the finer split; by shape only; DAMC_X3_NEGK_RULE pins it."""
     from damc import _lib
 
     L = _lib.lib()
@@ -174,13 +174,15 @@ def test_layer_sign_block_rule(monkeypatch):
     celeba64 = [up2(1024, 512, 4), up2(512, 256, 8), up2(256, 128, 16)]
     hq = [up2(2048, 1024, 4), up2(1024, 512, 8), up2(512, 512, 16), up2(512, 256, 32), up2(256, 128, 64)]
     assert blocks(cifar) == [(1024, 1024)] * 2
-    assert blocks(svhn) == [(512, 512)] * 2
+    assert blocks(svhn) == [(256, 256)] * 2
     assert blocks(celeba64) == [(512, 512)] * 3
     assert blocks(hq) == [(1024, 1024)] * 5
     monkeypatch.setenv("DAMC_X3_NEGK_RULE", "512")
     assert blocks(cifar) == [(512, 512)] * 2
     monkeypatch.setenv("DAMC_X3_NEGK_RULE", "1024")
     assert blocks(svhn) == [(1024, 1024)] * 2
+    monkeypatch.setenv("DAMC_X3_NEGK_RULE", "256")
+    assert blocks(cifar) == [(256, 256)] * 2
     d = _lib.Layer()
     d.kind = _lib.LAYER_SMALLC
     assert L.damc_x3_layer_sign_block(ctypes.byref(d), 0) == 0

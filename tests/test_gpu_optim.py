@@ -160,3 +160,33 @@ def test_more_tensors_than_one_launch(gpu_device):
         assert abs(float(dn) - float(tn)) / float(tn) < 1e-6
     for a, b in zip(mine, ref):
         assert _rel(a.detach(), b.detach()) < 2e-6
+
+
+def test_adam_step_counters_with_partial_gradients(gpu_device):
+    """damc.optim shares one step counter per group while every parameter is updated together (one CPU add per
+    step instead of a foreach over ~100 scalars); a step in which only some parameters carry a gradient gives those
+    their own counters first, so every parameter's count, its bias correction and the torch state_dict round trip
+    still match torch's AdamW."""
+    from damc import optim as dopt
+
+    ref = _params(gpu_device)
+    mine = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    kw = dict(lr=3e-4, betas=(0.5, 0.999), weight_decay=1e-4)
+    to, do = torch.optim.AdamW(ref, **kw), dopt.AdamW(mine, **kw)
+    for step in range(6):
+        _set_grads(ref, step)
+        _set_grads(mine, step)
+        if step == 3:  # every other parameter without a gradient this step
+            for i in range(0, len(ref), 2):
+                ref[i].grad = None
+                mine[i].grad = None
+        to.step()
+        do.step()
+    torch.cuda.synchronize()
+    for a, b in zip(mine, ref):
+        assert float(do.state[a]["step"]) == float(to.state[b]["step"])
+        assert _rel(a.detach(), b.detach()) < STEP_TOL
+    # the state_dict carries the per-parameter counts into torch's optimiser and back
+    to2 = torch.optim.AdamW(mine, **kw)
+    to2.load_state_dict(do.state_dict())
+    assert [float(to2.state[p]["step"]) for p in mine] == [float(to.state[p]["step"]) for p in ref]

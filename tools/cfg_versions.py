@@ -24,9 +24,12 @@ LEGS = {  # name: (constructor, nz, ngf, image size, B, sigma)
     "svhn64": ("_netG_svhn", 100, 64, 32, 64, 0.1),
     "celeba32": ("_netG_celeba64", 100, 128, 64, 32, 0.1),
     "hq8": ("_netG_celebaHQ", 128, 128, 256, 8, 1.0),
+    "celeba256": ("_netG_celeba64", 100, 128, 64, 256, 0.1),
+    "hq64": ("_netG_celebaHQ", 128, 128, 256, 64, 1.0),
 }
+DEFAULT = ["cifar16", "cifar128", "svhn64", "celeba32", "hq8"]
 dev = torch.device("cuda:0")
-for name in names or list(LEGS):
+for name in names or DEFAULT:
     ctor, nz, ngf, hw, B, sigma = LEGS[name]
     G = synth.load_into(getattr(dn, ctor)(nz=nz, ngf=ngf, nc=3), 0).to(dev).eval()
     E = synth.load_into(dn._netE(nz=nz), 10).to(dev).eval()
@@ -44,5 +47,5 @@ for name in names or list(LEGS):
             ts.append(a.elapsed_time(b) / 10)
     ts.sort()
     h = hashlib.sha1(z.cpu().numpy().tobytes()).hexdigest()[:12]
-    print("%-12s %-9s posterior step median %.4f ms (min %.4f max %.4f)  sha %s" % (
-        os.path.basename(tree.rstrip("/")), name, ts[len(ts) // 2], ts[0], ts[-1], h), flush=True)
+    print("%-12s %-9s %s posterior step median %.4f ms (min %.4f max %.4f)  sha %s" % (
+        os.path.basename(tree.rstrip("/")), name, os.environ.get("DAMC_X3_NEGK_RULE", "-"), ts[len(ts) // 2], ts[0], ts[-1], h), flush=True)
