@@ -341,6 +341,57 @@ int gemm(const float* A, long lda, const float* Bm, long ldb, const float* bias,
   return launch_gemm(a, A_DENSE, EPI_BIAS_ACT, O_DENSE, 1, name, 2.0 * M * N * K, s);
 }
 
+// several independent products of one stage (and the bias gradients as column sums) in ONE launch of the grouped
+// small-GEMM kernel (gemm.hip small_gemm_group_kernel; round 5: the Q update issued 53 GEMM launches of 4-20 us, each
+// latency-bound on its single-wave K chain).  DAMC_DN_GROUP=0 (read per call), DAMC_DN_SMALL_GEMM=0 or a member the
+// kernel does not take: every member on its own (gemm() above, launch_colsum for the column sums)
+struct Grp {
+  SmallGemm g[SG_GROUP_MAX];
+  int n = 0;
+  void mm(const float* A, long lda, const float* Bm, long ldb, const float* bias, float* C, long ldc, int M, int N,
+          int K) {
+    SmallGemm& d = g[n++];
+    d.A = A;
+    d.lda = lda;
+    d.B = Bm;
+    d.ldb = ldb;
+    d.bias = bias;
+    d.C = C;
+    d.ldc = ldc;
+    d.M = M;
+    d.N = N;
+    d.K = K;
+  }
+  // C (N) = column sums of X (R x N, row stride ld)
+  void colsum(const float* X, long R, int N, long ld, float* C) {
+    SmallGemm& d = g[n++];
+    d.a_ones = 1;
+    d.B = X;
+    d.ldb = ld;
+    d.C = C;
+    d.ldc = N;
+    d.M = 1;
+    d.N = N;
+    d.K = (int)R;
+  }
+  int run(float* slab, float* tmp, hipStream_t s) {
+    const char* eg = getenv("DAMC_DN_GROUP");
+    const char* esg = getenv("DAMC_DN_SMALL_GEMM");
+    if (!(eg && eg[0] == '0') && !(esg && esg[0] == '0')) {
+      const int rc = launch_small_gemm_group(g, n, s);
+      if (rc != DAMC_ERR_UNSUPPORTED) return rc;
+    }
+    for (int i = 0; i < n; ++i) {
+      const SmallGemm& d = g[i];
+      const int rc = d.a_ones ? launch_colsum(d.B, d.K, d.N, d.ldb, d.C, tmp, s)
+                              : gemm(d.A, d.lda, d.B, d.ldb, d.bias, d.C, d.ldc, d.M, d.N, d.K, "dn_gemm", s,
+                                     d.M <= 256 ? slab : nullptr);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+};
+
 // ------------------------------------------------------------------ workspace
 struct DW {
   // packed weights
@@ -504,25 +555,38 @@ int forward(const damc_denoiser_train_t* d, const float* zt, const float* se, co
   }
   // time MLP: temb = Lt2(silu(Lt1(se))) written into emb[:, :T] (se kept for dWt1)
   DAMC_CHECK(hipMemcpyAsync(w.se_in, se, sizeof(float) * B * T, hipMemcpyDeviceToDevice, s));
-  RC(gemm(w.se_in, T, w.T1_T, T, d->tb1, w.a1, T, B, T, T, "dn_gemm", s, w.slab));
+  {  // Lt1 and the input embedding's z B are independent: one launch
+    Grp gp;
+    gp.mm(w.se_in, T, w.T1_T, T, d->tb1, w.a1, T, B, T, T);
+    gp.mm(zt, nz, d->bmat, h, nullptr, w.v, h, B, h, nz);
+    RC(gp.run(w.slab, w.tmp, s));
+  }
   hipLaunchKernelGGL(silu_copy_kernel, grid1((long)B * T), dim3(256), 0, s, w.a1, (long)B * T, w.s1);
-  RC(gemm(w.s1, T, w.T2_T, T, d->tb2, w.emb, E, B, T, T, "dn_gemm", s, w.slab));
+  {
+    Grp gp;
+    gp.mm(w.s1, T, w.T2_T, T, d->tb2, w.emb, E, B, T, T);
+    RC(gp.run(w.slab, w.tmp, s));
+  }
   hipLaunchKernelGGL(emb_finish_kernel, grid1((long)B * E), dim3(256), 0, s, w.emb, xemb, B, T, X, w.semb);
-  // the 7 ctx Linears in one GEMM, then c_b = silu
-  RC(gemm(w.semb, E, w.WC_T, Dt, w.bC, w.u, Dt, B, Dt, E, "dn_gemm", s, w.slab));
+  {  // the 7 ctx Linears in one GEMM, then c_b = silu
+    Grp gp;
+    gp.mm(w.semb, E, w.WC_T, Dt, w.bC, w.u, Dt, B, Dt, E);
+    RC(gp.run(w.slab, w.tmp, s));
+  }
   BlockOff bo;
   for (int b = 0; b < 8; ++b) bo.off[b] = w.off[b];
   hipLaunchKernelGGL(ctx_silu_kernel, grid1((long)B * Dt), dim3(256), 0, s, w.u, B, bo, w.c);
   // input embedding
-  RC(gemm(zt, nz, d->bmat, h, nullptr, w.v, h, B, h, nz, "dn_gemm", s, w.slab));
   hipLaunchKernelGGL(input_emb_kernel, grid1((long)B * (2 * h + nz)), dim3(256), 0, s, w.v, zt, B, nz, w.X[0], w.zT);
   // blocks; skip inputs: out0 <- in2, out1 <- in1, out2 <- in0
   const int hs_of[7] = {-1, -1, -1, 2, 1, 0, -1};
   for (int b = 0; b < 7; ++b) {
     const int di = d->blocks[b].din, dd = d->blocks[b].dout;
     const float* cb = w.c + (long)B * w.off[b];
-    RC(gemm(w.X[b], di, w.WLS_T[b], 2 * dd, w.bLS[b], w.LS[b], 2 * dd, B, 2 * dd, di, "dn_gemm", s, w.slab));
-    RC(gemm(cb, dd, w.WBG_T[b], 2 * dd, w.bBG[b], w.BG[b], 2 * dd, B, 2 * dd, dd, "dn_gemm", s, w.slab));
+    Grp gp;
+    gp.mm(w.X[b], di, w.WLS_T[b], 2 * dd, w.bLS[b], w.LS[b], 2 * dd, B, 2 * dd, di);
+    gp.mm(cb, dd, w.WBG_T[b], 2 * dd, w.bBG[b], w.BG[b], 2 * dd, B, 2 * dd, dd);
+    RC(gp.run(w.slab, w.tmp, s));
     const bool last = b == 6;
     const float* hs = (!last && hs_of[b] >= 0) ? w.R[hs_of[b]] : nullptr;
     hipLaunchKernelGGL(csq_combine_kernel, grid1((long)B * dd), dim3(256), 0, s, w.LS[b], w.BG[b], B, dd, w.R[b],
@@ -543,11 +607,15 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
     const float* dR = b == 6 ? g : w.dR[b];
     const float* cb = w.c + (long)B * w.off[b];
     hipLaunchKernelGGL(csq_bwd_kernel, grid1((long)B * dd), dim3(256), 0, s, dR, w.LS[b], w.BG[b], B, dd, w.D, w.T);
-    RC(gemm(w.D, 3 * dd, w.WLS[b], di, nullptr, w.dX, di, B, di, 2 * dd, "dn_gemm", s, w.slab));
-    RC(gemm(w.D + dd, 3 * dd, w.WBG[b], dd, nullptr, w.dc + w.off[b], Dt, B, dd, 2 * dd, "dn_gemm", s, w.slab));
-    RC(gemm(w.T, B, w.X[b], di, nullptr, w.gWLS[b], di, 2 * dd, di, B, "dn_gemm", s));
-    RC(gemm(w.T + (long)dd * B, B, cb, dd, nullptr, w.gWBG[b], dd, 2 * dd, dd, B, "dn_gemm", s));
-    RC(launch_colsum(w.D, B, 3 * dd, 3 * dd, w.gbD[b], w.tmp, s));
+    {
+      Grp gp;
+      gp.mm(w.D, 3 * dd, w.WLS[b], di, nullptr, w.dX, di, B, di, 2 * dd);
+      gp.mm(w.D + dd, 3 * dd, w.WBG[b], dd, nullptr, w.dc + w.off[b], Dt, B, dd, 2 * dd);
+      gp.mm(w.T, B, w.X[b], di, nullptr, w.gWLS[b], di, 2 * dd, di, B);
+      gp.mm(w.T + (long)dd * B, B, cb, dd, nullptr, w.gWBG[b], dd, 2 * dd, dd, B);
+      gp.colsum(w.D, B, 3 * dd, 3 * dd, w.gbD[b]);
+      RC(gp.run(w.slab, w.tmp, s));
+    }
     if (b > 0) {
       const int a = pa[b], c = pc[b];
       const int da = d->blocks[a].dout;
@@ -560,28 +628,42 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
   }
   // input embedding (w.dX now holds dX0) -> dBm, dz
   hipLaunchKernelGGL(input_emb_bwd_kernel, grid1((long)B * h), dim3(256), 0, s, w.dX, w.v, B, nz, w.dv);
-  if (gr->bmat) RC(gemm(w.zT, B, w.dv, h, nullptr, gr->bmat, h, nz, h, B, "dn_gemm", s));
+  {
+    Grp gp;
+    if (gr->bmat) gp.mm(w.zT, B, w.dv, h, nullptr, gr->bmat, h, nz, h, B);
+    if (dzt) gp.mm(w.dv, h, w.BmT, nz, nullptr, w.dzp, nz, B, nz, h);
+    if (gp.n) RC(gp.run(w.slab, w.tmp, s));
+  }
   if (dzt) {
-    RC(gemm(w.dv, h, w.BmT, nz, nullptr, w.dzp, nz, B, nz, h, "dn_gemm", s, w.slab));
     hipLaunchKernelGGL(dz_kernel, grid1((long)B * nz), dim3(256), 0, s, d->residual ? g : nullptr, w.dX, w.dzp, B,
                        nz, dzt);
   }
   // ctx: du = dc * silu'(u); dsemb = du Wc; dWc = du^T semb; dbc = colsum(du)
   hipLaunchKernelGGL(dsilu_t_kernel, grid1((long)B * Dt), dim3(256), 0, s, w.dc, w.u, B, Dt, w.du, w.duT);
-  RC(gemm(w.du, Dt, w.WC, E, nullptr, w.dsemb, E, B, E, Dt, "dn_gemm", s, w.slab));
-  RC(gemm(w.duT, B, w.semb, E, nullptr, w.gWC, E, Dt, E, B, "dn_gemm", s));
-  RC(launch_colsum(w.du, B, Dt, Dt, w.gbC, w.tmp, s));
+  {
+    Grp gp;
+    gp.mm(w.du, Dt, w.WC, E, nullptr, w.dsemb, E, B, E, Dt);
+    gp.mm(w.duT, B, w.semb, E, nullptr, w.gWC, E, Dt, E, B);
+    gp.colsum(w.du, B, Dt, Dt, w.gbC);
+    RC(gp.run(w.slab, w.tmp, s));
+  }
   hipLaunchKernelGGL(emb_bwd_kernel, grid1((long)B * E), dim3(256), 0, s, w.dsemb, w.emb, B, T, X, w.dtemb, w.dtembT,
                      dxemb);
   // time MLP
-  if (gr->tw2) RC(gemm(w.dtembT, B, w.s1, T, nullptr, gr->tw2, T, T, T, B, "dn_gemm", s));
-  if (gr->tb2) RC(launch_colsum(w.dtemb, B, T, T, gr->tb2, w.tmp, s));
+  {
+    Grp gp;
+    if (gr->tw2) gp.mm(w.dtembT, B, w.s1, T, nullptr, gr->tw2, T, T, T, B);
+    if (gr->tb2) gp.colsum(w.dtemb, B, T, T, gr->tb2);
+    if (gr->tw1 || gr->tb1) gp.mm(w.dtemb, T, d->tw2, T, nullptr, w.ds1, T, B, T, T);
+    if (gp.n) RC(gp.run(w.slab, w.tmp, s));
+  }
   if (gr->tw1 || gr->tb1) {
-    RC(gemm(w.dtemb, T, d->tw2, T, nullptr, w.ds1, T, B, T, T, "dn_gemm", s, w.slab));
     hipLaunchKernelGGL(dsilu_t_kernel, grid1((long)B * T), dim3(256), 0, s, w.ds1, w.a1, B, T, w.da1, w.da1T);
     // dWt1 = da1^T se (se as kept by the forward)
-    if (gr->tw1) RC(gemm(w.da1T, B, w.se_in, T, nullptr, gr->tw1, T, T, T, B, "dn_gemm", s));
-    if (gr->tb1) RC(launch_colsum(w.da1, B, T, T, gr->tb1, w.tmp, s));
+    Grp gp;
+    if (gr->tw1) gp.mm(w.da1T, B, w.se_in, T, nullptr, gr->tw1, T, T, T, B);
+    if (gr->tb1) gp.colsum(w.da1, B, T, T, gr->tb1);
+    RC(gp.run(w.slab, w.tmp, s));
   }
   // scatter the stacked gradients
   CopyTable ct{};
@@ -618,6 +700,94 @@ int backward(const damc_denoiser_train_t* d, const float* g, int B, const damc_d
 
 }  // namespace
 }  // namespace damc
+
+// ------------------------------------------------------------------ Q.calculate_loss glue (round 5)
+namespace damc {
+namespace {
+// The noising around the denoiser in Q.calculate_loss (workspace/src/diffusion_net.py:633-639), the per-sample logsnr
+// input of Diffusion_UnetA.forward (:486-491) and its SinusoidalPosEmb (:447-461; the drop-in's fp64 sin / cos of the
+// fp32 angle, src/diffusion_net.py), each op rounded as PyTorch's ROCm kernels round it (no contraction; a division by
+// a Python scalar is a multiplication by its fp32 reciprocal): one thread per (sample, column) of max(nz, ntemb)
+__global__ void q_noise_glue_kernel(const float* __restrict__ u, const float* __restrict__ z,
+                                    const float* __restrict__ eps, int B, int nz, float lmin, float lmax,
+                                    const float* __restrict__ freqs, int ntemb, float* __restrict__ logsnr,
+                                    float* __restrict__ zt, float* __restrict__ temb) {
+  const int W = max(nz, ntemb);
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * W) return;
+  const int n = (int)(i / W), j = (int)(i - (long)n * W);
+  // logsnr_schedule_fn (diffusion_helper_func.py:41-50)
+  const float b = atanf(expf(mul_rn(-0.5f, lmax)));
+  const float a = sub_rn(atanf(expf(mul_rn(-0.5f, lmin))), b);
+  const float l = mul_rn(-2.0f, logf(tanf(add_rn(mul_rn(a, u[n]), b))));
+  if (j == 0 && logsnr) logsnr[n] = l;
+  if (j < nz) {  // diffusion_forward (:72-78): zt = z sqrt(sigmoid(l)) + sqrt(sigmoid(-l)) eps
+    const float sp = 1.0f / add_rn(1.0f, expf(-l)), sm = 1.0f / add_rn(1.0f, expf(l));
+    const long o = (long)n * nz + j;
+    zt[o] = add_rn(mul_rn(z[o], sqrtf(sp)), mul_rn(sqrtf(sm), eps[o]));
+  }
+  const int half = ntemb / 2;
+  if (j < half) {  // t_in = arctan(exp(-0.5 clamp(l, -20, 20))) / (pi / 2); x *= 1000 / max_time (max_time 1)
+    const float c = fminf(fmaxf(l, -20.0f), 20.0f);
+    const float t = mul_rn(mul_rn(atanf(expf(mul_rn(-0.5f, c))), 1.0f / 1.5707963267948966f), 1000.0f);
+    const float ang = mul_rn(t, freqs[j]);
+    temb[(long)n * ntemb + j] = (float)sin((double)ang);
+    temb[(long)n * ntemb + half + j] = (float)cos((double)ang);
+  }
+}
+
+// loss = 0.5 sum_j (eps - pred)^2 per sample (diffusion_net.py:642), and its gradient w.r.t. pred for an incoming
+// dL/dloss g: -((0.5 g) (2 (eps - pred))) as autograd's mul / sum / pow / sub backward rounds it
+__global__ void q_loss_fwd_kernel(const float* __restrict__ eps, const float* __restrict__ pred, int B, int nz,
+                                  float* __restrict__ loss) {
+  const int n = blockIdx.x, lane = threadIdx.x;
+  float acc = 0.f;
+  for (int j = lane; j < nz; j += 64) {
+    const float d = sub_rn(eps[(long)n * nz + j], pred[(long)n * nz + j]);
+    acc = add_rn(acc, mul_rn(d, d));
+  }
+  for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) loss[n] = mul_rn(0.5f, acc);
+}
+__global__ void q_loss_bwd_kernel(const float* __restrict__ eps, const float* __restrict__ pred,
+                                  const float* __restrict__ g, long gstride, int B, int nz, float* __restrict__ gpred) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * nz) return;
+  const int n = (int)(i / nz);
+  const float d = sub_rn(eps[i], pred[i]);
+  gpred[i] = -mul_rn(mul_rn(g[n * gstride], 0.5f), mul_rn(2.0f, d));
+}
+}  // namespace
+}  // namespace damc
+
+extern "C" int damc_q_noise_glue(const float* u, const float* z, const float* eps, int batch, int nz,
+                                 float logsnr_min, float logsnr_max, const float* freqs, int ntemb, float* logsnr,
+                                 float* zt, float* temb_in, void* stream) {
+  if (!u || !z || !eps || !freqs || !zt || !temb_in || batch <= 0 || nz <= 0 || ntemb < 2 || ntemb % 2)
+    return DAMC_ERR_ARG;
+  const long n = (long)batch * std::max(nz, ntemb);
+  hipLaunchKernelGGL(damc::q_noise_glue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), u,
+                     z, eps, batch, nz, logsnr_min, logsnr_max, freqs, ntemb, logsnr, zt, temb_in);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_q_loss_forward(const float* eps, const float* eps_pred, int batch, int nz, float* loss,
+                                   void* stream) {
+  if (!eps || !eps_pred || !loss || batch <= 0 || nz <= 0) return DAMC_ERR_ARG;
+  hipLaunchKernelGGL(damc::q_loss_fwd_kernel, dim3((unsigned)batch), dim3(64), 0, as_stream(stream), eps, eps_pred,
+                     batch, nz, loss);
+  return (int)hipGetLastError();
+}
+
+extern "C" int damc_q_loss_backward(const float* eps, const float* eps_pred, const float* grad_loss,
+                                    long grad_stride, int batch, int nz, float* grad_eps_pred, void* stream) {
+  if (!eps || !eps_pred || !grad_loss || !grad_eps_pred || batch <= 0 || nz <= 0 || grad_stride < 0)
+    return DAMC_ERR_ARG;
+  const long n = (long)batch * nz;
+  hipLaunchKernelGGL(damc::q_loss_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), eps,
+                     eps_pred, grad_loss, grad_stride, batch, nz, grad_eps_pred);
+  return (int)hipGetLastError();
+}
 
 using damc::DW;
 

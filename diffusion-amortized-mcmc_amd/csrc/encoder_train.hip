@@ -71,21 +71,6 @@ int up_split(int ho, int wo, int cin, int cout, int Bp, int* S, int* kper) {
   return 0;
 }
 
-// (co, (ky,kx,ci)) -> PyTorch (co, ci, ky, kx)
-__global__ void permute_dense_kernel(const float* __restrict__ g, int cout, int cin, int k, float* __restrict__ dw) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long n = (long)cout * cin * k * k;
-  if (i >= n) return;
-  long t = i;
-  const int kx = (int)(t % k);
-  t /= k;
-  const int ky = (int)(t % k);
-  t /= k;
-  const int ci = (int)(t % cin);
-  const int co = (int)(t / cin);
-  dw[i] = g[(long)co * k * k * cin + ((long)ky * k + kx) * cin + ci];
-}
-
 // NHWC (B, H, W, C) -> (B, H2, W2, C) with zeros beyond H x W (H2 >= H, W2 >= W), or the crop back (H2 <= H)
 __global__ void pad_crop_kernel(const float* __restrict__ x, int B, int H, int W, int C, float* __restrict__ y, int H2,
                                 int W2) {
@@ -105,6 +90,17 @@ int pad_crop(const float* x, int B, int H, int W, int C, float* y, int H2, int W
   const long n = (long)B * H2 * W2 * C;
   hipLaunchKernelGGL(pad_crop_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, B, H, W, C, y, H2, W2);
   return (int)hipGetLastError();
+}
+
+// per sample b: y[b][j][i] = x[b][i][j] for an R x C matrix (the dense last conv's (tap, ci) <-> (ci, tap) orders);
+// one thread per output element, outputs contiguous
+__global__ void batch_transpose_kernel(const float* __restrict__ x, int nb, int R, int C, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)R * C;
+  if (i >= nb * per) return;
+  const long b = i / per;
+  const int o = (int)(i - b * per), j = o / R, r = o - j * R;
+  y[i] = x[b * per + (long)r * C + j];
 }
 
 // (n, c) -> (c, n)
@@ -215,8 +211,8 @@ size_t carve(int B, int hin, int win, int cin, int cout, int k, int stride, int 
   } else if (c == CASE_DENSE) {
     const long KK = (long)k * k * cin;
     t.dyT = cv.take<float>((size_t)cout * B);
-    t.g = cv.take<float>((size_t)cout * KK);
-    t.wk = cv.take<float>((size_t)cout * KK);
+    t.g = cv.take<float>((size_t)B * KK);   // x in (ci, ky, kx) order per sample
+    t.wk = cv.take<float>((size_t)B * KK);  // dx in (ci, ky, kx) order per sample
   }
   if (b) *b = t;
   return c == CASE_NONE ? 0 : cv.off;
@@ -288,8 +284,15 @@ int backward_up(const float* x, const float* dy, const float* w, int B, int hin,
   a.Wout = win;
   a.act = DAMC_ACT_NONE;
   if (up_x3(cin, cout)) {
-    if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
-    a.A3 = t.dy3;
+    // dy staged as fp32 and split into limbs in registers (gemm.hip X3_F32A; bitwise the limb copy, no split launch);
+    // DAMC_ENC_BWD_F32A=0 (read per call) gathers the limbs of launch_split_x3
+    const char* ef = getenv("DAMC_ENC_BWD_F32A");
+    if (!(ef && ef[0] == '0')) {
+      a.a_f32 = 1;
+    } else {
+      if ((rc = launch_split_x3(dy, M * cout, t.dy3, s))) return rc;
+      a.A3 = t.dy3;
+    }
     a.B3 = reinterpret_cast<const unsigned short*>(t.wf + n);
     a.b_negblk = 1;  // damc_pack_generator_layer's x3 copy (up_view(...)'s forward sign block: generator.hip up2_negk_fwd)
     a.negk = x3_conv_negk((long)ho * wo, cin, 4 * cout, 4);
@@ -339,16 +342,21 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     return launch_smallc_wgrad(L, dy, x, B, t.part, t.tmp, dw, s);
   }
   if (cs == CASE_DENSE) {
-    const int KK = k * k * cin;
-    // dW = dy^T X (X = the NHWC input as (B, k*k*cin), (ky,kx,ci) order), then permuted to (co, ci, ky, kx)
+    // round 5: both products run in PyTorch's (ci, ky, kx) weight order, so neither the 8.4 M-weight gradient nor the
+    // weight itself is permuted (33.5 MB each way for Encoder_cifar10's last conv, 26 + 33 us); the B x k*k*cin
+    // input and input gradient are transposed per sample instead (4 MB at B = 128)
+    const int KK = k * k * cin, T = k * k;
+    const long nx = (long)B * KK;
+    // dW (co, (ci,ky,kx)) = dy^T X', X' = the NHWC input per sample in (ci, ky, kx) order
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)(((long)B * cout + 255) / 256)), dim3(256), 0, s, dy, B, cout,
                        t.dyT);
+    hipLaunchKernelGGL(batch_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s, x, B, T, cin, t.g);
     GemmArgs a;
     a.A = t.dyT;
     a.lda = B;
-    a.B = x;
+    a.B = t.g;
     a.ldb = KK;
-    a.C = t.g;
+    a.C = dw;
     a.ldc = KK;
     a.M = cout;
     a.N = KK;
@@ -359,18 +367,13 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     rc = launch_small_gemm(a.A, a.lda, a.B, a.ldb, nullptr, a.C, a.ldc, a.M, a.N, a.K, s);
     if (rc == DAMC_ERR_UNSUPPORTED) rc = launch_gemm(a, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_wgrad", 2.0 * cout * KK * B, s);
     if (rc) return rc;
-    const long n = (long)cout * KK;
-    hipLaunchKernelGGL(permute_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)t.g,
-                       cout, cin, k, dw);
-    if (dx) {  // dX = dy W, W as (co, (ky,kx,ci)) = the K-major conv packing
-      if ((rc = damc_pack_conv2d(w, cout, cin, k, t.wk, stream))) return rc;
-      if (!conv_kmajor_ok(cin)) return DAMC_ERR_UNSUPPORTED;  // damc_pack_conv2d chose the other layout
+    if (dx) {  // dX' = dy W with W (co, (ci,ky,kx)) as stored, then back to NHWC per sample
       GemmArgs d;
       d.A = dy;
       d.lda = cout;
-      d.B = t.wk;
+      d.B = w;
       d.ldb = KK;
-      d.C = dx;
+      d.C = t.wk;
       d.ldc = KK;
       d.M = B;
       d.N = KK;
@@ -379,6 +382,8 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
       rc = launch_small_gemm(d.A, d.lda, d.B, d.ldb, nullptr, d.C, d.ldc, d.M, d.N, d.K, s);
       if (rc == DAMC_ERR_UNSUPPORTED) rc = launch_gemm(d, A_DENSE, EPI_STORE, O_DENSE, 1, "enc_dgrad", 2.0 * B * KK * cout, s);
       if (rc) return rc;
+      hipLaunchKernelGGL(batch_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s,
+                         (const float*)t.wk, B, cin, T, dx);
     }
     return (int)hipGetLastError();
   }

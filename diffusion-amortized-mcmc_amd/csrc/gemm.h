@@ -269,6 +269,26 @@ int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double
 // fp32 products, fp32 accumulation
 int launch_small_gemm(const float* A, long lda, const float* B, long ldb, const float* bias, float* C, long ldc, int M,
                       int N, int K, hipStream_t s, int bias_mod = 0, int act = DAMC_ACT_NONE, float slope = 0.f);
+// up to SG_GROUP_MAX independent small GEMMs in one launch (gemm.hip small_gemm_group_kernel): one 16 x 16 tile per
+// 4-wave workgroup, K split over the waves, partials summed in a fixed order; a_ones (M = 1): A is a row of ones (C =
+// column sums of B)
+struct SmallGemm {
+  const float* A = nullptr;
+  const float* B = nullptr;
+  const float* bias = nullptr;
+  float* C = nullptr;
+  long lda = 0, ldb = 0, ldc = 0;
+  int M = 0, N = 0, K = 0, bias_mod = 0, act = DAMC_ACT_NONE;
+  float slope = 0.f;
+  int a_ones = 0;
+};
+constexpr int SG_GROUP_MAX = 8;
+struct SmallGemmGroup {
+  int n;
+  int tile_end[SG_GROUP_MAX];
+  SmallGemm d[SG_GROUP_MAX];
+};
+int launch_small_gemm_group(const SmallGemm* g, int n, hipStream_t s);
 int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const char* prof_name, double flops,
                 hipStream_t s);
 

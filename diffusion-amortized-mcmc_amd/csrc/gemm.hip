@@ -476,6 +476,86 @@ int launch_small_gemm(const float* A, long lda, const float* B, long ldb, const 
   return (int)hipGetLastError();
 }
 
+// Up to SG_GROUP_MAX independent small GEMMs (SmallGemm, gemm.h) in ONE launch, one 16 x 16 output tile per 4-wave
+// workgroup with K split over the waves in four contiguous runs of 16-k steps (a quarter of the single-wave kernel's
+// dependent load rounds), the wave partials summed in LDS in a fixed order ((w0 + w1) + w2) + w3.  a_ones: A is a row of
+// ones (M = 1): C = the column sums of B, the bias gradients of the denoiser's Linears as one more member of the group.
+template <int KU>
+__global__ __launch_bounds__(256) void small_gemm_group_kernel(SmallGemmGroup g) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int blk = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < g.n && blk >= g.tile_end[gi]) ++gi;  // workgroup-uniform
+  const SmallGemm& D = g.d[gi];
+  const int tile = blk - (gi ? g.tile_end[gi - 1] : 0);
+  const int M = D.M, N = D.N, K = D.K;
+  const int ntn = (N + 15) >> 4;
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int m = lane & 15, q = lane >> 4;
+  const int row = tm * 16 + m, col = tn * 16 + m;
+  const bool rok = row < M, cok = col < N;
+  const float* Ar = D.A + (long)(rok && !D.a_ones ? row : 0) * D.lda;
+  const float* Bc = D.B + (cok ? col : 0);
+  const long ldb = D.ldb;
+  const int k16 = (K + 15) >> 4, per = (k16 + 3) >> 2;
+  const int kb = wave * per * 16, ke = min(K, kb + per * 16);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += 16 * KU) {
+    f32x4 a[KU], b[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {  // K % 4 == 0: a lane's 4 k are all in range or all out
+      const int k = k0 + 16 * u + 4 * q;
+      const bool kin = k < ke;
+      const int kk = kin ? k : 0;
+      a[u] = D.a_ones ? f32x4{1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(Ar + kk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[u][e] = Bc[(long)(kk + e) * ldb];
+      if (!(rok && kin)) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!(cok && kin)) b[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][e], b[u][e], acc, 0, 0, 0);
+  }
+  if (wave) red[wave - 1][lane] = acc;
+  __syncthreads();
+  if (wave || !cok) return;
+  acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
+  const float bv = D.bias ? D.bias[D.bias_mod > 0 ? col % D.bias_mod : col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = tm * 16 + 4 * q + r;
+    if (rr < M) D.C[(long)rr * D.ldc + col] = act_apply(acc[r] + bv, D.act, D.slope);
+  }
+}
+
+int launch_small_gemm_group(const SmallGemm* g, int n, hipStream_t s) {
+  if (n < 1 || n > SG_GROUP_MAX) return DAMC_ERR_ARG;
+  SmallGemmGroup grp{};
+  long tot = 0;
+  double flops = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const SmallGemm& d = g[i];
+    if ((!d.A && !d.a_ones) || !d.B || !d.C || d.M <= 0 || d.N <= 0 || d.K <= 0 || d.ldb < d.N || d.ldc < d.N ||
+        (d.a_ones && d.M != 1) || (!d.a_ones && d.lda < d.K))
+      return DAMC_ERR_ARG;
+    if (d.K % 4 != 0 || (!d.a_ones && (d.lda % 4 != 0 || (reinterpret_cast<uintptr_t>(d.A) & 15) != 0)))
+      return DAMC_ERR_UNSUPPORTED;  // f32x4 A
+    grp.d[i] = d;
+    tot += (long)((d.M + 15) / 16) * ((d.N + 15) / 16);
+    if (tot >= (1L << 31)) return DAMC_ERR_UNSUPPORTED;
+    grp.tile_end[i] = (int)tot;
+    flops += 2.0 * d.M * d.N * d.K;
+  }
+  grp.n = n;
+  ProfScope ps("small_gemm_group", flops, s);
+  hipLaunchKernelGGL(small_gemm_group_kernel<4>, dim3((unsigned)tot), dim3(256), 0, s, grp);
+  return (int)hipGetLastError();
+}
+
 // ================================================================================================
 // K-major convolution engine (A_CONV with Cg % 32 == 0, B packed [n][k]).
 //

@@ -100,39 +100,59 @@ int launch_transpose_x3(const float* src32, const unsigned short* src3, int B, i
 }
 
 // ------------------------------------------------------------------------------ k4 s2 p1 slab reduce
-// one thread per (ci, co): the 16 taps, each a fixed-order sum over the split-K slices; tap (ky, kx)
-// comes from phase (py, px) = ((ky+1)&1, (kx+1)&1) and GEMM row (ty, tx) with ky = 3 - py - 2 ty
+// each of the 16 taps a fixed-order sum over the split-K slices; tap (ky, kx) comes from phase (py, px) =
+// ((ky+1)&1, (kx+1)&1) and GEMM row (ty, tx) with ky = 3 - py - 2 ty.  One workgroup per (ci, 16 consecutive co): thread (tap, co) sums its S slab values in order (16 co = one 64-B run
+// per tap), the 16 x 16 results go through LDS and leave as the 1 KB contiguous run dW[ci][co0 .. co0 + 15][16 taps]
+// (round 5: one thread per (ci, co) walking all 16 taps left the encoder's 64 -> 128 conv 8192 threads of 256 slab
+// loads each, 62 us; same sums, same order)
 __global__ __launch_bounds__(256) void up2_wgrad_reduce_kernel(const float* __restrict__ slabs, int S, int Cin,
                                                                int Cout, float* __restrict__ dW) {
+  __shared__ float t16[16][17];
+  const int ng = Cout / 16;
+  const int ci = blockIdx.x / ng, co0 = (blockIdx.x - ci * ng) * 16;
+  const int tap = threadIdx.x >> 4, cl = threadIdx.x & 15;
+  const int ky = tap >> 2, kx = tap & 3;
+  const long M = 4L * Cin;
+  const int py = (ky + 1) & 1, ty = (3 - ky - py) >> 1;
+  const int px = (kx + 1) & 1, tx = (3 - kx - px) >> 1;
+  const int ph = py * 2 + px, t = ty * 2 + tx;
+  const float* sp = slabs + ((long)ph * S * M + (long)t * Cin + ci) * Cout + co0 + cl;
+  float acc = 0.f;
+  for (int sl = 0; sl < S; ++sl) acc += sp[(long)sl * M * Cout];
+  t16[cl][tap] = acc;
+  __syncthreads();
+  dW[((long)ci * Cout + co0) * 16 + threadIdx.x] = t16[threadIdx.x >> 4][threadIdx.x & 15];
+}
+
+// any Cout: one thread per (ci, co), all 16 taps
+__global__ __launch_bounds__(256) void up2_wgrad_reduce_any_kernel(const float* __restrict__ slabs, int S, int Cin,
+                                                                   int Cout, float* __restrict__ dW) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)Cin * Cout) return;
   const int ci = (int)(i / Cout), co = (int)(i - (long)ci * Cout);
   const long M = 4L * Cin;
-  float out[16];
 #pragma unroll
-  for (int ky = 0; ky < 4; ++ky) {
+  for (int tap = 0; tap < 16; ++tap) {
+    const int ky = tap >> 2, kx = tap & 3;
     const int py = (ky + 1) & 1, ty = (3 - ky - py) >> 1;
-#pragma unroll
-    for (int kx = 0; kx < 4; ++kx) {
-      const int px = (kx + 1) & 1, tx = (3 - kx - px) >> 1;
-      const int ph = py * 2 + px, t = ty * 2 + tx;
-      const float* sp = slabs + ((long)ph * S * M + (long)t * Cin + ci) * Cout + co;
-      float acc = 0.f;
-      for (int sl = 0; sl < S; ++sl) acc += sp[(long)sl * M * Cout];
-      out[ky * 4 + kx] = acc;
-    }
+    const int px = (kx + 1) & 1, tx = (3 - kx - px) >> 1;
+    const int ph = py * 2 + px, t = ty * 2 + tx;
+    const float* sp = slabs + ((long)ph * S * M + (long)t * Cin + ci) * Cout + co;
+    float acc = 0.f;
+    for (int sl = 0; sl < S; ++sl) acc += sp[(long)sl * M * Cout];
+    dW[i * 16 + tap] = acc;
   }
-  f32x4* o = reinterpret_cast<f32x4*>(dW + i * 16);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) o[q] = f32x4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
 }
 
 int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float* dW, hipStream_t s) {
   if (!slabs || !dW || S < 1 || Cin <= 0 || Cout <= 0 || (uintptr_t)dW % 16 != 0) return DAMC_ERR_ARG;
   const long n = (long)Cin * Cout;
   ProfScope ps("wgrad_reduce", 0.0, s);
-  hipLaunchKernelGGL(up2_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slabs, S, Cin,
-                     Cout, dW);
+  if (Cout % 16 == 0)
+    hipLaunchKernelGGL(up2_wgrad_reduce_kernel, dim3((unsigned)(n / 16)), dim3(256), 0, s, slabs, S, Cin, Cout, dW);
+  else
+    hipLaunchKernelGGL(up2_wgrad_reduce_any_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slabs, S, Cin,
+                       Cout, dW);
   return (int)hipGetLastError();
 }
 
@@ -196,9 +216,12 @@ static long colsum_blocks(long R, int C) {
 }
 // float4 form: 256 row blocks at most (32 float4 rows per thread per pass at R = 131072, C = 64), one pass up to 32
 // rows per thread
+// at most 16 float4 lanes (64 channels) per workgroup: 16 row lanes, so a B = 128-row sum is 8 loads per thread across
+// C / 64 workgroups (round 5: 64 lanes left 4 row lanes walking 32 rows each in ONE workgroup, 6-12 us per call for the
+// Q update's 29 bias / InstanceNorm column sums)
 static int colsum4_lanes(int C4) {
   int cl = 1;
-  while (cl < C4 && cl < 64) cl <<= 1;
+  while (cl < C4 && cl < 16) cl <<= 1;
   return cl;
 }
 static long colsum4_blocks(long R, int C) {

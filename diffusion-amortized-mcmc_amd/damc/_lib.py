@@ -137,6 +137,9 @@ _SIGS = {
     "damc_denoiser_train_forward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _P, _P, _I, _P, _P, _SZ, _P]),
     "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
                                           _P, _P, _SZ, _P]),
+    "damc_q_noise_glue": (_I, [_P, _P, _P, _I, _I, _F, _F, _P, _I, _P, _P, _P, _P]),
+    "damc_q_loss_forward": (_I, [_P, _P, _I, _I, _P, _P]),
+    "damc_q_loss_backward": (_I, [_P, _P, _P, ctypes.c_long, _I, _I, _P, _P]),
     "damc_prior_langevin": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _P]),
     "damc_prior_langevin_engine": (_I, [ctypes.POINTER(Ebm), _P, _I, _I, _D, _I, _P, _U64, _U64, _U64, _P, _I, _P]),
     "damc_ebm_mfma_min_chains": (_I, []),

@@ -17,6 +17,7 @@ requiring grad) it is the plain HIP forward.
 """
 import contextlib
 import ctypes
+import os
 import weakref
 
 import torch
@@ -228,6 +229,70 @@ def denoiser_apply(p, zt, se, xemb):
     xemb and p's parameters (Diffusion_UnetA.forward, diffusion_net.py:477-533)."""
     params = [t for _, _, t in _denoiser_params(p)]
     return _DenoiserTrainFn.apply(zt, se, xemb, p, *params)
+
+
+# Q.calculate_loss's noising glue and loss on libdamc (q_noise_glue / q_loss); DAMC_Q_GLUE=0 at import keeps the
+# reference's torch ops around the denoiser (A/B)
+Q_GLUE = os.environ.get("DAMC_Q_GLUE") != "0"
+
+
+def _freqs(half, device):
+    """SinusoidalPosEmb's frequency table, computed as the drop-in computes it (host fp32 ops, then moved)."""
+    from src.diffusion_net import SinusoidalPosEmb
+
+    key = (half, str(device))
+    f = SinusoidalPosEmb._FREQS.get(key)
+    if f is None:
+        import math
+
+        f = torch.exp(torch.arange(half) * (-math.log(10000) / (half - 1))).to(device)
+        SinusoidalPosEmb._FREQS[key] = f
+    return f
+
+
+def q_noise_glue(q, u, z, eps, logsnr_out=None):
+    """(zt, temb_in) of Q.calculate_loss (diffusion_net.py:633-639, 486-491) in one launch (damc_q_noise_glue): the
+    schedule's logsnr of u, the forward-diffused zt = mean + std * eps and the denoiser's sinusoidal time embedding.
+    No gradient flows through any of it (u and eps are fresh draws; the caller keeps z without grad)."""
+    B, nz = z.shape
+    ntemb = q.p.ntemb
+    dev = z.device
+    zt = torch.empty(B, nz, dtype=torch.float32, device=dev)
+    se = torch.empty(B, ntemb, dtype=torch.float32, device=dev)
+    check(_lib.lib().damc_q_noise_glue(ptr(u), ptr(z), ptr(eps), B, nz, float(q.logsnr_min), float(q.logsnr_max),
+                                       ptr(_freqs(ntemb // 2, dev)), ntemb, ptr(logsnr_out), ptr(zt), ptr(se),
+                                       _lib.stream_ptr(dev)), "damc_q_noise_glue")
+    return zt, se
+
+
+class _QLossFn(torch.autograd.Function):
+    """0.5 * sum((eps - eps_pred) ** 2, dim=1) (diffusion_net.py:642) as one kernel each way."""
+
+    @staticmethod
+    def forward(ctx, eps, pred):
+        B, nz = pred.shape
+        loss = torch.empty(B, dtype=torch.float32, device=pred.device)
+        check(_lib.lib().damc_q_loss_forward(ptr(eps), ptr(pred), B, nz, ptr(loss), _lib.stream_ptr(pred.device)),
+              "damc_q_loss_forward")
+        ctx.save_for_backward(eps, pred)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        eps, pred = ctx.saved_tensors
+        B, nz = pred.shape
+        g = g.to(torch.float32)
+        stride = g.stride(0) if g.dim() == 1 else 0
+        if g.dim() == 1 and stride != 0 and not g.is_contiguous():
+            g, stride = g.contiguous(), 1
+        gp = torch.empty_like(pred)
+        check(_lib.lib().damc_q_loss_backward(ptr(eps), ptr(pred), ptr(g), stride, B, nz, ptr(gp),
+                                              _lib.stream_ptr(pred.device)), "damc_q_loss_backward")
+        return None, gp
+
+
+def q_loss(eps, eps_pred):
+    return _QLossFn.apply(eps.contiguous(), eps_pred)
 
 
 # ------------------------------------------------------------------------------- Q update: encoder

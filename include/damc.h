@@ -370,6 +370,21 @@ int damc_denoiser_train_backward(const damc_denoiser_train_t* d, const float* gr
                                  const damc_denoiser_grads_t* grads, float* grad_zt, float* grad_xemb,
                                  void* workspace, size_t workspace_bytes, void* stream);
 
+/* The rest of Q.calculate_loss around the denoiser (round 5; workspace/src/diffusion_net.py:633-642, no gradient
+ * flows through any of it): from u (B) ~ U[0,1) (the caller's torch.rand, :633) and eps (B, nz) (torch.randn_like,
+ * :636), logsnr (B) = logsnr_schedule_fn(u) (diffusion_helper_func.py:41-50; may be NULL), zt (B, nz) = the
+ * diffusion_forward mean + std * eps (:72-78), temb_in (B, ntemb) = SinusoidalPosEmb of Diffusion_UnetA's logsnr input
+ * (diffusion_net.py:447-461, 490-491) with freqs (ntemb / 2) the host's fp32 frequency table; one launch for what the
+ * reference issues as ~25 elementwise ops, each op rounded as PyTorch's ROCm kernels round it. */
+int damc_q_noise_glue(const float* u, const float* z, const float* eps, int batch, int nz, float logsnr_min,
+                      float logsnr_max, const float* freqs, int ntemb, float* logsnr, float* zt, float* temb_in,
+                      void* stream);
+/* loss (B) = 0.5 * sum_j (eps - eps_pred)^2 (diffusion_net.py:642), and grad_eps_pred (B, nz) from grad_loss (B, element
+ * stride grad_stride: 0 for the broadcast gradient of a .mean()) */
+int damc_q_loss_forward(const float* eps, const float* eps_pred, int batch, int nz, float* loss, void* stream);
+int damc_q_loss_backward(const float* eps, const float* eps_pred, const float* grad_loss, long grad_stride, int batch,
+                         int nz, float* grad_eps_pred, void* stream);
+
 /* --------------------------------------------------------------------------- optimiser steps
  * Replaces the G/E/Q updates' torch.nn.utils.clip_grad_norm_ + optim.Adam / optim.AdamW.step()
  * (train_gen_recon.py:155-157, 219-231, 240-241) by multi-tensor kernels.  A launch covers up to

@@ -388,3 +388,43 @@ def test_generator_second_backward_is_refused(gpu_device):
     b, _, _ = _hip_grads(G, z, x)
     for u, v in zip(a, b):
         assert np.array_equal(u, v)
+
+
+def test_q_noise_glue_matches_torch_ops(gpu_device):
+    """damc_q_noise_glue (logsnr schedule, forward diffusion, SinusoidalPosEmb of the logsnr input in one launch) and
+    damc_q_loss_* against the drop-in's torch ops on the same GPU tensors (diffusion_helper_func.py:41-50, 72-78,
+    diffusion_net.py:447-461, 486-491, 642): zt and the loss to fp32 rounding, the embedding to 1e-4 absolute (its
+    ~1000 rad arguments turn an ulp of the logsnr input into ~6e-5 of angle)."""
+    from damc import synth, training
+    from src import diffusion_helper_func as dh
+    from src import diffusion_net as dn
+
+    B, nz = 128, 128
+    Q = dn._netQ_U(nc=3, nz=nz, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=100,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0, net_arch="A",
+                   dataset="cifar10").to(gpu_device)
+    u = torch.from_numpy(synth.uniform_f32(71, 0, (B,), 0.0, 1.0)).to(gpu_device)
+    z = torch.from_numpy(synth.normal_f32(71, 1, (B, nz))).to(gpu_device)
+    eps = torch.from_numpy(synth.normal_f32(71, 2, (B, nz))).to(gpu_device)
+    lg = torch.empty(B, device=gpu_device)
+    zt, se = training.q_noise_glue(Q, u, z, eps, logsnr_out=lg)
+    l = dh.logsnr_schedule_fn(u, logsnr_max=Q.logsnr_max, logsnr_min=Q.logsnr_min)
+    fwd = dh.diffusion_forward(z, logsnr=l.reshape(B, 1))
+    zt_ref = fwd["mean"] + fwd["std"] * eps
+    t_in = torch.arctan(torch.exp(-0.5 * torch.clamp(l, min=-20.0, max=20.0))) / (0.5 * np.pi)
+    se_ref = Q.p.time_mlp[0](t_in)
+    dl = float(((lg - l).abs() / l.abs().clamp_min(1e-30)).max())
+    # zt = mean + std * eps cancels for some elements: its error is measured against |mean| + |std * eps|
+    dz = float(((zt - zt_ref).abs() / (fwd["mean"].abs() + (fwd["std"] * eps).abs())).max())
+    ds = float((se - se_ref).abs().max())
+    print("logsnr max rel %.2e (bitwise %s), zt max rel %.2e (bitwise %s), temb max abs %.2e (bitwise %s)"
+          % (dl, bool(torch.equal(lg, l)), dz, bool(torch.equal(zt, zt_ref)), ds, bool(torch.equal(se, se_ref))))
+    assert dl < 5e-7 and dz < 5e-7 and ds < 2.5e-4
+    pred = (zt_ref * 0.3).requires_grad_(True)
+    loss = training.q_loss(eps, pred)
+    loss.mean().backward()
+    pr = pred.detach().clone().requires_grad_(True)
+    loss_ref = 0.5 * torch.sum((eps - pr) ** 2, dim=1)
+    loss_ref.mean().backward()
+    assert rel_l2(loss.detach().cpu().numpy(), loss_ref.detach().cpu().numpy()) < 1e-6
+    assert rel_l2(pred.grad.cpu().numpy(), pr.grad.cpu().numpy()) < 1e-6

@@ -1,12 +1,11 @@
 #!/usr/bin/env python
-"""One Q update on the HIP path (bench.py q_update_bench's step_hip: Q.calculate_loss(x, z, mask).mean().backward()
-+ damc.optim's fused clip + AdamW; train_gen_recon.py:211-220) at the bench config (CIFAR-10 B=128, nif 64, nxemb 1024,
-ntemb 128), for rocprofv3 --kernel-trace --stats: 3 warm-up updates, then `calls` updates between two
-synchronisations (their kernels are the ones a trace window should take).  usage: python tools/q_update_trace.py
-[calls]"""
+"""Host-side profile of the Q update (tools/q_update_trace.py's step: Q.calculate_loss(...).mean().backward() +
+damc.optim's fused clip + AdamW) at the bench config: cProfile over `calls` updates after 3 warm-up updates, the top
+functions by own time and by cumulative time.  usage: python tools/q_update_hostprof.py [calls]"""
+import cProfile
 import os
+import pstats
 import sys
-import time
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(HERE, "diffusion-amortized-mcmc_amd"), HERE]
@@ -16,7 +15,7 @@ from damc import optim as dopt  # noqa: E402
 from damc import synth  # noqa: E402
 from src import diffusion_net as dn  # noqa: E402
 
-calls = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+calls = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 B, NZ = 128, 128
 dev = torch.device("cuda:0")
 Q = dn._netQ_U(nc=3, nz=NZ, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=100, logsnr_min=-5.1,
@@ -38,12 +37,12 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-a.record()
-t0 = time.perf_counter()
+pr = cProfile.Profile()
+pr.enable()
 for _ in range(calls):
     step()
-host = (time.perf_counter() - t0) * 1e3 / calls
-b.record()
-b.synchronize()
-print("Q update B=%d: %.3f ms per update (host submission %.3f ms per update)" % (B, a.elapsed_time(b) / calls, host))
+pr.disable()
+torch.cuda.synchronize()
+st = pstats.Stats(pr)
+st.sort_stats("tottime").print_stats(45)
+st.sort_stats("cumulative").print_stats(45)
