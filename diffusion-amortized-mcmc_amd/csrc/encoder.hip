@@ -849,6 +849,7 @@ extern "C" int damc_instnorm_lrelu_backward_nhwc(const float* y, const float* st
                      slope, (const float*)part, dy, bc);
   DAMC_LAUNCH_CHECK();
   // dgamma = sum_b bc[b][0][c], dbeta = sum_b bc[b][1][c]: fixed-order column sums over the B rows
+  if (dgamma && dbeta) return damc::launch_colsum2(bc, B, 2 * c, 2L * c, dgamma, dbeta, c, tmp, s);
   if (dgamma) {
     int rc = damc::launch_colsum(bc, B, c, 2L * c, dgamma, tmp, s);
     if (rc) return rc;

@@ -228,11 +228,9 @@ int backward_up(const float* x, const float* dy, const float* w, int B, int hin,
   damc_layer_t L = up_view(hin, win, cin, cout, ho, wo);
   // weight gradient: O_WGRAD with the transposed view's roles (input = dy, output gradient = x)
   if ((rc = launch_transpose_x3(dy, nullptr, B, ho, wo, cout, ho, wo, 1, 1, 0, 0, Bp, t.tin, nullptr, s))) return rc;
-  for (int ph = 0; ph < 4; ++ph) {
-    rc = launch_transpose_x3(x, nullptr, B, hin, win, cin, ho, wo, 2, 2, ph >> 1, ph & 1, Bp,
-                             t.tdl + (size_t)ph * cin * P * Bp * 3, nullptr, s);
-    if (rc) return rc;
-  }
+  if ((rc = launch_transpose_x3_4ph(x, nullptr, B, hin, win, cin, ho, wo, Bp, t.tdl, (long)cin * P * Bp * 3, nullptr,
+                                    0, s)))
+    return rc;
   {
     int S, kp;
     up_split(ho, wo, cin, cout, Bp, &S, &kp);

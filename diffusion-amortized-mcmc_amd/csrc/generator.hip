@@ -2238,12 +2238,9 @@ int train_backward(const damc_generator_t* g, int B, const float* z, const float
       const float* d32 = d_x3 ? nullptr : d;
       const unsigned short* d3 = d_x3 ? ws.h3[i] : nullptr;
       if (up2) {  // the 4 output phases of the gradient, each on the input grid
-        for (int ph = 0; ph < 4; ++ph) {
-          rc = damc::launch_transpose_x3(d32, d3, B, L.hout, L.wout, L.cout, L.hin, L.win, 2, 2, ph >> 1, ph & 1, Bp,
-                                         tw.tdl + (size_t)ph * L.cout * P * Bp * 3,
-                                         db ? tw.part + (size_t)ph * P * nb * L.cout : nullptr, s);
-          if (rc) return rc;
-        }
+        rc = damc::launch_transpose_x3_4ph(d32, d3, B, L.hout, L.wout, L.cout, L.hin, L.win, Bp, tw.tdl,
+                                           (long)L.cout * P * Bp * 3, db ? tw.part : nullptr, (long)P * nb * L.cout, s);
+        if (rc) return rc;
       } else {  // PROJ: rows (co, output pixel) = the PyTorch (Cin, Cout, k, k) column order
         rc = damc::launch_transpose_x3(d32, d3, B, L.hout, L.wout, L.cout, L.hout, L.wout, 1, 1, 0, 0, Bp, tw.tdl,
                                        db ? tw.part : nullptr, s);

@@ -11,6 +11,11 @@ namespace damc {
 // block) channel sums: part[(pq * (Bp / 32) + nb) * C + c] (bias gradients, reduced by launch_colsum).
 int launch_transpose_x3(const float* src32, const unsigned short* src3, int B, int H, int W, int C, int Hq, int Wq,
                         int sy, int sx, int oy, int ox, int Bp, unsigned short* dst, float* part, hipStream_t s);
+// the four output phases of a k4 s2 p1 layer's gradient (sy = sx = 2, offsets (ph >> 1, ph & 1)) in one launch: phase ph
+// to dst + ph * dst_pstride (and part + ph * part_pstride when part is set)
+int launch_transpose_x3_4ph(const float* src32, const unsigned short* src3, int B, int H, int W, int C, int Hq, int Wq,
+                            int Bp, unsigned short* dst, long dst_pstride, float* part, long part_pstride,
+                            hipStream_t s);
 
 // dW (Cin, Cout, 4, 4) of a k4 s2 p1 ConvT from the O_WGRAD slabs [4 phases][S][4 * Cin][Cout]
 int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float* dW, hipStream_t s);
@@ -18,6 +23,10 @@ int launch_up2_wgrad_reduce(const float* slabs, int S, int Cin, int Cout, float*
 // out[c] = sum over r < R of X[r * ld + c], fixed order (two passes through tmp when R is large)
 size_t colsum_tmp_floats(long R, int C);
 int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s);
+// column sums of X (R x C) with columns < split into out_lo and the rest into out_hi[c - split] (one launch when a single
+// pass covers R; else two launch_colsum calls)
+int launch_colsum2(const float* X, long R, int C, long ld, float* out_lo, float* out_hi, int split, float* tmp,
+                   hipStream_t s);
 
 // Output-layer (Cout <= 4) weight gradient, direct: h NHWC fp32, delta NHWC [pix][Cout]; part and tmp are
 // scratch (per-block partials in the PyTorch order, reduced by launch_colsum)

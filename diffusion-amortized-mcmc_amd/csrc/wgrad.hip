@@ -19,15 +19,22 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf16_bits_to_f32(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
 
 // ---------------------------------------------------------------------------------------- transpose
-// grid (Hq*Wq, Bp/32, ceil(C/64)), 256 threads: a 32-sample x 64-channel tile of one pixel through LDS
+// grid (Hq*Wq, Bp/32, nph * ceil(C/64)), 256 threads: a 32-sample x 64-channel tile of one pixel through LDS.  nph = 4
+// (round 5): the four output phases (py, px) = (ph >> 1, ph & 1) of a k4 s2 p1 layer in one launch (offsets oy + py,
+// ox + px; phase ph writes dst + ph * dst_pstride and part + ph * part_pstride), instead of four launches
 template <bool X3>
 __global__ __launch_bounds__(256) void transpose_x3_kernel(const float* __restrict__ src32,
                                                            const unsigned short* __restrict__ src3, int B, int H,
                                                            int W, int C, int Wq, int sy, int sx, int oy, int ox,
                                                            int Bp, int P, unsigned short* __restrict__ dst,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, int ncb, long dst_pstride,
+                                                           long part_pstride) {
   __shared__ float tile[64][33];
-  const int pq = blockIdx.x, nb = blockIdx.y, cb = blockIdx.z;
+  const int pq = blockIdx.x, nb = blockIdx.y, ph = blockIdx.z / ncb, cb = blockIdx.z - ph * ncb;
+  oy += ph >> 1;
+  ox += ph & 1;
+  dst += ph * dst_pstride;
+  if (part) part += ph * part_pstride;
   const int qy = pq / Wq, qx = pq - qy * Wq;
   const int y = sy * qy + oy, x = sx * qx + ox;
   const int tid = threadIdx.x;
@@ -88,14 +95,36 @@ int launch_transpose_x3(const float* src32, const unsigned short* src3, int B, i
   if (src3 && C % 8 != 0) return DAMC_ERR_ARG;
   if ((uintptr_t)dst % 16 != 0) return DAMC_ERR_ARG;
   if (sy * (Hq - 1) + oy >= H || sx * (Wq - 1) + ox >= W || oy < 0 || ox < 0) return DAMC_ERR_ARG;
-  const dim3 grid((unsigned)(Hq * Wq), (unsigned)(Bp / 32), (unsigned)((C + 63) / 64));
+  const int ncb = (C + 63) / 64;
+  const dim3 grid((unsigned)(Hq * Wq), (unsigned)(Bp / 32), (unsigned)ncb);
   ProfScope ps("wgrad_transpose", 0.0, s);
   if (src3)
     hipLaunchKernelGGL(transpose_x3_kernel<true>, grid, dim3(256), 0, s, nullptr, src3, B, H, W, C, Wq, sy, sx, oy,
-                       ox, Bp, Hq * Wq, dst, part);
+                       ox, Bp, Hq * Wq, dst, part, ncb, 0L, 0L);
   else
     hipLaunchKernelGGL(transpose_x3_kernel<false>, grid, dim3(256), 0, s, src32, nullptr, B, H, W, C, Wq, sy, sx, oy,
-                       ox, Bp, Hq * Wq, dst, part);
+                       ox, Bp, Hq * Wq, dst, part, ncb, 0L, 0L);
+  return (int)hipGetLastError();
+}
+
+int launch_transpose_x3_4ph(const float* src32, const unsigned short* src3, int B, int H, int W, int C, int Hq, int Wq,
+                            int Bp, unsigned short* dst, long dst_pstride, float* part, long part_pstride,
+                            hipStream_t s) {
+  if ((!src32) == (!src3) || !dst || B <= 0 || C <= 0 || Hq <= 0 || Wq <= 0 || Bp < B || Bp % 32 != 0)
+    return DAMC_ERR_ARG;
+  if (src3 && C % 8 != 0) return DAMC_ERR_ARG;
+  if ((uintptr_t)dst % 16 != 0 || (dst_pstride * 2) % 16 != 0) return DAMC_ERR_ARG;
+  if (2 * (Hq - 1) + 1 >= H || 2 * (Wq - 1) + 1 >= W) return DAMC_ERR_ARG;
+  const int ncb = (C + 63) / 64;
+  if (4L * ncb > 65535) return DAMC_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)(Hq * Wq), (unsigned)(Bp / 32), (unsigned)(4 * ncb));
+  ProfScope ps("wgrad_transpose", 0.0, s);
+  if (src3)
+    hipLaunchKernelGGL(transpose_x3_kernel<true>, grid, dim3(256), 0, s, nullptr, src3, B, H, W, C, Wq, 2, 2, 0, 0, Bp,
+                       Hq * Wq, dst, part, ncb, dst_pstride, part_pstride);
+  else
+    hipLaunchKernelGGL(transpose_x3_kernel<false>, grid, dim3(256), 0, s, src32, nullptr, B, H, W, C, Wq, 2, 2, 0, 0,
+                       Bp, Hq * Wq, dst, part, ncb, dst_pstride, part_pstride);
   return (int)hipGetLastError();
 }
 
@@ -181,8 +210,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
 
 // the same sums four channels per thread (C % 4 == 0, ld % 4 == 0, 16-B aligned): CL4 float4 lanes of 4 channels,
 // 256 / CL4 row lanes (16 at C = 64 instead of 4), so both passes keep many more loads in flight per thread-row
+// out2 (single pass only): float4 columns from split4 on go to out2 instead (two gradients sharing one row layout)
 __global__ __launch_bounds__(256) void colsum4_kernel(const float* __restrict__ X, long R, int C4, long ld4, int CL4,
-                                                      long rows_per, float* __restrict__ out) {
+                                                      long rows_per, float* __restrict__ out,
+                                                      float* __restrict__ out2 = nullptr, int split4 = 0) {
   __shared__ f32x4 red[256];
   const int RL = 256 / CL4;
   const int cl = threadIdx.x % CL4, rl = threadIdx.x / CL4;
@@ -200,7 +231,12 @@ __global__ __launch_bounds__(256) void colsum4_kernel(const float* __restrict__ 
     if (rl < h) red[threadIdx.x] += red[threadIdx.x + h * CL4];
     __syncthreads();
   }
-  if (rl == 0 && c4 < C4) reinterpret_cast<f32x4*>(out)[(long)blockIdx.y * C4 + c4] = red[cl];
+  if (rl == 0 && c4 < C4) {
+    if (out2 && c4 >= split4)
+      reinterpret_cast<f32x4*>(out2)[c4 - split4] = red[cl];
+    else
+      reinterpret_cast<f32x4*>(out)[(long)blockIdx.y * C4 + c4] = red[cl];
+  }
 }
 
 static int colsum_lanes(int C) {
@@ -231,6 +267,23 @@ static long colsum4_blocks(long R, int C) {
 
 size_t colsum_tmp_floats(long R, int C) {
   return (size_t)std::max(colsum_blocks(R, C), colsum4_blocks(R, C)) * C;
+}
+
+int launch_colsum2(const float* X, long R, int C, long ld, float* out_lo, float* out_hi, int split, float* tmp,
+                   hipStream_t s) {
+  if (!X || !out_lo || !out_hi || split <= 0 || split >= C) return DAMC_ERR_ARG;
+  const bool one = C % 4 == 0 && split % 4 == 0 && ld % 4 == 0 && colsum4_blocks(R, C) == 1 &&
+                   ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out_lo) |
+                     reinterpret_cast<uintptr_t>(out_hi)) & 15) == 0;
+  if (!one) {  // two column sums
+    const int rc = launch_colsum(X, R, split, ld, out_lo, tmp, s);
+    return rc ? rc : launch_colsum(X + split, R, C - split, ld, out_hi, tmp, s);
+  }
+  ProfScope ps("bias_grad", 0.0, s);
+  const int C4 = C / 4, CL4 = colsum4_lanes(C4);
+  hipLaunchKernelGGL(colsum4_kernel, dim3((unsigned)((C4 + CL4 - 1) / CL4), 1), dim3(256), 0, s, X, R, C4, ld / 4, CL4,
+                     R, out_lo, out_hi, split / 4);
+  return (int)hipGetLastError();
 }
 
 int launch_colsum(const float* X, long R, int C, long ld, float* out, float* tmp, hipStream_t s) {

@@ -121,15 +121,29 @@ class Adam(torch.optim.Optimizer):
         super().__setstate__(state)
         self.last_grad_norm = None
 
+    def zero_grad(self, set_to_none=True):
+        """torch.optim.Optimizer.zero_grad; set_to_none (the default) as a plain loop (torch's walks the same
+        parameters through its profiler scope and foreach grouping: ~0.1 ms of host time per Q update)."""
+        if not set_to_none:
+            return super().zero_grad(set_to_none=False)
+        for group in self.param_groups:
+            for p in group["params"]:
+                p.grad = None
+
     def _collect(self, group):
         """(params, grads, exp_avgs, exp_avg_sqs, steps) of the group's parameters that have a gradient."""
         ps, gs, ms, vs, steps = [], [], [], [], []
+        f32, strided = torch.float32, torch.strided
         for p in group["params"]:
             g = p.grad
             if g is None:
                 continue
-            _require_fp32_cuda(p, "param")
-            _require_fp32_cuda(g, "grad")
+            # _require_fp32_cuda on both, one expression on the common case (the checks themselves were ~0.1 ms per
+            # 100-parameter step)
+            if not (p.dtype is f32 and g.dtype is f32 and p.is_cuda and g.is_cuda and p.layout is strided and
+                    g.layout is strided and p.is_contiguous() and g.is_contiguous()):
+                _require_fp32_cuda(p, "param")
+                _require_fp32_cuda(g, "grad")
             st = self.state[p]
             if len(st) == 0:
                 st["step"] = torch.tensor(0.0, dtype=torch.float32)

@@ -179,6 +179,25 @@ def _denoiser_desc(p, params):
     return d
 
 
+def _grad_buffers(params, needed):
+    """Gradient tensors for the parameters whose entry of `needed` is set (None elsewhere): contiguous views of ONE
+    fp32 allocation, 16-B aligned each (one torch.empty and one split instead of an empty_like per parameter)."""
+    sizes, want = [], []
+    for p, n in zip(params, needed):
+        if n:
+            k = p.numel()
+            pad = (-k) % 4
+            sizes += [k, pad] if pad else [k]
+            want.append((p, len(sizes) - (2 if pad else 1)))
+        else:
+            want.append(None)
+    if not want or all(w is None for w in want):
+        return [None] * len(want)
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=params[0].device)
+    parts = flat.split(sizes)
+    return [None if w is None else parts[w[1]].view(w[0].shape) for w in want]
+
+
 class _DenoiserTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, zt, se, xemb, p, *params):
@@ -206,10 +225,8 @@ class _DenoiserTrainFn(torch.autograd.Function):
         dev = g.device
         g = g.to(torch.float32).contiguous()
         grads = _lib.DenoiserGrads()
-        outs = []
-        for k, ((key, b, _), p) in enumerate(zip(_denoiser_params(ctx.p), params)):
-            t = torch.empty_like(p) if ctx.needs_input_grad[4 + k] else None
-            outs.append(t)
+        outs = _grad_buffers(params, ctx.needs_input_grad[4:])
+        for (key, b, _), t in zip(_denoiser_params(ctx.p), outs):
             if t is not None:
                 if b is None:
                     setattr(grads, key, t.data_ptr())
@@ -347,6 +364,16 @@ def encoder_train_supported(enc, x):
     return ok
 
 
+# per-call scratch of the encoder's training forward / backward (packed weights, conv and InstanceNorm workspaces):
+# kernels are stream-ordered, so one buffer per purpose serves every stage and every call on a stream (round 5: ~20
+# torch.empty calls per Q update, ~0.1 ms of host time)
+_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd")}
+
+
+def _scratch(key, device, nbytes):
+    return _ENC_SCRATCH[key].get(device, max(int(nbytes), 16), key)
+
+
 class _EncoderTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stages, *params):
@@ -365,10 +392,10 @@ class _EncoderTrainFn(torch.autograd.Function):
             y = torch.empty(B, Ho, Wo, cout, dtype=torch.float32, device=dev)
             nbx = int(L.damc_conv2d_x3_workspace_bytes(B, H, W, cin, cout, k, s, p)) if limb else 0
             if nbx:  # the limb engine (fp32-accurate bf16 MFMA), as the Q(x) forward runs these convs (a10)
-                w3 = torch.empty(int(L.damc_conv2d_x3_bytes(cout, cin, k)) // 2, dtype=torch.int16, device=dev)
+                w3 = _scratch("w3", dev, L.damc_conv2d_x3_bytes(cout, cin, k))
                 check(L.damc_pack_conv2d_x3(ptr(conv.weight.detach().contiguous()), cout, cin, k, ptr(w3), stream),
                       "pack conv2d x3")
-                ws = torch.empty(nbx, dtype=torch.uint8, device=dev)
+                ws = _scratch("conv", dev, nbx)
                 check(L.damc_conv2d_x3_nhwc(ptr(h), B, H, W, cin, ptr(w3), ptr(conv.bias), cout, k, s, p, ptr(y),
                                             ptr(ws), nbx, stream), "conv2d x3")
             else:
@@ -382,8 +409,7 @@ class _EncoderTrainFn(torch.autograd.Function):
             if norm is not None:
                 out = torch.empty_like(y)
                 stats = torch.empty(B * cout * 2, dtype=torch.float32, device=dev)
-                ws = torch.empty(max(int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout)), 1), dtype=torch.float32,
-                                 device=dev)
+                ws = _scratch("in", dev, 4 * int(L.damc_instnorm_workspace_floats(B, Ho * Wo, cout)))
                 check(L.damc_instnorm_lrelu_train_nhwc(ptr(y), B, Ho * Wo, cout, ptr(norm.weight), ptr(norm.bias),
                                                        float(norm.eps), float(slope), ptr(out), ptr(stats), ptr(ws),
                                                        stream), "instnorm train")
@@ -400,7 +426,7 @@ class _EncoderTrainFn(torch.autograd.Function):
         stream = _lib.stream_ptr(dev)
         B = ctx.B
         params = ctx.saved_tensors
-        grads = [torch.empty_like(p) if ctx.needs_input_grad[2 + i] else None for i, p in enumerate(params)]
+        grads = _grad_buffers(params, ctx.needs_input_grad[2:])
         # parameter index of each stage's (conv.weight, conv.bias, norm.weight, norm.bias)
         idx, pos = [], 0
         for conv, norm, _ in ctx.stages:
@@ -415,8 +441,7 @@ class _EncoderTrainFn(torch.autograd.Function):
             j = idx[i]
             if norm is not None:
                 dy = torch.empty_like(y)
-                ws = torch.empty(max(int(L.damc_instnorm_bwd_workspace_floats(B, Ho * Wo, cout)), 1),
-                                 dtype=torch.float32, device=dev)
+                ws = _scratch("in_bwd", dev, 4 * int(L.damc_instnorm_bwd_workspace_floats(B, Ho * Wo, cout)))
                 check(L.damc_instnorm_lrelu_backward_nhwc(ptr(y), ptr(stats), ptr(dh), B, Ho * Wo, cout,
                                                           ptr(norm.weight), ptr(norm.bias), float(slope), ptr(dy),
                                                           ptr(grads[j + 2]), ptr(grads[j + 3]), ptr(ws), stream),
@@ -425,7 +450,7 @@ class _EncoderTrainFn(torch.autograd.Function):
                 dy = dh
             dx = torch.empty(B, H, W, cin, dtype=torch.float32, device=dev) if i > 0 else None
             nbytes = int(L.damc_conv2d_backward_workspace_bytes(B, H, W, cin, cout, k, s, p))
-            ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+            ws = _scratch("conv_bwd", dev, nbytes)
             dw = grads[j] if grads[j] is not None else torch.empty_like(conv.weight)
             check(L.damc_conv2d_backward_nhwc(ptr(h_in), ptr(dy), ptr(conv.weight), B, H, W, cin, cout, k, s, p,
                                               ptr(dx), ptr(dw), ptr(grads[j + 1]), ptr(ws), nbytes, stream),
