@@ -1150,8 +1150,8 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   // limb path's; waves 8 along M x 1 along N (each 32 x 128), so every A element is split by one wave only
   constexpr bool F32A = (V & X3_F32A) != 0;
   static_assert(!F32A || (OM != O_WGRAD && M16 && (V & 4) && (V & 256) && !WIDE && !P16 &&
-                          !(V & (8 | 16 | 32 | 64 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 131072))),
-                "F32A: the default 16x16-tile LDS-DMA path only");
+                          !(V & (32 | 64 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 131072))),
+                "F32A: the default 16x16-tile LDS-DMA path (A/B builds: + the channel-major walk 8, the raster 16)");
   constexpr int AROWB = F32A ? X3A_ROWB : X3_ROWB, ESZ = F32A ? 4 : 6;
   constexpr int AJ = (BM * (F32A ? 8 : X3_CHUNKS) + 511) / 512, BJ = BN * X3_CHUNKS / 512;  // NARROW: 1.5 -> 2
   constexpr int BUFB = BM * AROWB + BN * X3_ROWB;  // one LDS buffer (A image, then B image)
@@ -1371,7 +1371,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       // the same slice-major order (launch_split_x3_cmaj), so B stays the sequential column k0
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * 6, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(base + 512 * 16 * j), 16, (int)aoff[j], ci0 * ESZ, 0, 0);
     } else if constexpr ((V & 16384) != 0) {
       // timing probe (wrong results): no A DMA after the first tile
       if (k0 == kbeg) {
@@ -2687,7 +2687,7 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       a.ksplit = 1;
       a.kbpw = 1;
       a.kslab_reg = 0;
-      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | X3_NARROW>), dim3((unsigned)(nnm * ntn), 1, zdim), dim3(512), 0, s,
+      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, (V & ~(8 | 16)) | X3_NARROW>), dim3((unsigned)(nnm * ntn), 1, zdim), dim3(512), 0, s,
                          a);
       return 0;
     }
@@ -2770,6 +2770,17 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   a.ksplit = 1;
   a.kbpw = 1;
   a.kslab_reg = 0;
+  if constexpr ((V & X3_F32A) != 0 && OM == O_PHASE && !(V & 16)) {
+    // round 5: the unsplit F32A ConvT forward on the supertile raster (bit 16: each XCD's concurrent workgroups cover
+    // <= 8 M tiles x the 4 phases of an N tile, so the phases' overlapping input windows and weight panels are shared
+    // in its L2).  Bitwise the default raster; CIFAR B=128 upconv_fwd FETCH 1059 -> 705 MB per launch at the same
+    // time (548 vs 551 us; profiles/r05/walk_ab.txt).  DAMC_X3_RASTER=0 (read per call) keeps the default raster
+    const char* er = getenv("DAMC_X3_RASTER");
+    if (!(er && er[0] == '0')) {
+      hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | 16>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
+      return 0;
+    }
+  }
   if ((V & 16) && OM != O_WGRAD)  // supertile raster: phases folded into a 1-D grid
     hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V>), dim3(ntm * ntn * zdim, 1, 1), dim3(512), 0, s, a);
   else
@@ -3109,7 +3120,7 @@ static void launch_x3_narrow_split(const GemmArgs& a0, hipStream_t s) {
   a.k_per_z = a.negk;
   a.proj_nostore = 0;
   const int ntm = (a.M + 63) / 64, ntn = (a.N + X3_BN - 1) / X3_BN;
-  hipLaunchKernelGGL((gemm_x3_kernel<EPI, O_DENSE, DAMC_X3_VARIANT | X3_NARROW>), dim3(ntm * ntn, 1, ks), dim3(512), 0, s,
+  hipLaunchKernelGGL((gemm_x3_kernel<EPI, O_DENSE, (DAMC_X3_VARIANT & ~(8 | 16)) | X3_NARROW>), dim3(ntm * ntn, 1, ks), dim3(512), 0, s,
                      a);
   const long tot = (long)a.M * (a.N / 8);
   hipLaunchKernelGGL((x3_ksplit_reduce_kernel<EPI, O_DENSE>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a,
