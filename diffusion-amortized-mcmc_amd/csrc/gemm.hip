@@ -895,7 +895,11 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
 // walks a slice's 8 K tiles through a 2-3 deep LDS pipeline, latency-bound at this size).  The same 32x32x2 MFMA
 // sequence per output (k-quad q, then step s; lane half lk takes k = 8 q + 4 lk + s of each 32-deep tile) from zero
 // per slice, so every slab value is bitwise gemm_km_kernel's.
+// MT = 2 (round 5): M <= 64 as two 32-row tiles per wave (SVHN's per-config batch of 64 at nz = 100 left the tiled
+// kernel 22 us for a 52 MFLOP product), two K tiles' loads in flight so the fragments stay within the VGPRs
+template <int MT>
 __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
+  constexpr int KU = 4 / MT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lrow = lane & 31, lk = lane >> 5;
   const int z = blockIdx.x, n0 = blockIdx.y * 128 + wave * 32;
@@ -905,40 +909,51 @@ __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.N * (int)p.ldb * 4, 0x00020000);
   constexpr int OOB = 0x7FFFFFF0;
-  const int aoff = lrow < p.M ? (lrow * p.Cg + 4 * lk) * 4 : OOB;
+  int aoff[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) aoff[t] = 32 * t + lrow < p.M ? ((32 * t + lrow) * p.Cg + 4 * lk) * 4 : OOB;
   const int boff = n0 + lrow < p.N ? ((n0 + lrow) * (int)p.ldb + 4 * lk) * 4 : OOB;
-  f32x16 acc;
+  f32x16 acc[MT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int kt = 0; kt < nk; kt += 4) {
-    f32x4 fa[4][4], fb[4][4];
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  for (int kt = 0; kt < nk; kt += KU) {
+    f32x4 fa[MT][KU][4], fb[KU][4];
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool live = kt + u < nk;
         const int k0 = (kbeg + (kt + u) * KM_BK + 8 * q) * 4;
-        fa[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 ra, live ? aoff : OOB, live ? k0 : 0, 0));
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          fa[t][u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      ra, live ? aoff[t] : OOB, live ? k0 : 0, 0));
         fb[u][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                  rb, live ? boff : OOB, live ? k0 : 0, 0));
       }
     __builtin_amdgcn_sched_barrier(0);  // every load of the batch issued before the first MFMA waits on one
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KU; ++u) {
       if (kt + u >= nk) break;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][q][s2], fb[u][q][s2], acc, 0, 0, 0);
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[t][u][q][s2], fb[u][q][s2], acc[t], 0, 0, 0);
     }
   }
   float* Cz = p.C + (long)z * p.c_zstride;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = (r & 3) + 8 * (r >> 2) + 4 * lk, n = n0 + lrow;
-    if (m < p.M && n < p.N) Cz[(long)m * p.ldc + n] = acc[r];
-  }
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * lk, n = n0 + lrow;
+      if (m < p.M && n < p.N) Cz[(long)m * p.ldc + n] = acc[t][r];
+    }
 }
 
 template <int EPI, int OM, int PIPE = DAMC_KM_PIPE, int DBG = 0>
@@ -980,9 +995,13 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // dz_slabs at per-rank batches: km_skinny_kernel (bitwise gemm_km_kernel); DAMC_KM_SKINNY=0 (read per call) keeps
     // the tiled kernel
     const char* esk = getenv("DAMC_KM_SKINNY");
-    if (epi == EPI_STORE && om == O_DENSE && c.M <= 32 && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
+    if (epi == EPI_STORE && om == O_DENSE && c.M <= 64 && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
         c.kw == 1 && c.Cg == c.K && !(esk && esk[0] == '0')) {
-      hipLaunchKernelGGL(km_skinny_kernel, dim3((unsigned)zdim, (unsigned)((c.N + 127) / 128)), dim3(256), 0, s, c);
+      const dim3 g((unsigned)zdim, (unsigned)((c.N + 127) / 128));
+      if (c.M <= 32)
+        hipLaunchKernelGGL(km_skinny_kernel<1>, g, dim3(256), 0, s, c);
+      else
+        hipLaunchKernelGGL(km_skinny_kernel<2>, g, dim3(256), 0, s, c);
       continue;
     }
 #define DAMC_KM(E_, O_)                \

@@ -457,10 +457,11 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B, f32a
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [8, 16, 32])
+@pytest.mark.parametrize("B", [8, 16, 32, 48, 64])
 def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     """The first layer at per-rank batches (B <= 32): z . W on gemm.hip's x3_skinny_kernel and its input gradient's
-    split-K slabs on km_skinny_kernel (fragments straight into registers): 2 noisy posterior steps bitwise equal to
+    split-K slabs on km_skinny_kernel (fragments straight into registers; up to B = 64 as two 32-row tiles per wave,
+    round 5): 2 noisy posterior steps bitwise equal to
     the tiled kernels (DAMC_X3_SKINNY=0, DAMC_KM_SKINNY=0), with the skinny kernel reading the weights as fp32 rows
     split in registers (round 5, default) and as the packed limbs (DAMC_X3_SKINNY_F32B=0)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
