@@ -514,7 +514,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world))
-    dist = world > 1
+    # DAMC_BENCH_PG=1 (tests only): the process group and its barrier / MAX all-reduce even for one rank, so a 1-GPU box
+    # exercises RCCL (backend nccl) on the bench's own code path
+    dist = world > 1 or os.environ.get("DAMC_BENCH_PG") == "1"
     if args.dry_run:
         return dry_run(args, rank, world)
     # DAMC_DIST_BACKEND=gloo (tests only): several ranks sharing one GPU (RCCL needs one GPU per rank); the

@@ -24,8 +24,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(tmp, world, scaling, torchrun=False, **extra_env):
-    env = dict(os.environ, DAMC_DIST_BACKEND="gloo", DAMC_BENCH_DUMP=str(tmp), **extra_env)
+def _run(tmp, world, scaling, torchrun=False, backend="gloo", **extra_env):
+    os.makedirs(tmp, exist_ok=True)
+    env = dict(os.environ, DAMC_DIST_BACKEND=backend, DAMC_BENCH_DUMP=str(tmp), **extra_env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     args = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
@@ -86,3 +87,15 @@ def test_two_ranks_weak_scaling_line(tmp_path, gpu_device):
     assert [p["plan"]["post_start"] for p in parts] == [0, 128]
     # distinct global chains: the two ranks' noise streams differ, so their chains do too
     assert not torch.equal(parts[0]["z"], parts[1]["z"])
+
+
+def test_one_rank_over_rccl_is_the_plain_block(tmp_path, gpu_device):
+    """RCCL itself on a one-GPU box: bench.py under torch.distributed.run with one rank and backend nccl (RCCL), the
+    process group forced on (DAMC_BENCH_PG=1) so its barrier and MAX all-reduce run over RCCL; the rank's chains are
+    bitwise the plain single-process block (no collective touches the data path)."""
+    j = _run(tmp_path / "rccl", 1, "strong", torchrun=True, backend="nccl", DAMC_BENCH_PG="1")
+    ref = _run(tmp_path / "plain", 1, "strong")
+    assert j["n_gpus"] == 1 and j["value"] > 0
+    a = torch.load(tmp_path / "rccl" / "rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "plain" / "rank0.pt", weights_only=True)
+    assert torch.equal(a["z"], b["z"]) and torch.equal(a["p"], b["p"])
