@@ -11,6 +11,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "gemm.h"
 
 namespace {
 
@@ -982,4 +983,143 @@ extern "C" int damc_pack_ebm(const damc_ebm_t* e, float* w1t, float* w2t, void* 
 // SURVEY.md §8b name of the EBM per-op hook
 extern "C" int damc_ebm_grad(const damc_ebm_t* e, const float* z, int B, float* energy, float* grad, void* stream) {
   return damc_ebm_energy_grad(e, z, B, energy, grad, stream);
+}
+
+// ------------------------------------------------------------------------------------------------ E update
+// The E update of a training iteration (round 5; workspace/train_gen_recon.py:233-241: e_pos, e_neg = E(zk_pos),
+// E(zk_neg); (e_pos.mean() - e_neg.mean()).backward()) on the grouped small-GEMM kernel (gemm.hip
+// small_gemm_group_kernel, exact fp32 products, fp32 sums): the forward keeps the two hidden activations, the backward
+// is two elementwise kernels (LReLU' from the activations' signs, which are the pre-activations' signs for a positive
+// slope) and two grouped launches holding every weight / bias gradient and the input gradient.
+namespace {
+struct EtWs {
+  float *grow, *dh2, *dh2T, *dh1p, *dh1, *dh1T;
+};
+size_t et_carve(int nh, int B, char* base, EtWs* w) {
+  size_t off = 0;
+  auto take = [&](long n) {
+    float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((size_t)n * sizeof(float) + 255) / 256 * 256;
+    return p;
+  };
+  EtWs t;
+  t.grow = take(B);
+  t.dh2 = take((long)B * nh);
+  t.dh2T = take((long)B * nh);
+  t.dh1p = take((long)B * nh);
+  t.dh1 = take((long)B * nh);
+  t.dh1T = take((long)B * nh);
+  if (w) *w = t;
+  return off;
+}
+bool et_ok(const damc_ebm_t* e, int B) {
+  return e && e->nz > 0 && e->nh > 0 && B > 0 && B % 4 == 0 && e->nz % 4 == 0 && e->nh % 4 == 0 && e->w1 && e->b1 &&
+         e->w2 && e->b2 && e->w3 && e->b3;
+}
+// dh2 = (g w3) * lrelu'(h2), its transpose, and g as a contiguous row
+__global__ void et_dh2_kernel(const float* __restrict__ g, long gs, const float* __restrict__ w3,
+                              const float* __restrict__ h2, int B, int nh, float slope, float* __restrict__ grow,
+                              float* __restrict__ dh2, float* __restrict__ dh2T) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * nh) return;
+  const int b = (int)(i / nh), j = (int)(i - (long)b * nh);
+  const float gb = g[b * gs];
+  float v = mul_rn(gb, w3[j]);
+  if (!(h2[i] > 0.f)) v = mul_rn(v, slope);
+  dh2[i] = v;
+  dh2T[(long)j * B + b] = v;
+  if (j == 0) grow[b] = gb;
+}
+__global__ void et_mask_kernel(const float* __restrict__ d, const float* __restrict__ h, int B, int nh, float slope,
+                               float* __restrict__ o, float* __restrict__ oT) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * nh) return;
+  const int b = (int)(i / nh), j = (int)(i - (long)b * nh);
+  const float v = h[i] > 0.f ? d[i] : mul_rn(d[i], slope);
+  o[i] = v;
+  oT[(long)j * B + b] = v;
+}
+damc::SmallGemm sg(const float* A, long lda, const float* Bm, long ldb, int bt, const float* bias, float* C, long ldc,
+                   int M, int N, int K, int act, float slope) {
+  damc::SmallGemm d;
+  d.A = A;
+  d.lda = lda;
+  d.B = Bm;
+  d.ldb = ldb;
+  d.b_t = bt;
+  d.bias = bias;
+  d.C = C;
+  d.ldc = ldc;
+  d.M = M;
+  d.N = N;
+  d.K = K;
+  d.act = act;
+  d.slope = slope;
+  return d;
+}
+damc::SmallGemm sg_colsum(const float* X, long R, int N, long ld, float* C) {
+  damc::SmallGemm d;
+  d.a_ones = 1;
+  d.B = X;
+  d.ldb = ld;
+  d.C = C;
+  d.ldc = N;
+  d.M = 1;
+  d.N = N;
+  d.K = (int)R;
+  return d;
+}
+}  // namespace
+
+extern "C" size_t damc_ebm_train_workspace_bytes(const damc_ebm_t* e, int B) {
+  if (!et_ok(e, B)) return 0;
+  return et_carve(e->nh, B, nullptr, nullptr);
+}
+
+extern "C" int damc_ebm_train_forward(const damc_ebm_t* e, const float* z, int B, float* h1, float* h2, float* energy,
+                                      void* stream) {
+  if (!e || !z || !h1 || !h2 || !energy) return DAMC_ERR_ARG;
+  if (!et_ok(e, B)) return DAMC_ERR_UNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  const int nz = e->nz, nh = e->nh;
+  const damc::SmallGemm l1 = sg(z, nz, e->w1, nz, 1, e->b1, h1, nh, B, nh, nz, DAMC_ACT_LRELU, e->slope);
+  const damc::SmallGemm l2 = sg(h1, nh, e->w2, nh, 1, e->b2, h2, nh, B, nh, nh, DAMC_ACT_LRELU, e->slope);
+  const damc::SmallGemm l3 = sg(h2, nh, e->w3, nh, 1, e->b3, energy, 1, B, 1, nh, DAMC_ACT_NONE, 0.f);
+  int rc = damc::launch_small_gemm_group(&l1, 1, s);
+  if (!rc) rc = damc::launch_small_gemm_group(&l2, 1, s);
+  if (!rc) rc = damc::launch_small_gemm_group(&l3, 1, s);
+  return rc;
+}
+
+extern "C" int damc_ebm_train_backward(const damc_ebm_t* e, const float* z, const float* h1, const float* h2,
+                                       const float* grad_energy, long grad_stride, int B, const damc_ebm_grads_t* gr,
+                                       float* grad_z, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!e || !z || !h1 || !h2 || !grad_energy || !gr || grad_stride < 0) return DAMC_ERR_ARG;
+  if (!et_ok(e, B)) return DAMC_ERR_UNSUPPORTED;
+  const int nz = e->nz, nh = e->nh;
+  if (!workspace || workspace_bytes < et_carve(nh, B, nullptr, nullptr)) return DAMC_ERR_WORKSPACE;
+  EtWs w;
+  et_carve(nh, B, static_cast<char*>(workspace), &w);
+  hipStream_t s = as_stream(stream);
+  const long n = (long)B * nh;
+  hipLaunchKernelGGL(et_dh2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, grad_energy, grad_stride, e->w3,
+                     h2, B, nh, e->slope, w.grow, w.dh2, w.dh2T);
+  damc::SmallGemm g1[5];
+  int k = 0;
+  if (gr->w3) g1[k++] = sg(w.grow, B, h2, nh, 0, nullptr, gr->w3, nh, 1, nh, B, DAMC_ACT_NONE, 0.f);
+  if (gr->b3) g1[k++] = sg_colsum(w.grow, B, 1, 1, gr->b3);
+  if (gr->w2) g1[k++] = sg(w.dh2T, B, h1, nh, 0, nullptr, gr->w2, nh, nh, nh, B, DAMC_ACT_NONE, 0.f);
+  if (gr->b2) g1[k++] = sg_colsum(w.dh2, B, nh, nh, gr->b2);
+  const bool down = gr->w1 || gr->b1 || grad_z;
+  if (down) g1[k++] = sg(w.dh2, nh, e->w2, nh, 0, nullptr, w.dh1p, nh, B, nh, nh, DAMC_ACT_NONE, 0.f);
+  int rc = k ? damc::launch_small_gemm_group(g1, k, s) : 0;
+  if (rc || !down) return rc ? rc : (int)hipGetLastError();
+  hipLaunchKernelGGL(et_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)w.dh1p, h1, B, nh,
+                     e->slope, w.dh1, w.dh1T);
+  damc::SmallGemm g2[3];
+  k = 0;
+  if (gr->w1) g2[k++] = sg(w.dh1T, B, z, nz, 0, nullptr, gr->w1, nz, nh, nz, B, DAMC_ACT_NONE, 0.f);
+  if (gr->b1) g2[k++] = sg_colsum(w.dh1, B, nh, nh, gr->b1);
+  if (grad_z) g2[k++] = sg(w.dh1, nh, e->w1, nz, 0, nullptr, grad_z, nz, B, nz, nh, DAMC_ACT_NONE, 0.f);
+  return k ? damc::launch_small_gemm_group(g2, k, s) : (int)hipGetLastError();
 }

@@ -281,6 +281,7 @@ struct SmallGemm {
   int M = 0, N = 0, K = 0, bias_mod = 0, act = DAMC_ACT_NONE;
   float slope = 0.f;
   int a_ones = 0;
+  int b_t = 0;  // B given transposed: N rows of K (row stride ldb >= K, 16-B aligned), e.g. a PyTorch Linear weight
 };
 constexpr int SG_GROUP_MAX = 8;
 struct SmallGemmGroup {

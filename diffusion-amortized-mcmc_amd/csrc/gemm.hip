@@ -496,8 +496,8 @@ __global__ __launch_bounds__(256) void small_gemm_group_kernel(SmallGemmGroup g)
   const int row = tm * 16 + m, col = tn * 16 + m;
   const bool rok = row < M, cok = col < N;
   const float* Ar = D.A + (long)(rok && !D.a_ones ? row : 0) * D.lda;
-  const float* Bc = D.B + (cok ? col : 0);
   const long ldb = D.ldb;
+  const float* Bc = D.b_t ? D.B + (long)(cok ? col : 0) * ldb : D.B + (cok ? col : 0);
   const int k16 = (K + 15) >> 4, per = (k16 + 3) >> 2;
   const int kb = wave * per * 16, ke = min(K, kb + per * 16);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -509,8 +509,12 @@ __global__ __launch_bounds__(256) void small_gemm_group_kernel(SmallGemmGroup g)
       const bool kin = k < ke;
       const int kk = kin ? k : 0;
       a[u] = D.a_ones ? f32x4{1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(Ar + kk);
+      if (D.b_t) {
+        b[u] = *reinterpret_cast<const f32x4*>(Bc + kk);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) b[u][e] = Bc[(long)(kk + e) * ldb];
+        for (int e = 0; e < 4; ++e) b[u][e] = Bc[(long)(kk + e) * ldb];
+      }
       if (!(rok && kin)) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (!(cok && kin)) b[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -539,11 +543,12 @@ int launch_small_gemm_group(const SmallGemm* g, int n, hipStream_t s) {
   double flops = 0.0;
   for (int i = 0; i < n; ++i) {
     const SmallGemm& d = g[i];
-    if ((!d.A && !d.a_ones) || !d.B || !d.C || d.M <= 0 || d.N <= 0 || d.K <= 0 || d.ldb < d.N || d.ldc < d.N ||
-        (d.a_ones && d.M != 1) || (!d.a_ones && d.lda < d.K))
+    if ((!d.A && !d.a_ones) || !d.B || !d.C || d.M <= 0 || d.N <= 0 || d.K <= 0 || d.ldb < (d.b_t ? d.K : d.N) ||
+        d.ldc < d.N || (d.a_ones && d.M != 1) || (!d.a_ones && d.lda < d.K))
       return DAMC_ERR_ARG;
     if (d.K % 4 != 0 || (!d.a_ones && (d.lda % 4 != 0 || (reinterpret_cast<uintptr_t>(d.A) & 15) != 0)))
       return DAMC_ERR_UNSUPPORTED;  // f32x4 A
+    if (d.b_t && (d.ldb % 4 != 0 || (reinterpret_cast<uintptr_t>(d.B) & 15) != 0)) return DAMC_ERR_UNSUPPORTED;
     grp.d[i] = d;
     tot += (long)((d.M + 15) / 16) * ((d.N + 15) / 16);
     if (tot >= (1L << 31)) return DAMC_ERR_UNSUPPORTED;

@@ -98,6 +98,10 @@ class Encoder(ctypes.Structure):  # damc_encoder_t
                 ("layers", EncLayer * MAX_ENC_LAYERS), ("engine", ctypes.c_int)]
 
 
+class EbmGrads(ctypes.Structure):  # damc_ebm_grads_t
+    _fields_ = [(k, ctypes.c_void_p) for k in ("w1", "b1", "w2", "b2", "w3", "b3")]
+
+
 class AdamHparams(ctypes.Structure):
     _fields_ = [("neg_step_size", ctypes.c_float), ("one_minus_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("one_minus_beta2", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("eps", ctypes.c_float),
@@ -137,6 +141,10 @@ _SIGS = {
     "damc_denoiser_train_forward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _P, _P, _I, _P, _P, _SZ, _P]),
     "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
                                           _P, _P, _SZ, _P]),
+    "damc_ebm_train_workspace_bytes": (_SZ, [ctypes.POINTER(Ebm), _I]),
+    "damc_ebm_train_forward": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P, _P]),
+    "damc_ebm_train_backward": (_I, [ctypes.POINTER(Ebm), _P, _P, _P, _P, ctypes.c_long, _I, ctypes.POINTER(EbmGrads),
+                                     _P, _P, _SZ, _P]),
     "damc_q_noise_glue": (_I, [_P, _P, _P, _I, _I, _F, _F, _P, _I, _P, _P, _P, _P]),
     "damc_q_loss_forward": (_I, [_P, _P, _I, _I, _P, _P]),
     "damc_q_loss_backward": (_I, [_P, _P, _P, ctypes.c_long, _I, _I, _P, _P]),

@@ -312,6 +312,87 @@ def q_loss(eps, eps_pred):
     return _QLossFn.apply(eps.contiguous(), eps_pred)
 
 
+# ----------------------------------------------------------------------------------------- E update
+# e_pos, e_neg = E(zk_pos), E(zk_neg); (e_pos.mean() - e_neg.mean()).backward() (train_gen_recon.py:233-241) with
+# _netE's forward and backward on libdamc (damc_ebm_train_*): three small-GEMM launches forward, two elementwise and
+# two grouped launches backward, instead of ~25 PyTorch ops.  Shapes the C side does not take (batch or widths not a
+# multiple of 4, nez != 1, spectral norm, non-fp32 or misaligned tensors) keep the stock PyTorch modules.
+
+def _ebm_layers(E):
+    mods = list(E.ebm)
+    lins = [m for m in mods if isinstance(m, torch.nn.Linear)]
+    acts = [m for m in mods if isinstance(m, torch.nn.LeakyReLU)]
+    if len(mods) != 5 or len(lins) != 3 or len(acts) != 2 or mods[0] is not lins[0] or mods[2] is not lins[1]:
+        return None
+    if any(hasattr(m, "weight_orig") for m in lins) or acts[0].negative_slope != acts[1].negative_slope:
+        return None
+    if lins[2].out_features != 1 or any(m.bias is None for m in lins):
+        return None
+    return lins, float(acts[0].negative_slope)
+
+
+class _EbmTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, desc, slope, *params):
+        L = _lib.lib()
+        B = z.shape[0]
+        nh = desc.nh
+        dev = z.device
+        h = torch.empty(2, B, nh, dtype=torch.float32, device=dev)
+        e = torch.empty(B, dtype=torch.float32, device=dev)
+        check(L.damc_ebm_train_forward(ctypes.byref(desc), ptr(z), B, ptr(h[0]), ptr(h[1]), ptr(e),
+                                       _lib.stream_ptr(dev)), "damc_ebm_train_forward")
+        ctx.desc = desc
+        ctx.save_for_backward(z, h, *params)
+        return e
+
+    @staticmethod
+    def backward(ctx, g):
+        z, h = ctx.saved_tensors[:2]
+        params = ctx.saved_tensors[2:]
+        L = _lib.lib()
+        dev = g.device
+        B = z.shape[0]
+        g = g.to(torch.float32)
+        stride = g.stride(0)
+        if stride != 0 and not g.is_contiguous():
+            g, stride = g.contiguous(), 1
+        outs = _grad_buffers(params, ctx.needs_input_grad[3:])
+        grads = _lib.EbmGrads()
+        for k, t in zip(("w1", "b1", "w2", "b2", "w3", "b3"), outs):
+            if t is not None:
+                setattr(grads, k, t.data_ptr())
+        gz = torch.empty_like(z) if ctx.needs_input_grad[0] else None
+        nb = int(L.damc_ebm_train_workspace_bytes(ctypes.byref(ctx.desc), B))
+        ws = _scratch("ebm_bwd", dev, nb)
+        check(L.damc_ebm_train_backward(ctypes.byref(ctx.desc), ptr(z), ptr(h[0]), ptr(h[1]), ptr(g), stride, B,
+                                        ctypes.byref(grads), ptr(gz), ptr(ws), nb, _lib.stream_ptr(dev)),
+              "damc_ebm_train_backward")
+        ctx.desc = None
+        return (gz, None, None, *outs)
+
+
+def ebm_apply(E, z):
+    """E(z).squeeze() on libdamc with grad (the E update), or None where the C side does not take the module / input
+    (the caller then runs the stock modules)."""
+    lay = _ebm_layers(E)
+    if lay is None or z.dim() != 2 or z.dtype != torch.float32 or z.shape[0] % 4:
+        return None
+    lins, slope = lay
+    params = [t for m in lins for t in (m.weight, m.bias)]
+    if any(p.dtype != torch.float32 or not p.is_contiguous() or p.data_ptr() % 16 for p in params):
+        return None
+    z = z.contiguous()
+    if z.data_ptr() % 16:
+        return None
+    d = _lib.Ebm()
+    d.nz, d.nh, d.slope = lins[0].in_features, lins[0].out_features, slope
+    d.w1, d.b1, d.w2, d.b2, d.w3, d.b3 = [p.data_ptr() for p in params]
+    if int(_lib.lib().damc_ebm_train_workspace_bytes(ctypes.byref(d), z.shape[0])) == 0:
+        return None
+    return _EbmTrainFn.apply(z, d, slope, *params)
+
+
 # ------------------------------------------------------------------------------- Q update: encoder
 # Encoder_* (workspace/src/diffusion_net.py:227-413) as trained by Q.calculate_loss: forward on libdamc
 # keeping every conv output, InstanceNorm statistic and layer input; backward through
@@ -367,7 +448,7 @@ def encoder_train_supported(enc, x):
 # per-call scratch of the encoder's training forward / backward (packed weights, conv and InstanceNorm workspaces):
 # kernels are stream-ordered, so one buffer per purpose serves every stage and every call on a stream (round 5: ~20
 # torch.empty calls per Q update, ~0.1 ms of host time)
-_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd")}
+_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd", "ebm_bwd")}
 
 
 def _scratch(key, device, nbytes):

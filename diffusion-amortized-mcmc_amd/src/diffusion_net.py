@@ -113,6 +113,15 @@ class _netE(nn.Module):
                                  wrap(nn.Linear(ndf, nez)))
 
     def forward(self, z):
+        if z.is_cuda and torch.is_grad_enabled():
+            # ROCm with autograd on (the E update, train_gen_recon.py:233-241): forward and backward on libdamc
+            # (damc.training.ebm_apply); None where the C side does not take the module, then the stock layers
+            from damc import training
+
+            if training.ENABLED and (z.requires_grad or any(p.requires_grad for p in self.parameters())):
+                e = training.ebm_apply(self, z)
+                if e is not None:
+                    return e
         return self.ebm(z).squeeze()
 
 

@@ -385,6 +385,21 @@ int damc_q_loss_forward(const float* eps, const float* eps_pred, int batch, int 
 int damc_q_loss_backward(const float* eps, const float* eps_pred, const float* grad_loss, long grad_stride, int batch,
                          int nz, float* grad_eps_pred, void* stream);
 
+/* ------------------------------------------------------- E update (round 5; SURVEY §8f, train_gen_recon.py:233-241)
+ * E(z) of _netE (diffusion_net.py:207-223, e's PyTorch-layout w1..b3; w1t / w2t unused) keeping the hidden activations
+ * h1, h2 (B, nh) for the backward; energy (B).  Batch and the layer widths multiples of 4, weights 16-B aligned
+ * (DAMC_ERR_UNSUPPORTED otherwise: the caller keeps PyTorch). */
+typedef struct { /* gradients, PyTorch layouts (written, not accumulated; NULL entries are skipped) */
+  float *w1, *b1, *w2, *b2, *w3, *b3;
+} damc_ebm_grads_t;
+size_t damc_ebm_train_workspace_bytes(const damc_ebm_t* e, int batch);
+int damc_ebm_train_forward(const damc_ebm_t* e, const float* z, int batch, float* h1, float* h2, float* energy,
+                           void* stream);
+/* grad_energy (B, element stride grad_stride: 0 for a .mean()'s broadcast) -> grads and grad_z (B, nz) or NULL */
+int damc_ebm_train_backward(const damc_ebm_t* e, const float* z, const float* h1, const float* h2,
+                            const float* grad_energy, long grad_stride, int batch, const damc_ebm_grads_t* grads,
+                            float* grad_z, void* workspace, size_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------------------- optimiser steps
  * Replaces the G/E/Q updates' torch.nn.utils.clip_grad_norm_ + optim.Adam / optim.AdamW.step()
  * (train_gen_recon.py:155-157, 219-231, 240-241) by multi-tensor kernels.  A launch covers up to

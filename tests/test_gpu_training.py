@@ -428,3 +428,44 @@ def test_q_noise_glue_matches_torch_ops(gpu_device):
     loss_ref.mean().backward()
     assert rel_l2(loss.detach().cpu().numpy(), loss_ref.detach().cpu().numpy()) < 1e-6
     assert rel_l2(pred.grad.cpu().numpy(), pr.grad.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("nz", [128, 100])
+def test_e_update_matches_torch(gpu_device, nz):
+    """The E update (train_gen_recon.py:233-241): e_pos, e_neg = E(zk_pos), E(zk_neg) at B = 128 / 2B = 256, loss
+    e_pos.mean() - e_neg.mean(), backward — on libdamc (damc_ebm_train_*) against the stock modules on the same GPU
+    (training.stock_pytorch()): energies and every parameter gradient to rel-L2 1e-5 (fp32 sums in another order),
+    and the input gradient of E(z).sum() for a z that requires grad."""
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    E = synth.load_into(dn._netE(nz=nz), 10).to(gpu_device).train()
+    zp = torch.from_numpy(synth.normal_f32(81, 0, (128, nz))).to(gpu_device)
+    zn = torch.from_numpy(synth.normal_f32(81, 1, (256, nz))).to(gpu_device)
+
+    def run(stock):
+        for p in E.parameters():
+            p.grad = None
+        ctx = training.stock_pytorch() if stock else torch.enable_grad()
+        with ctx:
+            ep, en = E(zp), E(zn)
+            (ep.mean() - en.mean()).backward()
+            zz = zn.clone().requires_grad_(True)
+            gz = torch.autograd.grad(E(zz).sum(), zz)[0]
+        torch.cuda.synchronize()
+        return ep.detach(), en.detach(), [p.grad.clone() for p in E.parameters()], gz
+
+    calls = []
+    orig = training.ebm_apply
+    training.ebm_apply = lambda e, z: calls.append(1) or orig(e, z)
+    try:
+        hip = run(False)
+    finally:
+        training.ebm_apply = orig
+    assert len(calls) == 3  # every E(z) above ran on libdamc
+    ref = run(True)
+    assert rel_l2(hip[0].cpu().numpy(), ref[0].cpu().numpy()) < 1e-5
+    assert rel_l2(hip[1].cpu().numpy(), ref[1].cpu().numpy()) < 1e-5
+    for a, b in zip(hip[2], ref[2]):
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) < 1e-5
+    assert rel_l2(hip[3].cpu().numpy(), ref[3].cpu().numpy()) < 1e-5
