@@ -186,3 +186,83 @@ def test_layer_sign_block_rule(monkeypatch):
     d = _lib.Layer()
     d.kind = _lib.LAYER_SMALLC
     assert L.damc_x3_layer_sign_block(ctypes.byref(d), 0) == 0
+
+
+def test_round5_host_only_entry_points():
+    """Host-side argument checks of the round-5 entry points (no kernel is launched): the E-update workspace is 0 for
+    shapes the C side does not take (batch or widths not a multiple of 4), the glue / loss calls refuse NULL
+    pointers and odd embedding widths."""
+    from damc import _lib
+
+    L = _lib.lib()
+    e = _lib.Ebm()
+    e.nz, e.nh, e.slope = 128, 200, 0.2
+    assert L.damc_ebm_train_workspace_bytes(ctypes.byref(e), 128) == 0  # no weight pointers
+    e.w1 = e.b1 = e.w2 = e.b2 = e.w3 = e.b3 = 256  # host-only size query: any non-null address
+    assert L.damc_ebm_train_workspace_bytes(ctypes.byref(e), 128) > 0
+    assert L.damc_ebm_train_workspace_bytes(ctypes.byref(e), 130) == 0
+    e.nh = 202
+    assert L.damc_ebm_train_workspace_bytes(ctypes.byref(e), 128) == 0
+    assert L.damc_q_noise_glue(None, None, None, 128, 128, -5.1, 9.8, None, 128, None, None, None, None) == 1001
+    assert L.damc_q_noise_glue(8, 8, 8, 128, 128, -5.1, 9.8, 8, 127, None, 8, 8, None) == 1001
+    assert L.damc_q_loss_forward(None, None, 128, 128, None, None) == 1001
+    assert L.damc_q_loss_backward(8, 8, 8, -1, 128, 128, 8, None) == 1001
+
+
+def test_optim_step_counters_with_a_fixed_subset_host_only():
+    """damc.optim's step counters on CPU scalars (no kernel): when the same subset of a group's parameters has
+    gradients every step, each parameter's count is the number of steps it took part in (torch's semantics), and
+    the updated subset ends up sharing ONE counter private to it (the fast path of later steps)."""
+    import torch
+
+    from damc import optim
+
+    ps = [torch.nn.Parameter(torch.zeros(2)) for _ in range(4)]
+    opt = optim.AdamW(ps)
+    group = opt.param_groups[0]
+
+    def advance(active):
+        for i, p in enumerate(ps):
+            p.grad = torch.ones(2) if i in active else None
+        steps = []
+        for p in ps:
+            if p.grad is None:
+                continue
+            st = opt.state[p]
+            if not st:
+                st["step"] = torch.tensor(0.0)
+            steps.append(st["step"])
+        return opt._advance_steps(group, steps)
+
+    assert advance({0, 1, 2, 3}) == 1.0
+    assert advance({0, 1, 2}) == 2.0
+    assert advance({0, 1, 2}) == 3.0
+    assert advance({0, 1, 2}) == 4.0
+    assert [float(opt.state[p]["step"]) for p in ps] == [4.0, 4.0, 4.0, 1.0]
+    shared = opt.state[ps[0]]["step"]
+    assert opt.state[ps[1]]["step"] is shared and opt.state[ps[2]]["step"] is shared
+    assert opt.state[ps[3]]["step"] is not shared
+    assert advance({3}) == 2.0  # the left-out parameter keeps its own count
+    assert [float(opt.state[p]["step"]) for p in ps] == [4.0, 4.0, 4.0, 2.0]
+    assert advance({0, 1, 2, 3}) is None  # counts differ: one launch per value (the caller's slow path)
+
+
+def test_grad_buffers_and_ebm_eligibility_host_only():
+    """training._grad_buffers: one fp32 allocation, a view per needed parameter with its shape, 16-B aligned starts,
+    None where no gradient is needed; training._ebm_layers accepts _netE's default topology only."""
+    import torch
+
+    from damc import training
+    from src import diffusion_net as dn
+
+    params = [torch.zeros(3, 5), torch.zeros(7), torch.zeros(2, 2), torch.zeros(6)]
+    out = training._grad_buffers(params, [True, False, True, True])
+    assert out[1] is None
+    assert [tuple(t.shape) for t in out if t is not None] == [(3, 5), (2, 2), (6,)]
+    base = out[0].untyped_storage().data_ptr()
+    assert all(t.untyped_storage().data_ptr() == base and (t.data_ptr() - base) % 16 == 0 for t in out if t is not None)
+    assert all(t.is_contiguous() for t in out if t is not None)
+    assert training._grad_buffers(params, [False] * 4) == [None] * 4
+    assert training._ebm_layers(dn._netE(nz=128)) is not None
+    assert training._ebm_layers(dn._netE(nz=128, nez=2)) is None
+    assert training._ebm_layers(dn._netE(nz=128, e_sn=True)) is None
