@@ -269,7 +269,7 @@ def q_forward(Q, x=None, b=None, device=None, cond_w=-1, zt=None, seed=None, cha
     global index of row 0 — a shard that passes its slice of the global zt, the global seed and its slice
     start reproduces its rows of the 1-GPU sweep bit for bit."""
     if cond_w is not None and cond_w > 0 and x is not None:
-        raise NotImplementedError("classifier-free guidance (cond_w > 0) is dead code in the reference drivers")
+        return _q_forward_guided(Q, x, float(cond_w))
     if x is not None:
         assert b is None and device is None
         b = len(x)
@@ -284,4 +284,38 @@ def q_forward(Q, x=None, b=None, device=None, cond_w=-1, zt=None, seed=None, cha
     if zt.shape != (b, Q.nz):
         raise _lib.DamcError("zt must be (%d, %d)" % (b, Q.nz))
     reverse_sweep(Q, xemb, zt, seed=seed, chain_base=chain_base)
+    return zt
+
+
+def _q_forward_guided(Q, x, w):
+    """Classifier-free guidance (cond_w > 0, diffusion_net.py:595-620; round 5): the reference's step loop with its
+    draws in its order (zt from the host generator, then per step a fresh prior embedding's noise and the step's
+    noise on the device), each step's two denoiser evaluations on libdamc (Diffusion_UnetA.forward ->
+    damc.training.denoiser_apply, the training kernels' forward) and the prior embedding on damc_gemm; the guidance
+    combination and the schedule algebra are the reference's own tensor formulas (src/diffusion_helper_func.py).
+    Unlike the unguided sweep (one team launch), this runs one denoiser launch sequence per evaluation: the
+    reference's drivers never set cond_w."""
+    from src.diffusion_helper_func import diffusion_reverse, logsnr_schedule_fn, pred_x_from_eps
+
+    b, device, n = len(x), x.device, int(Q.n_interval)
+    xemb = encoder_forward(Q.encoder, x)
+    zt = torch.randn(b, Q.nz).to(device)
+    for i in reversed(range(0, n)):
+        i_tensor = torch.ones(b, dtype=torch.float).to(device) * float(i)
+        logsnr_t = logsnr_schedule_fn(i_tensor / (n - 1.0), logsnr_min=Q.logsnr_min, logsnr_max=Q.logsnr_max)
+        logsnr_s = logsnr_schedule_fn(torch.clamp(i_tensor - 1.0, min=0.0) / (n - 1.0), logsnr_min=Q.logsnr_min,
+                                      logsnr_max=Q.logsnr_max)
+        eps_pred = Q.p(z=zt, logsnr=logsnr_t, xemb=xemb)
+        xemb_unc = prior_embedding(Q, torch.randn(b, Q.nz, device=device))
+        eps_pred_unc = Q.p(z=zt, logsnr=logsnr_t, xemb=xemb_unc)
+        eps_pred = (1 + w) * eps_pred - w * eps_pred_unc
+        logsnr_t = logsnr_t.reshape((b, 1))
+        logsnr_s = logsnr_s.reshape((b, 1))
+        pred_z = pred_x_from_eps(z=zt, eps=eps_pred, logsnr=logsnr_t)
+        if i == 0:
+            zt = pred_z
+        else:
+            dist = diffusion_reverse(x=pred_z, z_t=zt, logsnr_s=logsnr_s, logsnr_t=logsnr_t, pred_var_type=Q.var_type)
+            eps = torch.randn_like(zt)
+            zt = dist["mean"] + dist["std"] * eps if Q.with_noise else dist["mean"]
     return zt

@@ -30,9 +30,39 @@ def _act_of(mod):
     raise NotImplementedError("unsupported activation %r" % (mod,))
 
 
+def _sn_hook(m):
+    from torch.nn.utils.spectral_norm import SpectralNorm
+
+    for h in m._forward_pre_hooks.values():
+        if isinstance(h, SpectralNorm):
+            return h
+    return None
+
+
 def _require_plain_param(m):
-    if hasattr(m, "weight_orig"):
-        raise NotImplementedError("spectral-norm generators (use_spc_norm=True) are not supported by the HIP path")
+    """A layer whose weight the plan can read: a plain parameter, or nn.utils.spectral_norm's (the reference's sn,
+    diffusion_net.py:8-16) recomputed by _live_weight."""
+    if hasattr(m, "weight_orig") and _sn_hook(m) is None:
+        raise NotImplementedError("a reparametrised weight other than nn.utils.spectral_norm's")
+
+
+def _live_weight(m):
+    """The weight m's forward would use.  A spectral-norm layer (use_spc_norm=True generators, e_sn=True EBMs:
+    diffusion_net.py:8-16, 21-44, 208-210) recomputes it in its forward pre-hook from weight_orig and the u, v vectors;
+    in eval mode -- the mode the reference runs G and E in for the Langevin chains and the sweeps
+    (train_gen_recon.py:191-193) -- without a power iteration, so the value is fixed and is what every forward of the
+    chain would use: it is computed here the way the hook does and set as the hook sets it.  In train mode every
+    forward advances u and v once, which one packing per call cannot follow through the chain's per-step forwards."""
+    h = _sn_hook(m)
+    if h is None:
+        return m.weight
+    if m.training:
+        raise NotImplementedError("spectral-norm layers in train mode: every forward runs a power iteration (call "
+                                  ".eval() before the Langevin chains, as the reference's drivers do)")
+    with torch.no_grad():
+        w = h.compute_weight(m, do_power_iteration=False)
+    setattr(m, h.name, w)
+    return w
 
 
 class GeneratorPlan:
@@ -129,7 +159,7 @@ class GeneratorPlan:
         stream = _lib.stream_ptr(device)
         self._keep = []
         for i, m in enumerate(self.modules):
-            w = m.weight.detach()
+            w = _live_weight(m).detach()
             if w.device != device or w.dtype != torch.float32 or not w.is_contiguous():
                 w = w.to(device=device, dtype=torch.float32).contiguous()
                 self._keep.append(w)
@@ -191,7 +221,7 @@ class EbmPlan:
                 self._keep.append(t)
             return t
 
-        (w1, b1), (w2, b2), (w3, b3) = [(dev(m.weight), dev(m.bias)) for m in self.lin]
+        (w1, b1), (w2, b2), (w3, b3) = [(dev(_live_weight(m)), dev(m.bias)) for m in self.lin]
         if self.device != device:
             self.w1t = torch.empty(self.nz * self.nh, dtype=torch.float32, device=device)
             self.w2t = torch.empty(self.nh * self.nh, dtype=torch.float32, device=device)

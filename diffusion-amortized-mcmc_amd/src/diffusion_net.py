@@ -57,7 +57,8 @@ class _GeneratorBase(nn.Module):
     def forward(self, z):
         # ROCm tensors run on libdamc: the forward, and under autograd the training backward
         # (damc.training: dL/dW, dL/db, dL/dz for the G update, train_gen_recon.py:222-231).
-        # Spectral-norm generators (use_spc_norm=True, default False) are outside the HIP path.
+        # Spectral-norm generators (use_spc_norm=True, default False) run their forward on the stock layers (the
+        # Langevin chains, gen_samples and the sweeps take them on libdamc in eval mode: damc.plans._live_weight).
         if z.is_cuda and not self._spc:
             from damc import training
 

@@ -254,3 +254,51 @@ def test_failed_team_launch_is_rescued_bitwise(am, gpu_device, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(zt2, zt)
     assert L.damc_sweep_team_failures(dev) == before + 1
+
+
+def test_classifier_free_guidance_matches_stock_modules(gpu_device):
+    """Q(x, cond_w=w > 0) (diffusion_net.py:603-606; round 5): the guided step loop with its denoiser evaluations on
+    libdamc against the reference's loop on the stock modules (training.stock_pytorch()), both from the same torch
+    seed so every draw (zt on the host generator, the per-step prior-embedding and step noise on the device) is the
+    same; 10 steps at the reference's defaults, end point to rel-L2 1e-4 (fp32 sums in other orders)."""
+    from damc import synth, training
+    from src import diffusion_helper_func as dh
+    from src import diffusion_net as dn
+
+    Q = dn._netQ_U(nc=3, nz=128, nxemb=1024, ntemb=128, nif=64, diffusion_residual=True, n_interval=10,
+                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, dataset="cifar10")
+    synth.load_into(Q, 20)
+    Q.to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(93, 0, (16, 3, 32, 32))).to(gpu_device)
+    w = 0.5
+    torch.manual_seed(7)
+    with torch.no_grad():
+        z_hip = Q(x, cond_w=w)
+
+    def reference():  # diffusion_net.py:585-622 on the stock modules
+        b, n = len(x), Q.n_interval
+        xemb = Q.encoder(x)
+        zt = torch.randn(b, Q.nz).to(gpu_device)
+        for i in reversed(range(0, n)):
+            it = torch.ones(b, dtype=torch.float).to(gpu_device) * float(i)
+            lt = dh.logsnr_schedule_fn(it / (n - 1.0), logsnr_min=Q.logsnr_min, logsnr_max=Q.logsnr_max)
+            ls = dh.logsnr_schedule_fn(torch.clamp(it - 1.0, min=0.0) / (n - 1.0), logsnr_min=Q.logsnr_min,
+                                       logsnr_max=Q.logsnr_max)
+            e = Q.p(z=zt, logsnr=lt, xemb=xemb)
+            eu = Q.p(z=zt, logsnr=lt, xemb=Q.prior_emb(torch.randn(b, Q.nz, device=gpu_device)))
+            e = (1 + w) * e - w * eu
+            lt, ls = lt.reshape((b, 1)), ls.reshape((b, 1))
+            pz = dh.pred_x_from_eps(z=zt, eps=e, logsnr=lt)
+            if i == 0:
+                zt = pz
+            else:
+                d = dh.diffusion_reverse(x=pz, z_t=zt, logsnr_s=ls, logsnr_t=lt, pred_var_type=Q.var_type)
+                zt = d["mean"] + d["std"] * torch.randn_like(zt)
+        return zt
+
+    torch.manual_seed(7)
+    with training.stock_pytorch(), torch.no_grad():
+        z_ref = reference()
+    err = rel_l2(z_hip.cpu().numpy(), z_ref.cpu().numpy())
+    print("guided Q(x) end point rel-L2 vs stock modules %.2e" % err)
+    assert torch.isfinite(z_hip).all() and err < 1e-4

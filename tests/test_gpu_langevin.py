@@ -502,3 +502,40 @@ def test_lds_staged_gather_is_bitwise_the_direct_gather(lv, gpu_device, monkeypa
         out[mode] = z.cpu()
     assert torch.isfinite(out["1"]).all()
     assert torch.equal(out["0"], out["1"])
+
+
+def test_spectral_norm_nets_in_eval_mode(lv, gpu_device):
+    """use_spc_norm=True generators and e_sn=True EBMs (nn.utils.spectral_norm, diffusion_net.py:8-16, 21-44, 208-210)
+    on the HIP path in eval mode, the mode of the reference's Langevin chains (train_gen_recon.py:191-193): after a few
+    train-mode forwards have moved u and v, the posterior chain (10 no-noise steps) and the prior chain match the
+    oracle on the weights the layers' own forward pre-hooks compute; train mode is refused."""
+    from damc import synth
+    from damc import training
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=16, nc=3, use_spc_norm=True), 4).to(gpu_device)
+    E = synth.load_into(dn._netE(nz=128, e_sn=True), 5).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(91, 0, (8, 128))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(91, 1, (8, 3, 32, 32))).to(gpu_device)
+    with training.stock_pytorch(), torch.no_grad():
+        for _ in range(3):  # power iterations move u, v away from their initial values
+            G.train()(z0)
+            E.train()(z0)
+    G.eval()
+    E.eval()
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, E, 10, 0.3, 0.1, False)
+    with training.stock_pytorch(), torch.no_grad():
+        G(z0)  # the hooks set every layer's weight (eval: no power iteration)
+        E(z0)
+    L, P = orc.generator_layers(G), orc.ebm_params(E)
+    ref = orc.posterior_langevin(L, P, z0.cpu(), x.cpu(), 10, 0.3, 0.1)
+    assert rel_l2(z.cpu().numpy(), ref.numpy()) < 2e-4
+    zp = torch.cat([z0, z0]).contiguous()
+    lv.prior_langevin(zp, E, 5, 0.4, False)
+    refp = orc.prior_langevin(P, torch.cat([z0, z0]).cpu(), 5, 0.4)
+    assert rel_l2(zp.cpu().numpy(), refp.numpy()) < 1e-5
+    G.train()
+    with pytest.raises(NotImplementedError):
+        lv.posterior_langevin(z0.clone(), x, G, E, 1, 0.3, 0.1, False)
