@@ -404,3 +404,183 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
     return rc;
   return dx ? pad_crop(t.dxp, B, hin + 1, win + 1, cin, dx, hin, win, s) : 0;
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// The whole encoder of the Q update in two calls (round 5): damc_encoder_train_forward runs every stage the way
+// damc.training's per-stage loop did (conv on the limb engine or the fp32 engine, InstanceNorm + LeakyReLU keeping
+// the conv output and the statistics), damc_encoder_train_backward every stage's InstanceNorm and Conv2d backward;
+// the host issues one call each way instead of ~4 per stage (the Q update is host-bound).
+namespace {
+struct EncTrainPlan {
+  int n, H[DAMC_MAX_ENC_LAYERS + 1], W[DAMC_MAX_ENC_LAYERS + 1];
+  bool limb[DAMC_MAX_ENC_LAYERS];
+  size_t nbx[DAMC_MAX_ENC_LAYERS], wbytes[DAMC_MAX_ENC_LAYERS], convws[DAMC_MAX_ENC_LAYERS];
+  size_t inws[DAMC_MAX_ENC_LAYERS], inbws[DAMC_MAX_ENC_LAYERS], cbws[DAMC_MAX_ENC_LAYERS];
+  long x_off, y_off[DAMC_MAX_ENC_LAYERS], st_off[DAMC_MAX_ENC_LAYERS], out_off[DAMC_MAX_ENC_LAYERS];
+  size_t saved_floats;
+  // workspace regions (bytes)
+  size_t w_at, conv_at, in_at, inb_at, cb_at, bufa_at, bufb_at, ws_bytes;
+};
+
+inline size_t up256(size_t b) { return (b + 255) / 256 * 256; }
+
+// 0 = supported (p filled), else a DAMC error code
+int enc_train_plan(const damc_encoder_t* e, int B, EncTrainPlan* p) {
+  if (!e || B <= 0 || e->n_layers < 1 || e->n_layers > DAMC_MAX_ENC_LAYERS || e->nc <= 0 || e->h <= 0 || e->w <= 0)
+    return DAMC_ERR_ARG;
+  p->n = e->n_layers;
+  p->H[0] = e->h;
+  p->W[0] = e->w;
+  long off = 0;
+  auto take = [&](long floats) {
+    const long o = off;
+    off += (floats + 63) / 64 * 64;  // 256-B aligned views
+    return o;
+  };
+  p->x_off = take((long)B * e->h * e->w * e->nc);
+  size_t wmax = 0, cmax = 0, imax = 0, ibmax = 0, cbmax = 0, amax = 0;
+  int cin_expect = e->nc;
+  for (int i = 0; i < p->n; ++i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    if (L.cin != cin_expect || L.cout <= 0 || L.k <= 0 || L.stride <= 0 || !L.w_src) return DAMC_ERR_ARG;
+    const bool norm = L.in_gamma != nullptr;
+    if (norm != (i + 1 < p->n) || (norm && !L.in_beta) || !L.bias) return DAMC_ERR_UNSUPPORTED;
+    const int hin = p->H[i], win = p->W[i];
+    const int ho = (hin + 2 * L.pad - L.k) / L.stride + 1, wo = (win + 2 * L.pad - L.k) / L.stride + 1;
+    if (ho <= 0 || wo <= 0) return DAMC_ERR_ARG;
+    p->H[i + 1] = ho;
+    p->W[i + 1] = wo;
+    p->nbx[i] = e->engine == DAMC_ENGINE_LIMB
+                    ? damc_conv2d_x3_workspace_bytes(B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad)
+                    : 0;
+    p->limb[i] = p->nbx[i] > 0;
+    if (p->limb[i]) {
+      p->wbytes[i] = damc_conv2d_x3_bytes(L.cout, L.cin, L.k);
+      p->convws[i] = p->nbx[i];
+    } else {
+      p->wbytes[i] = (size_t)L.cout * L.cin * L.k * L.k * sizeof(float);
+      p->convws[i] = damc_conv2d_workspace_floats(B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad) * sizeof(float);
+    }
+    p->cbws[i] = damc_conv2d_backward_workspace_bytes(B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad);
+    if (p->cbws[i] == 0) return DAMC_ERR_UNSUPPORTED;
+    const long act = (long)B * ho * wo * L.cout;
+    if (norm) {
+      p->inws[i] = damc_instnorm_workspace_floats(B, ho * wo, L.cout) * sizeof(float);
+      p->inbws[i] = damc_instnorm_bwd_workspace_floats(B, ho * wo, L.cout) * sizeof(float);
+      p->y_off[i] = take(act);
+      p->st_off[i] = take(2L * B * L.cout);
+      p->out_off[i] = take(act);
+    } else {
+      p->inws[i] = p->inbws[i] = 0;
+      p->y_off[i] = p->st_off[i] = p->out_off[i] = -1;
+      if (ho != 1 || wo != 1) return DAMC_ERR_UNSUPPORTED;  // xemb = the last conv's (B, cout) output
+    }
+    wmax = std::max(wmax, p->wbytes[i]);
+    cmax = std::max(cmax, p->convws[i]);
+    imax = std::max(imax, p->inws[i]);
+    ibmax = std::max(ibmax, p->inbws[i]);
+    cbmax = std::max(cbmax, p->cbws[i]);
+    amax = std::max(amax, (size_t)act);
+    amax = std::max(amax, (size_t)B * hin * win * L.cin);
+    cin_expect = L.cout;
+  }
+  p->saved_floats = (size_t)off;
+  size_t w = 0;
+  p->w_at = w;
+  w += up256(wmax);
+  p->conv_at = w;
+  w += up256(cmax);
+  p->in_at = w;
+  w += up256(imax);
+  p->inb_at = w;
+  w += up256(ibmax);
+  p->cb_at = w;
+  w += up256(cbmax);
+  p->bufa_at = w;
+  w += up256(amax * sizeof(float));
+  p->bufb_at = w;
+  w += up256(amax * sizeof(float));
+  p->ws_bytes = std::max<size_t>(w, 256);
+  return 0;
+}
+}  // namespace
+
+extern "C" size_t damc_encoder_train_saved_floats(const damc_encoder_t* e, int B) {
+  EncTrainPlan p;
+  return enc_train_plan(e, B, &p) ? 0 : p.saved_floats;
+}
+
+extern "C" size_t damc_encoder_train_workspace_bytes(const damc_encoder_t* e, int B) {
+  EncTrainPlan p;
+  return enc_train_plan(e, B, &p) ? 0 : p.ws_bytes;
+}
+
+extern "C" int damc_encoder_train_forward(const damc_encoder_t* e, const float* x, int B, float* saved, float* xemb,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
+  EncTrainPlan p;
+  int rc = enc_train_plan(e, B, &p);
+  if (rc) return rc;
+  if (!x || !saved || !xemb) return DAMC_ERR_ARG;
+  if (!workspace || workspace_bytes < p.ws_bytes) return DAMC_ERR_WORKSPACE;
+  char* ws = static_cast<char*>(workspace);
+  float* h = saved + p.x_off;
+  if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, h, stream))) return rc;
+  for (int i = 0; i < p.n; ++i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    const int hin = p.H[i], win = p.W[i], ho = p.H[i + 1], wo = p.W[i + 1];
+    const bool norm = L.in_gamma != nullptr;
+    float* y = norm ? saved + p.y_off[i] : xemb;
+    if (p.limb[i]) {
+      if ((rc = damc_pack_conv2d_x3(L.w_src, L.cout, L.cin, L.k, ws + p.w_at, stream))) return rc;
+      rc = damc_conv2d_x3_nhwc(h, B, hin, win, L.cin, ws + p.w_at, L.bias, L.cout, L.k, L.stride, L.pad, y,
+                               ws + p.conv_at, p.convws[i], stream);
+    } else {
+      float* wp = reinterpret_cast<float*>(ws + p.w_at);
+      if ((rc = damc_pack_conv2d(L.w_src, L.cout, L.cin, L.k, wp, stream))) return rc;
+      rc = damc_conv2d_nhwc(h, B, hin, win, L.cin, wp, L.bias, L.cout, L.k, L.stride, L.pad, y,
+                            reinterpret_cast<float*>(ws + p.conv_at), p.convws[i] / sizeof(float), stream);
+    }
+    if (rc) return rc;
+    if (!norm) break;
+    float* out = saved + p.out_off[i];
+    if ((rc = damc_instnorm_lrelu_train_nhwc(y, B, ho * wo, L.cout, L.in_gamma, L.in_beta, L.in_eps, L.slope, out,
+                                             saved + p.st_off[i], reinterpret_cast<float*>(ws + p.in_at), stream)))
+      return rc;
+    h = out;
+  }
+  return 0;
+}
+
+extern "C" int damc_encoder_train_backward(const damc_encoder_t* e, const float* saved, const float* grad_xemb, int B,
+                                           const damc_encoder_grads_t* g, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  EncTrainPlan p;
+  int rc = enc_train_plan(e, B, &p);
+  if (rc) return rc;
+  if (!saved || !grad_xemb || !g) return DAMC_ERR_ARG;
+  if (!workspace || workspace_bytes < p.ws_bytes) return DAMC_ERR_WORKSPACE;
+  char* ws = static_cast<char*>(workspace);
+  float* bufa = reinterpret_cast<float*>(ws + p.bufa_at);
+  float* bufb = reinterpret_cast<float*>(ws + p.bufb_at);
+  const float* dh = grad_xemb;
+  for (int i = p.n - 1; i >= 0; --i) {
+    const damc_enc_layer_t& L = e->layers[i];
+    const int hin = p.H[i], win = p.W[i], ho = p.H[i + 1], wo = p.W[i + 1];
+    const float* dy = dh;
+    if (L.in_gamma) {
+      if ((rc = damc_instnorm_lrelu_backward_nhwc(saved + p.y_off[i], saved + p.st_off[i], dh, B, ho * wo, L.cout,
+                                                  L.in_gamma, L.in_beta, L.slope, bufa, g->gamma[i], g->beta[i],
+                                                  reinterpret_cast<float*>(ws + p.inb_at), stream)))
+        return rc;
+      dy = bufa;
+    }
+    const float* hin_p = i == 0 ? saved + p.x_off : saved + p.out_off[i - 1];
+    float* dw = g->w[i] ? g->w[i] : reinterpret_cast<float*>(ws + p.w_at);  // dw is required by the conv backward
+    if (!g->w[i] && p.wbytes[i] < (size_t)L.cout * L.cin * L.k * L.k * sizeof(float)) return DAMC_ERR_WORKSPACE;
+    if ((rc = damc_conv2d_backward_nhwc(hin_p, dy, L.w_src, B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad,
+                                        i > 0 ? bufb : nullptr, dw, g->b[i], ws + p.cb_at, p.cbws[i], stream)))
+      return rc;
+    dh = bufb;
+  }
+  return 0;
+}

@@ -98,6 +98,10 @@ class Encoder(ctypes.Structure):  # damc_encoder_t
                 ("layers", EncLayer * MAX_ENC_LAYERS), ("engine", ctypes.c_int)]
 
 
+class EncoderGrads(ctypes.Structure):  # damc_encoder_grads_t
+    _fields_ = [(k, ctypes.c_void_p * MAX_ENC_LAYERS) for k in ("w", "b", "gamma", "beta")]
+
+
 class EbmGrads(ctypes.Structure):  # damc_ebm_grads_t
     _fields_ = [(k, ctypes.c_void_p) for k in ("w1", "b1", "w2", "b2", "w3", "b3")]
 
@@ -141,6 +145,11 @@ _SIGS = {
     "damc_denoiser_train_forward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _P, _P, _I, _P, _P, _SZ, _P]),
     "damc_denoiser_train_backward": (_I, [ctypes.POINTER(DenoiserTrain), _P, _I, ctypes.POINTER(DenoiserGrads), _P,
                                           _P, _P, _SZ, _P]),
+    "damc_encoder_train_saved_floats": (_SZ, [ctypes.POINTER(Encoder), _I]),
+    "damc_encoder_train_workspace_bytes": (_SZ, [ctypes.POINTER(Encoder), _I]),
+    "damc_encoder_train_forward": (_I, [ctypes.POINTER(Encoder), _P, _I, _P, _P, _P, _SZ, _P]),
+    "damc_encoder_train_backward": (_I, [ctypes.POINTER(Encoder), _P, _P, _I, ctypes.POINTER(EncoderGrads), _P, _SZ,
+                                         _P]),
     "damc_ebm_train_workspace_bytes": (_SZ, [ctypes.POINTER(Ebm), _I]),
     "damc_ebm_train_forward": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P, _P]),
     "damc_ebm_train_backward": (_I, [ctypes.POINTER(Ebm), _P, _P, _P, _P, ctypes.c_long, _I, ctypes.POINTER(EbmGrads),

@@ -448,7 +448,7 @@ def encoder_train_supported(enc, x):
 # per-call scratch of the encoder's training forward / backward (packed weights, conv and InstanceNorm workspaces):
 # kernels are stream-ordered, so one buffer per purpose serves every stage and every call on a stream (round 5: ~20
 # torch.empty calls per Q update, ~0.1 ms of host time)
-_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd", "ebm_bwd")}
+_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd", "ebm_bwd", "enc_train")}
 
 
 def _scratch(key, device, nbytes):
@@ -541,7 +541,87 @@ class _EncoderTrainFn(torch.autograd.Function):
         return (None, None, *grads)
 
 
+# round 5: the whole encoder in one library call each way (damc_encoder_train_forward / _backward) instead of ~4 calls
+# per stage from Python; DAMC_ENC_TRAIN_FUSED=0 (read at import) keeps the per-stage Function above
+ENC_TRAIN_FUSED = os.environ.get("DAMC_ENC_TRAIN_FUSED") != "0"
+_ENC_DESC = weakref.WeakKeyDictionary()  # encoder -> (key of parameter pointers and input shape, descriptor, sizes)
+
+
+def _enc_train_desc(enc, stages, params, x):
+    """The damc_encoder_t of the training calls, cached per encoder while its parameters' storage and the input
+    shape stay the same (the descriptor holds raw pointers, read by the library at each call)."""
+    key = (tuple(p.data_ptr() for p in params), tuple(x.shape), _lib.current_engine())
+    c = _ENC_DESC.get(enc)
+    if c is not None and c[0] == key:
+        return c[1], c[2], c[3]
+    d = _lib.Encoder()
+    B, C, H, W = x.shape
+    d.n_layers, d.nc, d.h, d.w = len(stages), C, H, W
+    d.engine = _lib.current_engine()
+    for i, (conv, norm, slope) in enumerate(stages):
+        L = d.layers[i]
+        L.cin, L.cout, L.k = conv.in_channels, conv.out_channels, conv.kernel_size[0]
+        L.stride, L.pad = conv.stride[0], conv.padding[0]
+        L.w_src, L.bias = conv.weight.data_ptr(), conv.bias.data_ptr()
+        if norm is not None:
+            L.in_gamma, L.in_beta, L.in_eps = norm.weight.data_ptr(), norm.bias.data_ptr(), float(norm.eps)
+        L.slope = float(slope) if slope is not None else 0.0
+    lib = _lib.lib()
+    nsaved = int(lib.damc_encoder_train_saved_floats(ctypes.byref(d), B))
+    nws = int(lib.damc_encoder_train_workspace_bytes(ctypes.byref(d), B))
+    _ENC_DESC[enc] = (key, d, nsaved, nws)
+    return d, nsaved, nws
+
+
+class _EncoderTrainFusedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, enc, stages, *params):
+        L = _lib.lib()
+        dev = x.device
+        xc = x.detach().float().contiguous()
+        d, nsaved, nws = _enc_train_desc(enc, stages, params, xc)
+        if nsaved == 0 or nws == 0:
+            raise _lib.DamcError("encoder configuration not supported by damc_encoder_train_forward")
+        B = xc.shape[0]
+        saved = torch.empty(nsaved, dtype=torch.float32, device=dev)
+        xemb = torch.empty(B, stages[-1][0].out_channels, dtype=torch.float32, device=dev)
+        check(L.damc_encoder_train_forward(ctypes.byref(d), ptr(xc), B, ptr(saved), ptr(xemb),
+                                           ptr(_scratch("enc_train", dev, nws)), nws, _lib.stream_ptr(dev)),
+              "damc_encoder_train_forward")
+        ctx.d, ctx.nws, ctx.saved_buf, ctx.B = d, nws, saved, B
+        ctx.save_for_backward(*params)  # autograd's version check: no in-place update before the backward
+        return xemb
+
+    @staticmethod
+    def backward(ctx, g):
+        L = _lib.lib()
+        dev = g.device
+        params = ctx.saved_tensors
+        grads = _grad_buffers(params, ctx.needs_input_grad[3:])
+        gs = _lib.EncoderGrads()
+        j = 0
+        for i in range(ctx.d.n_layers):
+            has_norm = bool(ctx.d.layers[i].in_gamma)
+            gs.w[i] = None if grads[j] is None else grads[j].data_ptr()
+            gs.b[i] = None if grads[j + 1] is None else grads[j + 1].data_ptr()
+            if has_norm:
+                gs.gamma[i] = None if grads[j + 2] is None else grads[j + 2].data_ptr()
+                gs.beta[i] = None if grads[j + 3] is None else grads[j + 3].data_ptr()
+                j += 4
+            else:
+                j += 2
+        g = g.to(torch.float32).contiguous()
+        check(L.damc_encoder_train_backward(ctypes.byref(ctx.d), ptr(ctx.saved_buf), ptr(g), ctx.B, ctypes.byref(gs),
+                                            ptr(_scratch("enc_train", dev, ctx.nws)), ctx.nws, _lib.stream_ptr(dev)),
+              "damc_encoder_train_backward")
+        ctx.saved_buf = ctx.d = None
+        return (None, None, None, *grads)
+
+
 def encoder_apply(enc, x):
     """xemb = Encoder_*(x) on the HIP path, differentiable w.r.t. the encoder's parameters (not x)."""
     stages = _enc_stages(enc)
-    return _EncoderTrainFn.apply(x, stages, *_enc_params(stages))
+    params = _enc_params(stages)
+    if ENC_TRAIN_FUSED:
+        return _EncoderTrainFusedFn.apply(x, enc, stages, *params)
+    return _EncoderTrainFn.apply(x, stages, *params)

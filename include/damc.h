@@ -276,6 +276,23 @@ size_t damc_q_encoder_workspace_bytes(const damc_encoder_t* enc, int batch);
 int damc_q_encoder_fwd(const damc_encoder_t* enc, const float* x, int batch, float* xemb, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* The encoder of the Q update in two calls (round 5; Encoder_* forward and backward inside Q.calculate_loss,
+ * diffusion_net.py:624-645, train_gen_recon.py:211-220): every layer's w_src = its PyTorch Conv2d weight, bias set,
+ * in_gamma / in_beta on every layer but the last, whose output is 1 x 1 (xemb (B, cout)); engine as for
+ * damc_q_encoder_fwd.  The forward keeps in `saved` (damc_encoder_train_saved_floats floats) the NHWC input, every
+ * conv output, InstanceNorm statistics and activation; the backward maps grad_xemb (B, nemb) to the gradients
+ * (written, not accumulated; NULL entries skipped).  One workspace size serves both calls; 0 = not supported. */
+typedef struct {
+  float *w[DAMC_MAX_ENC_LAYERS], *b[DAMC_MAX_ENC_LAYERS], *gamma[DAMC_MAX_ENC_LAYERS], *beta[DAMC_MAX_ENC_LAYERS];
+} damc_encoder_grads_t;
+size_t damc_encoder_train_saved_floats(const damc_encoder_t* enc, int batch);
+size_t damc_encoder_train_workspace_bytes(const damc_encoder_t* enc, int batch);
+int damc_encoder_train_forward(const damc_encoder_t* enc, const float* x, int batch, float* saved, float* xemb,
+                               void* workspace, size_t workspace_bytes, void* stream);
+int damc_encoder_train_backward(const damc_encoder_t* enc, const float* saved, const float* grad_xemb, int batch,
+                                const damc_encoder_grads_t* grads, void* workspace, size_t workspace_bytes,
+                                void* stream);
+
 /* Dense fp32 MFMA GEMM: C(M,N) = act(A(M,K) · B(K,N) + bias) with B row-major (K,N) */
 int damc_gemm(const float* a, int lda, const float* b, int ldb, const float* bias, float* c, int ldc, int m,
               int n, int k, int act, float slope, void* stream);

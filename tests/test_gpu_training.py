@@ -260,7 +260,7 @@ def test_odd_k4s2_conv_backward(gpu_device, B, cin, cout):
 
 @pytest.mark.parametrize("name,B,nif", [("cifar10", 128, 64), ("celeba64", 8, 64), ("celebaHQ", 8, 64),
                                         ("celebaHQ", 2, 4)])
-def test_encoder_train_stagewise(gpu_device, name, B, nif):
+def test_encoder_train_stagewise(gpu_device, monkeypatch, name, B, nif):
     """Encoder training at full width (nif 64, nemb 1024): CIFAR-10 at the bench size B=128, and the CelebA-64 /
     CelebA-HQ encoders (diffusion_net.py:268-372; 64x64 and 256x256 inputs, 5 and 7 convolutions) at B=8, their
     per-rank batch.  The libdamc backward replayed
@@ -284,6 +284,9 @@ def test_encoder_train_stagewise(gpu_device, name, B, nif):
     x = torch.from_numpy(synth.uniform_f32(6, 0, (B, 3, hw, hw))).to(gpu_device)
     g = torch.from_numpy(synth.normal_f32(6, 1, (B, 1024))).to(gpu_device)
     assert training.encoder_train_supported(enc, x)
+    # the per-stage Function (its saved tensors are what this test replays); the one-call path runs the same library
+    # ops in the same order (test_encoder_train_one_call_is_bitwise_the_stage_calls)
+    monkeypatch.setattr(training, "ENC_TRAIN_FUSED", False)
     cap = {}
     orig = training._EncoderTrainFn.forward
 
@@ -469,3 +472,30 @@ def test_e_update_matches_torch(gpu_device, nz):
     for a, b in zip(hip[2], ref[2]):
         assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) < 1e-5
     assert rel_l2(hip[3].cpu().numpy(), ref[3].cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("name,B,nif", [("cifar10", 128, 64), ("celeba64", 8, 64), ("celebaHQ", 2, 4)])
+def test_encoder_train_one_call_is_bitwise_the_stage_calls(gpu_device, monkeypatch, name, B, nif):
+    """damc_encoder_train_forward / _backward (the whole encoder of the Q update in one call each way, round 5) run the
+    same library ops in the same order as the per-stage Function (DAMC_ENC_TRAIN_FUSED=0): xemb and every parameter
+    gradient bitwise equal."""
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    hw = {"cifar10": 32, "celeba64": 64, "celebaHQ": 256}[name]
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=nif), 4).to(gpu_device).train()
+    x = torch.from_numpy(synth.uniform_f32(6, 0, (B, 3, hw, hw))).to(gpu_device)
+    g = torch.from_numpy(synth.normal_f32(6, 1, (B, 1024))).to(gpu_device)
+    assert training.encoder_train_supported(enc, x)
+    out = {}
+    for fused in (False, True):
+        monkeypatch.setattr(training, "ENC_TRAIN_FUSED", fused)
+        for p in enc.parameters():
+            p.grad = None
+        xe = enc(x)
+        xe.backward(g)
+        torch.cuda.synchronize()
+        out[fused] = (xe.detach().clone(), [p.grad.clone() for p in enc.parameters()])
+    assert torch.equal(out[False][0], out[True][0])
+    for a, b in zip(out[False][1], out[True][1]):
+        assert torch.equal(a, b)
