@@ -278,7 +278,12 @@ def q_forward(Q, x=None, b=None, device=None, cond_w=-1, zt=None, seed=None, cha
     else:
         device = torch.device(device) if device is not None else torch.device("cuda")
         xemb = prior_embedding(Q, torch.randn(b, Q.nz, device=device))
-    zt = torch.randn(b, Q.nz).to(device) if zt is None else zt.to(device=device, dtype=torch.float32).clone()
+    if zt is None:  # the reference's host-generator draw, copied without blocking the host (training.to_device_async)
+        from .training import to_device_async
+
+        zt = to_device_async(torch.randn(b, Q.nz), device)
+    else:
+        zt = zt.to(device=device, dtype=torch.float32).clone()
     if zt.device.type != "cuda":
         raise _lib.DamcError("the HIP sweep needs a ROCm device (got %s)" % zt.device)
     if zt.shape != (b, Q.nz):

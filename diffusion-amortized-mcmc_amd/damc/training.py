@@ -253,6 +253,14 @@ def denoiser_apply(p, zt, se, xemb):
 Q_GLUE = os.environ.get("DAMC_Q_GLUE") != "0"
 
 
+def to_device_async(t, device):
+    """t (a host tensor) on device without blocking the host: through pinned memory (PyTorch's caching host
+    allocator keeps the block until the copy has run) with a non-blocking copy; the same values as t.to(device)."""
+    if t.device.type != "cpu" or torch.device(device).type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def _freqs(half, device):
     """SinusoidalPosEmb's frequency table, computed as the drop-in computes it (host fp32 ops, then moved)."""
     from src.diffusion_net import SinusoidalPosEmb

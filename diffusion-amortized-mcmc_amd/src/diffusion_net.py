@@ -316,16 +316,20 @@ class _netQ_U(nn.Module):
         else:
             assert mask is None
             xemb = self.prior_emb(torch.randn(len(z), self.nz, device=z.device))
-        u = torch.rand(len(z)).to(z.device)
         if z.is_cuda and xemb is not None and not z.requires_grad and z.dtype == torch.float32:
             from damc import training
 
             if training.ENABLED and training.Q_GLUE:
+                # the reference's host-generator draw, copied through pinned memory without blocking: a pageable
+                # host-to-device copy waits for the whole stream to drain (tools/h2d_probe.py), which serialised the
+                # host's and the GPU's halves of every Q update
+                u = training.to_device_async(torch.rand(len(z)), z.device)
                 # ROCm: the schedule, the forward diffusion, the time embedding and the loss around the denoiser as
                 # libdamc kernels (damc.training.q_noise_glue / q_loss); the draws stay torch's, in the same order
                 eps = torch.randn_like(z)
                 zt, se = training.q_noise_glue(self, u, z.contiguous(), eps)
                 return training.q_loss(eps, training.denoiser_apply(self.p, zt, se, xemb))
+        u = torch.rand(len(z)).to(z.device)
         logsnr = logsnr_schedule_fn(u, logsnr_max=self.logsnr_max, logsnr_min=self.logsnr_min)
         fwd = diffusion_forward(z, logsnr=logsnr.reshape(len(z), 1))
         eps = torch.randn_like(z)
