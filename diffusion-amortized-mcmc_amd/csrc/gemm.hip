@@ -907,7 +907,8 @@ __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
   constexpr int KU = 4 / MT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lrow = lane & 31, lk = lane >> 5;
-  const int z = blockIdx.x, n0 = blockIdx.y * 128 + wave * 32;
+  // blockIdx.z: 32 MT-row block of the rows (round 5: M up to 128 as two 64-row blocks)
+  const int z = blockIdx.x, n0 = blockIdx.y * 128 + wave * 32, rb0 = blockIdx.z * 32 * MT;
   const int kbeg = z * p.k_per_z, kend = min(p.K, kbeg + p.k_per_z);
   const int nk = kend > kbeg ? (kend - kbeg) / KM_BK : 0;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.Cg * 4, 0x00020000);
@@ -916,7 +917,8 @@ __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
   constexpr int OOB = 0x7FFFFFF0;
   int aoff[MT];
 #pragma unroll
-  for (int t = 0; t < MT; ++t) aoff[t] = 32 * t + lrow < p.M ? ((32 * t + lrow) * p.Cg + 4 * lk) * 4 : OOB;
+  for (int t = 0; t < MT; ++t)
+    aoff[t] = rb0 + 32 * t + lrow < p.M ? ((rb0 + 32 * t + lrow) * p.Cg + 4 * lk) * 4 : OOB;
   const int boff = n0 + lrow < p.N ? ((n0 + lrow) * (int)p.ldb + 4 * lk) * 4 : OOB;
   f32x16 acc[MT];
 #pragma unroll
@@ -956,7 +958,7 @@ __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * lk, n = n0 + lrow;
+      const int m = rb0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * lk, n = n0 + lrow;
       if (m < p.M && n < p.N) Cz[(long)m * p.ldc + n] = acc[t][r];
     }
 }
@@ -1000,9 +1002,13 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // dz_slabs at per-rank batches: km_skinny_kernel (bitwise gemm_km_kernel); DAMC_KM_SKINNY=0 (read per call) keeps
     // the tiled kernel
     const char* esk = getenv("DAMC_KM_SKINNY");
-    if (epi == EPI_STORE && om == O_DENSE && c.M <= 64 && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
+    // rows: up to 64 (two 32-row tiles per wave); DAMC_KM_SKINNY_ROWS (read per call) moves the limit for A/B (128, as
+    // two 64-row blocks: 38.3 us against the tiled kernel's 28.6 at the headline's B = 128, profiles/r05/skinny128_ab.txt)
+    const char* ekr = getenv("DAMC_KM_SKINNY_ROWS");
+    const int km_rows = ekr ? atoi(ekr) : 64;
+    if (epi == EPI_STORE && om == O_DENSE && c.M <= km_rows && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
         c.kw == 1 && c.Cg == c.K && !(esk && esk[0] == '0')) {
-      const dim3 g((unsigned)zdim, (unsigned)((c.N + 127) / 128));
+      const dim3 g((unsigned)zdim, (unsigned)((c.N + 127) / 128), c.M <= 32 ? 1u : (unsigned)((c.M + 63) / 64));
       if (c.M <= 32)
         hipLaunchKernelGGL(km_skinny_kernel<1>, g, dim3(256), 0, s, c);
       else
@@ -3151,6 +3157,14 @@ static void launch_x3_narrow_split(const GemmArgs& a0, hipStream_t s) {
                      1);
 }
 
+// the skinny first-layer kernel's row limit: 32.  DAMC_X3_SKINNY_ROWS (read per call) moves it for A/B; at the
+// headline's B = 128 the skinny form (8 x N / 64 workgroups, bitwise the same) took 81.8 us against 30.4 us for the
+// 128 x 256 layout (profiles/r05/skinny128_ab.txt)
+static int x3_skinny_max_rows() {
+  const char* e = getenv("DAMC_X3_SKINNY_ROWS");
+  return e ? atoi(e) : 32;
+}
+
 static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStream_t s) {
   const int taps = a.Cg > 0 ? a.K / a.Cg : 0;
   if (!(a.a_f32 ? a.A != nullptr : a.A3 != nullptr) || !a.B3 || a.Cg % X3_BK != 0 || taps * a.Cg != a.K || a.kw <= 0 ||
@@ -3216,7 +3230,7 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // the first layer at per-rank batches: the skinny kernel (bitwise the 128 x 256 layout); DAMC_X3_SKINNY=0 (read
     // per call) keeps the tiled kernel
     const char* esk = getenv("DAMC_X3_SKINNY");
-    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 32 && c.K <= c.negk && c.Hin == 1 && c.Win == 1 &&
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= x3_skinny_max_rows() && c.K <= c.negk && c.Hin == 1 && c.Win == 1 &&
         c.kw == 1 && c.Cg == c.K && c.A3 && !c.a_f32 && !c.proj_out && !(esk && esk[0] == '0')) {
       // fp32 weights split in registers where the caller passes them (2/3 of the limb bytes; bitwise the same
       // operands); DAMC_X3_SKINNY_F32B=0 (read per call) reads the limbs

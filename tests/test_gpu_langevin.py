@@ -457,7 +457,7 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B, f32a
     assert torch.equal(out["0"], out["1"])
 
 
-@pytest.mark.parametrize("B", [8, 16, 32, 48, 64])
+@pytest.mark.parametrize("B", [8, 16, 32, 48, 64, 128])
 def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     """The first layer at per-rank batches (B <= 32): z . W on gemm.hip's x3_skinny_kernel and its input gradient's
     split-K slabs on km_skinny_kernel (fragments straight into registers; up to B = 64 as two 32-row tiles per wave,
