@@ -470,7 +470,8 @@ __global__ __launch_bounds__(512) void conv3_in_fused_kernel(const float* __rest
 // activation instead of two, one launch instead of three).
 template <int NIT>
 // y32 != NULL: the result leaves as fp32 NHWC at y32 instead of limbs (the next conv stages it as fp32, gemm.hip
-// X3_F32A); y32 may be y itself (every thread writes only the elements it read, after both block sums)
+// X3_F32A); y32 may be y itself (every thread writes only the elements it read, after both block sums); chw: fp32 in
+// CHW order per sample instead (the dense head's input; y32 must then be another buffer)
 // slab != NULL: y was not written; the conv's ks split-K slabs (register layout of the 256 x 128 limb tiles, as
 // x3_ksplit_reduce_tile_kernel reads them, sstride4 f32x4 per slab, ntn 128-channel tiles) are summed here in the
 // reduce's order from 0, then the conv bias added: the reduce + epilogue's arithmetic, so the values are bitwise C's
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           float eps, float slope, unsigned short* __restrict__ y3,
                                                           float* y32, const float* __restrict__ slab, int ks, int ntn,
-                                                          long sstride4, const float* __restrict__ cbias) {
+                                                          long sstride4, const float* __restrict__ cbias, int chw) {
   __shared__ float red[4][32];
   __shared__ float st[2][32];
   const int b = blockIdx.x, c0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -563,7 +564,10 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW
       o[e] = u > 0.f ? u : u * slope;
     }
     const long off = ((long)b * HW + p) * C + c0 + 8 * q;
-    if (y32) {
+    if (y32 && chw) {  // fp32 CHW (the dense head's rows, enc_head_x3_kernel); y32 is then not y
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y32[((long)b * C + c0 + 8 * q + e) * HW + p] = o[e];
+    } else if (y32) {
       *reinterpret_cast<f32x4*>(y32 + off) = f32x4{o[0], o[1], o[2], o[3]};
       *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
     } else {
@@ -571,6 +575,169 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW
     }
   }
 }
+
+// The encoder's last conv when it covers its whole input (k x k, stride 1, no padding, on a k x k map: every Encoder_*,
+// diffusion_net.py:258-260): a Linear of the sample's CHW-flattened activation on the PyTorch weight itself, rows
+// [cout][cin k k].  The limb product of the limb engine (three RNE bf16 limbs per operand, six MFMAs per K tile, one
+// fp32 accumulation block per 512 k with the weight negated on odd blocks) without the limb copy of the weight: both
+// operands are read as fp32 and split into limbs once per workgroup on their way into LDS.  One workgroup = 128 rows x
+// 64 columns x one 512-k sign block; 8 waves of 32 x 32.  The block's sum (sign restored, exact) goes to its slab;
+// enc_head_reduce_kernel adds the slabs in order and the bias.  Replaces the packing of the weight's limbs (84 MB of
+// traffic at nemb = 1024) and a 64 x 128-tile limb GEMM over it.
+typedef __bf16 hb8 __attribute__((ext_vector_type(8)));
+constexpr int HD_BM = 128, HD_BN = 64, HD_KT = 32, HD_NEGK = 512, HD_THREADS = 512;
+constexpr int HD_ROWS = HD_BM + HD_BN;                           // LDS rows per limb plane (A rows, then B rows)
+constexpr size_t HD_LDS = 2 * 3 * HD_ROWS * 4 * sizeof(hb8);     // two K tiles x three limb planes: 72 KB
+
+// 16-B slot of (row, octet q) in a limb plane of 64-B rows.  ds_read_b128 serves a wave in four groups of 16 lanes
+// (MI355X_MICROARCH.md, LDS): a fragment read's group holds rows m, m + 12 (octet q) and m + 4, m + 8 (octet q ^ 1) of
+// each m % 4 class; the octet swizzle by (row >> 2) & 3 (0 -> 0, 1 -> 2, 2 -> 3, 3 -> 1) gives the 16 lanes of every
+// group 16 distinct slots mod 16, i.e. all 64 banks once
+__device__ __forceinline__ int hd_slot(int row, int q) {
+  return row * 4 + (q ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));
+}
+// the engine's RNE limb split of 8 values times sg (exact: a sign)
+__device__ __forceinline__ void hd_split(const f32x4 (&x)[2], float sg, hb8& h, hb8& m, hb8& l) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = sg * x[e >> 2][e & 3];
+    const __bf16 b0 = (__bf16)v;
+    const float r1 = sub_rn(v, (float)b0);
+    const __bf16 b1 = (__bf16)r1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)sub_rn(r1, (float)b1);
+  }
+}
+
+// grid (N / 64, K / 512, ceil(M / 128)); A [M][K] fp32 (CHW rows), W [N][K]; slab [K / 512][M][N]
+__global__ __launch_bounds__(HD_THREADS) void enc_head_x3_kernel(const float* __restrict__ A,
+                                                                 const float* __restrict__ W, int M, int N, int K,
+                                                                 float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) hb8 hl[];  // [2 K tiles][3 limbs][HD_ROWS][4 slots]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * HD_BN, kb = blockIdx.y, r0 = blockIdx.z * HD_BM;
+  const float sg = (kb & 1) ? -1.f : 1.f;
+  // staging: thread = (row fr, octet fq) of the A tile; the first 256 threads also of the B tile
+  const int fr = tid >> 2, fq = tid & 3;
+  const bool a_live = r0 + fr < M, b_fill = fr < HD_BN;
+  const float* ap = A + (long)(a_live ? r0 + fr : 0) * K + (long)kb * HD_NEGK + 8 * fq;
+  const float* bp = W + (long)(n0 + (b_fill ? fr : 0)) * K + (long)kb * HD_NEGK + 8 * fq;
+  f32x4 pa[2], pb[2];
+  auto gload = [&](int t) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    pa[0] = a_live ? *reinterpret_cast<const f32x4*>(ap + t * HD_KT) : z;
+    pa[1] = a_live ? *reinterpret_cast<const f32x4*>(ap + t * HD_KT + 4) : z;
+    if (b_fill) {
+      pb[0] = *reinterpret_cast<const f32x4*>(bp + t * HD_KT);
+      pb[1] = *reinterpret_cast<const f32x4*>(bp + t * HD_KT + 4);
+    }
+  };
+  auto lstore = [&](int buf) {
+    hb8* p = hl + buf * 3 * HD_ROWS * 4;
+    hb8 h, m, l;
+    hd_split(pa, 1.f, h, m, l);
+    int s = hd_slot(fr, fq);
+    p[s] = h;
+    p[HD_ROWS * 4 + s] = m;
+    p[2 * HD_ROWS * 4 + s] = l;
+    if (b_fill) {
+      hd_split(pb, sg, h, m, l);
+      s = hd_slot(HD_BM + fr, fq);
+      p[s] = h;
+      p[HD_ROWS * 4 + s] = m;
+      p[2 * HD_ROWS * 4 + s] = l;
+    }
+  };
+  const int wr = wave & 3, wc = wave >> 2, m = lane & 15, q = lane >> 4;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  constexpr int NT = HD_NEGK / HD_KT;
+  for (int t = 0; t < NT; ++t) {
+    if (t + 1 < NT) gload(t + 1);
+    const hb8* p = hl + (t & 1) * 3 * HD_ROWS * 4;
+    hb8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) {
+        fa[i][l] = p[l * HD_ROWS * 4 + hd_slot(32 * wr + 16 * i + m, q)];
+        fb[i][l] = p[l * HD_ROWS * 4 + hd_slot(HD_BM + 32 * wc + 16 * i + m, q)];
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+      }
+    if (t + 1 < NT) lstore((t + 1) & 1);
+    __syncthreads();
+  }
+  float* sl = slab + (long)kb * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 32 * wr + 16 * i + 4 * q + r, col = n0 + 32 * wc + 16 * j + m;
+        if (row < M) sl[(long)row * N + col] = sg * acc[i][j][r];
+      }
+}
+
+// out[m][n] = (((slab 0 + slab 1) + ...) + slab nblk-1) + bias[n]   (N % 4 == 0)
+__global__ __launch_bounds__(256) void enc_head_reduce_kernel(const float* __restrict__ slab, int nblk, long mn4, int N,
+                                                              const float* __restrict__ bias, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= mn4) return;
+  const f32x4* s = reinterpret_cast<const f32x4*>(slab);
+  f32x4 v = s[i];
+  for (int kb = 1; kb < nblk; ++kb) v += s[(long)kb * mn4 + i];
+  if (bias) {
+    const int n = (int)((4 * i) % N);
+    v += f32x4{bias[n], bias[n + 1], bias[n + 2], bias[n + 3]};
+  }
+  reinterpret_cast<f32x4*>(out)[i] = v;
+}
+
+}  // namespace
+
+namespace damc {
+int launch_dense_head_x3(const float* a, const float* w, const float* bias, int M, int N, int K, float* slab,
+                         size_t slab_floats, float* out, hipStream_t s) {
+  if (!a || !w || !slab || !out || M <= 0 || N <= 0 || N % HD_BN != 0 || K <= 0 || K % HD_NEGK != 0 ||
+      (uintptr_t)a % 16 || (uintptr_t)w % 16 || (uintptr_t)slab % 16 || (uintptr_t)out % 16)
+    return DAMC_ERR_UNSUPPORTED;
+  const int nblk = K / HD_NEGK;
+  if (slab_floats < (size_t)nblk * M * N) return DAMC_ERR_WORKSPACE;
+  static const bool lds_ok = [] {
+    return hipFuncSetAttribute((const void*)enc_head_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)HD_LDS) == hipSuccess;
+  }();
+  if (!lds_ok) return DAMC_ERR_UNSUPPORTED;
+  ProfScope ps("enc_head", 2.0 * M * (double)K * N * 6, s);
+  hipLaunchKernelGGL(enc_head_x3_kernel, dim3(N / HD_BN, nblk, (M + HD_BM - 1) / HD_BM), dim3(HD_THREADS), HD_LDS, s,
+                     a, w, M, N, K, slab);
+  const long mn4 = (long)M * N / 4;
+  hipLaunchKernelGGL(enc_head_reduce_kernel, dim3((unsigned)((mn4 + 255) / 256)), dim3(256), 0, s, slab, nblk, mn4, N,
+                     bias, out);
+  return (int)hipGetLastError();
+}
+}  // namespace damc
+
+namespace {
 
 // pixel splits of the statistics pass: <= 64 pixels per split (the Welford chain of a thread is serial),
 // merged with Chan's formula
@@ -876,6 +1043,7 @@ struct EncShapes {
   bool limb[DAMC_MAX_ENC_LAYERS] = {};
   bool first_fused = false;  // layer 0 as conv3_stats + conv3_apply_x3 (no stored conv output, no NHWC copy)
   int first_rows = 1, first_strips = 1;
+  bool head_geom = false;  // the last conv fits enc_head_x3_kernel (its slabs are in ks_max)
 };
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
@@ -933,6 +1101,15 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
     sh->in_max = std::max(sh->in_max, (size_t)B * F0.cout * (sh->first_strips * 3 + 2));
     sh->a3_max = std::max(sh->a3_max, (size_t)B * e->h * e->w * F0.cout * 6);
   }
+  // the dense head: the last conv covers its k x k input, reads the PyTorch weight (w_src), and the norm before it is
+  // the one-pass kernel (which then writes the head's CHW rows)
+  const int nl = e->n_layers - 1;
+  const damc_enc_layer_t& LH = e->layers[nl];
+  const long KH = (long)LH.cin * LH.k * LH.k;
+  sh->head_geom = nl >= 2 && sh->limb[nl] && LH.w_src && LH.stride == 1 && LH.pad == 0 && sh->h[nl] == LH.k &&
+                  sh->w[nl] == LH.k && LH.cout % HD_BN == 0 && KH % HD_NEGK == 0 && e->layers[nl - 1].in_gamma &&
+                  e->layers[nl - 1].cout % 32 == 0;
+  if (sh->head_geom) sh->ks_max = std::max(sh->ks_max, (size_t)(KH / HD_NEGK) * B * LH.cout);
   return true;
 }
 
@@ -1070,13 +1247,18 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   const char* pc = getenv("DAMC_ENC_PACK_CHECK");
   const bool pack_check = pc && pc[0] == '1';
   if (pack_check && (rc = (int)hipMemsetAsync(pack_err, 0, sizeof(int), s))) return rc;
+  const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel norm below
+  // the last conv as the dense head (enc_head_x3_kernel) where it fits; DAMC_ENC_HEAD=0 (read per call): on the limb
+  // GEMM over its packed weight limbs
+  const char* hde = getenv("DAMC_ENC_HEAD");
+  const bool head = sh.head_geom && !(hde && hde[0] == '0') && !(io && io[0] == '0') && (uintptr_t)xemb % 16 == 0;
   // the w_src layers' limb operands, all in one launch: as extra workgroups of the one-pass first layer when it runs
   // (conv3_in_fused_kernel), else on their own before it
   damc::PackConvList pl{};
   if (wsrc) {
     for (int i = 0; i < n; ++i) {
       const damc_enc_layer_t& L = e->layers[i];
-      if (!L.w_src) continue;
+      if (!L.w_src || (head && i == n - 1)) continue;  // (the head reads the fp32 weight itself)
       unsigned short* y = reinterpret_cast<unsigned short*>(wsrc + sh.wsrc_off[i]);
       if (pl.n < 8 && damc::pack_conv_x3_many_ok(L.w_src, L.cin, L.k)) {
         pl.w[pl.n] = L.w_src;
@@ -1150,12 +1332,17 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     return rc;
   }
   if (!pl_done && (rc = damc::launch_pack_conv_x3_many(pl, s))) return rc;
-  const char* io = getenv("DAMC_ENC_IN_ONEPASS");  // (read per call) 0: the three-kernel norm below
   const char* isl = getenv("DAMC_ENC_IN_SLABS");   // (read per call) 0: the split-K reduce kernel writes C first
   for (int i = i0; i < n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     float* out = (i + 1 == n) ? xemb : buf[(i + 1) & 1];
     const int hw = sh.h[i + 1] * sh.w[i + 1];
+    if (head && i == n - 1) {  // its CHW rows are in buf[(i + 1) & 1] (written by the norm before it)
+      if ((rc = damc::launch_dense_head_x3(buf[(i + 1) & 1], L.w_src, L.bias, B, L.cout, L.cin * L.k * L.k, kslab,
+                                           sh.ks_max, xemb, s)))
+        return rc;
+      continue;
+    }
     // the norm after this conv is the one-pass kernel; it then also sums the conv's split-K slabs itself
     const bool in1 = L.in_gamma && i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0');
     int ks_def = 0;
@@ -1185,19 +1372,21 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     if (in1) {
       ProfScope ps("instnorm", 0.0, s);
       const dim3 g(B, L.cout / 32);
-      float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
+      // in place: the next conv's fp32 input; before the head: its CHW rows, into this layer's (consumed) input buffer
+      const int chw = head && i + 2 == n;
+      float* y32 = chw ? buf[i & 1] : f32a_layer(i + 1) ? out : nullptr;
       const int ntn = (L.cout + 127) / 128;
       const long sstride4 = (long)((B * hw + 255) / 256) * ntn * (256 * 128 / 4);
       const float* sl = ks_def > 0 ? kslab : nullptr;
       if (hw <= 64)
         hipLaunchKernelGGL(in_fused_x3_kernel<1>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias, chw);
       else if (hw <= 128)
         hipLaunchKernelGGL(in_fused_x3_kernel<2>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias, chw);
       else
         hipLaunchKernelGGL(in_fused_x3_kernel<4>, g, dim3(256), 0, s, out, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps,
-                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias);
+                           L.slope, a3, y32, sl, ks_def, ntn, sstride4, L.bias, chw);
       DAMC_LAUNCH_CHECK();
       in32 = y32 != nullptr;
       a3_ready = !in32;

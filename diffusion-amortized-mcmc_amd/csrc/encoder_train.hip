@@ -413,7 +413,7 @@ extern "C" int damc_conv2d_backward_nhwc(const float* x, const float* dy, const 
 namespace {
 struct EncTrainPlan {
   int n, H[DAMC_MAX_ENC_LAYERS + 1], W[DAMC_MAX_ENC_LAYERS + 1];
-  bool limb[DAMC_MAX_ENC_LAYERS];
+  bool limb[DAMC_MAX_ENC_LAYERS], head[DAMC_MAX_ENC_LAYERS];
   size_t nbx[DAMC_MAX_ENC_LAYERS], wbytes[DAMC_MAX_ENC_LAYERS], convws[DAMC_MAX_ENC_LAYERS];
   size_t inws[DAMC_MAX_ENC_LAYERS], inbws[DAMC_MAX_ENC_LAYERS], cbws[DAMC_MAX_ENC_LAYERS];
   long x_off, y_off[DAMC_MAX_ENC_LAYERS], st_off[DAMC_MAX_ENC_LAYERS], out_off[DAMC_MAX_ENC_LAYERS];
@@ -461,6 +461,11 @@ int enc_train_plan(const damc_encoder_t* e, int B, EncTrainPlan* p) {
       p->wbytes[i] = (size_t)L.cout * L.cin * L.k * L.k * sizeof(float);
       p->convws[i] = damc_conv2d_workspace_floats(B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad) * sizeof(float);
     }
+    // the dense head (launch_dense_head_x3) for a last conv covering its input; its slabs in the conv workspace
+    const long KH = (long)L.cin * L.k * L.k;
+    p->head[i] = p->limb[i] && !norm && L.pad == 0 && ho == 1 && wo == 1 && L.k == hin && L.k == win &&
+                 L.cout % 64 == 0 && KH % 512 == 0 && (uintptr_t)L.w_src % 16 == 0;
+    if (p->head[i]) p->convws[i] = std::max(p->convws[i], (size_t)(KH / 512) * B * L.cout * sizeof(float));
     p->cbws[i] = damc_conv2d_backward_workspace_bytes(B, hin, win, L.cin, L.cout, L.k, L.stride, L.pad);
     if (p->cbws[i] == 0) return DAMC_ERR_UNSUPPORTED;
     const long act = (long)B * ho * wo * L.cout;
@@ -524,13 +529,25 @@ extern "C" int damc_encoder_train_forward(const damc_encoder_t* e, const float* 
   if (!workspace || workspace_bytes < p.ws_bytes) return DAMC_ERR_WORKSPACE;
   char* ws = static_cast<char*>(workspace);
   float* h = saved + p.x_off;
+  const char* hde = getenv("DAMC_ENC_HEAD");  // (read per call) 0: the last conv on the limb GEMM, as in the stage calls
+  const bool head_on = !(hde && hde[0] == '0');
   if ((rc = damc_nchw_to_nhwc(x, B, e->nc, e->h * e->w, h, stream))) return rc;
   for (int i = 0; i < p.n; ++i) {
     const damc_enc_layer_t& L = e->layers[i];
     const int hin = p.H[i], win = p.W[i], ho = p.H[i + 1], wo = p.W[i + 1];
     const bool norm = L.in_gamma != nullptr;
     float* y = norm ? saved + p.y_off[i] : xemb;
-    if (p.limb[i]) {
+    if (p.head[i] && head_on && (uintptr_t)xemb % 16 == 0) {
+      // the last conv as the inference encoder's dense head (no limb copy of the weight): the NHWC input (kept for the
+      // backward) per sample to (ci, ky, kx) order in bufa, then the head's two launches
+      const int T = L.k * L.k, K = T * L.cin;
+      float* a = reinterpret_cast<float*>(ws + p.bufa_at);
+      const long nx = (long)B * K;
+      hipLaunchKernelGGL(batch_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, as_stream(stream), h,
+                         B, T, L.cin, a);
+      rc = launch_dense_head_x3(a, L.w_src, L.bias, B, L.cout, K, reinterpret_cast<float*>(ws + p.conv_at),
+                                p.convws[i] / sizeof(float), xemb, as_stream(stream));
+    } else if (p.limb[i]) {
       if ((rc = damc_pack_conv2d_x3(L.w_src, L.cout, L.cin, L.k, ws + p.w_at, stream))) return rc;
       rc = damc_conv2d_x3_nhwc(h, B, hin, win, L.cin, ws + p.w_at, L.bias, L.cout, L.k, L.stride, L.pad, y,
                                ws + p.conv_at, p.convws[i], stream);

@@ -261,6 +261,12 @@ __device__ __forceinline__ void pack_conv_x3_block(const PackConvList& l, int bl
   }
 }
 
+// the encoder's dense head (encoder.hip enc_head_x3_kernel): out[M][N] = A . W^T + bias on the limb product, A [M][K]
+// and W [N][K] fp32 (a PyTorch Conv2d weight covering its whole input, with A the samples' CHW rows); N % 64 == 0,
+// K % 512 == 0, 16-B aligned A / W / slab / out; slab: K / 512 * M * N floats of scratch
+int launch_dense_head_x3(const float* a, const float* w, const float* bias, int M, int N, int K, float* slab,
+                         size_t slab_floats, float* out, hipStream_t s);
+
 // O_WGRAD on the limb engine: zdim = wg_phases * split-K slices
 int launch_wgrad_x3(const GemmArgs& a, int slices, const char* prof_name, double flops, hipStream_t s);
 

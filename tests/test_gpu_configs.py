@@ -329,6 +329,33 @@ def test_encoder_f32a_convs_are_bitwise(gpu_device, monkeypatch, name, B):
         assert torch.equal(v, outs["00"]), k
 
 
+@pytest.mark.parametrize("name,B,hw,nc", [("cifar10", 128, 32, 3), ("cifar10", 200, 32, 3), ("celeba64", 32, 64, 3),
+                                         ("mnist", 64, 28, 1)])
+def test_encoder_dense_head_vs_fp64(gpu_device, monkeypatch, name, B, hw, nc):
+    """The last conv as the dense head (encoder.hip enc_head_x3_kernel: the PyTorch weight read as fp32 and split into
+    limbs in the kernel, one workgroup per 128 rows x 64 columns x 512-k sign block, slabs summed in order) and on the
+    limb GEMM over the packed weight limbs (DAMC_ENC_HEAD=0): both against fp64 within 3x the fp32 reference's distance;
+    B = 200 has a partial 128-row block, mnist a 3 x 3 head (K = 4608).  The head's two launches appear in a profile
+    of the call as enc_head_x3_kernel / enc_head_reduce_kernel."""
+    from damc import amortizer, synth
+    from oracle import damc_oracle as orc
+    from src import diffusion_net as dn
+
+    enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=nc, nemb=1024, nif=64), 3).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(13, 4, (B, nc, hw, hw))).to(gpu_device)
+    monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
+    outs = {}
+    for h in "10":
+        monkeypatch.setenv("DAMC_ENC_HEAD", h)
+        outs[h] = amortizer.encoder_forward(enc, x).cpu().numpy()
+    with torch.no_grad():
+        e32 = orc.encoder_forward(enc.cpu(), x.cpu()).numpy()
+        e64 = orc.encoder_forward(enc.double(), x.cpu().double()).numpy()
+    _check("Encoder_%s B=%d xemb, dense head" % (name, B), outs["1"], e32, e64, 1e-7)
+    _check("Encoder_%s B=%d xemb, limb GEMM head" % (name, B), outs["0"], e32, e64, 1e-7)
+    assert not np.array_equal(outs["1"], outs["0"])  # (the head ran: its K order differs from the GEMM's)
+
+
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
 def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
     """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch (extra workgroups of the
@@ -342,6 +369,8 @@ def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, nam
     enc = synth.load_into(getattr(dn, "Encoder_" + name)(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
     x = torch.from_numpy(synth.uniform_f32(13, 2, (B, 3, hw, hw))).to(gpu_device)
     monkeypatch.setenv("DAMC_ENC_PACK_CHECK", "1")
+    # (the last conv on the limb GEMM in both: the dense head reads w_src as fp32, test_encoder_dense_head_vs_fp64)
+    monkeypatch.setenv("DAMC_ENC_HEAD", "0")
     monkeypatch.setenv("DAMC_ENC_WSRC", "1")
     a = amortizer.encoder_forward(enc, x).cpu()
     monkeypatch.setenv("DAMC_ENC_WSRC", "0")

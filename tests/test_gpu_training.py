@@ -488,8 +488,10 @@ def test_encoder_train_one_call_is_bitwise_the_stage_calls(gpu_device, monkeypat
     g = torch.from_numpy(synth.normal_f32(6, 1, (B, 1024))).to(gpu_device)
     assert training.encoder_train_supported(enc, x)
     out = {}
-    for fused in (False, True):
-        monkeypatch.setattr(training, "ENC_TRAIN_FUSED", fused)
+    for fused, head in ((False, "0"), (True, "0"), ("head", "1")):
+        # DAMC_ENC_HEAD=0: the one-call forward's last conv on the limb GEMM like the stage calls; "1": the dense head
+        monkeypatch.setenv("DAMC_ENC_HEAD", head)
+        monkeypatch.setattr(training, "ENC_TRAIN_FUSED", bool(fused))
         for p in enc.parameters():
             p.grad = None
         xe = enc(x)
@@ -498,4 +500,11 @@ def test_encoder_train_one_call_is_bitwise_the_stage_calls(gpu_device, monkeypat
         out[fused] = (xe.detach().clone(), [p.grad.clone() for p in enc.parameters()])
     assert torch.equal(out[False][0], out[True][0])
     for a, b in zip(out[False][1], out[True][1]):
+        assert torch.equal(a, b)
+    # the dense head changes xemb's rounding only (another K order); the backward reads the saved activations and the
+    # upstream gradient, never xemb, so every gradient is still bitwise
+    e = rel_l2(out["head"][0].cpu().numpy(), out[True][0].cpu().numpy())
+    print("%s B=%d xemb dense head vs limb GEMM: rel %.2e" % (name, B, e))
+    assert 0 < e < 1e-5 if nif == 64 else e < 1e-5
+    for a, b in zip(out["head"][1], out[True][1]):
         assert torch.equal(a, b)
