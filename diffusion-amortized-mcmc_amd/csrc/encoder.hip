@@ -610,44 +610,65 @@ __device__ __forceinline__ void hd_split(const f32x4 (&x)[2], float sg, hb8& h, 
   }
 }
 
-// grid (N / 64, K / 512, ceil(M / 128)); A [M][K] fp32 (CHW rows), W [N][K]; slab [K / 512][M][N]
+typedef __bf16 hb4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void hd_split4(const f32x4& x, float sg, hb4& h, hb4& m, hb4& l) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float v = sg * x[e];
+    const __bf16 b0 = (__bf16)v;
+    const float r1 = sub_rn(v, (float)b0);
+    const __bf16 b1 = (__bf16)r1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)sub_rn(r1, (float)b1);
+  }
+}
+
+// grid N / 64 * K / 512 * ceil(M / 128) (1-D); A [M][K] fp32 (CHW rows), W [N][K]; slab [K / 512][M][N].  PD K tiles
+// of global loads in flight per thread (register stages; the K loop is unrolled so every stage index is static): at
+// one workgroup per CU no other wave covers a tile's load latency
+template <int PD>
 __global__ __launch_bounds__(HD_THREADS) void enc_head_x3_kernel(const float* __restrict__ A,
                                                                  const float* __restrict__ W, int M, int N, int K,
-                                                                 float* __restrict__ slab) {
+                                                                 float* __restrict__ slab, int xcd) {
   extern __shared__ __attribute__((aligned(16))) hb8 hl[];  // [2 K tiles][3 limbs][HD_ROWS][4 slots]
+  constexpr int NT = HD_NEGK / HD_KT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * HD_BN, kb = blockIdx.y, r0 = blockIdx.z * HD_BM;
+  // XCD-aware tile order: workgroup L runs on XCD L % 8 (round-robin dispatch), so tile u = (L % 8) * (T / 8) + L / 8
+  // gives each XCD a contiguous run of tiles, n fastest: a sign block's 128 x 512 A block is fetched into one XCD's
+  // L2 (2 blocks per XCD at CIFAR B=128) instead of all eight
+  const int T = gridDim.x, L = blockIdx.x;
+  const int u = ((T & 7) || !xcd) ? L : (L & 7) * (T >> 3) + (L >> 3);
+  const int nn = N / HD_BN, nkb = K / HD_NEGK, rem = u % (nn * nkb);
+  const int n0 = (rem % nn) * HD_BN, kb = rem / nn, r0 = (u / (nn * nkb)) * HD_BM;
   const float sg = (kb & 1) ? -1.f : 1.f;
-  // staging: thread = (row fr, octet fq) of the A tile; the first 256 threads also of the B tile
-  const int fr = tid >> 2, fq = tid & 3;
-  const bool a_live = r0 + fr < M, b_fill = fr < HD_BN;
-  const float* ap = A + (long)(a_live ? r0 + fr : 0) * K + (long)kb * HD_NEGK + 8 * fq;
-  const float* bp = W + (long)(n0 + (b_fill ? fr : 0)) * K + (long)kb * HD_NEGK + 8 * fq;
-  f32x4 pa[2], pb[2];
-  auto gload = [&](int t) {
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    pa[0] = a_live ? *reinterpret_cast<const f32x4*>(ap + t * HD_KT) : z;
-    pa[1] = a_live ? *reinterpret_cast<const f32x4*>(ap + t * HD_KT + 4) : z;
-    if (b_fill) {
-      pb[0] = *reinterpret_cast<const f32x4*>(bp + t * HD_KT);
-      pb[1] = *reinterpret_cast<const f32x4*>(bp + t * HD_KT + 4);
-    }
+  // staging: thread = (row fr, octet fq) of the A tile and (row br, half octet bh) of the B tile: every thread issues
+  // the same loads (no branch, so the waits can count outstanding loads per stage); rows past M (a partial last row
+  // block) load row M - 1 again: an MFMA output row reads only its own A row, and those rows are never stored
+  const int fr = tid >> 2, fq = tid & 3, br = tid >> 3, bh = tid & 7;
+  const float* ap = A + (long)min(r0 + fr, M - 1) * K + (long)kb * HD_NEGK + 8 * fq;
+  const float* bp = W + (long)(n0 + br) * K + (long)kb * HD_NEGK + 4 * bh;
+  f32x4 pa[PD][2], pb[PD];
+  auto gload = [&](int t, int st) {
+    pa[st][0] = *reinterpret_cast<const f32x4*>(ap + t * HD_KT);
+    pa[st][1] = *reinterpret_cast<const f32x4*>(ap + t * HD_KT + 4);
+    pb[st] = *reinterpret_cast<const f32x4*>(bp + t * HD_KT);
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, int st) {
     hb8* p = hl + buf * 3 * HD_ROWS * 4;
     hb8 h, m, l;
-    hd_split(pa, 1.f, h, m, l);
-    int s = hd_slot(fr, fq);
+    hd_split(pa[st], 1.f, h, m, l);
+    const int s = hd_slot(fr, fq);
     p[s] = h;
     p[HD_ROWS * 4 + s] = m;
     p[2 * HD_ROWS * 4 + s] = l;
-    if (b_fill) {
-      hd_split(pb, sg, h, m, l);
-      s = hd_slot(HD_BM + fr, fq);
-      p[s] = h;
-      p[HD_ROWS * 4 + s] = m;
-      p[2 * HD_ROWS * 4 + s] = l;
-    }
+    hb4 h4, m4, l4;
+    hd_split4(pb[st], sg, h4, m4, l4);
+    hb4* p4 = reinterpret_cast<hb4*>(p);
+    const int s4 = 2 * hd_slot(HD_BM + br, bh >> 1) + (bh & 1);
+    p4[s4] = h4;
+    p4[2 * HD_ROWS * 4 + s4] = m4;
+    p4[4 * HD_ROWS * 4 + s4] = l4;
   };
   const int wr = wave & 3, wc = wave >> 2, m = lane & 15, q = lane >> 4;
   f32x4 acc[2][2];
@@ -655,12 +676,14 @@ __global__ __launch_bounds__(HD_THREADS) void enc_head_x3_kernel(const float* __
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gload(0);
-  lstore(0);
+#pragma unroll
+  for (int st = 0; st < PD && st < NT; ++st) gload(st, st);
+  lstore(0, 0);
   __syncthreads();
-  constexpr int NT = HD_NEGK / HD_KT;
+#pragma unroll
   for (int t = 0; t < NT; ++t) {
-    if (t + 1 < NT) gload(t + 1);
+    // stage t % PD held tile t, in LDS since the end of the last iteration: it takes tile t + PD
+    if (t + PD < NT) gload(t + PD, t % PD);
     const hb8* p = hl + (t & 1) * 3 * HD_ROWS * 4;
     hb8 fa[2][3], fb[2][3];
 #pragma unroll
@@ -682,7 +705,7 @@ __global__ __launch_bounds__(HD_THREADS) void enc_head_x3_kernel(const float* __
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
       }
-    if (t + 1 < NT) lstore((t + 1) & 1);
+    if (t + 1 < NT) lstore((t + 1) & 1, (t + 1) % PD);
     __syncthreads();
   }
   float* sl = slab + (long)kb * M * N;
@@ -698,13 +721,22 @@ __global__ __launch_bounds__(HD_THREADS) void enc_head_x3_kernel(const float* __
 }
 
 // out[m][n] = (((slab 0 + slab 1) + ...) + slab nblk-1) + bias[n]   (N % 4 == 0)
-__global__ __launch_bounds__(256) void enc_head_reduce_kernel(const float* __restrict__ slab, int nblk, long mn4, int N,
-                                                              const float* __restrict__ bias, float* __restrict__ out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+// 64-thread workgroups: 512 of them at CIFAR B=128 (256-thread groups left half the CUs without one)
+__global__ __launch_bounds__(64) void enc_head_reduce_kernel(const float* __restrict__ slab, int nblk, long mn4, int N,
+                                                             const float* __restrict__ bias, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 64 + threadIdx.x;
   if (i >= mn4) return;
   const f32x4* s = reinterpret_cast<const f32x4*>(slab);
   f32x4 v = s[i];
-  for (int kb = 1; kb < nblk; ++kb) v += s[(long)kb * mn4 + i];
+  int kb = 1;
+  for (; kb + 8 <= nblk; kb += 8) {  // eight slabs' loads in flight, then their adds in order
+    f32x4 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = s[(long)(kb + u) * mn4 + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; kb < nblk; ++kb) v += s[(long)kb * mn4 + i];
   if (bias) {
     const int n = (int)((4 * i) % N);
     v += f32x4{bias[n], bias[n + 1], bias[n + 2], bias[n + 3]};
@@ -723,15 +755,25 @@ int launch_dense_head_x3(const float* a, const float* w, const float* bias, int 
   const int nblk = K / HD_NEGK;
   if (slab_floats < (size_t)nblk * M * N) return DAMC_ERR_WORKSPACE;
   static const bool lds_ok = [] {
-    return hipFuncSetAttribute((const void*)enc_head_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    return hipFuncSetAttribute((const void*)enc_head_x3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)HD_LDS) == hipSuccess &&
+           hipFuncSetAttribute((const void*)enc_head_x3_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)HD_LDS) == hipSuccess;
   }();
   if (!lds_ok) return DAMC_ERR_UNSUPPORTED;
   ProfScope ps("enc_head", 2.0 * M * (double)K * N * 6, s);
-  hipLaunchKernelGGL(enc_head_x3_kernel, dim3(N / HD_BN, nblk, (M + HD_BM - 1) / HD_BM), dim3(HD_THREADS), HD_LDS, s,
-                     a, w, M, N, K, slab);
+  const long nwg = (long)(N / HD_BN) * nblk * ((M + HD_BM - 1) / HD_BM);
+  if (nwg > 0x7fffffffL) return DAMC_ERR_UNSUPPORTED;
+  const dim3 g((unsigned)nwg);
+  const char* pd = getenv("DAMC_ENC_HEAD_PD");  // (read per call) 1: one K tile of loads in flight (A/B)
+  const char* xe = getenv("DAMC_ENC_HEAD_XCD");  // (read per call) 0: tiles in launch order (A/B)
+  const int xcd = !(xe && xe[0] == '0');
+  if (pd && pd[0] == '1')
+    hipLaunchKernelGGL(enc_head_x3_kernel<1>, g, dim3(HD_THREADS), HD_LDS, s, a, w, M, N, K, slab, xcd);
+  else
+    hipLaunchKernelGGL(enc_head_x3_kernel<4>, g, dim3(HD_THREADS), HD_LDS, s, a, w, M, N, K, slab, xcd);
   const long mn4 = (long)M * N / 4;
-  hipLaunchKernelGGL(enc_head_reduce_kernel, dim3((unsigned)((mn4 + 255) / 256)), dim3(256), 0, s, slab, nblk, mn4, N,
+  hipLaunchKernelGGL(enc_head_reduce_kernel, dim3((unsigned)((mn4 + 63) / 64)), dim3(64), 0, s, slab, nblk, mn4, N,
                      bias, out);
   return (int)hipGetLastError();
 }

@@ -348,6 +348,10 @@ def test_encoder_dense_head_vs_fp64(gpu_device, monkeypatch, name, B, hw, nc):
     for h in "10":
         monkeypatch.setenv("DAMC_ENC_HEAD", h)
         outs[h] = amortizer.encoder_forward(enc, x).cpu().numpy()
+    monkeypatch.setenv("DAMC_ENC_HEAD", "1")
+    for env, v in (("DAMC_ENC_HEAD_PD", "1"), ("DAMC_ENC_HEAD_XCD", "0")):  # schedule and tile order only: bitwise
+        monkeypatch.setenv(env, v)
+        assert np.array_equal(amortizer.encoder_forward(enc, x).cpu().numpy(), outs["1"]), env
     with torch.no_grad():
         e32 = orc.encoder_forward(enc.cpu(), x.cpu()).numpy()
         e64 = orc.encoder_forward(enc.double(), x.cpu().double()).numpy()
