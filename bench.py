@@ -424,11 +424,16 @@ def q_update_bench(device, with_torch=True):
         Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
         opt_d.clip_and_step(100)
 
+    def six(fn):  # the reference's six consecutive Q updates per iteration (train_gen_recon.py:211-220): an update's
+        return lambda: [fn() for _ in range(6)]  # host half overlaps the previous update's kernels, as in training
+
     out = {"config": "cifar10 Q update B=128 (nif 64, nxemb 1024, ntemb 128): loss fwd+bwd, clip, AdamW",
-           "hip_ms": round(event_ms(step_hip), 3)}
+           "hip_ms": round(event_ms(six(step_hip)) / 6, 3), "hip_ms_isolated": round(event_ms(step_hip), 3),
+           "timing": "hip_ms / torch_ms: six back-to-back updates per sample / 6 (the training loop's form); "
+                     "hip_ms_isolated: one update per sample (its host time not overlapped)"}
     if with_torch:
         with training.stock_pytorch():
-            out["torch_ms"] = round(event_ms(step), 3)
+            out["torch_ms"] = round(event_ms(six(step)) / 6, 3)
         out["speedup_vs_torch"] = round(out["torch_ms"] / out["hip_ms"], 2)
     return out
 

@@ -152,9 +152,11 @@ __global__ void in_merge_kernel(const float* __restrict__ part, int B, int C, in
 
 // the normalise + affine + LeakyReLU of in_apply_kernel (same fmaf), written as the next convolution's limbs (x3
 // octets) instead of fp32 in place: the limb engine reads nothing else.  One thread per (pixel, channel octet).
-__global__ __launch_bounds__(256) void in_apply_x3_kernel(const float* __restrict__ y, long n8, int HW, int C,
+// y32 != NULL: fp32 in place instead (y32 == y; every thread rewrites only the octet it read), for a next conv that
+// stages its input as fp32 (gemm.hip X3_F32A)
+__global__ __launch_bounds__(256) void in_apply_x3_kernel(const float* y, long n8, int HW, int C,
                                                           const float* __restrict__ ss, float slope,
-                                                          unsigned short* __restrict__ y3) {
+                                                          unsigned short* __restrict__ y3, float* y32) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n8) return;
   const int C8 = C / 8;
@@ -173,7 +175,12 @@ __global__ __launch_bounds__(256) void in_apply_x3_kernel(const float* __restric
     const float t = fmaf(v[e], sa[e], sb[e]);
     v[e] = t > 0.f ? t : t * slope;
   }
-  damc::store_x3_octet(v, y3 + 24 * i);
+  if (y32) {
+    *reinterpret_cast<f32x4*>(y32 + 8 * i) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(y32 + 8 * i + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    damc::store_x3_octet(v, y3 + 24 * i);
+  }
 }
 
 // ---- the first layer (Conv2d k3 s1 p1 on the nc <= 4 image channels, then InstanceNorm + LeakyReLU) in two passes
@@ -282,12 +289,13 @@ __global__ __launch_bounds__(256) void conv3_stats_kernel(const float* __restric
   }
 }
 
-// pass 2: grid (B, S strips); wave w takes octets w, w+4, ..., lanes pixels; writes the limbs of lrelu(IN(y))
+// pass 2: grid (B, S strips); wave w takes octets w, w+4, ..., lanes pixels; writes the limbs of lrelu(IN(y)), or the
+// fp32 values (NHWC) at y32 for an F32A next conv
 template <int CIN>
 __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __restrict__ x, int H, int W, int C, int R,
                                                              const float* __restrict__ w, const float* __restrict__ bias,
                                                              const float* __restrict__ ss, float slope,
-                                                             unsigned short* __restrict__ y3) {
+                                                             unsigned short* __restrict__ y3, float* __restrict__ y32) {
   extern __shared__ __attribute__((aligned(16))) float sm3[];  // [9 CIN][C] weights, [C] bias, then the window
   const int b = blockIdx.x, s = blockIdx.y, r0 = s * R, rows = min(R, H - r0);
   float* wl = sm3;
@@ -311,7 +319,13 @@ __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __rest
         const float t = fmaf(v[e], sb[c0 + e], sb[C + c0 + e]);
         v[e] = t > 0.f ? t : t * slope;
       }
-      damc::store_x3_octet(v, y3 + 3 * ((((long)b * H + r0 + r) * W + xx) * C + c0));
+      const long off = (((long)b * H + r0 + r) * W + xx) * C + c0;
+      if (y32) {
+        *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        damc::store_x3_octet(v, y3 + 3 * off);
+      }
     }
   }
 }
@@ -1345,7 +1359,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       pl_done = true;
     }
     const int nconv = B * (C / 16), npk = pl_done ? 0 : pl.blk0[pl.n];
-    float* y32 = (one && f32a_layer(1)) ? buf[1] : nullptr;
+    float* y32 = f32a_layer(1) ? buf[1] : nullptr;
     const size_t smp = std::max(sm1, pl_done ? (size_t)0 : (size_t)pl.lds);
 #define DAMC_C1(CIN_)                                                                                               \
   if (one && L.cin == CIN_) {                                                                                       \
@@ -1362,7 +1376,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
                        L.in_beta, L.in_eps, ssb);                                                                   \
     hipLaunchKernelGGL(conv3_apply_x3_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,   \
-                       ssb, L.slope, a3);                                                                           \
+                       ssb, L.slope, a3, y32);                                                                      \
   }
     DAMC_C3(1) DAMC_C3(3) DAMC_C3(4)
 #undef DAMC_C3
@@ -1440,10 +1454,12 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       hipLaunchKernelGGL(in_merge_kernel, dim3((B * L.cout + 255) / 256), dim3(256), 0, s, inws, B, L.cout, S,
                          L.in_gamma, L.in_beta, L.in_eps, ssb);
       const long n8 = (long)B * hw * (L.cout / 8);
+      float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
       hipLaunchKernelGGL(in_apply_x3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, out, n8, hw, L.cout,
-                         ssb, L.slope, a3);
+                         ssb, L.slope, a3, y32);
       DAMC_LAUNCH_CHECK();
-      a3_ready = true;
+      in32 = y32 != nullptr;
+      a3_ready = !in32;
     } else if ((rc = damc_instnorm_lrelu_nhwc(out, B, hw, L.cout, L.in_gamma, L.in_beta, L.in_eps, L.slope, inws,
                                               stream))) {
       return rc;

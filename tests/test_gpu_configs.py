@@ -360,6 +360,30 @@ def test_encoder_dense_head_vs_fp64(gpu_device, monkeypatch, name, B, hw, nc):
     assert not np.array_equal(outs["1"], outs["0"])  # (the head ran: its K order differs from the GEMM's)
 
 
+def test_encoder_descriptor_cache_follows_the_parameters(gpu_device, monkeypatch):
+    """EncoderPlan caches its descriptor while the parameters keep their storages.  Values rewritten in place (the
+    EMA update's .data.copy_, the fp32-packed first layer included) and a parameter replaced by a new tensor are both
+    seen: the next call equals a fresh plan's, under the library packing and DAMC_ENC_WSRC=0."""
+    from damc import amortizer, synth
+    from src import diffusion_net as dn
+
+    for wsrc in "10":
+        monkeypatch.setenv("DAMC_ENC_WSRC", wsrc)
+        enc = synth.load_into(dn.Encoder_cifar10(nc=3, nemb=1024, nif=64), 3).to(gpu_device).eval()
+        x = torch.from_numpy(synth.uniform_f32(13, 5, (16, 3, 32, 32))).to(gpu_device)
+        a = amortizer.encoder_forward(enc, x)
+        assert torch.equal(amortizer.encoder_forward(enc, x), a)  # (the cached call)
+        with torch.no_grad():
+            enc.net[0].weight.mul_(0.5)
+            enc.net[4].weight.mul_(0.75)
+        b = amortizer.encoder_forward(enc, x)
+        assert torch.equal(b, amortizer.EncoderPlan(enc).forward(x)) and not torch.equal(a, b)
+        last = enc.net[-1]
+        last.weight = torch.nn.Parameter(last.weight.detach() * 0.5)
+        c = amortizer.encoder_forward(enc, x)
+        assert torch.equal(c, amortizer.EncoderPlan(enc).forward(x)) and not torch.equal(b, c)
+
+
 @pytest.mark.parametrize("name,B", [("cifar10", 128), ("celeba64", 32)])
 def test_encoder_library_packed_weights_are_bitwise(gpu_device, monkeypatch, name, B):
     """damc_enc_layer_t.w_src: the library packs every limb layer's PyTorch weight in one launch (extra workgroups of the
