@@ -191,33 +191,45 @@ __global__ __launch_bounds__(256) void in_apply_x3_kernel(const float* y, long n
 // octet at a time (its 8 x 9 CIN weights wave-uniform: scalar loads, no LDS traffic) and its lanes own pixels, whose
 // 9 CIN window values are read from LDS once for the 8 channels.  Both passes evaluate y with conv3_octet (fixed tap
 // order, one fmaf chain per channel), so the statistics describe exactly the values pass 2 normalises.
-template <int CIN>
+// PX horizontally adjacent pixels (x .. x + PX - 1 of row r) x one channel octet: the window values of the run are read
+// once (3 x (PX + 2) x CIN instead of PX x 9 CIN) and each weight pair once per run; every output keeps the same fmaf
+// chain (tap order, from 0, then + bias), so PX changes no value
+template <int CIN, int PX>
 __device__ __forceinline__ void conv3_octet(const float* __restrict__ win, int ld, int r, int x,
                                             const float* __restrict__ wl, int C, int c0, const float* __restrict__ bl,
-                                            float (&y)[8]) {
-  float xv[9 * CIN];
+                                            float (&y)[PX][8]) {
+  float xv[3][PX + 2][CIN];
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
+    for (int cx = 0; cx < PX + 2; ++cx)
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci) xv[ky][cx][ci] = win[((r + ky) * ld + x + cx) * CIN + ci];
+  float acc[PX][8];
+#pragma unroll
+  for (int px = 0; px < PX; ++px)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[px][e] = 0.f;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-      for (int ci = 0; ci < CIN; ++ci) xv[(ky * 3 + kx) * CIN + ci] = win[((r + ky) * ld + x + kx) * CIN + ci];
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int ci = 0; ci < CIN; ++ci) {  // wl: the LDS copy of damc_pack_conv2d's [(ky, kx, ci)][co] (a wave-uniform
+        const int t = (ky * 3 + kx) * CIN + ci;  // address: broadcast reads)
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wl + t * C + c0);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(wl + t * C + c0 + 4);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-  for (int t = 0; t < 9 * CIN; ++t) {  // wl: the LDS copy of damc_pack_conv2d's [(ky, kx, ci)][co] (a wave-uniform
-    const f32x4 w0 = *reinterpret_cast<const f32x4*>(wl + t * C + c0);  // address: broadcast reads)
-    const f32x4 w1 = *reinterpret_cast<const f32x4*>(wl + t * C + c0 + 4);
-    acc[0] = fmaf(w0.x, xv[t], acc[0]);
-    acc[1] = fmaf(w0.y, xv[t], acc[1]);
-    acc[2] = fmaf(w0.z, xv[t], acc[2]);
-    acc[3] = fmaf(w0.w, xv[t], acc[3]);
-    acc[4] = fmaf(w1.x, xv[t], acc[4]);
-    acc[5] = fmaf(w1.y, xv[t], acc[5]);
-    acc[6] = fmaf(w1.z, xv[t], acc[6]);
-    acc[7] = fmaf(w1.w, xv[t], acc[7]);
+        for (int px = 0; px < PX; ++px)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[px][e] = fmaf(wv[e], xv[ky][px + kx][ci], acc[px][e]);
+      }
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) y[e] = acc[e] + bl[c0 + e];
+  for (int px = 0; px < PX; ++px)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[px][e] = acc[px][e] + bl[c0 + e];
 }
 // the strip's input window: rows r0-1 .. r0+R of sample b, columns -1 .. W, zero outside, [row][col][ci] in LDS
 template <int CIN>
@@ -231,8 +243,9 @@ __device__ __forceinline__ void conv3_stage(const float* __restrict__ x, int b, 
 }
 
 // pass 1: grid (B, S strips of R rows); wave w takes octets w, w+4, ...; each lane a Welford chain over its pixels per
-// channel, then the 64 lanes merged (Chan, fixed butterfly order); part [B][C][S][3] as in_stats_kernel's
-template <int CIN>
+// channel (runs of PX pixels, W % PX == 0), then the 64 lanes merged (Chan, fixed butterfly order); part [B][C][S][3]
+// as in_stats_kernel's
+template <int CIN, int PX>
 __global__ __launch_bounds__(256) void conv3_stats_kernel(const float* __restrict__ x, int H, int W, int C, int R,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           float* __restrict__ part) {
@@ -252,21 +265,25 @@ __global__ __launch_bounds__(256) void conv3_stats_kernel(const float* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = Wf{0.f, 0.f, 0.f};
     float n = 0.f;
-    for (int p = lane; p < npix; p += 64) {
-      // the weights are re-read from LDS per pixel (broadcast reads); held in registers across the loop they took
+#pragma unroll 1
+    for (int p = lane * PX; p < npix; p += 64 * PX) {
+      // the weights are re-read from LDS per run (broadcast reads); held in registers across the loop they took
       // 216 VGPRs and left one wave per SIMD
       asm volatile("" ::: "memory");
       const int r = p / W, xx = p - r * W;
-      float y[8];
-      conv3_octet<CIN>(win, W + 2, r, xx, wl, C, c0, bl, y);
-      n += 1.f;
-      const float inv = 1.f / n;
+      float y[PX][8];
+      conv3_octet<CIN, PX>(win, W + 2, r, xx, wl, C, c0, bl, y);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = y[e] - a[e].mean;
-        a[e].mean += d * inv;
-        a[e].m2 += d * (y[e] - a[e].mean);
-        a[e].n = n;
+      for (int px = 0; px < PX; ++px) {
+        n += 1.f;
+        const float inv = 1.f / n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = y[px][e] - a[e].mean;
+          a[e].mean += d * inv;
+          a[e].m2 += d * (y[px][e] - a[e].mean);
+          a[e].n = n;
+        }
       }
     }
 #pragma unroll
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(256) void conv3_stats_kernel(const float* __restric
 
 // pass 2: grid (B, S strips); wave w takes octets w, w+4, ..., lanes pixels; writes the limbs of lrelu(IN(y)), or the
 // fp32 values (NHWC) at y32 for an F32A next conv
-template <int CIN>
+template <int CIN, int PX>
 __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __restrict__ x, int H, int W, int C, int R,
                                                              const float* __restrict__ w, const float* __restrict__ bias,
                                                              const float* __restrict__ ss, float slope,
@@ -309,22 +326,27 @@ __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __rest
   const float* sb = ss + (long)b * 2 * C;
   for (int o = wave; o < C / 8; o += 4) {
     const int c0 = __builtin_amdgcn_readfirstlane(o * 8);
-    for (int p = lane; p < npix; p += 64) {
-      asm volatile("" ::: "memory");  // weights re-read from LDS per pixel (see conv3_stats_kernel)
+#pragma unroll 1
+    for (int p = lane * PX; p < npix; p += 64 * PX) {
+      asm volatile("" ::: "memory");  // weights re-read from LDS per run (see conv3_stats_kernel)
       const int r = p / W, xx = p - r * W;
-      float v[8];
-      conv3_octet<CIN>(win, W + 2, r, xx, wl, C, c0, bl, v);
+      float y[PX][8];
+      conv3_octet<CIN, PX>(win, W + 2, r, xx, wl, C, c0, bl, y);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float t = fmaf(v[e], sb[c0 + e], sb[C + c0 + e]);
-        v[e] = t > 0.f ? t : t * slope;
-      }
-      const long off = (((long)b * H + r0 + r) * W + xx) * C + c0;
-      if (y32) {
-        *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else {
-        damc::store_x3_octet(v, y3 + 3 * off);
+      for (int px = 0; px < PX; ++px) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = fmaf(y[px][e], sb[c0 + e], sb[C + c0 + e]);
+          v[e] = t > 0.f ? t : t * slope;
+        }
+        const long off = (((long)b * H + r0 + r) * W + xx + px) * C + c0;
+        if (y32) {
+          *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          damc::store_x3_octet(v, y3 + 3 * off);
+        }
       }
     }
   }
@@ -1369,16 +1391,20 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   }
     DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
 #undef DAMC_C1
-#define DAMC_C3(CIN_)                                                                                               \
-  if (!one && L.cin == CIN_) {                                                                                      \
-    hipLaunchKernelGGL(conv3_stats_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,    \
-                       inws);                                                                                       \
+#define DAMC_C3(CIN_, PX_, PA_)                                                                                     \
+  if (!one && L.cin == CIN_ && px == PX_) {                                                                         \
+    hipLaunchKernelGGL((conv3_stats_kernel<CIN_, PX_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,     \
+                       L.bias, inws);                                                                               \
     hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
                        L.in_beta, L.in_eps, ssb);                                                                   \
-    hipLaunchKernelGGL(conv3_apply_x3_kernel<CIN_>, dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed, L.bias,   \
-                       ssb, L.slope, a3, y32);                                                                      \
+    hipLaunchKernelGGL((conv3_apply_x3_kernel<CIN_, PA_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,  \
+                       L.bias, ssb, L.slope, a3, y32);                                                              \
   }
-    DAMC_C3(1) DAMC_C3(3) DAMC_C3(4)
+    // runs of 4 pixels per lane in the statistics pass (the apply pass keeps one: its 2- and 4-pixel forms took 256 VGPRs)
+    // where the rows allow it (DAMC_ENC_FIRST_PX=1, read per call: one pixel per lane)
+    const char* fpx = getenv("DAMC_ENC_FIRST_PX");
+    const int px = (W % 4 == 0 && !(fpx && fpx[0] == '1')) ? 4 : 1;
+    DAMC_C3(1, 1, 1) DAMC_C3(3, 1, 1) DAMC_C3(4, 1, 1) DAMC_C3(1, 4, 1) DAMC_C3(3, 4, 1) DAMC_C3(4, 4, 1)
 #undef DAMC_C3
     DAMC_LAUNCH_CHECK();
     in32 = y32 != nullptr;
