@@ -205,11 +205,46 @@ def test_team_sweep_is_deterministic(am, gpu_device):
     assert np.array_equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("B", [37, 128])
+def test_limb_hyper_gemms_vs_fp32_engine(am, gpu_device, monkeypatch, B):
+    """The hyper GEMMs on the limb product (denoiser.hip hyper_x3_kernel, round 5: the PyTorch Wg / Wb rows read as
+    fp32 and split in the kernel) against the fp32-MFMA grouped launch (DAMC_SWEEP_HYPER=fp32): the first step's eps
+    agrees to rel-L2 1e-5, and a 10-step sweep's end point is as close to the fp64 oracle (same injected noise): within
+    3x the fp32 engine's distance (+1e-6).  B=37 leaves a partial 128-row tile in every block."""
+    from damc import synth
+    from oracle import damc_oracle as orc
+
+    n = 10
+    Q = _wide_q(gpu_device, n)
+    xemb = torch.from_numpy(synth.normal_f32(7, 1, (B, 1024))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(8, 1, (B, 128))).to(gpu_device)
+    noise = torch.from_numpy(synth.normal_f32(9, 1, (n - 1, B, 128))).to(gpu_device)
+    res = {}
+    for mode in ("limb", "fp32"):
+        monkeypatch.setenv("DAMC_SWEEP_HYPER", mode)
+        zt = zt0.clone()
+        eps = am.reverse_sweep(Q, xemb, zt, noise=noise, eps_log_steps=1)
+        torch.cuda.synchronize()
+        res[mode] = (zt.cpu().numpy(), eps.cpu().numpy())
+    with torch.no_grad():
+        z64, _ = orc.reverse_sweep(Q.cpu().double(), xemb.cpu().double(), zt0.cpu().double(), noise.cpu().double(), n,
+                                   -5.1, 9.8, "large")
+    z64 = z64.numpy()
+    e_l, e_f = rel_l2(res["limb"][0], z64), rel_l2(res["fp32"][0], z64)
+    d1 = rel_l2(res["limb"][1][0], res["fp32"][1][0])
+    print("B=%d eps1 limb vs fp32 %.2e; end |limb-fp64| %.2e |fp32-fp64| %.2e" % (B, d1, e_l, e_f))
+    assert np.isfinite(res["limb"][0]).all()
+    assert d1 <= 1e-5
+    assert e_l <= 3 * e_f + 1e-6
+
+
 @pytest.mark.gpu
 def test_grouped_hyper_gemms_are_bitwise_the_separate_launches(am, gpu_device, monkeypatch):
-    """The seven hyper GEMMs run as one grouped launch; the same tiles as seven launches, bit for bit."""
+    """The seven hyper GEMMs on the fp32-MFMA engine (DAMC_SWEEP_HYPER=fp32) run as one grouped launch; the same tiles
+    as seven launches, bit for bit."""
     from damc import synth
 
+    monkeypatch.setenv("DAMC_SWEEP_HYPER", "fp32")
     Q = _wide_q(gpu_device, 20)
     xemb = torch.from_numpy(synth.normal_f32(7, 0, (128, 1024))).to(gpu_device)
     zt0 = torch.from_numpy(synth.normal_f32(8, 0, (128, 128))).to(gpu_device)
