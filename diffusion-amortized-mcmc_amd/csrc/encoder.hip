@@ -533,7 +533,23 @@ __global__ __launch_bounds__(256) void in_fused_x3_kernel(const float* y, int HW
       const int r = rm & 3;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
-      for (int sl = 0; sl < ks; ++sl) {
+      int sl = 0;
+      for (; sl + 2 <= ks; sl += 2) {  // two slabs' 16 loads in flight, then their adds in slab order
+        const float* s0 = slab + ((long)sl * sstride4 + base) * 4 + r;
+        const float* s1 = s0 + sstride4 * 4;
+        float t0[8], t1[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t0[e] = s0[4 * e];
+          t1[e] = s1[4 * e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[it][e] += t0[e];
+          v[it][e] += t1[e];
+        }
+      }
+      for (; sl < ks; ++sl) {
         const float* src = slab + ((long)sl * sstride4 + base) * 4 + r;
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[it][e] += src[4 * e];
