@@ -1,5 +1,5 @@
 """Reverse sweep (CIFAR Q, B=128, 100 steps, the bench's config) wall time per call over DAMC_SWEEP_HYPER (limb /
-fp32), interleaved; three back-to-back calls per sample as in bench.py.  usage: python tools/sweep_hyper_ab.py [reps]"""
+fp32), interleaved; three back-to-back calls per sample as in bench.py.  usage: python tools/sweep_hyper_ab.py [reps] [mode,...]  (mode: limb / fp32, or VAR=value)"""
 import os
 import sys
 
@@ -31,8 +31,11 @@ def sweep():
 
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(reps):
-    for mode in ("limb", "fp32"):
-        os.environ["DAMC_SWEEP_HYPER"] = mode
+    for mode in sys.argv[2].split(",") if len(sys.argv) > 2 else ("limb", "fp32"):
+        var, _, val = mode.partition("=")
+        if not val:  # a bare mode name: DAMC_SWEEP_HYPER
+            var, val = "DAMC_SWEEP_HYPER", mode
+        os.environ[var] = val
         sweep()
         ts = []
         for _ in range(5):
