@@ -2594,8 +2594,9 @@ __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int 
 // latency-bound at 4 K tiles.  Same fragments (octet q of the tile per lane quarter), the same six-product MFMA
 // sequence and the same block fold (fmaf(+1, acc, 0)), then gemm_x3_kernel's octet epilogue (x3_octet_epilogue):
 // every output is bitwise the 128 x 256 kernel's (tests/test_gpu_langevin.py).
-// Round 5: each wave takes 16 rows x 16 NTW columns (NTW = 1: 4x the waves of the 64-column form, so a CU holds 16
-// waves and keeps 4 K tiles' loads in flight per lane -- the 64-column wave serialised its loads at 86 VGPRs), and
+// Round 5: each wave takes 16 rows x 16 NTW columns (NTW = 2 by default: twice the waves of the 64-column form, which
+// serialised its loads at 86 VGPRs, and half those of NTW = 1, whose 1024 workgroups measured 5-17 us slower per CIFAR
+// B=16 step), and
 // F32B reads the weights as fp32 rows split in registers with the packer's RNE split (2/3 of the limb bytes).  The
 // MFMA sequence per output is unchanged, so every output is still bitwise the 128 x 256 kernel's.
 template <bool F32B, int NTW>
@@ -3263,7 +3264,12 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       // operands); DAMC_X3_SKINNY_F32B=0 (read per call) reads the limbs
       const char* efb = getenv("DAMC_X3_SKINNY_F32B");
       const dim3 gsk((unsigned)((c.N + 63) / 64), (unsigned)((c.M + 15) / 16));
-      if (c.b32k && (c.K % 32) == 0 && (uintptr_t)c.b32k % 16 == 0 && !(efb && efb[0] == '0'))
+      // 32 columns per wave by default (NTW = 2: CIFAR B=16 step -5 to -17 us, B=32 -4 us against 16 columns, same-box
+      // pairs in profiles/r05/skinny_ntw_ab.txt); DAMC_X3_SKINNY_NTW=1 (read per call) keeps 16
+      const char* ent = getenv("DAMC_X3_SKINNY_NTW");
+      if (!(ent && ent[0] == '1') && c.b32k && (c.K % 32) == 0 && (uintptr_t)c.b32k % 16 == 0 && !(efb && efb[0] == '0'))
+        hipLaunchKernelGGL((x3_skinny_kernel<true, 2>), dim3((unsigned)((c.N + 127) / 128), gsk.y), dim3(256), 0, s, c);
+      else if (c.b32k && (c.K % 32) == 0 && (uintptr_t)c.b32k % 16 == 0 && !(efb && efb[0] == '0'))
         hipLaunchKernelGGL((x3_skinny_kernel<true, 1>), gsk, dim3(256), 0, s, c);
       else
         hipLaunchKernelGGL((x3_skinny_kernel<false, 1>), gsk, dim3(256), 0, s, c);
