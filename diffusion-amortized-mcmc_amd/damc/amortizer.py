@@ -329,14 +329,14 @@ def q_forward(Q, x=None, b=None, device=None, cond_w=-1, zt=None, seed=None, cha
     return zt
 
 
-def _q_forward_guided(Q, x, w):
+def _q_forward_guided(Q, x, w, eps_trace=None):
     """Classifier-free guidance (cond_w > 0, diffusion_net.py:595-620; round 5): the reference's step loop with its
     draws in its order (zt from the host generator, then per step a fresh prior embedding's noise and the step's
     noise on the device), each step's two denoiser evaluations on libdamc (Diffusion_UnetA.forward ->
     damc.training.denoiser_apply, the training kernels' forward) and the prior embedding on damc_gemm; the guidance
     combination and the schedule algebra are the reference's own tensor formulas (src/diffusion_helper_func.py).
     Unlike the unguided sweep (one team launch), this runs one denoiser launch sequence per evaluation: the
-    reference's drivers never set cond_w."""
+    reference's drivers never set cond_w.  eps_trace (tests): a list that receives each step's guided eps_pred."""
     from src.diffusion_helper_func import diffusion_reverse, logsnr_schedule_fn, pred_x_from_eps
 
     b, device, n = len(x), x.device, int(Q.n_interval)
@@ -351,6 +351,8 @@ def _q_forward_guided(Q, x, w):
         xemb_unc = prior_embedding(Q, torch.randn(b, Q.nz, device=device))
         eps_pred_unc = Q.p(z=zt, logsnr=logsnr_t, xemb=xemb_unc)
         eps_pred = (1 + w) * eps_pred - w * eps_pred_unc
+        if eps_trace is not None:
+            eps_trace.append(eps_pred.clone())
         logsnr_t = logsnr_t.reshape((b, 1))
         logsnr_s = logsnr_s.reshape((b, 1))
         pred_z = pred_x_from_eps(z=zt, eps=eps_pred, logsnr=logsnr_t)

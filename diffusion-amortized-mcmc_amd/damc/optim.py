@@ -121,6 +121,17 @@ class Adam(torch.optim.Optimizer):
         super().__setstate__(state)
         self.last_grad_norm = None
 
+    def state_dict(self):
+        """torch.optim.Optimizer.state_dict with a private ``step`` tensor per parameter.  ``_advance_steps`` lets the
+        parameters of a group share one counter; torch's own state_dict (and torch.save / torch.load after it) would
+        keep that sharing, and a stock Adam / AdamW that loads it adds 1 to the shared tensor once per parameter
+        (every count 6.0 instead of 3.0 after one resumed step).  The clones carry the same values, so the
+        dict interchanges with torch's; this optimiser's own state keeps the shared counter."""
+        sd = super().state_dict()
+        sd["state"] = {k: ({**v, "step": v["step"].clone()} if isinstance(v.get("step"), torch.Tensor) else v)
+                       for k, v in sd["state"].items()}
+        return sd
+
     def zero_grad(self, set_to_none=True):
         """torch.optim.Optimizer.zero_grad; set_to_none (the default) as a plain loop (torch's walks the same
         parameters through its profiler scope and foreach grouping: ~0.1 ms of host time per Q update)."""

@@ -141,24 +141,41 @@ _DN_PARAMS = weakref.WeakKeyDictionary()  # denoiser -> (entries, owning (module
 def _denoiser_params(p):
     """[(field, block index or None, parameter)] in a fixed order.  Cached per module (walking ~60 submodule
     attributes costs ~0.1 ms of host time per call, twice per Q update); the cache is revalidated every call against
-    the owning modules' parameter dicts, so a parameter replaced by assignment is picked up."""
+    the owning modules' parameter dicts, so a parameter replaced by assignment is picked up, and against every
+    parent-to-child link of the module tree it walked (a replaced submodule, e.g. ``blk._skip =
+    nn.Linear(...)``, leaves the old module's parameter dict intact, so the parameter check alone would hit)."""
     c = _DN_PARAMS.get(p)
-    if c is not None and all(d.get(k) is t for (d, k), (_, _, t) in zip(c[1], c[0])):
+    if (c is not None and all(d.get(k) is t for (d, k), (_, _, t) in zip(c[1], c[0])) and
+            all(d.get(k) is m for d, k, m in c[2])):
         return c[0]
-    t1, t2 = p.time_mlp[1], p.time_mlp[3]
+    links = []
+
+    def child(parent, name):
+        m = parent._modules[name]
+        links.append((parent._modules, name, m))
+        return m
+
+    tm = child(p, "time_mlp")
+    t1, t2 = child(tm, "1"), child(tm, "3")
+    blocks = []
+    for seq in ("in_layers", "mid_layers", "out_layers"):
+        ml = child(p, seq)
+        blocks += [child(ml, k) for k in list(ml._modules)]
+    assert blocks == _blocks_of(p)
     out = [("bmat", None, p.B), ("tw1", None, t1.weight), ("tb1", None, t1.bias), ("tw2", None, t2.weight),
            ("tb2", None, t2.bias)]
     own = [(p._parameters, "B"), (t1._parameters, "weight"), (t1._parameters, "bias"), (t2._parameters, "weight"),
            (t2._parameters, "bias")]
-    for b, blk in enumerate(_blocks_of(p)):
-        lc = blk._layer_ctx[1]
-        mods = (blk._layer[0], blk._layer[0], blk._skip, blk._skip, blk._hyper_gate, blk._hyper_gate,
-                blk._hyper_bias, lc, lc)
+    for b, blk in enumerate(blocks):
+        lc = child(child(blk, "_layer_ctx"), "1")
+        l0 = child(child(blk, "_layer"), "0")
+        sk, hg, hb = child(blk, "_skip"), child(blk, "_hyper_gate"), child(blk, "_hyper_bias")
+        mods = (l0, l0, sk, sk, hg, hg, hb, lc, lc)
         names = ("weight", "bias", "weight", "bias", "weight", "bias", "weight", "weight", "bias")
         for key, m, nm in zip(_BLOCK_KEYS, mods, names):
             out.append((key, b, getattr(m, nm)))
             own.append((m._parameters, nm))
-    _DN_PARAMS[p] = (out, own)
+    _DN_PARAMS[p] = (out, own, links)
     return out
 
 
@@ -284,6 +301,9 @@ def q_noise_glue(q, u, z, eps, logsnr_out=None):
     dev = z.device
     zt = torch.empty(B, nz, dtype=torch.float32, device=dev)
     se = torch.empty(B, ntemb, dtype=torch.float32, device=dev)
+    # the kernel indexes u, z and eps as dense rows; a strided eps (randn_like keeps z's strides) would otherwise be
+    # read in its storage order while q_loss reads the logical eps
+    u, z, eps = u.contiguous(), z.contiguous(), eps.contiguous()
     check(_lib.lib().damc_q_noise_glue(ptr(u), ptr(z), ptr(eps), B, nz, float(q.logsnr_min), float(q.logsnr_max),
                                        ptr(_freqs(ntemb // 2, dev)), ntemb, ptr(logsnr_out), ptr(zt), ptr(se),
                                        _lib.stream_ptr(dev)), "damc_q_noise_glue")
@@ -333,6 +353,10 @@ def _ebm_layers(E):
     if len(mods) != 5 or len(lins) != 3 or len(acts) != 2 or mods[0] is not lins[0] or mods[2] is not lins[1]:
         return None
     if any(hasattr(m, "weight_orig") for m in lins) or acts[0].negative_slope != acts[1].negative_slope:
+        return None
+    # the backward (ebm.hip et_dh2_kernel / et_mask_kernel) reads LReLU' from the sign of the post-activation, which is
+    # the pre-activation's sign only for a slope >= 0: other slopes keep the stock modules
+    if not acts[0].negative_slope >= 0:
         return None
     if lins[2].out_features != 1 or any(m.bias is None for m in lins):
         return None

@@ -24,19 +24,19 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(tmp, world, scaling, torchrun=False, backend="gloo", **extra_env):
+def _run(tmp, world, scaling, torchrun=False, backend="gloo", extra_args=(), timeout=240, **extra_env):
     os.makedirs(tmp, exist_ok=True)
     env = dict(os.environ, DAMC_DIST_BACKEND=backend, DAMC_BENCH_DUMP=str(tmp), **extra_env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     args = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
-            "--scaling", scaling]
+            "--scaling", scaling] + list(extra_args)
     if torchrun:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     else:
         cmd = [sys.executable] + args
-    r = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     return json.loads(line)

@@ -190,3 +190,13 @@ def test_adam_step_counters_with_partial_gradients(gpu_device):
     to2 = torch.optim.AdamW(mine, **kw)
     to2.load_state_dict(do.state_dict())
     assert [float(to2.state[p]["step"]) for p in mine] == [float(to.state[p]["step"]) for p in ref]
+    # ... and the stock optimiser keeps stepping from there exactly as torch's own (a shared counter in
+    # the state_dict was advanced once per parameter by torch's step)
+    _set_grads(ref, 6)
+    _set_grads(mine, 6)
+    to.step()
+    to2.step()
+    torch.cuda.synchronize()
+    assert [float(to2.state[p]["step"]) for p in mine] == [float(to.state[p]["step"]) for p in ref]
+    for a, b in zip(mine, ref):
+        assert _rel(a.detach(), b.detach()) < STEP_TOL

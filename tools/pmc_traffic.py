@@ -59,12 +59,14 @@ def main():
     for c in sorted(set(f) | set(w)):
         rd = 2.0 * f.get(c, 0.0) * 1024
         wr = w.get(c, 0.0) * 1024
-        res[c] = dict(fetch_bytes_per_launch=rd, write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr,
+        res[c] = dict(fetch_bytes_per_launch=rd, fetch_size_uncorrected_bytes=f.get(c, 0.0) * 1024,
+                      write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr,
                       correction="FETCH_SIZE x2 (gfx950 half-count), KiB->B")
     json.dump(res, open(out, "w"), indent=1)
     for c, v in res.items():
-        print("%-18s read %8.1f MB  write %8.1f MB" % (c, v["fetch_bytes_per_launch"] / 1e6,
-                                                   v["write_bytes_per_launch"] / 1e6))
+        print("%-18s read %8.1f MB (FETCH_SIZE %8.1f MB x2)  write %8.1f MB" % (
+            c, v["fetch_bytes_per_launch"] / 1e6, v["fetch_size_uncorrected_bytes"] / 1e6,
+            v["write_bytes_per_launch"] / 1e6))
 
 
 if __name__ == "__main__":
