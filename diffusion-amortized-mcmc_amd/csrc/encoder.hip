@@ -1187,9 +1187,12 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
                     (F0.cin == 1 || F0.cin == 3 || F0.cin == 4) && F0.cout % 64 == 0 && F0.cout <= 512 &&
                     F0.in_gamma && F0.w_packed && !damc::conv_kmajor_ok(F0.cin) && e->w <= 1024;
   if (sh->first_fused) {
-    // ~1024 blocks over the batch (each strip's lanes merge their statistics once, a butterfly per channel octet),
-    // at most 64 strips per sample, at least 128 pixels per strip
-    const int want = std::max(1, std::min(64, 1024 / B));
+    // strips per sample from the sample's shape alone, never the batch (each strip's lanes merge their statistics once,
+    // a butterfly per channel octet, and in_merge_kernel adds the strips in order: the strip partition sets the
+    // rounding, so a batch sharded over ranks must keep the whole batch's partition to reproduce its xemb bit for bit;
+    // round 5 took ~1024 / B strips, and 8 x B=8 CelebA-HQ shards differed from B=64 in every row,
+    // tests/test_gpu_strong_scaling.py): ~512 pixels per strip, at most 64 strips, at least 128 pixels per strip
+    const int want = std::max(1, std::min(64, e->h * e->w / 512));
     sh->first_rows = std::max((e->h + want - 1) / want, (128 + e->w - 1) / e->w);
     sh->first_strips = (e->h + sh->first_rows - 1) / sh->first_rows;
     sh->in_max = std::max(sh->in_max, (size_t)B * F0.cout * (sh->first_strips * 3 + 2));

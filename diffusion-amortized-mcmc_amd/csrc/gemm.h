@@ -115,7 +115,19 @@ struct GemmArgs {
   // split-K slab layout: 0 row-major [M][N] per block; 1 the 256 x 128 kernel's register layout, per block
   // [tile][wave][4 x 4 tiles][64 lanes] f32x4 (16-B stores straight from the accumulators; the reduce maps back)
   int kslab_reg = 0;
+  // split-K in-GEMM ordered fix-up (gemm.hip X3_FIXUP; register-layout slabs on the F32A path, grids of <= 256
+  // workgroups): 2 X3_KTICKETS words -- an arrival counter per (phase, output tile), then a claim word per (phase, tile,
+  // slice) -- zero when the call began; each launch tags the words it touches with its epoch (kepoch = ++*kepoch_ctr, a
+  // host counter of the call, < 2^16), so one zeroing per call serves all of its launches; null: the separate reduce
+  // launch.  Callers set them only where they zeroed the words (the posterior call, once per call)
+  unsigned* kticket = nullptr;
+  unsigned* kepoch_ctr = nullptr;
+  unsigned kepoch = 0;
+  unsigned* fixup_probe = nullptr;  // damc_x3_fixup_probe's counters (diagnostics; null: off)
 };
+// words per half of GemmArgs::kticket (counters, claims): a split grid has < 256 unsplit tiles x phases, the fix-up grid
+// <= 256 workgroups
+constexpr int X3_KTICKETS = 1024;
 // k per sign block of a limb-engine conv weight (GemmArgs::negk), from the conv's shape alone (never the batch, so a
 // batch split over ranks runs the blocks, slabs and sums of the whole batch).  W16 = (256 x 128 output tiles of the
 // GEMM at 16 samples) x K measures how finely a 16-sample batch must split K to fill the chip:

@@ -1062,6 +1062,11 @@ constexpr int X3_F32A = 2097152, X3A_ROWB = 128;
 // 74 KB of LDS so two workgroups share a CU: a small-batch conv fills the chip without split-K slabs (every output
 // takes the default tile's MFMA sequence, so it is bitwise the default and the split forms)
 constexpr int X3_NARROW = 4194304;
+// split-K with the in-GEMM ordered fix-up (GemmArgs::kticket; the F32A register-slab path): the last workgroup of a
+// tile to arrive sums the tile's slabs in slab order and runs the unsplit epilogue, so no reduce launch follows
+constexpr int X3_FIXUP = 8388608;
+constexpr int X3_FIXUP_WAIT = 3000;  // the fix-up's bounded wait for the other slices: 30 us of s_memrealtime (100 MHz)
+static unsigned* g_fixup_probe = nullptr;  // damc_x3_fixup_probe (diagnostics)
 __device__ __forceinline__ int f32a_swz(int r) { return ((r >> 1) & 7) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
 static_assert(X3_NEGK % 32 == 0 && (X3_NEGK & (X3_NEGK - 1)) == 0, "sign blocks are whole K tiles, a power of two");
 constexpr int X3_CHUNKS = 12;  // 16-B chunks per row and K tile (4 octets x 3 limbs)
@@ -1110,6 +1115,25 @@ __device__ __forceinline__ void proj16(const float* tile, int ts, int r0, int C,
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc[t], 0, 0, 0);
     }
+  }
+}
+
+// proj16 with the b operands preloaded into registers (w[g][t] = weight row 16 t + m, k = 16 g + 4 q .. + 3, as
+// x3_ksplit_reduce_proj_kernel holds them): the same MFMA sequence per output, so bitwise proj16
+template <int NT>
+__device__ __forceinline__ void proj16_pre(const float* tile, int ts, int r0, int C, const f32x4 (&w)[PROJ_CHUNK / 16][4],
+                                           f32x4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63, m = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < PROJ_CHUNK / 16; ++g) {
+    if (16 * g >= C) break;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(tile + (r0 + m) * ts + 16 * g + 4 * q);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], w[g][t][e], acc[t], 0, 0, 0);
   }
 }
 
@@ -1224,6 +1248,9 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   // compile-time variant, so the block-total registers of the unsplit kernel drop out
   constexpr bool KREG = (V & 1048576) != 0;
   static_assert(!KREG || (M16 && !(V & (32 | 2048 | 65536 | 131072 | 262144 | 524288))), "KREG: default tiles only");
+  // in-GEMM ordered fix-up of the split-K slabs (round 6; the protocol is described where the epilogue runs it)
+  constexpr bool FIXUP = (V & X3_FIXUP) != 0;
+  static_assert(!FIXUP || (KREG && F32A), "FIXUP: the F32A register-slab split-K path");
   const int nslz = KSPLIT ? p.ksplit / p.kbpw : 1;
   const int zph = KSPLIT ? z / nslz : z, zsl = KSPLIT ? z - zph * nslz : 0;
   if (OM == O_PHASE) {
@@ -1719,7 +1746,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
             acc16[i][j] *= sg;
             if (m0 + wave * 32 + a * 16 < p.M) {
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl, voff,
-                                                     soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, 0);
+                                                     soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, FIXUP ? 16 : 0);
               // wait states before any VALU may rewrite the store's data VGPRs: the register allocator reuses them
               // for the next tile's scaled copy at once, and without these nops 3 of every 16 slab tiles held the
               // next tile's values (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt).  Observed with ROCm 7.2.0's
@@ -2187,9 +2214,8 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
     c[2] = t1;
     c[3] = r1;
   }
-  if (KREG) return;  // every block already in its slab
-  // the last partial block
-  {
+  if (KREG && !FIXUP) return;  // every block already in its slab
+  if constexpr (!FIXUP) {  // the last partial block
     const float sg = (p.b_negblk && nk > 0 && (((nk - 1 + kt0) >> FLOG) & 1)) ? -1.f : 1.f;
     if (M16) {
       constexpr int MI = NARROW ? 2 : 4;
@@ -2212,66 +2238,16 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   // 2 x 16-B fp32 stores and (C3) 3 x 16-B limb stores per octet, each row's 128 channels contiguous
   constexpr int TS = BN + 4;  // tile row stride (floats): 4-row groups of a 16x16 store land 16 banks apart
   static_assert(BM * TS * 4 + BM * 8 <= 2 * (BM + BN) * X3_ROWB, "epilogue tile exceeds the LDS");
+  static_assert(!FIXUP || BM * TS * 4 + BM * 8 <= 2 * (BM + BN) * X3_ROWB - 16, "the fix-up's last word overlaps the tile");
   float* tile = reinterpret_cast<float*>(smem);
   long* rowtab = reinterpret_cast<long*>(smem + BM * TS * 4);
-  if (tid < BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
-  if (F32A) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          tile[(wave * 32 + (i >> 1) * 16 + 4 * (lane >> 4) + r) * TS + ((i & 1) * 4 + j) * 16 + (lane & 15)] =
-              acc16[i][j][r];
-  } else if (NARROW) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          tile[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 32 + j * 16 + (lane & 15)] = acc16[i][j][r];
-  } else if (M16) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          tile[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 64 + j * 16 + (lane & 15)] = acc16[i][j][r];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          tile[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TS + wn * 64 + j * 32 + (lane & 31)] =
-              acc[i][j][r];
-  }
-  __syncthreads();
-  if (KSPLIT) {  // row-major slabs (one block per workgroup): the fp32 tile into its slab; the reduce applies the epilogue
-    float* sl = p.kslab + ((long)zph * p.ksplit + zsl) * p.M * p.N;
-#pragma unroll 2
-    for (int it = 0; it < BM * BN / 8 / 512; ++it) {
-      const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
-      const int m = m0 + row, n = n0 + oct * 8;
-      if (m >= p.M || n >= p.N) continue;
-      float* d = sl + (long)m * p.N + n;
-      *reinterpret_cast<f32x4*>(d) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8);
-      *reinterpret_cast<f32x4*>(d + 4) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8 + 4);
-    }
-    return;
-  }
   float* Cz = p.C;
-  if ((OM == O_DENSE || OM == O_WGRAD) && Cz) Cz += (long)z * p.c_zstride;
-#pragma unroll 2
-  for (int it = 0; it < BM * BN / 8 / 512; ++it) {
-    const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
+  if ((OM == O_DENSE || OM == O_WGRAD) && Cz) Cz += (long)(KSPLIT ? zph : z) * p.c_zstride;
+  // one (row, channel octet) of the tile through the epilogue (bias + act / LReLU' mask, sign bits, fp32, limbs)
+  auto octet = [&](int row, int oct) {
     const int n = n0 + oct * 8;
     const long rowoff = rowtab[row];
-    if (rowoff < 0 || n >= p.N) continue;
+    if (rowoff < 0 || n >= p.N) return;
     const long idx = rowoff + n;
     const f32x4 t0 = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8);
     const f32x4 t1 = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8 + 4);
@@ -2322,43 +2298,270 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
-  }
-  if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A)) {
-    // fused output-layer projection (GemmArgs::proj_out), proj16 as proj_rows_kernel, P indexed by the output pixel,
-    // one chain per 128-channel chunk into partial buffer chunk (proj_rows_kernel's chunking).  WIDE: the tile holds
-    // every channel (n0 == 0, N <= 256), 8 waves x 16 rows, all chunks.  F32A: the tile holds channels n0 .. n0 + 127
-    // = chunk n0 / 128, 8 waves x 32 rows (two 16-row groups each)
-    if (p.proj_out) {
-      __syncthreads();
-      const int m = lane & 15, q = lane >> 4;
-      auto store = [&](auto NT_) {
-        constexpr int NT = decltype(NT_)::value;
-        constexpr int RG = F32A ? 2 : 1;
+  };
+  // FIXUP: the output-layer projection's weights (proj16's b operands of this N tile's chunk), preloaded into registers
+  // while the slices wait, so a band's projection does not chain on their loads (proj16_pre)
+  f32x4 pw[PROJ_CHUNK / 16][4];
+  // the epilogue of tile rows [r_lo, r_hi) (the whole tile except in the fix-up's bands; rowtab is -1 outside)
+  auto epilogue = [&](int r_lo, int r_hi) {
+    if constexpr (FIXUP) {
+      for (int id = tid; id < (r_hi - r_lo) * (BN / 8); id += 512) octet(r_lo + id / (BN / 8), id % (BN / 8));
+    } else {
+#pragma unroll 2
+      for (int it = 0; it < BM * BN / 8 / 512; ++it) {
+        const int id = tid + 512 * it;
+        octet(id / (BN / 8), id % (BN / 8));
+      }
+    }
+    if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A)) {
+      // fused output-layer projection (GemmArgs::proj_out), proj16 as proj_rows_kernel, P indexed by the output pixel,
+      // one chain per 128-channel chunk into partial buffer chunk (proj_rows_kernel's chunking).  WIDE: the tile holds
+      // every channel (n0 == 0, N <= 256), 8 waves x 16 rows, all chunks.  F32A: the tile holds channels n0 .. n0 + 127
+      // = chunk n0 / 128, 8 waves x 32 rows (two 16-row groups each)
+      if (p.proj_out) {
+        __syncthreads();
+        const int m = lane & 15, q = lane >> 4;
+        auto store = [&](auto NT_) {
+          constexpr int NT = decltype(NT_)::value;
+          constexpr int RG = F32A ? 2 : 1;
 #pragma unroll
-        for (int g = 0; g < RG; ++g) {
-          const int r0 = F32A ? wave * 32 + g * 16 : wave * 16;
-          for (int c0 = 0; c0 < (F32A ? BN : p.N); c0 += PROJ_CHUNK) {
-            const int cc = F32A ? n0 : c0;  // global channel of the chunk's first column
-            if (cc >= p.N) break;
-            f32x4 acc[NT];
-            proj16<NT>(tile + c0, TS, r0, min(PROJ_CHUNK, p.N - cc), p.proj_w + cc, p.proj_ldw, acc);
-            float* Pc = p.proj_out + (cc / PROJ_CHUNK) * p.proj_pstride;
+          for (int g = 0; g < RG; ++g) {
+            const int r0 = F32A ? wave * 32 + g * 16 : wave * 16;
+            if (r0 + 16 <= r_lo || r0 >= r_hi) continue;  // FIXUP: a 16-row group outside the band (wave-uniform)
+            for (int c0 = 0; c0 < (F32A ? BN : p.N); c0 += PROJ_CHUNK) {
+              const int cc = F32A ? n0 : c0;  // global channel of the chunk's first column
+              if (cc >= p.N) break;
+              f32x4 acc[NT];
+              if constexpr (FIXUP)
+                proj16_pre<NT>(tile + c0, TS, r0, min(PROJ_CHUNK, p.N - cc), pw, acc);
+              else
+                proj16<NT>(tile + c0, TS, r0, min(PROJ_CHUNK, p.N - cc), p.proj_w + cc, p.proj_ldw, acc);
+              float* Pc = p.proj_out + (cc / PROJ_CHUNK) * p.proj_pstride;
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
+              for (int t = 0; t < NT; ++t)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const long ro = rowtab[r0 + 4 * q + r];
-                if (ro >= 0) Pc[(ro / p.ldc) * (16 * NT) + 16 * t + m] = acc[t][r];
-              }
+                for (int r = 0; r < 4; ++r) {
+                  const long ro = rowtab[r0 + 4 * q + r];
+                  if (ro >= 0) Pc[(ro / p.ldc) * (16 * NT) + 16 * t + m] = acc[t][r];
+                }
+            }
+          }
+        };
+        if (p.proj_np == 32)
+          store(std::integral_constant<int, 2>{});
+        else
+          store(std::integral_constant<int, 4>{});
+      }
+    }
+  };
+  if constexpr (FIXUP) {
+    // ---- split-K in-GEMM ordered fix-up, spread over the tile's slices (MI355X_MICROARCH.md, inter-workgroup visibility,
+    // first row of the sc1 hand-off table).  Every slice stored its slabs sc1 (write-through); each wave drains them,
+    // then behind a barrier lane 0 counts the slice in (one agent-scope CAS on the tile's epoch-tagged counter) and waits,
+    // bounded, until every slice of the tile has arrived (the launch has <= 256 workgroups at one per CU, so they are
+    // co-resident on an otherwise idle chip).  Slice j then claims band j of the tile's 16-row tiles (a CAS on the band's
+    // claim word, exactly once per launch) and sums the band's slabs 0 .. ksplit - 1 in order with sc1 loads into the LDS
+    // tile -- x3_ksplit_reduce_tile_kernel's order and roundings -- and runs the unsplit epilogue on those rows.  The last
+    // slice to arrive never waits: after its own band it claims every band still unclaimed (a slice whose wait ran out
+    // leaves its band), so each band is combined exactly once whatever the residency.  Words are tagged with the launch's
+    // epoch (GemmArgs::kepoch), so the counters need zeroing once per call, not per launch.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long t_drained = __builtin_amdgcn_s_memrealtime();
+    // LDS words past the epilogue's tile and row table, in the one LDS array: [0] own band claimed, [1] last, [2] bands
+    unsigned* sw = reinterpret_cast<unsigned*>(smem + sizeof(smem) - 16);
+    const int ntile = ((p.M + BM - 1) / BM) * ntn;
+    const int tix = zph * ntile + tm * ntn + tn;
+    const int nband = min(nslz, 16);
+    const unsigned ep = p.kepoch;
+    unsigned* cnt = p.kticket + tix;
+    unsigned* claim = p.kticket + X3_KTICKETS + (long)tix * nslz;
+    auto try_claim = [&](int b) -> bool {
+      unsigned w = __hip_atomic_load(claim + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((w >> 16) != ep)
+        if (__hip_atomic_compare_exchange_strong(claim + b, &w, (ep << 16) | 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          return true;
+      return false;
+    };
+    if constexpr (OM == O_PHASE && EPI == EPI_BIAS_ACT) {
+      if (p.proj_out) {  // F32A: this N tile is the chunk n0 / PROJ_CHUNK
+        const int cw = min(PROJ_CHUNK, p.N - n0), nt = p.proj_np / 16, mm = lane & 15, qq = lane >> 4;
+        // buffer loads, zeros past the chunk's columns or rows through an out-of-range offset (no branch per load)
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)p.proj_w, (short)0, p.proj_np * p.proj_ldw * 4, 0x00020000);
+#pragma unroll
+        for (int g = 0; g < PROJ_CHUNK / 16; ++g)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            pw[g][t] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           rw, (16 * g < cw && t < nt) ? (n0 + (16 * t + mm) * p.proj_ldw + 16 * g + 4 * qq) * 4
+                                                       : (int)KM_OOB, 0, 0));
+      }
+    }
+    if (tid == 0) {
+      unsigned w = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), mine;
+      for (;;) {
+        mine = ((w >> 16) == ep ? (w & 0xFFFFu) : 0u) + 1u;
+        if (__hip_atomic_compare_exchange_strong(cnt, &w, (ep << 16) | mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;
+      }
+      const bool last = mine == (unsigned)nslz;
+      bool ok = last;
+      if (!last) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long dt = 0;
+        for (;;) {
+          const unsigned v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          dt = __builtin_amdgcn_s_memrealtime() - t0;
+          if ((v >> 16) == ep && (v & 0xFFFFu) >= (unsigned)nslz) {
+            ok = true;
+            break;
+          }
+          if (dt > (unsigned long long)X3_FIXUP_WAIT) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (p.fixup_probe) {
+          atomicMax(p.fixup_probe + 3, (unsigned)dt);
+          atomicAdd(p.fixup_probe + 4, (unsigned)dt);
+        }
+      }
+      sw[0] = (ok && zsl < nband && try_claim(zsl)) ? 1u : 0u;
+      sw[1] = last ? 1u : 0u;
+      if (p.fixup_probe) {
+        atomicAdd(p.fixup_probe, 1u);
+        if (!ok) atomicAdd(p.fixup_probe + 1, 1u);
+        if (last) atomicAdd(p.fixup_probe + 5, 1u);
+      }
+    }
+    __syncthreads();
+    // damc_clock_probe on a fix-up launch (diagnostics): realtime stamps {K-loop end, slabs drained, wait over, bands
+    // done} instead of the clock pairs
+    unsigned long long* ck = (p.clk && tid == 0)
+                                 ? p.clk + 4 * ((blockIdx.z * gridDim.x + blockIdx.x) % (unsigned)p.clk_n) : nullptr;
+    if (ck) {
+      ck[0] = ck[3];  // K-loop end
+      ck[1] = t_drained;
+      ck[2] = __builtin_amdgcn_s_memrealtime();  // wait over
+    }
+    const bool own_ok = sw[0] != 0, last = sw[1] != 0;
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.kslab + (long)zph * p.ksplit * ntile * (BM * BN)), (short)0, p.ksplit * ntile * (BM * BN) * 4,
+        0x00020000);
+    // band b = 16-row tiles [16 b / nband, 16 (b + 1) / nband): thread (wn = tid >> 8, column tile ci, lane l) owns one
+    // f32x4 of the register slab layout per row tile (rows 4 (l >> 4) .. + 3, column wn 64 + ci 16 + (l & 15)); the
+    // (row tile, slab) pairs go 16 loads at a time, each added into the LDS tile in slab order (0 + slab 0 + slab 1 ..)
+    auto band = [&](int b) {
+      const int rt0 = b * 16 / nband, rt1 = (b + 1) * 16 / nband, np = (rt1 - rt0) * p.ksplit;
+      const int wnb = tid >> 8, ci = (tid >> 6) & 3;
+      __syncthreads();  // the previous band's epilogue is done with the tile
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // the running sum of the current row tile's slabs
+      for (int q0 = 0; q0 < np; q0 += 16) {
+        f32x4 t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int q = q0 + k, rt = rt0 + q / p.ksplit, sl = q - (q / p.ksplit) * p.ksplit;
+          const int off = ((((rt >> 2) * 2 + wnb) * 16 + (rt & 3) * 4 + ci) * 64 + lane) * 16;
+          // no branch around the load (a "load or zero" select made each load wait for the last one): an invalid
+          // pair's offset falls outside the buffer, which returns zeros
+          t[k] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl, (q < np && m0 + rt * 16 < p.M) ? off : (int)KM_OOB,
+                                                           (sl * ntile + tm * ntn + tn) * (BM * BN * 4), 16));
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all 16 loads issued before the first add waits on one
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int q = q0 + k, rt = rt0 + q / p.ksplit, sl = q - (q / p.ksplit) * p.ksplit;
+          // 0 + slab 0 + slab 1 + ..., as the reduce; pairs past the band leave acc alone (a select, no branch)
+          const f32x4 nx = (sl == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc) + t[k];
+          acc = q < np ? nx : acc;
+          if (q < np && sl == p.ksplit - 1) {
+            float* d = tile + (rt * 16 + 4 * (lane >> 4)) * TS + wnb * 64 + ci * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d[r * TS] = acc[r];
           }
         }
-      };
-      if (p.proj_np == 32)
-        store(std::integral_constant<int, 2>{});
-      else
-        store(std::integral_constant<int, 4>{});
+      }
+      if (tid < BM)
+        rowtab[tid] = (tid >= rt0 * 16 && tid < rt1 * 16 && m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px)
+                                                                           : -1L;
+      __syncthreads();
+      epilogue(rt0 * 16, rt1 * 16);
+    };
+    if (own_ok) band(zsl);
+    if (last) {
+      if (wave == 0) {  // the bands nobody claimed, one CAS per band in parallel lanes
+        const bool got = lane < nband && lane != zsl && try_claim(lane);
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(got);
+        if (lane == 0) {
+          sw[2] = (unsigned)m;
+          if (p.fixup_probe && m) atomicAdd(p.fixup_probe + 2, (unsigned)__builtin_popcountll(m));
+        }
+      }
+      __syncthreads();
+      unsigned m = sw[2];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        band(b);
+      }
     }
+    if (ck) ck[3] = __builtin_amdgcn_s_memrealtime();
+    return;
   }
+  if (tid < BM) rowtab[tid] = (m0 + tid < p.M) ? gemm_row_offset<OM>(p, m0 + tid, py, px) : -1L;
+  if (F32A) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wave * 32 + (i >> 1) * 16 + 4 * (lane >> 4) + r) * TS + ((i & 1) * 4 + j) * 16 + (lane & 15)] =
+              acc16[i][j][r];
+  } else if (NARROW) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 32 + j * 16 + (lane & 15)] = acc16[i][j][r];
+  } else if (M16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * TS + wn * 64 + j * 16 + (lane & 15)] = acc16[i][j][r];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          tile[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TS + wn * 64 + j * 32 + (lane & 31)] =
+              acc[i][j][r];
+  }
+  __syncthreads();
+  if (KSPLIT && !FIXUP) {  // row-major slabs (one block per workgroup): the fp32 tile into its slab; the reduce applies the epilogue
+    float* sl = p.kslab + ((long)zph * p.ksplit + zsl) * p.M * p.N;
+#pragma unroll 2
+    for (int it = 0; it < BM * BN / 8 / 512; ++it) {
+      const int id = tid + 512 * it, row = id / (BN / 8), oct = id % (BN / 8);
+      const int m = m0 + row, n = n0 + oct * 8;
+      if (m >= p.M || n >= p.N) continue;
+      float* d = sl + (long)m * p.N + n;
+      *reinterpret_cast<f32x4*>(d) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8);
+      *reinterpret_cast<f32x4*>(d + 4) = *reinterpret_cast<const f32x4*>(tile + row * TS + oct * 8 + 4);
+    }
+    return;
+  }
+  epilogue(0, BM);
 }
 
 // the split-K reduce: one thread per (phase, row, channel octet); the slices in fixed order, then the limb GEMM's
@@ -2786,6 +2989,25 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
       a.k_per_z = a.K / ks * bpw;
       if constexpr ((V & ~X3_F32A) == DAMC_X3_VARIANT && OM != O_WGRAD && (V & 1) && (V & 4) &&
                     !(V & (32 | 2048 | 65536 | 131072 | 262144 | 524288))) {
+        if constexpr ((V & X3_F32A) != 0 && ((EPI == EPI_BIAS_ACT && OM == O_PHASE) || (EPI == EPI_MASK && OM == O_DENSE))) {
+          // round 6, opt-in (DAMC_X3_FIXUP=1, read per call): the in-GEMM ordered fix-up instead of the reduce launch
+          // (bitwise; gemm_x3_kernel X3_FIXUP) where the caller provides zeroed counters.  Measured slower at every
+          // per-rank batch (CIFAR B=16 0.474-0.485 against 0.410 ms per step, SVHN B=64 0.386-0.391 against
+          // 0.216-0.226; profiles/r06/fixup_ab.txt): the slabs' write-through, the wait for the tile's slowest slice
+          // and the bands' reads of 32 MB of slabs put 15-20 us on every launch's tail (profiles/r06/fixup_timeline.txt),
+          // more than the 9-17 us reduce launch they replace
+          const char* ef = getenv("DAMC_X3_FIXUP");
+          const long grid = (long)ntm * ntn * zdim * (ks / bpw);
+          if (a.kslab_reg && a.kticket && a.kepoch_ctr && *a.kepoch_ctr < 65535u && ef && ef[0] == '1' &&
+              grid <= 256 && grid <= X3_KTICKETS && (long)ks * ntm * ntn * BM * BN * 4 < (1L << 31)) {
+            a.kepoch = ++*a.kepoch_ctr;  // this launch's tag on the counters and claims (16 bits; zeroed per call)
+            a.fixup_probe = g_fixup_probe;
+            a.proj_nostore = nostore0;  // the epilogue runs the fused projection itself, as the unsplit kernel does
+            hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | 1048576 | X3_FIXUP>), dim3(ntm * ntn, 1, zdim * ks / bpw),
+                               dim3(512), 0, s, a);
+            return 0;
+          }
+        }
         if (a.kslab_reg)
           hipLaunchKernelGGL((gemm_x3_kernel<EPI, OM, V | 1048576>), dim3(ntm * ntn, 1, zdim * ks / bpw), dim3(512), 0,
                              s, a);
@@ -3437,6 +3659,8 @@ int launch_gemm(const GemmArgs& a, AMode am, Epi epi, OMode om, int zdim, const 
   return DAMC_ERR_UNSUPPORTED;
 }
 
+void set_fixup_probe(unsigned* buf) { g_fixup_probe = buf; }
+
 void set_clock_probe(unsigned long long* buf, int n) {
   g_clk = (buf && n > 0) ? buf : nullptr;
   g_clk_n = g_clk ? n : 0;
@@ -3447,6 +3671,11 @@ void set_clock_probe(unsigned long long* buf, int n) {
 #ifndef DAMC_GEMM_NO_C_API
 extern "C" int damc_clock_probe(unsigned long long* buf, int n_slots) {
   damc::set_clock_probe(buf, n_slots);
+  return 0;
+}
+
+extern "C" int damc_x3_fixup_probe(unsigned* buf) {
+  damc::set_fixup_probe(buf);
   return 0;
 }
 

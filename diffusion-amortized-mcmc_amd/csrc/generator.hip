@@ -1712,9 +1712,17 @@ struct Workspace {
   float* pbuf;            // per-tap projections of the output layer (two-stage forward)
   float* kslab;           // split-K slabs of the limb-engine convolutions at small batch (or nullptr)
   long kslab_floats;
+  unsigned* kticket_mem;  // split-K fix-up counters and claims (2 damc::X3_KTICKETS words, with kslab)
+  unsigned* kticket;      // = kticket_mem once this call has zeroed them (the posterior call), else nullptr
+  unsigned kepoch;        // the call's fix-up launches so far (GemmArgs::kepoch_ctr)
   int nslab;
   size_t bytes;
 };
+
+__global__ void zero_u32_kernel(unsigned* __restrict__ p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
 
 size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
   size_t off = 0;
@@ -1766,9 +1774,13 @@ size_t carve(const damc_generator_t* g, int B, char* base, Workspace* w) {
       ksf = std::max(ksf, damc::x3_ksplit_floats(B * L.hin * L.win, L.cin, 16 * L.cout, 1, up2_negk_bwd(L)));
   }
   float* ks = ksf ? take(ksf) : nullptr;
+  unsigned* tk = ksf ? reinterpret_cast<unsigned*>(take(2 * damc::X3_KTICKETS)) : nullptr;
   if (w) {
     w->kslab = ks;
     w->kslab_floats = ksf;
+    w->kticket_mem = tk;
+    w->kticket = nullptr;
+    w->kepoch = 0;
     w->z3 = z3;
     w->delta = d;
     w->slabs = sl;
@@ -1905,6 +1917,8 @@ int forward_hidden(const damc_generator_t* g, const float* z, int B, Workspace& 
         if (!h_f32(g, i) && !f32a) a.C = nullptr;
         a.kslab = ws.kslab;  // split-K when the batch leaves the grid under-filled
         a.kslab_floats = ws.kslab_floats;
+        a.kticket = ws.kticket;
+        a.kepoch_ctr = &ws.kepoch;
         if (proj && i + 2 == g->n_layers) {  // the output layer's per-tap projections (smallc_fwd_twostage's stage 1)
           const damc_layer_t& F = g->layers[i + 1];
           a.proj_w = F.w_bwd;
@@ -2035,6 +2049,8 @@ int dgrad_layer(const damc_generator_t* g, int B, Workspace& ws, int i, const fl
         a.negk = up2_negk_bwd(L);
         a.kslab = ws.kslab;
         a.kslab_floats = ws.kslab_floats;
+        a.kticket = ws.kticket;
+        a.kepoch_ctr = &ws.kepoch;
         if (hbits(g, i - 1)) {
           a.mask_sgn = ws.hb[i - 1];
           a.mask = nullptr;
@@ -2560,6 +2576,14 @@ extern "C" int damc_posterior_langevin(const damc_generator_t* g, const damc_ebm
   const bool proj = !(sf && sf[0] == '0') && proj_fusable(g, ws);
   const bool z3_use = x3_proj(g->layers[0]) && ws.z3;
   bool z3_ready = false;
+  if (ws.kticket_mem && n_steps > 0) {
+    // the split-K GEMMs' in-GEMM fix-up counters and claims (damc::GemmArgs::kticket): zeroed once per call by a kernel
+    // (a stream-ordered node like any other under graph capture); the call's launches tag them with their epochs
+    hipLaunchKernelGGL(zero_u32_kernel, dim3((2 * damc::X3_KTICKETS + 255) / 256), dim3(256), 0, s, ws.kticket_mem,
+                       2 * damc::X3_KTICKETS);
+    DAMC_LAUNCH_CHECK();
+    ws.kticket = ws.kticket_mem;
+  }
   for (int i = 0; i < n_steps; ++i) {
     float* dg = diag ? diag + 4 * i : nullptr;
     if ((rc = forward_hidden(g, z, B, ws, s, z3_ready, f32a, proj))) return rc;

@@ -262,6 +262,10 @@ int damc_x3_layer_sign_block(const damc_layer_t* L, int input_grad);
  * clock the chip holds in that loop is d(memtime) / d(realtime) x 100 MHz.  buf = NULL switches it off.  Not
  * thread-safe; keep it off in timed work (bench.py runs it on one extra block). */
 int damc_clock_probe(unsigned long long* buf, int n_slots);
+/* diagnostics: while buf (8 uint32, device memory, zeroed by the caller) is set, every split-K launch with the in-GEMM
+ * fix-up (gemm.hip X3_FIXUP) adds to it: [0] workgroups, [1] waits that ran out, [2] bands the last arrivers took over,
+ * [3] the longest wait (s_memrealtime ticks, 100 MHz), [4] the waits' total ticks, [5] last arrivers.  NULL: off */
+int damc_x3_fixup_probe(unsigned* buf);
 /* a Conv2d weight in its PyTorch layout (cout, cin, k, k), cin % 32 == 0 -> the limb engine's B operand of the
  * conv (damc_conv2d_x3_bytes bytes), in one pass */
 int damc_pack_conv2d_x3(const float* w, int cout, int cin, int k, void* w_x3, void* stream);

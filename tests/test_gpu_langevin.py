@@ -335,36 +335,46 @@ def test_g_update_backward_runs_on_the_forward_engine(gpu_device):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B", [4, 16])
-def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, B):
-    """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block (damc_x3_sign_block() k) per slice, reduced
-    in the kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full CIFAR
-    width with DAMC_X3_KSPLIT=0 vs the default (F32A, register slabs); and the opt-in 64 x 128 tile on the
-    limb-gathering path (gemm.hip X3_NARROW, DAMC_X3_NARROW=1 with DAMC_X3_F32A=0, which replaces split-K where it
-    fills the chip) against both."""
+@pytest.mark.parametrize("net,B", [("cifar10", 4), ("cifar10", 16), ("svhn", 64), ("celeba64", 32), ("celebaHQ", 8)])
+def test_split_k_is_bitwise_the_unsplit_kernel(lv, gpu_device, monkeypatch, net, B):
+    """Split-K of the limb-engine convs at small batch (gemm.hip x3_ksplit: one sign block per slice, summed in the
+    kernel's order and rounding) gives the same bits as the unsplit kernel: 3 posterior steps at full width with
+    DAMC_X3_KSPLIT=0 vs the default -- F32A, register slabs, the reduce launch with the fused output-layer projection
+    -- vs the two-kernel projection (DAMC_REDUCE_PROJ=0) and the round-6 in-GEMM ordered fix-up (DAMC_X3_FIXUP=1,
+    opt-in: every slice of a tile combines one band of its rows once all slices have arrived, the last arriver takes
+    any unclaimed band); and, at CIFAR, the opt-in 64 x 128 tile on the limb-gathering path (gemm.hip X3_NARROW,
+    DAMC_X3_NARROW=1 with DAMC_X3_F32A=0) against all of them.  Per-rank batches of the BASELINE configs: CIFAR B=16
+    (8-way headline), SVHN B=64, CelebA-64 B=32, CelebA-HQ B=8."""
     from damc import synth
     from src import diffusion_net as dn
 
-    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=128, nc=3), 0).to(gpu_device).eval()
-    E = synth.load_into(dn._netE(nz=128), 10).to(gpu_device).eval()
-    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, 32, 32))).to(gpu_device)
-    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, 128))).to(gpu_device)
+    ctor, nz, hw, ngf, sigma = {"cifar10": ("_netG_cifar10", 128, 32, 128, 0.1), "svhn": ("_netG_svhn", 100, 32, 64, 0.1),
+                                "celeba64": ("_netG_celeba64", 100, 64, 128, 0.1),
+                                "celebaHQ": ("_netG_celebaHQ", 128, 256, 128, 1.0)}[net]
+    G = synth.load_into(getattr(dn, ctor)(nz=nz, ngf=ngf, nc=3), 0).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=nz), 10).to(gpu_device).eval()
+    x = torch.from_numpy(synth.uniform_f32(1, 0, (B, 3, hw, hw))).to(gpu_device)
+    z0 = torch.from_numpy(synth.normal_f32(2, 0, (B, nz))).to(gpu_device)
     out = {}
-    for mode, split, narrow in (("unsplit", "0", "0"), ("split", "1", "0"), ("split2", "1", "0"), ("narrow", "1", "1")):
-        # split2: the reduce and the output-layer projection as two kernels (DAMC_REDUCE_PROJ=0) instead of the fused
+    modes = [("unsplit", "0", "0", "0", "1"), ("split", "1", "0", "0", "1"), ("fixup", "1", "0", "1", "1"),
+             ("reduce2", "1", "0", "0", "0")]
+    if net == "cifar10":
+        modes.append(("narrow", "1", "1", "1", "1"))
+    for mode, split, narrow, fixup, rproj in modes:
+        # reduce2: the reduce and the output-layer projection as two kernels (DAMC_REDUCE_PROJ=0) instead of the fused
         # x3_ksplit_reduce_proj_kernel
-        monkeypatch.setenv("DAMC_REDUCE_PROJ", "0" if mode == "split2" else "1")
+        monkeypatch.setenv("DAMC_X3_FIXUP", fixup)
+        monkeypatch.setenv("DAMC_REDUCE_PROJ", rproj)
         monkeypatch.setenv("DAMC_X3_KSPLIT", split)
         monkeypatch.setenv("DAMC_X3_NARROW", narrow)
         monkeypatch.setenv("DAMC_X3_F32A", "0" if narrow == "1" else "1")  # the 64 x 128 tile gathers limbs
         z = z0.clone()
-        lv.posterior_langevin(z, x, G, E, 3, 0.1, 0.1, True, seed=77)
+        lv.posterior_langevin(z, x, G, E, 3, sigma, 0.1, True, seed=77)
         torch.cuda.synchronize()
         out[mode] = z.cpu()
-    assert torch.isfinite(out["split"]).all()
-    assert torch.equal(out["unsplit"], out["split"])
-    assert torch.equal(out["unsplit"], out["split2"])
-    assert torch.equal(out["unsplit"], out["narrow"])
+    assert torch.isfinite(out["split"]).all() and not torch.equal(out["split"], z0.cpu())
+    for mode in out:
+        assert torch.equal(out["unsplit"], out[mode]), mode
 
 
 @pytest.mark.parametrize("net,B", [("cifar10", 5), ("cifar10", 128), ("celeba64", 4)])
