@@ -1745,16 +1745,17 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
             const int a = i >> 1, wnp = i & 1;
             acc16[i][j] *= sg;
             if (m0 + wave * 32 + a * 16 < p.M) {
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl, voff,
-                                                     soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, FIXUP ? 16 : 0);
-              // wait states before any VALU may rewrite the store's data VGPRs: the register allocator reuses them
-              // for the next tile's scaled copy at once, and without these nops 3 of every 16 slab tiles held the
-              // next tile's values (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt).  Observed with ROCm 7.2.0's
-              // clang 22 (roc-7.2.0 26014); the cause (a missed VMEM-store-data hazard) is not pinned, so
-              // test_f32a_posterior_is_bitwise (B=16, register slabs) is the required gate for any toolchain change
-              __builtin_amdgcn_sched_barrier(0);
-              asm volatile("s_nop 4");
-              __builtin_amdgcn_sched_barrier(0);
+              // the whole offset in the VGPR, soffset the inline constant 0 (round 6; was SGPR soffset + an `s_nop 4`):
+              // the VMEM-store-data hazard -- a > 64-bit store's data VGPRs rewritten by the next VALU before the store
+              // has read them -- needs a wait state that LLVM's GCNHazardRecognizer (createsVALUHazard) inserts only
+              // for MUBUF stores whose soffset is not an SGPR; with an SGPR soffset it assumed the exemption, the
+              // register allocator reused the data VGPRs for the next tile's scaled copy at once, and 3 of every 16
+              // slab tiles held the next tile's values on gfx950 (gemm_bench eq, profiles/r04/f32a_kreg_hazard.txt).
+              // With soffset = 0 the recognizer pads the hazard itself (profiles/r06/kreg_store_isa.txt);
+              // test_f32a_posterior_is_bitwise (B=16, register slabs) stays the gate
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc16[i][j]), rsl,
+                                                     voff + soff + (wnp * 1024 + (a * 4 + j) * 64) * 16, 0,
+                                                     FIXUP ? 16 : 0);
             }
             acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
