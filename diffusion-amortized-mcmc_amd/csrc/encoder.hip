@@ -352,6 +352,171 @@ __global__ __launch_bounds__(256) void conv3_apply_x3_kernel(const float* __rest
   }
 }
 
+// ---- the first layer on the limb MFMA (round 6; DAMC_ENC_FIRST_MFMA=0 keeps the fmaf-chain passes above): the k3 conv
+// on CIN <= 3 channels has K = 9 CIN <= 32, one K tile of v_mfma_f32_16x16x32_bf16.  A 16-pixel group's im2col rows
+// (k = (ky 3 + kx) CIN + ci, zero past 9 CIN) come from the LDS window, each value split into its three RNE bf16 limbs
+// (the GEMM engine's split3), the weights' limbs ([(ky, kx, ci)][co], damc_pack_conv2d's layout) sit in registers, and
+// every output is the six limb products summed smallest first into fp32 (the limb engine's arithmetic: error at or
+// below the fp32-MFMA engine's), plus the bias.  Pass 1 (STATS) runs a Welford chain per lane
+// and channel over the lane's pixels (4 per group), merged over the lanes of a channel (butterfly) and the 4 waves
+// (fixed order) into part [B][C][S][3] as conv3_stats_kernel does; pass 2 recomputes y with the same code (so the
+// statistics describe exactly the values it normalises), applies lrelu(y scale + shift) and writes the NHWC activation
+// as fp32 for an F32A next conv, or as its limbs.  Wave w takes the strip's 16-pixel groups w, w + 4, ...; W % 16 == 0.
+typedef __bf16 c3b8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void c3_split8(const float (&v)[8], c3b8& h, c3b8& m, c3b8& l) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 b0 = (__bf16)v[e];
+    const float r1 = sub_rn(v[e], (float)b0);
+    const __bf16 b1 = (__bf16)r1;
+    h[e] = b0;
+    m[e] = b1;
+    l[e] = (__bf16)sub_rn(r1, (float)b1);
+  }
+}
+template <int CIN, int NT, bool STATS>
+__global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict__ x, int H, int W, int C, int R,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         float* __restrict__ part, const float* __restrict__ ss,
+                                                         float slope, float* __restrict__ y32,
+                                                         unsigned short* __restrict__ y3) {
+  static_assert(9 * CIN <= 32 && NT * 16 <= 128, "one K tile, at most 128 channels");
+  extern __shared__ __attribute__((aligned(16))) float c3win[];  // the (R+2) x (W+2) x CIN window
+  __shared__ Wf c3red[4][NT * 16];
+  constexpr int OLD = NT * 16 + 4;  // the output staging tile's row stride (floats)
+  __shared__ __attribute__((aligned(16))) float c3out[STATS ? 1 : 4][16][OLD];
+  const int b = blockIdx.x, s = blockIdx.y, S = gridDim.y, r0 = s * R, rows = min(R, H - r0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
+  conv3_stage<CIN>(x, b, H, W, r0, R, c3win);
+  // the weights' limbs: tile t, lane (channel 16 t + n, k-octet kq)
+  c3b8 wb[NT][3];
+  float bl[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * kq + e;
+      v[e] = k < 9 * CIN ? w[(long)k * C + 16 * t + n] : 0.f;
+    }
+    c3_split8(v, wb[t][0], wb[t][1], wb[t][2]);
+    bl[t] = bias ? bias[16 * t + n] : 0.f;
+  }
+  // the lane's im2col offsets within the window for its k-octet: tap (ky, kx) and ci of k = 8 kq + e
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * kq + e, tap = k / CIN, ci = k - tap * CIN;
+    koff[e] = k < 9 * CIN ? ((tap / 3) * (W + 2) + tap % 3) * CIN + ci : -1;
+  }
+  __syncthreads();
+  const int ngrp = rows * W / 16;
+  Wf a[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) a[t] = Wf{0.f, 0.f, 0.f};
+  float nn = 0.f;
+  float scl[NT], shf[NT];
+  if constexpr (!STATS) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      scl[t] = ss[(long)b * 2 * C + 16 * t + n];
+      shf[t] = ss[(long)b * 2 * C + C + 16 * t + n];
+    }
+  }
+  for (int g = wave; g < ngrp; g += 4) {
+    // A: pixel m = 16 g + (lane & 15) of the strip (one row: W % 16 == 0), k-octet kq
+    const int p = 16 * g + n, r = p / W, xx = p - r * W;
+    const int base = (r * (W + 2) + xx) * CIN;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = koff[e] >= 0 ? c3win[base + koff[e]] : 0.f;
+    c3b8 ah, am, al;
+    c3_split8(v, ah, am, al);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wb[t][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wb[t][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[t][2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wb[t][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[t][1], c, 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[t][0], c, 0, 0, 0);
+    }
+    // lane (n, kq) holds y[pixel 16 g + 4 kq + i][channel 16 t + n], i = 0..3
+    if constexpr (STATS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        nn += 1.f;
+        const float inv = 1.f / nn;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float y = acc[t][i] + bl[t];
+          const float d = y - a[t].mean;
+          a[t].mean += d * inv;
+          a[t].m2 += d * (y - a[t].mean);
+          a[t].n = nn;
+        }
+      }
+    } else {
+      // through the wave's LDS tile to whole channel octets per lane: 16-B fp32 stores, or the limbs
+      // (damc::store_x3_octet, the F32A conv's in-register split), so both output forms carry the same values
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float tt = fmaf(acc[t][i] + bl[t], scl[t], shf[t]);
+          c3out[wave][4 * kq + i][16 * t + n] = tt > 0.f ? tt : tt * slope;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int p0 = 16 * g, rr = p0 / W, x0 = p0 - rr * W;
+      const long obase = (((long)b * H + r0 + rr) * W + x0) * C;
+#pragma unroll
+      for (int it = 0; it < 2 * NT * 16 / 64; ++it) {  // 16 pixels x NT * 2 octets
+        const int id = lane + 64 * it, pp = id / (2 * NT), oc = id - pp * (2 * NT);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = c3out[wave][pp][8 * oc + e];
+        const long off = obase + (long)pp * C + 8 * oc;
+        if (y32) {
+          *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          damc::store_x3_octet(v, y3 + 3 * off);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the wave's next group
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  if constexpr (STATS) {
+    // the four lanes of a channel (kq = 0..3), then the waves in order
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const Wf o{__shfl_xor(a[t].n, off), __shfl_xor(a[t].mean, off), __shfl_xor(a[t].m2, off)};
+        a[t] = (lane & off) ? wmerge(o, a[t]) : wmerge(a[t], o);
+      }
+    if (kq == 0)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) c3red[wave][16 * t + n] = a[t];
+    __syncthreads();
+    for (int c = threadIdx.x; c < NT * 16; c += 256) {
+      Wf m = c3red[0][c];
+#pragma unroll
+      for (int v = 1; v < 4; ++v) m = wmerge(m, c3red[v][c]);
+      float* op = part + (((long)b * C + c) * S + s) * 3;
+      op[0] = m.n;
+      op[1] = m.mean;
+      op[2] = m.m2;
+    }
+  }
+}
+
 // wave reduce-scatter of N per-lane values: halving exchanges (N/2 + N/4 + ... shuffles instead of 6 N), then a plain
 // butterfly over the lanes left sharing a channel; every lane returns the wave total of channel ch (fixed order)
 template <int N>
@@ -1411,7 +1576,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     DAMC_C1(1) DAMC_C1(3) DAMC_C1(4)
 #undef DAMC_C1
 #define DAMC_C3(CIN_, PX_, PA_)                                                                                     \
-  if (!one && L.cin == CIN_ && px == PX_) {                                                                         \
+  if (!one && !mf && L.cin == CIN_ && px == PX_) {                                                                  \
     hipLaunchKernelGGL((conv3_stats_kernel<CIN_, PX_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,     \
                        L.bias, inws);                                                                               \
     hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
@@ -1419,6 +1584,24 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     hipLaunchKernelGGL((conv3_apply_x3_kernel<CIN_, PA_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,  \
                        L.bias, ssb, L.slope, a3, y32);                                                              \
   }
+    // round 6: both passes on the limb MFMA (conv3_mfma_kernel; CelebA-HQ B=64 first layer 0.87 -> see DESIGN.md) where
+    // K = 9 CIN fits one K tile, C is 64 or 128, rows are whole 16-pixel groups and the next conv stages fp32;
+    // DAMC_ENC_FIRST_MFMA=0 (read per call) keeps the fmaf-chain passes below
+    const char* fmf = getenv("DAMC_ENC_FIRST_MFMA");
+    const bool mf = !one && !(fmf && fmf[0] == '0') && (L.cin == 1 || L.cin == 3) && (C == 64 || C == 128) &&
+                    W % 16 == 0;
+    const size_t smw = (size_t)(R + 2) * (W + 2) * L.cin * sizeof(float);
+#define DAMC_C3M(CIN_, NT_)                                                                                          \
+  if (mf && L.cin == CIN_ && C == 16 * NT_) {                                                                        \
+    hipLaunchKernelGGL((conv3_mfma_kernel<CIN_, NT_, true>), dim3(B, S), dim3(256), smw, s, x, H, W, C, R, L.w_packed,\
+                       L.bias, inws, nullptr, 0.f, nullptr, nullptr);                                                \
+    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
+                       L.in_beta, L.in_eps, ssb);                                                                   \
+    hipLaunchKernelGGL((conv3_mfma_kernel<CIN_, NT_, false>), dim3(B, S), dim3(256), smw, s, x, H, W, C, R,           \
+                       L.w_packed, L.bias, nullptr, ssb, L.slope, y32, a3);                                          \
+  }
+    DAMC_C3M(1, 4) DAMC_C3M(3, 4) DAMC_C3M(1, 8) DAMC_C3M(3, 8)
+#undef DAMC_C3M
     // runs of 4 pixels per lane in the statistics pass (the apply pass keeps one: its 2- and 4-pixel forms took 256 VGPRs)
     // where the rows allow it (DAMC_ENC_FIRST_PX=1, read per call: one pixel per lane)
     const char* fpx = getenv("DAMC_ENC_FIRST_PX");
