@@ -1411,12 +1411,15 @@ int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int
   a.kslab = kslab;
   a.kslab_floats = (long)kslab_floats;
   a.ksplit_deferred = defer;
+  a.kwalk = damc::x3_conv_walk(L.k, L.cin);  // the weight operand's K order (every packer of it reads the same rule)
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
                            2.0 * a.M * (double)L.cout * a.K, s);
 }
 }  // namespace
 
 extern "C" int damc_x3_sign_block(void) { return damc::X3_NEGK; }
+
+extern "C" int damc_x3_conv_walk(int k, int cin) { return damc::x3_conv_walk(k, cin); }
 
 extern "C" size_t damc_conv2d_x3_bytes(int cout, int cin, int k) {
   if (cout <= 0 || cin <= 0 || k <= 0 || !damc::conv_kmajor_ok(cin) || cout % 8 != 0 || k * k > 32) return 0;
@@ -1638,7 +1641,10 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       const void* wl = L.w_x3 ? L.w_x3 : L.w_src ? static_cast<const void*>(wsrc + sh.wsrc_off[i]) : nullptr;
       if (!wl) {  // the limb copy from the fp32 packing
         const int K = L.k * L.k * L.cin;
-        if ((rc = damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s))) return rc;
+        if ((rc = damc::x3_conv_walk(L.k, L.cin)
+                      ? damc::launch_split_x3_walk(L.w_packed, (long)L.cout * K, K, L.cin, w3, s)
+                      : damc::launch_split_x3_conv(L.w_packed, (long)L.cout * K, K, L.cin, w3, s)))
+          return rc;
         wl = w3;
       }
       if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max,

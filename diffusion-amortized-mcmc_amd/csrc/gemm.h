@@ -124,7 +124,31 @@ struct GemmArgs {
   unsigned* kepoch_ctr = nullptr;
   unsigned kepoch = 0;
   unsigned* fixup_probe = nullptr;  // damc_x3_fixup_probe's counters (diagnostics; null: off)
+  // limb engine, A_CONV (not O_WGRAD): 1 = the K walk of a 4 x 4 conv is channel-slice-major with parity-grouped taps
+  // (x3_walk_tap): K tile kt = 32 channels 32 (kt / 16) .. of tap x3_walk_tap(kt % 16), and the weight operand is
+  // packed in that order (x3_conv_walk); 0 = tap-major
+  int kwalk = 0;
 };
+// opt-in (round 6): the encoder's 4 x 4 convs walk K slice-major with their taps grouped by (ky, kx) parity: a stride-2
+// tap reads one parity class of the input pixels, the four taps of a class read the same pixels shifted, and a
+// 32-channel slice keeps a workgroup's reuse distance within the XCD's L2.  At CelebA-HQ B=64 it cuts FETCH per conv
+// 2.4x (2862 / 2043 / 1142 / 349 MB -> 1183 / 739 / 370 / 168 MB) at the same time (1422 vs 1437 us for the first
+// k4 s2 conv; the convs run at 200-230 TFLOP/s, compute-bound like the generator's), and measured 2-4 % slower on the
+// CIFAR / CelebA-64 encoders (profiles/r06/enc_walk_ab.txt), so tap-major stays the default.  position pos -> tap
+__host__ __device__ inline int x3_walk_tap(int pos) {
+  const int c = pos >> 2, j = pos & 3;
+  return ((c >> 1) + 2 * (j >> 1)) * 4 + (c & 1) + 2 * (j & 1);
+}
+__host__ __device__ inline int x3_walk_pos(int tap) {
+  const int ky = tap >> 2, kx = tap & 3;
+  return (((ky & 1) << 1) | (kx & 1)) * 4 + ((ky >> 1) << 1) + (kx >> 1);
+}
+// whether a k x k conv on cin channels takes the walk (packers and GEMM launches of one call read it alike);
+// DAMC_ENC_WALK=1 (read per call) enables it
+inline int x3_conv_walk(int k, int cin) {
+  const char* e = getenv("DAMC_ENC_WALK");
+  return (k == 4 && cin % 32 == 0 && e && e[0] == '1') ? 1 : 0;
+}
 // words per half of GemmArgs::kticket (counters, claims): a split grid has < 256 unsplit tiles x phases, the fix-up grid
 // <= 256 workgroups
 constexpr int X3_KTICKETS = 1024;
@@ -183,6 +207,8 @@ int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned
 // slice-major with sign-alternating blocks when the default variant walks channel-major (DAMC_X3_VARIANT & 8),
 // else tap-major (launch_split_x3_negblk)
 int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk = X3_NEGK);
+// the same for a 4 x 4 conv's K-major rows (K = 16 Cg, Cg % 32 == 0) in the x3_conv_walk order
+int launch_split_x3_walk(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk = X3_NEGK);
 // generator-layer packing through LDS tiles (fp32 + x3 in one pass; damc_pack_generator_layer); 1 = layout not
 // covered (the caller falls back to the element-wise packing + launch_split_x3_conv)
 int launch_pack_up2_tiled(const float* w, int cin, int cout, float* wf, unsigned short* wf3, float* wb,
@@ -197,6 +223,7 @@ int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short
 // n <= 8 layers, each cin % 128 == 0 or cin == 64, k * k <= 32, w 16-B aligned; returns 1 (nothing launched) otherwise
 struct PackConvList {
   int n;
+  int walk[8];  // layer i's limbs in the x3_conv_walk order (pack_conv_x3_many_prep fills it)
   const float* w[8];
   unsigned short* y[8];
   int cin[8], taps[8], cc[8], blk0[9];
@@ -261,15 +288,18 @@ __device__ __forceinline__ void pack_conv_x3_block(const PackConvList& l, int bl
     }
   }
   __syncthreads();
-  const int oc = CC / 8, cin8 = cin / 8;
-  unsigned short* o = l.y[li] + 24L * ((long)co * taps * cin8 + cc0 / 8);
+  const int oc = CC / 8, cin8 = cin / 8, walk = l.walk[li];
+  unsigned short* o = l.y[li] + 24L * (long)co * taps * cin8;
   for (int q = tid; q < taps * oc; q += nthr) {
-    const int tap = q / oc, c8 = q - tap * oc;
-    const float sg = (((tap * cin + cc0 + c8 * 8) / X3_NEGK) & 1) ? -1.f : 1.f;
+    const int tap = q / oc, c8 = q - tap * oc, c = cc0 + c8 * 8;
+    // the octet's K index in the walk the GEMM runs: tap-major (tap cin + c), or slice-major with the taps in
+    // x3_walk_pos order; the sign block follows it
+    const int kk = walk ? (c >> 5) * taps * 32 + x3_walk_pos(tap) * 32 + (c & 31) : tap * cin + c;
+    const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = sg * pk_t[(c8 * 8 + e) * tp1 + tap];
-    store_x3_octet(v, o + 24L * ((long)tap * cin8 + c8));
+    store_x3_octet(v, o + 24L * (kk >> 3));
   }
 }
 

@@ -1342,9 +1342,20 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
   }
 
   int tap = 0, ci0 = 0, tky = 0, tkx = 0;
-  if (OM != O_WGRAD && kbeg > 0) {  // a split slice starts mid-walk (tap-major: K tile = (tap, 32 channels))
-    tap = kbeg / Cg;
-    ci0 = kbeg - tap * Cg;
+  // GemmArgs::kwalk (a 4 x 4 conv, the default / F32A LDS-DMA paths): K tile kt = channels 32 (kt / 16) .. of tap
+  // x3_walk_tap(kt % 16); wpos = kt % 16
+  const bool walk = OM == O_DENSE && p.kwalk != 0;  // (the encoder's convs; compile-time off for the ConvT phases)
+  int wpos = 0;
+  if (OM != O_WGRAD && kbeg > 0) {  // a split slice starts mid-walk
+    if (walk) {
+      const int kt = kbeg / X3_BK;
+      wpos = kt & 15;
+      ci0 = (kt >> 4) * X3_BK;
+      tap = x3_walk_tap(wpos);
+    } else {  // tap-major: K tile = (tap, 32 channels)
+      tap = kbeg / Cg;
+      ci0 = kbeg - tap * Cg;
+    }
     tky = tap / kw;
     tkx = tap - tky * kw;
   }
@@ -1355,14 +1366,19 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
     for (int j = 0; j < AJ; ++j) aoff[j] = ((amask[j] >> (tap & 31)) & 1u) ? (unsigned)(abase[j] + toff) : KM_OOB;
   };
   set_tap();
-  u32x4 ra[AJ], rb[BJ];
-  auto load_ab = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < AJ; ++j)
-      ra[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)aoff[j], ci0 * 6, 0));
-#pragma unroll
-    for (int j = 0; j < BJ; ++j)
-      rb[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)boff[j], k0 * 6, 0));
+  // the next K tile's (channels, tap): tap-major, or the 4 x 4 conv walk
+  auto next_ktile = [&]() {
+    if (walk) {
+      if (++wpos == 16) {
+        wpos = 0;
+        ci0 += X3_BK;
+      }
+      tap = x3_walk_tap(wpos);
+      tky = tap >> 2;
+      tkx = tap & 3;
+      set_tap();
+      return;
+    }
     ci0 += X3_BK;
     if (ci0 == Cg) {
       ci0 = 0;
@@ -1373,6 +1389,16 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       }
       set_tap();
     }
+  };
+  u32x4 ra[AJ], rb[BJ];
+  auto load_ab = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+      ra[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)aoff[j], ci0 * 6, 0));
+#pragma unroll
+    for (int j = 0; j < BJ; ++j)
+      rb[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)boff[j], k0 * 6, 0));
+    next_ktile();
   };
   auto store_ab = [&](int buf) {
     unsigned char* base = smem + buf * (BM + BN) * X3_ROWB;
@@ -1454,18 +1480,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t)(base + BM * AROWB + 512 * 16 * j), 16,
                                                (V & 4096) ? ((tid * 16 + 8192 * j) & 0xFFFF) : (int)boff[j],
                                                (V & 4096) ? 0 : k0 * 6, 0, 0);
-    if constexpr (OM != O_WGRAD && !CMAJ) {
-      ci0 += X3_BK;
-      if (ci0 == Cg) {
-        ci0 = 0;
-        ++tap;
-        if (++tkx == kw) {
-          tkx = 0;
-          ++tky;
-        }
-        set_tap();
-      }
-    }
+    if constexpr (OM != O_WGRAD && !CMAJ) next_ktile();
   };
 
   // 65536 / 131072 (A/B): the default path's DMA in two parts, B and half of A at the tile start, the other half of A
@@ -1621,16 +1636,7 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t)(dst + 512 * 16 * j), 16, (int)aoff[j], ci0 * ESZ, 0, 0);
-      ci0 += X3_BK;
-      if (ci0 == Cg) {
-        ci0 = 0;
-        ++tap;
-        if (++tkx == kw) {
-          tkx = 0;
-          ++tky;
-        }
-        set_tap();
-      }
+      next_ktile();
     };
     auto dma_b = [&](int k0, int buf) {
       unsigned char* dst = smem + buf * BUFB + BM * X3A_ROWB + wbase;
@@ -2945,7 +2951,8 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     // 32 x 32 wave tile reads 2x the LDS fragments per MFMA and stages 1.5x the bytes per flop
     const char* en = getenv("DAMC_X3_NARROW");
     const long nnm = (a.M + 63) / 64;
-    if (a.kslab && !a.proj_out && en && en[0] == '1' && (long)ntm * ntn * zdim < 256 && nnm * ntn * zdim >= 256) {
+    if (a.kslab && !a.proj_out && !a.kwalk && en && en[0] == '1' && (long)ntm * ntn * zdim < 256 &&
+        nnm * ntn * zdim >= 256) {
       a.ksplit = 1;
       a.kbpw = 1;
       a.kslab_reg = 0;
@@ -3143,6 +3150,38 @@ int launch_split_x3_cmaj(const float* x, long n, int K, int Cg, int sw, unsigned
   return (int)hipGetLastError();
 }
 
+// rows of K = 16 Cg values in tap-major order [tap][c] -> x3 in the 4 x 4 conv walk (x3_conv_walk: [c / 32][x3_walk_pos
+// (tap)][c % 32]), sign blocks counted in the walk order
+__global__ void split_x3_walk_kernel(const float* __restrict__ x, long n8, int K8, int Cg8,
+                                     unsigned short* __restrict__ y, int negk) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // source octet
+  if (i >= n8) return;
+  const long row = i / K8;
+  const int k8 = (int)(i - row * K8);
+  const int tp = k8 / Cg8, c = (k8 - tp * Cg8) * 8;
+  const int kk = (c >> 5) * 16 * 32 + x3_walk_pos(tp) * 32 + (c & 31);
+  const float sg = ((kk / negk) & 1) ? -1.f : 1.f;
+  const f32x4 v0 = reinterpret_cast<const f32x4*>(x)[2 * i];
+  const f32x4 v1 = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
+  const float v[8] = {sg * v0.x, sg * v0.y, sg * v0.z, sg * v0.w, sg * v1.x, sg * v1.y, sg * v1.z, sg * v1.w};
+  bf16x8 h, m, l;
+  split3_octet(v, h, m, l);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * (row * K8 + (kk >> 3));
+  o[0] = h;
+  o[1] = m;
+  o[2] = l;
+}
+
+int launch_split_x3_walk(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk) {
+  if (Cg <= 0 || Cg % 32 != 0 || K != 16 * Cg || n % K != 0 || ((uintptr_t)x | (uintptr_t)y) % 16 != 0)
+    return DAMC_ERR_ARG;
+  const long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(split_x3_walk_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, n8, K / 8, Cg / 8,
+                     y, negk);
+  return (int)hipGetLastError();
+}
+
 int launch_split_x3_conv(const float* x, long n, int K, int Cg, unsigned short* y, hipStream_t s, int negk) {
   if ((DAMC_X3_VARIANT & 8) != 0 && Cg % 32 == 0) return launch_split_x3_cmaj(x, n, K, Cg, 32, y, s, negk);
   return launch_split_x3_negblk(x, n, K, y, s, negk);
@@ -3273,7 +3312,7 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
 // floats of the PyTorch layout, read 4 taps at a time as f32x4 (k * k % 4 == 0); adjacent threads write adjacent
 // 48-B limb octets of each tap (the thread-per-output-octet kernel above reads 4 B at a 64-B stride, every line 16x)
 __global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, int cin, int k,
-                                         unsigned short* __restrict__ y) {
+                                         unsigned short* __restrict__ y, int walk) {
   // one thread per (co, 4-tap group, channel octet), octets fastest: 4x the threads of one per (co, octet) walking
   // all its taps (CIFAR encoder: 4 launches 69 -> ~25 us per Q(x) call), same values and stores
   const int cin8 = cin / 8, taps = k * k, K8 = taps * cin8, tq = taps / 4;
@@ -3283,20 +3322,21 @@ __global__ void pack_conv_x3_taps_kernel(const float* __restrict__ w, int cout, 
   const long r = i / cin8;
   const int t0 = 4 * (int)(r % tq), co = (int)(r / tq);
   const f32x4* src = reinterpret_cast<const f32x4*>(w + ((long)co * cin + c8 * 8) * taps);
-  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3 * ((long)co * K8 + c8);
+  bf16x8* o = reinterpret_cast<bf16x8*>(y) + 3L * co * K8;
   f32x4 q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] = src[(e * taps + t0) / 4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int kk = (t0 + t) * cin + c8 * 8;
+    const int c = c8 * 8;  // the octet's K index in the GEMM's walk (x3_conv_walk), which also sets its sign block
+    const int kk = walk ? (c >> 5) * taps * 32 + x3_walk_pos(t0 + t) * 32 + (c & 31) : (t0 + t) * cin + c;
     const float sg = ((kk / X3_NEGK) & 1) ? -1.f : 1.f;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = sg * q[e][t];
     bf16x8 h, m, l;
     split3_octet(v, h, m, l);
-    bf16x8* d = o + 3L * (t0 + t) * cin8;
+    bf16x8* d = o + 3L * (kk >> 3);
     d[0] = h;
     d[1] = m;
     d[2] = l;
@@ -3324,6 +3364,7 @@ int pack_conv_x3_many_prep(PackConvList& l) {
         !(l.cin[i] % 128 == 0 || l.cin[i] == 64) || l.blk0[i + 1] <= 0)
       return 1;
     l.cc[i] = l.cin[i] % 128 == 0 ? 128 : 64;
+    l.walk[i] = l.taps[i] == 16 ? x3_conv_walk(4, l.cin[i]) : 0;
     sm = std::max(sm, (size_t)l.cc[i] * (l.taps[i] + 1) * sizeof(float));
   }
   for (int i = 0; i < l.n; ++i) {
@@ -3366,9 +3407,10 @@ int launch_pack_conv_x3(const float* w, int cout, int cin, int k, unsigned short
   if ((k * k) % 4 == 0 && (uintptr_t)w % 16 == 0) {
     const long nt = (long)cout * (k * k / 4) * (cin / 8);
     hipLaunchKernelGGL(pack_conv_x3_taps_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, cout, cin, k,
-                       y);
+                       y, x3_conv_walk(k, cin));
     return (int)hipGetLastError();
   }
+  if (x3_conv_walk(k, cin)) return DAMC_ERR_UNSUPPORTED;  // (k = 4: the taps kernel above always takes it)
   const long n = (long)cout * k * k * cin / 8;
   hipLaunchKernelGGL(pack_conv_x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, cout, cin, k, y);
   return (int)hipGetLastError();
@@ -3422,6 +3464,9 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       taps % a.kw != 0 || taps > 32)
     return DAMC_ERR_ARG;
   if ((om == O_PHASE) != (zdim == 4) || (om == O_DENSE && zdim != 1)) return DAMC_ERR_ARG;
+  // the 4 x 4 conv walk (GemmArgs::kwalk): O_DENSE, 16 taps of whole 32-channel slices, the default / F32A tiles only
+  if (a.kwalk && (om != O_DENSE || taps != 16 || a.kw != 4 || a.Cg % 32 != 0 || (DAMC_X3_VARIANT & ~0x105) != 0))
+    return DAMC_ERR_ARG;
   if (((uintptr_t)a.A3 | (uintptr_t)a.A | (uintptr_t)a.B3 | (uintptr_t)a.C | (uintptr_t)a.C3 | (uintptr_t)a.mask) % 16 !=
       0)
     return DAMC_ERR_ARG;
@@ -3481,7 +3526,8 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     // the first layer at per-rank batches: the skinny kernel (bitwise the 128 x 256 layout); DAMC_X3_SKINNY=0 (read
     // per call) keeps the tiled kernel
     const char* esk = getenv("DAMC_X3_SKINNY");
-    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= x3_skinny_max_rows() && c.K <= c.negk && c.Hin == 1 && c.Win == 1 &&
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && !c.kwalk && c.M <= x3_skinny_max_rows() && c.K <= c.negk && c.Hin == 1 &&
+        c.Win == 1 &&
         c.kw == 1 && c.Cg == c.K && c.A3 && !c.a_f32 && !c.proj_out && !(esk && esk[0] == '0')) {
       // fp32 weights split in registers where the caller passes them (2/3 of the limb bytes; bitwise the same
       // operands); DAMC_X3_SKINNY_F32B=0 (read per call) reads the limbs
@@ -3499,7 +3545,7 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       continue;
     }
     const char* ens = getenv("DAMC_X3_NARROW_SPLIT");  // (read per call) 0: the 128 x 256 layout below
-    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32 && !c.proj_out && c.kslab &&
+    if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32 && !c.proj_out && c.kslab && !c.kwalk &&
         c.K % c.negk == 0 && c.K / c.negk >= 8 && c.N % 8 == 0 && (long)(c.K / c.negk) * c.M * c.N <= c.kslab_floats &&
         !(ens && ens[0] == '0')) {
       launch_x3_narrow_split<EPI_BIAS_ACT>(c, s);

@@ -184,6 +184,7 @@ _SIGS = {
     "damc_conv2d_x3_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "damc_clock_probe": (_I, [_P, _I]),
     "damc_x3_fixup_probe": (_I, [_P]),
+    "damc_x3_conv_walk": (_I, [_I, _I]),
     "damc_pack_conv2d_x3": (_I, [_P, _I, _I, _I, _P, _P]),
     "damc_sweep_workspace_bytes": (_SZ, [ctypes.POINTER(Denoiser), _I, _I]),
     "damc_sweep_team_failures": (ctypes.c_long, [_I]),

@@ -253,6 +253,11 @@ size_t damc_conv2d_x3_bytes(int cout, int cin, int k);
 /* k per sign block of the limb engine's weight operands (odd blocks stored negated; = its MFMA accumulation block
  * and its split-K granule) for the encoder's convs (damc_pack_conv2d_x3): the build's DAMC_X3_NEGK, 512 by default */
 int damc_x3_sign_block(void);
+/* 1 when a k x k Conv2d on cin channels has its limb weight operand (damc_pack_conv2d_x3) and its encoder GEMMs in the
+ * 4 x 4 conv walk (k = 4, cin % 32 == 0: K index = (ci / 32) 512 + p 32 + ci % 32 with p the parity-grouped position of
+ * tap (ky, kx): ((ky % 2) 2 + kx % 2) 4 + (ky / 2) 2 + kx / 2; sign blocks counted in that order), 0 when tap-major
+ * [(ky, kx, ci)]; opt-in: DAMC_ENC_WALK=1 (read per call) selects the walk, tap-major otherwise */
+int damc_x3_conv_walk(int k, int cin);
 /* the sign block of a generator UP2 layer's limb weights (damc_pack_generator_layer), forward (input_grad = 0,
  * K = 4 Cin) or input gradient (1, K = 16 Cout): 512 or 1024 by the layer's shape alone (gemm.h x3_conv_negk);
  * 0 for a layer without limb weights */

@@ -174,6 +174,14 @@ def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     torch.cuda.synchronize()
     K = k * k * cin
     v = w.permute(0, 2, 3, 1).reshape(cout, K)
+    if L.damc_x3_conv_walk(k, cin):  # 4 x 4 convs: slice-major, parity-grouped taps (damc_x3_conv_walk, round 6)
+        walk = []
+        for sl in range(cin // 32):
+            for pos in range(16):
+                c, j = pos // 4, pos % 4
+                tap = ((c >> 1) + 2 * (j >> 1)) * 4 + (c & 1) + 2 * (j & 1)
+                walk += [tap * cin + 32 * sl + i for i in range(32)]
+        v = v[:, torch.tensor(walk)]
     nk = int(L.damc_x3_sign_block())  # k per sign block
     sg = torch.where((torch.arange(K) // nk) % 2 == 1, -1.0, 1.0)
     v = v * sg
