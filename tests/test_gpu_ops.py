@@ -154,7 +154,7 @@ def test_z_update_hook_vs_oracle(gpu_device):
 
 @pytest.mark.parametrize("cout,cin,k", [(16, 64, 4), (24, 32, 4), (40, 512, 4), (8, 32, 3), (16, 64, 1), (8, 32, 5),
                                          (8, 128, 4), (16, 256, 3), (8, 64, 5), (8, 512, 3), (8, 96, 4)])
-def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
+def test_pack_conv2d_x3_matches_limb_split(gpu_device, monkeypatch, cout, cin, k):
     """damc_pack_conv2d_x3 (the encoder's per-call weight operand, Encoder_* convs, diffusion_net.py:227-372):
     PyTorch (cout, cin, k, k) -> K-major [co][(ky, kx, ci)] with the odd sign blocks negated, as three RNE bf16
     limbs h = bf16(v), m = bf16(v - h), l = bf16(v - h - m) per 8-value octet; bit-exact against the same split in
@@ -166,6 +166,15 @@ def test_pack_conv2d_x3_matches_limb_split(gpu_device, cout, cin, k):
     L = _lib.lib()
     g = torch.Generator().manual_seed(cout * 7 + cin + k)
     w = torch.randn(cout, cin, k, k, generator=g) * torch.exp(torch.randn(cout, cin, k, k, generator=g) * 3)
+    for walk in ("0", "1"):  # the opt-in 4 x 4 conv walk (DAMC_ENC_WALK=1, round 6) and the default tap-major order
+        monkeypatch.setenv("DAMC_ENC_WALK", walk)
+        _check_pack_conv2d_x3(L, w, gpu_device, cout, cin, k)
+
+
+def _check_pack_conv2d_x3(L, w, gpu_device, cout, cin, k):
+    from damc import _lib
+    from damc._lib import ptr
+
     nb = int(L.damc_conv2d_x3_bytes(cout, cin, k))
     assert nb == cout * k * k * cin * 6
     out = torch.zeros(nb // 2, dtype=torch.int16, device=gpu_device)
