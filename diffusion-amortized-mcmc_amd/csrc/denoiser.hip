@@ -373,8 +373,8 @@ struct TsArgs {
                       // it holds no sentinel; 0: the drained-flag protocol (DAMC_SWEEP_SENT=0, read per call)
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
-  uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin, wait end, reduced,
-                      // published}
+  uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin (sent 2: task start),
+                      // wait end, reduced, published}
   int dbg;            // timing experiments only (DAMC_SWEEP_DBG, wrong results): 1 no drain before the flag,
                       // 2 no payload loads, 4 no MFMA, 8 no epilogue operand loads, 16 no output stores,
                       // 32 no zB / sin / cos (in0), 64 no z loads (in0); tests: 4096 every workgroup reports a
@@ -698,6 +698,8 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
         if (tid == TS_PUB && sent < 2) __hip_atomic_store(myflag, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
+      // tools: with the data-driven hand-off there is no flag wait, so the first stamp marks the task's start instead
+      if (tr && sent == 2) trs[0] = __builtin_amdgcn_s_memrealtime();
       const bool final_ = j == 6;
       const float* wbase = lds + lbase[j];
       // a skip half (produced at stage sb = 7 k + srcB, two or more stages back) always goes first, so every slot sums
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
 
           // ---- wait for stage s - 1 of the team (once per stage)
           if (!waited) {
-            if (tr) trs[0] = __builtin_amdgcn_s_memrealtime();
+            if (tr && sent < 2) trs[0] = __builtin_amdgcn_s_memrealtime();
             if (s > 0 && sent < 2 && !ts_wait(teamflags, T, s, a.err, a.budget, &sflag, a.diag)) return;
             if (tr) trs[1] = __builtin_amdgcn_s_memrealtime();
             known = s;
