@@ -283,7 +283,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
     sk += red[w][er][8 + ec];
   }
   // ConcatSquashLinearSkipCtx.forward: ret = layer(x) * gate + bias; ret + skip(x)
-  const float o = ((l + bl) * gate + hb) + (sk + bs);
+  const float o = __builtin_fmaf(l + bl, gate, hb) + (sk + bs);  // the fma spelled out: every sweep form rounds alike
   if (!a.final_) {
     if (!(a.dbg & 16)) a.out[(long)erow * a.dout + ecol] = o;
     if (a.trace && tid == 0) { a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 1] = __builtin_amdgcn_s_memrealtime(); a.trace[((long)a.li * 512 + blockIdx.x) * 8 + 5] = __builtin_amdgcn_s_memtime(); }
@@ -315,6 +315,9 @@ __device__ __forceinline__ float ld_sc1_f(const float* p) {
 __device__ __forceinline__ void st_sc1_f(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a plain store to a global pointer the compiler cannot prove global (read from memory): as a global_store, since
+// a FLAT store in flight makes every later vmcnt wait of the wave a full drain (the counter may run out of order)
+__device__ __forceinline__ void st_global(float* p, float v) { *(__attribute__((address_space(1))) float*)p = v; }
 
 // ------------------------------------------------------------------------------ team sweep (one launch, default)
 // The whole dependent chain of a sweep as ONE launch of P = 8 T workgroups, one per CU, with every chain weight
@@ -373,6 +376,9 @@ struct TsArgs {
                       // it holds no sentinel; 0: the drained-flag protocol (DAMC_SWEEP_SENT=0, read per call)
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
+  int early;          // data-driven hand-off: a task issues its handed-off loads before its setup (DAMC_SWEEP_EARLY=0:
+                      // after it, the round-5 order; same values)
+  int fast;           // 128 / 100: sweep_fast_kernel<fast, 128> (the shapes compiled in; DAMC_SWEEP_FAST=0: off)
   uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin (sent 2: task start),
                       // wait end, reduced, published}
   int dbg;            // timing experiments only (DAMC_SWEEP_DBG, wrong results): 1 no drain before the flag,
@@ -441,6 +447,7 @@ __device__ __forceinline__ bool ts_wait(const unsigned* fl, int T, unsigned need
 // exactly the TS_SENT pattern could still reach the ring.  Then the consumers' bounded wait expires (20 ms),
 // team_finish_kernel recomputes the sweep bitwise and the process stays on the launch chain: slow, never wrong.
 constexpr unsigned TS_SENT = 0x7FC0DEADu;
+constexpr unsigned TS_OOB = 0xF0000000u;  // a buffer offset past any descriptor of the team kernel: the load reads 0
 // a re-read loop gives up past the budget (setting the error word) or once another workgroup has failed
 __device__ __forceinline__ bool ts_giveup(uint64_t t0, unsigned it, int* err, long budget) {
   if ((it & 15) != 15) return false;
@@ -536,10 +543,12 @@ __device__ __forceinline__ void ts_load(f32x4 (&x)[N], int kps, const __amdgpu_b
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4;
   const int kq = kps >> 2, ng = kq >> 4, kbase = wave * kq;
+  // every lane issues all N loads, out-of-range ones at an offset past the descriptor (they read 0): no branch per load
+  // and a fixed count, so the waits for earlier loads count exactly (TS_OOB)
 #pragma unroll
   for (int c = 0; c < N; ++c) {
     const int k = kbase + 16 * c + 4 * q;
-    x[c] = (c < ng && rok && k < wsrc) ? ld_sc1(rs, (soff + (long)row * wsrc + k) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    x[c] = ld_sc1(rs, (c < ng && rok && k < wsrc) ? (soff + (long)row * wsrc + k) * 4 : (long)TS_OOB);
   }
 }
 template <int N>
@@ -580,13 +589,19 @@ __device__ __forceinline__ void ts_ready(f32x4 (&x)[N], int kps, const __amdgpu_
 // lane (TS_PUB): 384.  The data-driven hand-off (sent 2, the default) has neither, so it runs 4 waves, one per SIMD,
 // which lifts the register cap from 256 to 512 per lane: at 384 threads the kernel spilled 38 VGPRs to scratch (152 B
 // per lane) once the sentinel re-read paths were added, +17 % sweep time (round 4 A/B).
-template <int NT>
+// EARLY (4-wave data-driven form only, the default; the host takes it when every block's halves fit one load chunk):
+// a task issues its handed-off loads first, then its epilogue operands as buffer loads every lane issues, so the
+// flight of the hand-off covers the task's setup and every wait counts its loads exactly.  Same values and MFMA
+// order as the other form (DAMC_SWEEP_EARLY=0).
+template <int NT, bool EARLY>
 __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
+  static_assert(!EARLY || NT == 256, "the early-issue form is the data-driven (4-wave) one");
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   __shared__ int sflag;
   __shared__ uint64_t trs[3];                    // tools only: this stage's stamps
   __shared__ float tabs[8 * TS_TAB_STEPS];       // the step table (n <= TS_TAB_STEPS)
   __shared__ int lbase[7];                       // LDS float offset of block j's first owned tile
+  __shared__ int tinfo[7][2];                    // block j: {column tiles this slot owns, the first one}
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [wlds weights][TM][emb_ld(kpa0)] in0 image
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, q = lane >> 4;
@@ -614,6 +629,8 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
       int tn0;
       const int c = ts_tiles(a.b[j], T, slot, &tn0);
       lbase[j] = off;
+      tinfo[j][0] = c;
+      tinfo[j][1] = tn0;
       off += c * 16 * (a.b[j].kpa + a.b[j].kpb);
     }
   }
@@ -644,8 +661,11 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
   __syncthreads();
 
   const SweepCall* call = a.call;
-  const int with_noise = call->with_noise;
-  const float* noise = call->noise;
+  // the call's values are wave-uniform: in scalar registers, so branches and descriptors built on them stay scalar
+  const int with_noise = __builtin_amdgcn_readfirstlane(call->with_noise);
+  const float* noise = reinterpret_cast<const float*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)call->noise)) |
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)call->noise >> 32)) << 32));
   float* eps_log = call->eps_log;
   const int eps_log_steps = call->eps_log_steps;
   const uint64_t seed = call->seed, chain_base = call->chain_base, step_offset = call->step_offset;
@@ -689,8 +709,9 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
     for (int j = 0; j < 7; ++j) {
       const TsBlock& b = a.b[j];
       const unsigned s = 7u * k + j;
-      int tn0;
-      const int nt = ts_tiles(b, T, slot, &tn0);
+      // the slot's tiles of block j from the prologue's table (two integer divisions per task otherwise)
+      const int nt = __builtin_amdgcn_readfirstlane(tinfo[j][0]);
+      const int tn0 = __builtin_amdgcn_readfirstlane(tinfo[j][1]);
       // tools only: the poll wave keeps its stamps in LDS (a global store in front of its poll would delay it);
       // the publishing lane writes them out after the flag
       const bool tr = a.trace != nullptr && tid == (NT > 256 ? 256 : 0);
@@ -718,11 +739,58 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
         for (int i = 0; i < nt; ++i) {
           const int tn = tn0 + i * T, n0 = tn * TC;
           const float* wl = wbase + (long)i * 16 * (b.kpa + b.kpb);
-          // ---- independent of the previous stage: epilogue operands, the skip half
           const int erow = r0 + er, ecol = n0 + ec;
           const bool eok = tid < TM * TC && erow < B && ecol < b.dout;
-          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f;
-          if (eok && !(a.dbg & 8)) {
+          const int xrow = r0 + m;
+          const bool xok = xrow < B;
+          // ---- data-driven hand-off (sent 2): the task's handed-off loads go out first, skip half before the
+          // previous block's half (loads return in order), so their flight covers the setup below; the values and
+          // the MFMA order are those of the paths after the wait (skip half first)
+          // (no cw term: every wave computes in the 4-wave instantiation, and the branch must stay wave-uniform to the
+          // compiler, or the other path's loads count against this one's waits)
+          const bool early = EARLY && j > 0;
+          f32x4 xs[CH_CHUNK], xa[CH_CHUNK], zv4[EMB_G];
+          if (early) {
+            if (skip_early) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
+            ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
+          }
+          auto load_z = [&]() {
+#pragma unroll
+            for (int g = 0; g < EMB_G; ++g) {
+              const int kk = 16 * g + 4 * q;
+              zv4[g] = ld_sc1(rz, (cw && xok && kk < nz && !(a.dbg & 64)) ? ((long)xrow * nz + kk) * 4 : (long)TS_OOB);
+            }
+          };
+          if (EARLY && j == 0) load_z();
+          // ---- independent of the previous stage: epilogue operands, the skip half
+          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f, xl = 0.f, xp = 0.f;
+          if constexpr (EARLY) {
+            // the same operands as below, as buffer loads that every lane issues (out-of-range offsets read 0): a
+            // fixed load count behind the handed-off loads, so the waits for those count exactly
+            const bool ld = eok && !(a.dbg & 8);
+            const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(a.gh + (long)k * B * a.ldgh), (short)0, B * (int)a.ldgh * 4, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rb =
+                __builtin_amdgcn_make_buffer_rsrc((void*)b.bls, (short)0, b.ntn * 16 * 4, 0x00020000);
+            const bool nu = final_ && !last && with_noise && noise;  // uniform: the descriptor stays scalar
+            const bool nl = ld && nu;
+            const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(nu ? noise + (long)noisy_k * B * nz : b.bls), (short)0, nu ? B * nz * 4 : 0, 0x00020000);
+            const int gofs = ld ? (erow * (int)a.ldgh + b.ghoff + ecol) * 4 : (int)TS_OOB;
+            // xi first: every stage consumes the last of these loads (bs), so none is still in flight at the next task;
+            // the Philox draw goes to its own register (a write to a register with a load in flight waits for it)
+            xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, nl ? (erow * nz + ecol) * 4 : (int)TS_OOB, 0, 0));
+            gate = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, gofs, 0, 0));
+            hb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, ld ? gofs + b.dout * 4 : (int)TS_OOB, 0, 0));
+            bl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ld ? (tn * 16 + ec) * 4 : (int)TS_OOB, 0, 0));
+            bs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ld ? (tn * 16 + 8 + ec) * 4 : (int)TS_OOB, 0, 0));
+            if (ld && final_ && !last && with_noise && !noise) {
+              float n4[4];
+              philox_normal4(seed, chain_base + erow, step_offset + noisy_k, (uint32_t)(ecol >> 2), DAMC_STREAM_SWEEP,
+                             n4);
+              xp = pick4(n4, ecol);
+            }
+          } else if (eok && !(a.dbg & 8)) {
             const float* ghr = a.gh + ((long)k * B + erow) * a.ldgh + b.ghoff;
             gate = ghr[ecol];
             hb = ghr[b.dout + ecol];
@@ -739,17 +807,16 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               }
             }
           }
-          const int xrow = r0 + m;
-          const bool xok = xrow < B;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           // a skip half that is complete already: its loads now (they land during the wait), its MFMAs while the
           // previous block's half is in flight
-          const bool pre = skip_early && b.kpb <= 64 * CH_CHUNK && b.kpa <= 64 * CH_CHUNK;
-          f32x4 xs[CH_CHUNK];
-          if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
-          if (skip_early && !pre && cw)
-            ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
-                           sent, a.err, a.budget);
+          const bool pre = !EARLY && skip_early && b.kpb <= 64 * CH_CHUNK && b.kpa <= 64 * CH_CHUNK;
+          if constexpr (!EARLY) {
+            if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
+            if (skip_early && !pre && cw)
+              ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
+                             sent, a.err, a.budget);
+          }
           const int half = nz >> 1;
 
           // ---- wait for stage s - 1 of the team (once per stage)
@@ -762,24 +829,14 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           }
 
           if (j == 0) {  // in0: [sin 2pi zB, cos 2pi zB, z] of the 16 rows into LDS (as chain_kernel<true>)
-            f32x4 zv4[EMB_G];
-#pragma unroll
-            for (int g = 0; g < EMB_G; ++g) {
-              const int kk = 16 * g + 4 * q;
-              zv4[g] = (cw && xok && kk < nz && !(a.dbg & 64)) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4)
-                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            if constexpr (!EARLY) load_z();
             if (sent && cw && __any(any_sent(zv4))) {  // z of this step not landed yet: re-read (bounded)
               const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
               unsigned it = 0;
               do {
                 __builtin_amdgcn_s_sleep(1);
                 if (ts_giveup(t0, ++it, a.err, a.budget)) break;
-#pragma unroll
-                for (int g = 0; g < EMB_G; ++g) {
-                  const int kk = 16 * g + 4 * q;
-                  zv4[g] = (xok && kk < nz) ? ld_sc1(rz, ((long)xrow * nz + kk) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-                }
+                load_z();
               } while (__any(any_sent(zv4)));
             }
             if (cw && wave * 16 < half && !(a.dbg & 32)) {  // wave w: B^T columns 16 w .. 16 w + 15 (nz <= 128), in registers
@@ -812,8 +869,14 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
             __syncthreads();
             if (cw) ts_half<true>(acc, wl, b.kpa, rr, 0, 0, xrow, xok, embs, ld0, a.dbg);
+          } else if constexpr (EARLY) {
+            if (skip_early) {
+              ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
+              ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
+            }
+            ts_ready<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, a.err, a.budget);
+            ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw && pre) {
-            f32x4 xa[CH_CHUNK];
             ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
             if (sent) ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
             ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
@@ -837,7 +900,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               sk += red[w][er][8 + ec];
             }
             // ConcatSquashLinearSkipCtx.forward: ret = layer(x) * gate + bias; ret + skip(x)
-            const float o = ((l + bl) * gate + hb) + (sk + bs);
+            const float o = __builtin_fmaf(l + bl, gate, hb) + (sk + bs);  // the fma spelled out: every sweep form rounds alike
             if (!final_) {
               if (!(a.dbg & 16)) st_sc1_f(rslot + b.ooff + (long)erow * b.dout + ecol, o);
             } else {  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
@@ -853,14 +916,14 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
                 } while (is_sent(zv));
               }
               const float eps = a.residual ? zv + o : o;
-              if (eps_log && k < eps_log_steps) eps_log[(long)k * B * nz + zi] = eps;
+              if (eps_log && k < eps_log_steps) st_global(eps_log + (long)k * B * nz + zi, eps);
               const float pred = mul_rn(c0, sub_rn(zv, mul_rn(eps, c1)));
               float zn;
               if (last) {
                 zn = pred;
               } else {
                 zn = add_rn(mul_rn(c2, zv), mul_rn(c3, pred));
-                if (with_noise) zn = add_rn(zn, mul_rn(c4, xi));
+                if (with_noise) zn = add_rn(zn, mul_rn(c4, EARLY ? (noise ? xl : xp) : xi));
               }
               st_sc1_f(zk1 + zi, zn);
             }
@@ -880,6 +943,362 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
         tg[3] = __builtin_amdgcn_s_memrealtime();
       }
     }
+  }
+}
+
+// ---- the team sweep with the shapes compiled in (the default at the reference's denoiser, nf = 4: w = 128, and
+// nz = 128 or 100).  sweep_team_kernel reads each block's widths, offsets and source blocks from the kernel
+// arguments per task and keeps ~60 derived masks live across its block loop; at 100 SGPRs it spills them to VGPR
+// lanes, and a task's setup ran ~1 us of v_readlane / v_writelane and scalar loads before its first MFMA
+// (tools/sweep_timeline.py: 1.04-1.32 us from task start to wake, 2.8 us per task with every load and MFMA switched
+// off).  Here the block loop is unrolled over compile-time blocks, so every width, K padding, column offset and
+// source block is a constant, and each task:
+//   * issues its handed-off loads first (the skip half, then the previous block's half; loads return in order), then
+//     its epilogue operands as buffer loads that every lane issues (out-of-range offsets read 0), so their flight
+//     covers the rest of the setup and every wait counts its loads exactly;
+//   * double-buffers the wave-partial LDS tile, so one barrier per task goes (the next task writes the other buffer;
+//     a wave reaches that task's barrier only after its epilogue reads of this one).
+// Arithmetic, fragment order and MFMA order are sweep_team_kernel's (sent 2), so team_finish_kernel's rescue and the
+// tests' bitwise gates hold unchanged.
+constexpr int fs_dout(int j, int nz, int w) { return j == 0 ? w : (j <= 4 ? 2 * w : (j == 5 ? w : nz)); }
+constexpr int fs_srcb(int j) { return j == 4 ? 2 : (j == 5 ? 1 : (j == 6 ? 0 : -1)); }
+constexpr int fs_wa(int j, int nz, int w) { return j == 0 ? 2 * nz : fs_dout(j - 1, nz, w); }
+constexpr int fs_wb(int j, int nz, int w) { return fs_srcb(j) >= 0 ? fs_dout(fs_srcb(j), nz, w) : 0; }
+constexpr int fs_pad64(int x) { return (x + 63) / 64 * 64; }
+constexpr int fs_coloff(int j, int nz, int w) { return j == 0 ? 0 : fs_coloff(j - 1, nz, w) + fs_dout(j - 1, nz, w); }
+constexpr int fs_sumdout(int nz, int w) { return fs_coloff(7, nz, w); }
+
+// per-thread and per-step state of the fast team kernel (force-inlined: it lives in registers)
+struct FsCtx {
+  const TsArgs* a;
+  float (*red)[4][TM][16];  // [2] wave partials, double-buffered
+  uint64_t* trs;
+  float* lds;
+  const int* lbase;
+  const int (*tinfo)[2];
+  float* embs;
+  int tid, lane, wave, m, q, er, ec, team, slot, T, B, nrt;
+  int par;  // which red buffer the next task writes
+  // step
+  int k, noisy_k;
+  bool last;
+  float c0, c1, c2, c3, c4;
+  float* rslot;
+  const float* zk;
+  float* zk1;
+  __amdgpu_buffer_rsrc_t rr, rz;
+  // call
+  const float* noise;
+  float* eps_log;
+  int with_noise, eps_log_steps;
+  uint64_t seed, chain_base, step_offset;
+};
+
+template <int J, int NZ, int W>
+__device__ __forceinline__ void fs_block(FsCtx& c, const f32x4 (&bv)[EMB_G]) {
+  constexpr int DOUT = fs_dout(J, NZ, W), WA = fs_wa(J, NZ, W), WB = fs_wb(J, NZ, W);
+  constexpr int KPA = fs_pad64(WA), KPB = fs_pad64(WB), SB = fs_srcb(J);
+  constexpr int NTN = (DOUT + TC - 1) / TC, COL = fs_coloff(J, NZ, W), LDGH = 2 * fs_sumdout(NZ, W);
+  constexpr bool FINAL = J == 6;
+  static_assert(KPA <= 64 * CH_CHUNK && KPB <= 64 * CH_CHUNK, "one load chunk per half");
+  const TsArgs& a = *c.a;
+  const int B = c.B, tid = c.tid, wave = c.wave, m = c.m, q = c.q, er = c.er, ec = c.ec;
+  const int nt = __builtin_amdgcn_readfirstlane(c.tinfo[J][0]);
+  const int tn0 = __builtin_amdgcn_readfirstlane(c.tinfo[J][1]);
+  if (nt == 0) return;
+  const bool tr = a.trace != nullptr && tid == 0;
+  if (tr) c.trs[0] = __builtin_amdgcn_s_memrealtime();
+  const float* wbase = c.lds + c.lbase[J];
+  const int ld0 = emb_ld(fs_pad64(2 * NZ));
+  // this step's gate / hyper-bias rows, the block's biases, the injected noise (uniform descriptors)
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.gh + (long)c.k * B * LDGH), (short)0, B * LDGH * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.b[J].bls, (short)0, NTN * 16 * 4, 0x00020000);
+  const bool nu = FINAL && !c.last && c.with_noise && c.noise;
+  const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(nu ? c.noise + (long)c.noisy_k * B * NZ : a.b[J].bls), (short)0, nu ? B * NZ * 4 : 0, 0x00020000);
+#pragma unroll 1
+  for (int rt = 0; rt < c.nrt; ++rt) {
+    const int r0 = (c.team + 8 * rt) * TM;
+#pragma unroll 1
+    for (int i = 0; i < nt; ++i) {
+      const int tn = tn0 + i * c.T, n0 = tn * TC;
+      const float* wl = wbase + i * 16 * (KPA + KPB);
+      const int erow = r0 + er, ecol = n0 + ec;
+      const bool eok = tid < TM * TC && erow < B && ecol < DOUT;
+      const int xrow = r0 + m;
+      const bool xok = xrow < B;
+      // ---- handed-off loads first
+      f32x4 xs[CH_CHUNK], xa[CH_CHUNK], zv4[EMB_G];
+      auto load_z = [&]() {
+#pragma unroll
+        for (int g = 0; g < EMB_G; ++g) {
+          const int kk = 16 * g + 4 * q;
+          zv4[g] = ld_sc1(c.rz, (xok && kk < NZ) ? ((long)xrow * NZ + kk) * 4 : (long)TS_OOB);
+        }
+      };
+      if constexpr (J == 0) {
+        load_z();
+      } else {
+        if constexpr (SB >= 0) ts_load<CH_CHUNK>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok);
+        ts_load<CH_CHUNK>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok);
+      }
+      // ---- epilogue operands (xi first: the last load, bs, is consumed by every block, so nothing is in flight at
+      // the next task; the Philox draw has its own register)
+      const int gofs = eok ? (erow * LDGH + 2 * COL + ecol) * 4 : (int)TS_OOB;
+      const float xl = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rn, (eok && nu) ? (erow * NZ + ecol) * 4 : (int)TS_OOB, 0, 0));
+      const float gate = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, gofs, 0, 0));
+      const float hb = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rg, eok ? gofs + DOUT * 4 : (int)TS_OOB, 0, 0));
+      const float bl = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rb, eok ? (tn * 16 + ec) * 4 : (int)TS_OOB, 0, 0));
+      const float bs = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rb, eok ? (tn * 16 + 8 + ec) * 4 : (int)TS_OOB, 0, 0));
+      float xp = 0.f;
+      if constexpr (FINAL) {
+        if (eok && !c.last && c.with_noise && !c.noise) {
+          float n4[4];
+          philox_normal4(c.seed, c.chain_base + erow, c.step_offset + c.noisy_k, (uint32_t)(ecol >> 2),
+                         DAMC_STREAM_SWEEP, n4);
+          xp = pick4(n4, ecol);
+        }
+      }
+      if (tr && i == 0 && rt == 0) c.trs[1] = __builtin_amdgcn_s_memrealtime();
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (J == 0) {  // in0: [sin 2pi zB, cos 2pi zB, z] of the 16 rows into LDS (sweep_team_kernel's code)
+        constexpr int HALF = NZ / 2;
+        if (__any(any_sent(zv4))) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          unsigned it = 0;
+          do {
+            __builtin_amdgcn_s_sleep(1);
+            if (ts_giveup(t0, ++it, a.err, a.budget)) break;
+            load_z();
+          } while (__any(any_sent(zv4)));
+        }
+        if (wave * 16 < HALF) {
+          const int col = wave * 16 + m;
+          const bool cok = col < HALF;
+          const f32x4 e4 = emb_zb(zv4, bv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rrow = 4 * q + r;
+            if (cok) {
+              const float t = e4[r] - rintf(e4[r]);
+              const bool ok = r0 + rrow < B;
+              c.embs[rrow * ld0 + col] = ok ? __builtin_amdgcn_sinf(t) : 0.f;
+              c.embs[rrow * ld0 + HALF + col] = ok ? __builtin_amdgcn_cosf(t) : 0.f;
+            }
+          }
+        }
+        if (wave == 0) {
+#pragma unroll
+          for (int g = 0; g < EMB_G; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int kk = 16 * g + 4 * q + e;
+              if (kk < NZ) c.embs[m * ld0 + 2 * HALF + kk] = zv4[g][e];
+            }
+        }
+        for (int cc = 2 * HALF + NZ + tid; cc < KPA; cc += 256)
+#pragma unroll
+          for (int r = 0; r < TM; ++r) c.embs[r * ld0 + cc] = 0.f;
+        __syncthreads();
+        ts_half<true>(acc, wl, KPA, c.rr, 0, 0, xrow, xok, c.embs, ld0, 0);
+      } else {
+        if constexpr (SB >= 0) {
+          ts_ready<CH_CHUNK>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok, a.err, a.budget);
+          ts_mfma<CH_CHUNK>(acc, wl + 16 * KPA, KPB, xs, 0);
+        }
+        ts_ready<CH_CHUNK>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok, a.err, a.budget);
+        ts_mfma<CH_CHUNK>(acc, wl, KPA, xa, 0);
+      }
+      float (*red)[TM][16] = c.red[c.par];
+      c.par ^= 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][4 * q + r][m] = acc[r];
+      __syncthreads();
+      if (tr && i == 0 && rt == 0) c.trs[2] = __builtin_amdgcn_s_memrealtime();
+      if (eok) {
+        float l = 0.f, sk = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // fixed order: deterministic
+          l += red[w][er][ec];
+          sk += red[w][er][8 + ec];
+        }
+        const float o = __builtin_fmaf(l + bl, gate, hb) + (sk + bs);  // the fma spelled out: every sweep form rounds alike
+        if constexpr (!FINAL) {
+          st_sc1_f(c.rslot + (long)B * COL + (long)erow * DOUT + ecol, o);
+        } else {  // reverse step (diffusion_net.py:601-620): eps = z + out; pred = c0 (z - eps c1)
+          const long zi = (long)erow * NZ + ecol;
+          float zv = ld_sc1_f(c.zk + zi);
+          if (is_sent(zv)) {  // this thread's own store of the previous step, not landed yet
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned it = 0;
+            do {
+              __builtin_amdgcn_s_sleep(1);
+              if (ts_giveup(t0, ++it, a.err, a.budget)) break;
+              zv = ld_sc1_f(c.zk + zi);
+            } while (is_sent(zv));
+          }
+          const float eps = a.residual ? zv + o : o;
+          if (c.eps_log && c.k < c.eps_log_steps) st_global(c.eps_log + (long)c.k * B * NZ + zi, eps);
+          const float pred = mul_rn(c.c0, sub_rn(zv, mul_rn(eps, c.c1)));
+          float zn;
+          if (c.last) {
+            zn = pred;
+          } else {
+            zn = add_rn(mul_rn(c.c2, zv), mul_rn(c.c3, pred));
+            if (c.with_noise) zn = add_rn(zn, mul_rn(c.c4, c.noise ? xl : xp));
+          }
+          st_sc1_f(c.zk1 + zi, zn);
+        }
+      }
+    }
+  }
+  if (tr) {
+    const unsigned s = 7u * c.k + J;
+    uint64_t* tg = a.trace + ((long)blockIdx.x * 7 * a.n + s) * 4;
+    tg[0] = c.trs[0];
+    tg[1] = c.trs[1];
+    tg[2] = c.trs[2];
+    tg[3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <int NZ, int W>
+__global__ __launch_bounds__(256) void sweep_fast_kernel(TsArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[2][4][TM][16];
+  __shared__ uint64_t trs[3];                    // tools only: this stage's stamps
+  __shared__ float tabs[7 * TS_TAB_STEPS];       // the step table without its pad column (n <= TS_TAB_STEPS): the
+                                                 // static LDS plus the largest weight set fits the CU's 160 KB
+  __shared__ int lbase[7];
+  __shared__ int tinfo[7][2];
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [wlds weights][TM][emb_ld(kpa0)] in0 image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T, team = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int B = a.B, G = a.G;
+  if (team >= G || slot >= T) return;
+  if (a.dbg & 4096) {  // tests only: report a failed wait at once
+    if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (a.n <= TS_TAB_STEPS)
+    for (int i = tid; i < 7 * a.n; i += 256) tabs[i] = a.tab[8 * (i / 7) + i % 7];
+  // ---- the owned weight tiles into LDS (sweep_team_kernel's layout)
+  if (tid == 0) {
+    int off = 0;
+    for (int j = 0; j < 7; ++j) {
+      int tn0;
+      const int cnt = ts_tiles(a.b[j], T, slot, &tn0);
+      lbase[j] = off;
+      tinfo[j][0] = cnt;
+      tinfo[j][1] = tn0;
+      off += cnt * 16 * (a.b[j].kpa + a.b[j].kpb);
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < 7; ++j) {
+    const TsBlock& b = a.b[j];
+    int tn0;
+    const int cnt = ts_tiles(b, T, slot, &tn0);
+    for (int i = 0; i < cnt; ++i) {
+      const int tn = tn0 + i * T;
+      float* dst = lds + lbase[j] + (long)i * 16 * (b.kpa + b.kpb);
+      for (int h = 0; h < 2; ++h) {
+        const int kps = h ? b.kpb : b.kpa, wsrc = h ? b.wb : b.wa, k0 = h ? b.wa : 0;
+        const int ng = kps >> 6;
+        const int units = 4 * ng * 64;
+        f32x4* d4 = reinterpret_cast<f32x4*>(dst + (h ? 16 * b.kpa : 0));
+        for (int u = tid; u < units; u += 256) {
+          const int l = u & 63, g = (u >> 6) % ng, w = (u >> 6) / ng;
+          const int mm = l & 15, qq = l >> 4;
+          const int kk = w * (kps >> 2) + 16 * g + 4 * qq;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (kk < wsrc) v = *reinterpret_cast<const f32x4*>(b.w + ((long)tn * 16 + mm) * b.kp + k0 + kk);
+          d4[u] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  FsCtx c;
+  c.a = &a;
+  c.red = red;
+  c.trs = trs;
+  c.lds = lds;
+  c.lbase = lbase;
+  c.tinfo = tinfo;
+  c.embs = lds + a.wlds;
+  c.tid = tid;
+  c.lane = lane;
+  c.wave = wave;
+  c.m = lane & 15;
+  c.q = lane >> 4;
+  c.er = tid >> 3;
+  c.ec = tid & 7;
+  c.team = team;
+  c.slot = slot;
+  c.T = T;
+  c.B = B;
+  c.nrt = (G - team + 7) / 8;
+  c.par = 0;
+  const SweepCall* call = a.call;
+  c.with_noise = __builtin_amdgcn_readfirstlane(call->with_noise);
+  c.noise = reinterpret_cast<const float*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)call->noise)) |
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)call->noise >> 32)) << 32));
+  c.eps_log = call->eps_log;
+  c.eps_log_steps = call->eps_log_steps;
+  c.seed = call->seed;
+  c.chain_base = call->chain_base;
+  c.step_offset = call->step_offset;
+  // in0: wave w's B^T column tile (columns 16 w .. 16 w + 15 of zB), in registers for the whole sweep
+  f32x4 bv[EMB_G];
+  {
+    int tn0;
+    const bool own0 = ts_tiles(a.b[0], T, slot, &tn0) > 0;
+    const int col = wave * 16 + c.m;
+#pragma unroll
+    for (int g = 0; g < EMB_G; ++g) {
+      const int kk = 16 * g + 4 * c.q;
+      bv[g] = (own0 && col < NZ / 2 && kk < NZ) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * NZ + kk)
+                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const long ring_bytes = a.ring_step * 4;
+  for (int k = 0; k < a.n; ++k) {
+    float tb[7];
+    if (a.n <= TS_TAB_STEPS) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) tb[i] = tabs[7 * k + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) tb[i] = a.tab[8 * k + i];
+    }
+    c.k = k;
+    c.c0 = tb[0];
+    c.c1 = tb[1];
+    c.c2 = tb[2];
+    c.c3 = tb[3];
+    c.c4 = tb[4];
+    c.last = tb[5] != 0.f;
+    c.noisy_k = (int)tb[6];
+    c.rslot = a.ring + (long)k * a.ring_step;
+    c.zk = a.zring + (long)k * B * NZ;
+    c.zk1 = a.zring + (long)(k + 1) * B * NZ;
+    c.rr = __builtin_amdgcn_make_buffer_rsrc((void*)c.rslot, (short)0, (int)ring_bytes, 0x00020000);
+    c.rz = __builtin_amdgcn_make_buffer_rsrc((void*)c.zk, (short)0, B * NZ * 4, 0x00020000);
+    fs_block<0, NZ, W>(c, bv);
+    fs_block<1, NZ, W>(c, bv);
+    fs_block<2, NZ, W>(c, bv);
+    fs_block<3, NZ, W>(c, bv);
+    fs_block<4, NZ, W>(c, bv);
+    fs_block<5, NZ, W>(c, bv);
+    fs_block<6, NZ, W>(c, bv);
   }
 }
 
@@ -1031,7 +1450,7 @@ __global__ __launch_bounds__(256) void team_finish_kernel(TsArgs a, float* zt, i
               l += red[w][er][ec];
               sk += red[w][er][8 + ec];
             }
-            const float o = ((l + bl) * gate + hb) + (sk + bs);
+            const float o = __builtin_fmaf(l + bl, gate, hb) + (sk + bs);  // the fma spelled out: every sweep form rounds alike
             if (!final_) {
               rslot[b.ooff + (long)erow * b.dout + ecol] = o;
             } else {
@@ -1549,9 +1968,15 @@ int team_slots() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     cached[dev] = (cus % 8 == 0 && cus >= 8) ? std::min(cus / 8, TS_MAXT) : -1;
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<TS_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<TS_THREADS, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)TS_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)TS_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TS_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)sweep_fast_kernel<128, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TS_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)sweep_fast_kernel<100, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)TS_LDS_MAX);
   }
   return std::max(cached[dev], 0);
@@ -1622,10 +2047,17 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
     if (ok_sm[dev] != sm) {
       int per = 0;
       int per2 = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel<TS_THREADS>, TS_THREADS, sm) !=
+      int per3 = 0, per4 = 0, per5 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel<TS_THREADS, false>, TS_THREADS, sm) !=
               hipSuccess || per < 1 ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, sweep_team_kernel<256>, 256, sm) != hipSuccess ||
-          per2 < 1)
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, sweep_team_kernel<256, false>, 256, sm) != hipSuccess ||
+          per2 < 1 ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, sweep_team_kernel<256, true>, 256, sm) != hipSuccess ||
+          per3 < 1 ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, sweep_fast_kernel<128, 128>, 256, sm) != hipSuccess ||
+          per4 < 1 ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per5, sweep_fast_kernel<100, 128>, 256, sm) != hipSuccess ||
+          per5 < 1)
         return DAMC_ERR_UNSUPPORTED;
       ok_sm[dev] = sm;
     }
@@ -1649,6 +2081,28 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
   a->diag = w.diag;
   a->budget = 2000000;  // 20 ms at 100 MHz per wait: a stage takes microseconds
   a->wlds = (int)wl;
+  const char* ee = getenv("DAMC_SWEEP_EARLY");  // (read per call) 0: handed-off loads after the task's setup
+  a->early = !(ee && ee[0] == '0') && (long)B * a->ldgh * 4 < (1L << 31);  // 32-bit buffer offsets into a step's gh
+  for (int j = 1; j < 7; ++j)  // every block's halves in one load chunk
+    if (a->b[j].kpa > 64 * CH_CHUNK || a->b[j].kpb > 64 * CH_CHUNK) a->early = 0;
+  // the shape-specialised kernel: only where every block matches the compiled-in table
+  const char* fe = getenv("DAMC_SWEEP_FAST");  // (read per call) 0: the generic team kernel
+  a->fast = 0;
+  if (!(fe && fe[0] == '0') && (d->nz == 128 || d->nz == 100) && (long)B * a->ldgh * 4 < (1L << 31)) {
+    const int nz = d->nz, w = 128;
+    bool ok = a->ldgh == 2L * fs_sumdout(nz, w);
+    for (int j = 0; j < 7 && ok; ++j) {
+      const TsBlock& p = a->b[j];
+      ok = p.dout == fs_dout(j, nz, w) && p.wa == fs_wa(j, nz, w) && p.wb == fs_wb(j, nz, w) &&
+           p.kpa == fs_pad64(fs_wa(j, nz, w)) && p.kpb == fs_pad64(fs_wb(j, nz, w)) && p.srcB == fs_srcb(j) &&
+           p.ooff == (long)B * fs_coloff(j, nz, w) && p.ghoff == 2 * fs_coloff(j, nz, w);
+    }
+    if (ok) {  // its static LDS differs from the generic kernel's: the launch must fit the CU
+      hipFuncAttributes fa;
+      const void* fn = nz == 128 ? (const void*)sweep_fast_kernel<128, 128> : (const void*)sweep_fast_kernel<100, 128>;
+      if (hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.sharedSizeBytes + sm <= 160 * 1024) a->fast = nz;
+    }
+  }
   static const int dbg = [] {
     const char* e = getenv("DAMC_SWEEP_DBG");
     return e ? atoi(e) : 0;
@@ -1714,10 +2168,16 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
     DAMC_CHECK(hipMalloc(&a.trace, tbytes));
     DAMC_CHECK(hipMemsetAsync(a.trace, 0, tbytes, s));
   }
-  if (a.sent == 2)
-    hipLaunchKernelGGL(sweep_team_kernel<256>, dim3(P), dim3(256), smem, s, a);
+  if (a.sent == 2 && a.fast == 128)
+    hipLaunchKernelGGL((sweep_fast_kernel<128, 128>), dim3(P), dim3(256), smem, s, a);
+  else if (a.sent == 2 && a.fast == 100)
+    hipLaunchKernelGGL((sweep_fast_kernel<100, 128>), dim3(P), dim3(256), smem, s, a);
+  else if (a.sent == 2 && a.early)
+    hipLaunchKernelGGL((sweep_team_kernel<256, true>), dim3(P), dim3(256), smem, s, a);
+  else if (a.sent == 2)
+    hipLaunchKernelGGL((sweep_team_kernel<256, false>), dim3(P), dim3(256), smem, s, a);
   else
-    hipLaunchKernelGGL(sweep_team_kernel<TS_THREADS>, dim3(P), dim3(TS_THREADS), smem, s, a);
+    hipLaunchKernelGGL((sweep_team_kernel<TS_THREADS, false>), dim3(P), dim3(TS_THREADS), smem, s, a);
   DAMC_LAUNCH_CHECK();
   if (trace) {  // tools/sweep_trace.py reads the dump: P, n, G, then the stamps
     std::vector<uint64_t> h((size_t)P * 7 * n * 4);
