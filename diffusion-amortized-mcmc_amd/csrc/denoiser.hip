@@ -376,8 +376,6 @@ struct TsArgs {
                       // it holds no sentinel; 0: the drained-flag protocol (DAMC_SWEEP_SENT=0, read per call)
   long budget;        // wait budget in 100 MHz ticks
   int wlds;           // weight LDS floats per workgroup (host maximum over slots)
-  int early;          // data-driven hand-off: a task issues its handed-off loads before its setup (DAMC_SWEEP_EARLY=0:
-                      // after it, the round-5 order; same values)
   int fast;           // 128 / 100: sweep_fast_kernel<fast, 128> (the shapes compiled in; DAMC_SWEEP_FAST=0: off)
   uint64_t* trace;    // tools only (DAMC_SWEEP_TRACE): [P][7n][4] 100 MHz stamps {wait begin (sent 2: task start),
                       // wait end, reduced, published}
@@ -589,13 +587,8 @@ __device__ __forceinline__ void ts_ready(f32x4 (&x)[N], int kps, const __amdgpu_
 // lane (TS_PUB): 384.  The data-driven hand-off (sent 2, the default) has neither, so it runs 4 waves, one per SIMD,
 // which lifts the register cap from 256 to 512 per lane: at 384 threads the kernel spilled 38 VGPRs to scratch (152 B
 // per lane) once the sentinel re-read paths were added, +17 % sweep time (round 4 A/B).
-// EARLY (4-wave data-driven form only, the default; the host takes it when every block's halves fit one load chunk):
-// a task issues its handed-off loads first, then its epilogue operands as buffer loads every lane issues, so the
-// flight of the hand-off covers the task's setup and every wait counts its loads exactly.  Same values and MFMA
-// order as the other form (DAMC_SWEEP_EARLY=0).
-template <int NT, bool EARLY>
+template <int NT>
 __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
-  static_assert(!EARLY || NT == 256, "the early-issue form is the data-driven (4-wave) one");
   __shared__ __attribute__((aligned(16))) float red[4][TM][16];
   __shared__ int sflag;
   __shared__ uint64_t trs[3];                    // tools only: this stage's stamps
@@ -743,17 +736,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           const bool eok = tid < TM * TC && erow < B && ecol < b.dout;
           const int xrow = r0 + m;
           const bool xok = xrow < B;
-          // ---- data-driven hand-off (sent 2): the task's handed-off loads go out first, skip half before the
-          // previous block's half (loads return in order), so their flight covers the setup below; the values and
-          // the MFMA order are those of the paths after the wait (skip half first)
-          // (no cw term: every wave computes in the 4-wave instantiation, and the branch must stay wave-uniform to the
-          // compiler, or the other path's loads count against this one's waits)
-          const bool early = EARLY && j > 0;
           f32x4 xs[CH_CHUNK], xa[CH_CHUNK], zv4[EMB_G];
-          if (early) {
-            if (skip_early) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
-            ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
-          }
           auto load_z = [&]() {
 #pragma unroll
             for (int g = 0; g < EMB_G; ++g) {
@@ -761,36 +744,9 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               zv4[g] = ld_sc1(rz, (cw && xok && kk < nz && !(a.dbg & 64)) ? ((long)xrow * nz + kk) * 4 : (long)TS_OOB);
             }
           };
-          if (EARLY && j == 0) load_z();
           // ---- independent of the previous stage: epilogue operands, the skip half
-          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f, xl = 0.f, xp = 0.f;
-          if constexpr (EARLY) {
-            // the same operands as below, as buffer loads that every lane issues (out-of-range offsets read 0): a
-            // fixed load count behind the handed-off loads, so the waits for those count exactly
-            const bool ld = eok && !(a.dbg & 8);
-            const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(a.gh + (long)k * B * a.ldgh), (short)0, B * (int)a.ldgh * 4, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rb =
-                __builtin_amdgcn_make_buffer_rsrc((void*)b.bls, (short)0, b.ntn * 16 * 4, 0x00020000);
-            const bool nu = final_ && !last && with_noise && noise;  // uniform: the descriptor stays scalar
-            const bool nl = ld && nu;
-            const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(nu ? noise + (long)noisy_k * B * nz : b.bls), (short)0, nu ? B * nz * 4 : 0, 0x00020000);
-            const int gofs = ld ? (erow * (int)a.ldgh + b.ghoff + ecol) * 4 : (int)TS_OOB;
-            // xi first: every stage consumes the last of these loads (bs), so none is still in flight at the next task;
-            // the Philox draw goes to its own register (a write to a register with a load in flight waits for it)
-            xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, nl ? (erow * nz + ecol) * 4 : (int)TS_OOB, 0, 0));
-            gate = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, gofs, 0, 0));
-            hb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, ld ? gofs + b.dout * 4 : (int)TS_OOB, 0, 0));
-            bl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ld ? (tn * 16 + ec) * 4 : (int)TS_OOB, 0, 0));
-            bs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ld ? (tn * 16 + 8 + ec) * 4 : (int)TS_OOB, 0, 0));
-            if (ld && final_ && !last && with_noise && !noise) {
-              float n4[4];
-              philox_normal4(seed, chain_base + erow, step_offset + noisy_k, (uint32_t)(ecol >> 2), DAMC_STREAM_SWEEP,
-                             n4);
-              xp = pick4(n4, ecol);
-            }
-          } else if (eok && !(a.dbg & 8)) {
+          float gate = 0.f, hb = 0.f, bl = 0.f, bs = 0.f, xi = 0.f;
+          if (eok && !(a.dbg & 8)) {
             const float* ghr = a.gh + ((long)k * B + erow) * a.ldgh + b.ghoff;
             gate = ghr[ecol];
             hb = ghr[b.dout + ecol];
@@ -810,13 +766,11 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           // a skip half that is complete already: its loads now (they land during the wait), its MFMAs while the
           // previous block's half is in flight
-          const bool pre = !EARLY && skip_early && b.kpb <= 64 * CH_CHUNK && b.kpa <= 64 * CH_CHUNK;
-          if constexpr (!EARLY) {
-            if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
-            if (skip_early && !pre && cw)
-              ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
-                             sent, a.err, a.budget);
-          }
+          const bool pre = skip_early && b.kpb <= 64 * CH_CHUNK && b.kpa <= 64 * CH_CHUNK;
+          if (pre && cw) ts_load<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok);
+          if (skip_early && !pre && cw)
+            ts_half<false>(acc, wl + 16 * b.kpa, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, nullptr, 0, a.dbg,
+                           sent, a.err, a.budget);
           const int half = nz >> 1;
 
           // ---- wait for stage s - 1 of the team (once per stage)
@@ -829,7 +783,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
           }
 
           if (j == 0) {  // in0: [sin 2pi zB, cos 2pi zB, z] of the 16 rows into LDS (as chain_kernel<true>)
-            if constexpr (!EARLY) load_z();
+            load_z();
             if (sent && cw && __any(any_sent(zv4))) {  // z of this step not landed yet: re-read (bounded)
               const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
               unsigned it = 0;
@@ -869,13 +823,6 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
               for (int r = 0; r < TM; ++r) embs[r * ld0 + c] = 0.f;
             __syncthreads();
             if (cw) ts_half<true>(acc, wl, b.kpa, rr, 0, 0, xrow, xok, embs, ld0, a.dbg);
-          } else if constexpr (EARLY) {
-            if (skip_early) {
-              ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
-              ts_mfma<CH_CHUNK>(acc, wl + 16 * b.kpa, b.kpb, xs, a.dbg);
-            }
-            ts_ready<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok, a.err, a.budget);
-            ts_mfma<CH_CHUNK>(acc, wl, b.kpa, xa, a.dbg);
           } else if (cw && pre) {
             ts_load<CH_CHUNK>(xa, b.kpa, rr, a.b[b.srcA].ooff, b.wa, xrow, xok);
             if (sent) ts_ready<CH_CHUNK>(xs, b.kpb, rr, a.b[b.srcB].ooff, b.wb, xrow, xok, a.err, a.budget);
@@ -923,7 +870,7 @@ __global__ __launch_bounds__(NT) void sweep_team_kernel(TsArgs a) {
                 zn = pred;
               } else {
                 zn = add_rn(mul_rn(c2, zv), mul_rn(c3, pred));
-                if (with_noise) zn = add_rn(zn, mul_rn(c4, EARLY ? (noise ? xl : xp) : xi));
+                if (with_noise) zn = add_rn(zn, mul_rn(c4, xi));
               }
               st_sc1_f(zk1 + zi, zn);
             }
@@ -1968,11 +1915,9 @@ int team_slots() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     cached[dev] = (cus % 8 == 0 && cus >= 8) ? std::min(cus / 8, TS_MAXT) : -1;
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<TS_THREADS, false>,
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<TS_THREADS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)TS_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)TS_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)sweep_team_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)TS_LDS_MAX);
     (void)hipFuncSetAttribute((const void*)sweep_fast_kernel<128, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)TS_LDS_MAX);
@@ -2047,13 +1992,11 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
     if (ok_sm[dev] != sm) {
       int per = 0;
       int per2 = 0;
-      int per3 = 0, per4 = 0, per5 = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel<TS_THREADS, false>, TS_THREADS, sm) !=
+      int per4 = 0, per5 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sweep_team_kernel<TS_THREADS>, TS_THREADS, sm) !=
               hipSuccess || per < 1 ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, sweep_team_kernel<256, false>, 256, sm) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, sweep_team_kernel<256>, 256, sm) != hipSuccess ||
           per2 < 1 ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, sweep_team_kernel<256, true>, 256, sm) != hipSuccess ||
-          per3 < 1 ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, sweep_fast_kernel<128, 128>, 256, sm) != hipSuccess ||
           per4 < 1 ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&per5, sweep_fast_kernel<100, 128>, 256, sm) != hipSuccess ||
@@ -2081,10 +2024,6 @@ int team_plan(const damc_denoiser_t* d, const SweepWs& w, int B, int n, TsArgs* 
   a->diag = w.diag;
   a->budget = 2000000;  // 20 ms at 100 MHz per wait: a stage takes microseconds
   a->wlds = (int)wl;
-  const char* ee = getenv("DAMC_SWEEP_EARLY");  // (read per call) 0: handed-off loads after the task's setup
-  a->early = !(ee && ee[0] == '0') && (long)B * a->ldgh * 4 < (1L << 31);  // 32-bit buffer offsets into a step's gh
-  for (int j = 1; j < 7; ++j)  // every block's halves in one load chunk
-    if (a->b[j].kpa > 64 * CH_CHUNK || a->b[j].kpb > 64 * CH_CHUNK) a->early = 0;
   // the shape-specialised kernel: only where every block matches the compiled-in table
   const char* fe = getenv("DAMC_SWEEP_FAST");  // (read per call) 0: the generic team kernel
   a->fast = 0;
@@ -2172,12 +2111,10 @@ int run_chain_team(TsArgs& a, int P, size_t smem, const float* coef, hipStream_t
     hipLaunchKernelGGL((sweep_fast_kernel<128, 128>), dim3(P), dim3(256), smem, s, a);
   else if (a.sent == 2 && a.fast == 100)
     hipLaunchKernelGGL((sweep_fast_kernel<100, 128>), dim3(P), dim3(256), smem, s, a);
-  else if (a.sent == 2 && a.early)
-    hipLaunchKernelGGL((sweep_team_kernel<256, true>), dim3(P), dim3(256), smem, s, a);
   else if (a.sent == 2)
-    hipLaunchKernelGGL((sweep_team_kernel<256, false>), dim3(P), dim3(256), smem, s, a);
+    hipLaunchKernelGGL((sweep_team_kernel<256>), dim3(P), dim3(256), smem, s, a);
   else
-    hipLaunchKernelGGL((sweep_team_kernel<TS_THREADS, false>), dim3(P), dim3(TS_THREADS), smem, s, a);
+    hipLaunchKernelGGL((sweep_team_kernel<TS_THREADS>), dim3(P), dim3(TS_THREADS), smem, s, a);
   DAMC_LAUNCH_CHECK();
   if (trace) {  // tools/sweep_trace.py reads the dump: P, n, G, then the stamps
     std::vector<uint64_t> h((size_t)P * 7 * n * 4);
