@@ -135,14 +135,28 @@ __global__ __launch_bounds__(256) void in_apply_kernel(float* y, int B, int HW, 
 
 // (scale, shift) of every (sample, channel) from the S statistics partials, merged once (in_apply_kernel's merge,
 // same order): ss [B][2][C]
-__global__ void in_merge_kernel(const float* __restrict__ part, int B, int C, int S, const float* gamma,
-                                const float* beta, float eps, float* __restrict__ ss) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
+// one wave per (sample, channel): lane s loads strip s (one coalesced 12-B record per lane; S <= 64), and the strips
+// merge as a fixed pairwise tree over lanes (strides 1, 2, 4, ...; an empty lane is an exact identity of wmerge).
+// Round 5's one-thread-per-(sample, channel) left fold issued S dependent merges behind S scattered loads: 22 us per
+// CelebA-HQ B=8 layer for 1024 threads (profiles/r06/enc_hq_b8_dispatches.txt).  The tree depends on S alone, which
+// depends on the map size alone (in_splits), so a batch sharded over ranks merges exactly as the whole batch.
+__global__ __launch_bounds__(256) void in_merge_kernel(const float* __restrict__ part, int B, int C, int S,
+                                                       const float* gamma, const float* beta, float eps,
+                                                       float* __restrict__ ss) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= B * C) return;  // wave-uniform
   const int b = i / C, c = i - b * C;
-  const float* pp = part + (long)i * S * 3;
-  Wf a{pp[0], pp[1], pp[2]};
-  for (int s = 1; s < S; ++s) a = wmerge(a, Wf{pp[3 * s], pp[3 * s + 1], pp[3 * s + 2]});
+  Wf a{0.f, 0.f, 0.f};
+  if (lane < S) {
+    const float* pp = part + ((long)i * S + lane) * 3;
+    a = Wf{pp[0], pp[1], pp[2]};
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const Wf o{__shfl_down(a.n, off), __shfl_down(a.mean, off), __shfl_down(a.m2, off)};
+    if ((lane & (2 * off - 1)) == 0) a = wmerge(a, o);
+  }
+  if (lane != 0) return;
   const float var = a.m2 / a.n;
   const float rstd = 1.f / sqrtf(var + eps);
   const float scale = rstd * gamma[c];
@@ -1353,7 +1367,7 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
                     F0.in_gamma && F0.w_packed && !damc::conv_kmajor_ok(F0.cin) && e->w <= 1024;
   if (sh->first_fused) {
     // strips per sample from the sample's shape alone, never the batch (each strip's lanes merge their statistics once,
-    // a butterfly per channel octet, and in_merge_kernel adds the strips in order: the strip partition sets the
+    // a butterfly per channel octet, and in_merge_kernel merges the strips in a fixed tree: the strip partition sets the
     // rounding, so a batch sharded over ranks must keep the whole batch's partition to reproduce its xemb bit for bit;
     // round 5 took ~1024 / B strips, and 8 x B=8 CelebA-HQ shards differed from B=64 in every row,
     // tests/test_gpu_strong_scaling.py): ~512 pixels per strip, at most 64 strips, at least 128 pixels per strip
@@ -1582,7 +1596,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   if (!one && !mf && L.cin == CIN_ && px == PX_) {                                                                  \
     hipLaunchKernelGGL((conv3_stats_kernel<CIN_, PX_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,     \
                        L.bias, inws);                                                                               \
-    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
+    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 3) / 4), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
                        L.in_beta, L.in_eps, ssb);                                                                   \
     hipLaunchKernelGGL((conv3_apply_x3_kernel<CIN_, PA_>), dim3(B, S), dim3(256), sm, s, x, H, W, C, R, L.w_packed,  \
                        L.bias, ssb, L.slope, a3, y32);                                                              \
@@ -1598,7 +1612,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
   if (mf && L.cin == CIN_ && C == 16 * NT_) {                                                                        \
     hipLaunchKernelGGL((conv3_mfma_kernel<CIN_, NT_, true>), dim3(B, S), dim3(256), smw, s, x, H, W, C, R, L.w_packed,\
                        L.bias, inws, nullptr, 0.f, nullptr, nullptr);                                                \
-    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
+    hipLaunchKernelGGL(in_merge_kernel, dim3((B * C + 3) / 4), dim3(256), 0, s, inws, B, C, S, L.in_gamma,        \
                        L.in_beta, L.in_eps, ssb);                                                                   \
     hipLaunchKernelGGL((conv3_mfma_kernel<CIN_, NT_, false>), dim3(B, S), dim3(256), smw, s, x, H, W, C, R,           \
                        L.w_packed, L.bias, nullptr, ssb, L.slope, y32, a3);                                          \
@@ -1685,7 +1699,7 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       float* ssb = inws + (size_t)B * L.cout * S * 3;
       ProfScope ps("instnorm", 0.0, s);
       hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, out, B, hw, L.cout, S, inws);
-      hipLaunchKernelGGL(in_merge_kernel, dim3((B * L.cout + 255) / 256), dim3(256), 0, s, inws, B, L.cout, S,
+      hipLaunchKernelGGL(in_merge_kernel, dim3((B * L.cout + 3) / 4), dim3(256), 0, s, inws, B, L.cout, S,
                          L.in_gamma, L.in_beta, L.in_eps, ssb);
       const long n8 = (long)B * hw * (L.cout / 8);
       float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
