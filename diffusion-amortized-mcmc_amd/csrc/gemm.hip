@@ -3429,6 +3429,7 @@ int launch_split_x3(const float* x, long n, unsigned short* y, hipStream_t s) {
 // damc_clock_probe: the buffer O_PHASE limb-engine launches stamp (null: off)
 static unsigned long long* g_clk = nullptr;
 static int g_clk_n = 0;
+static unsigned g_clk_launch = 0;  // DAMC_CLOCK_REGIONS=R (tools): every limb-engine launch stamps region launch % R
 
 // an at-most-128-row GEMM whose K holds >= 8 sign blocks (the encoder's last conv: M = B, N = nemb, K = 16 Cin): the
 // 64 x 128 tile split into its sign blocks (row-major slabs, x3_ksplit_reduce_kernel), 4x the workgroups of the
@@ -3494,9 +3495,14 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     const long nb = std::min(per, nimg - b0);
     GemmArgs c = a;
     if (nimg > per) c.ksplit_deferred = nullptr;  // one launch's slabs only
-    if (om == O_PHASE && g_clk) {
-      c.clk = g_clk;
-      c.clk_n = g_clk_n;
+    static const int regions = [] {
+      const char* e = getenv("DAMC_CLOCK_REGIONS");
+      return e ? std::max(1, atoi(e)) : 1;
+    }();
+    if (g_clk && (om == O_PHASE || regions > 1)) {
+      const int per_region = g_clk_n / regions;
+      c.clk = g_clk + 4L * per_region * (g_clk_launch++ % regions);
+      c.clk_n = per_region;
     }
     if (a.A3) c.A3 = a.A3 + b0 * img * 3;
     if (a.a_f32) c.A = a.A + b0 * img;
@@ -3711,6 +3717,7 @@ void set_fixup_probe(unsigned* buf) { g_fixup_probe = buf; }
 void set_clock_probe(unsigned long long* buf, int n) {
   g_clk = (buf && n > 0) ? buf : nullptr;
   g_clk_n = g_clk ? n : 0;
+  g_clk_launch = 0;
 }
 
 }  // namespace damc

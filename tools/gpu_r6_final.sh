@@ -1,0 +1,17 @@
+# round 6 final evidence on HEAD: every GPU test, the default bench line, rocprof stats + PMC traffic + clock of the
+# bench (tools/profile_round.sh), one-step dispatch traces at the per-rank batches, a clean default sweep profile
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r6z}; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 450 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+tail -c 600 $O/bench.json
+bash tools/profile_round.sh $O/prof || exit 1
+for cfg in "_netG_cifar10 128 128 32 16 cifar10_b16" "_netG_svhn 100 64 32 64 svhn_b64"; do
+  set -- $cfg
+  timeout -s KILL 120 rocprofv3 --kernel-trace -d $O/$6 -o run --output-format csv -- python3 tools/cfg_profile.py $1 $2 $3 $4 $5 4 > $O/$6.log 2>&1 || exit 1
+  f=$(find $O/$6 -name '*kernel_trace.csv' | head -1)
+  python3 tools/dispatch_list.py $f "$6: one posterior step (round 6 end, HEAD)" > $O/$6_dispatches.txt || exit 1
+done
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/sweep -o run --output-format csv -- python3 tools/sweep_profile.py 128 > $O/sweep.log 2>&1 || exit 1
+echo done
