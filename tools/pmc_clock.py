@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Effective clock per kernel class under load: GRBM_GUI_ACTIVE (summed over the 8 XCDs by rocprofv3) / 8 /
 the class's average kernel duration from the kernel-trace pass (MI355X_MICROARCH.md 'DVFS give-back').
-The quotient reads high on dispatches shorter than ~0.3 ms; the upconv classes run ~0.55 ms.
+The quotient reads high on dispatches shorter than ~0.3 ms (6.8 GHz on the 9 us split_x3): only classes whose average
+dispatch is at least MIN_MS are printed (the upconv classes, ~0.55 ms).
 
 usage: tools/pmc_clock.py CLOCK_DIR TRACE_DIR
 """
@@ -10,6 +11,8 @@ import sys
 from collections import defaultdict
 
 from pmc_traffic import classify
+
+MIN_MS = 0.3
 
 
 def main():
@@ -30,7 +33,7 @@ def main():
             m[c] += 1
     print("%-18s %12s %12s %10s" % ("class", "GUI_ACTIVE", "avg ms", "clock GHz"))
     for c in sorted(act):
-        if not m.get(c):
+        if not m.get(c) or dur[c] / m[c] * 1e3 < MIN_MS:  # GUI_ACTIVE / duration is not a clock on short dispatches
             continue
         a, d = act[c] / n[c], dur[c] / m[c]
         print("%-18s %12.0f %12.4f %10.3f" % (c, a, d * 1e3, a / 8.0 / d / 1e9))
