@@ -471,6 +471,17 @@ def upconv_fwd_algorithmic_bytes(bsz):
     return tot / len(UPCONV_FWD_LAYERS)
 
 
+def upconv_dgrad_algorithmic_bytes(bsz):
+    """Algorithmic HBM bytes of one upconv_dgrad launch (the input gradient through the same two ConvT layers), averaged
+    over the class's two layers: the fp32 output gradient read once (F32A stages fp32), the weight's limb copy read once,
+    the previous layer's sign bits read once (the epilogue's LReLU' mask), and the fp32 input gradient written once."""
+    tot = 0.0
+    for cin, hin, cout, _ in UPCONV_FWD_LAYERS:
+        npix_in, npix_out = bsz * hin * hin, bsz * 4 * hin * hin
+        tot += 4.0 * npix_out * cout + 6.0 * 16 * cin * cout + npix_in * cin / 8.0 + 4.0 * npix_in * cin
+    return tot / len(UPCONV_FWD_LAYERS)
+
+
 def launch_ranks(n, argv):
     """`bench.py --gpus N` outside a launcher: run N ranks under torch.distributed.run as a CHILD process (this
     process has not touched the GPU, and is never replaced by exec) and return its exit code.  Rank 0 prints the
@@ -690,7 +701,8 @@ def main():
         achieved = flops_per_launch / avg_s / 1e12
         peak = limb_peak
         traffic, fetch_raw = traffic_from_profiles(dom)
-        algo_bytes = upconv_fwd_algorithmic_bytes(plan["post_count"]) if dom == "upconv_fwd" else None
+        algo_bytes = (upconv_fwd_algorithmic_bytes if dom == "upconv_fwd" else upconv_dgrad_algorithmic_bytes)(
+            plan["post_count"])
         gemm_ms = sum(breakdown[k]["total_ms"] for k in breakdown if k.startswith(("upconv", "proj"))) or None
         gemm_fl = sum(breakdown[k]["flops"] for k in breakdown if k.startswith(("upconv", "proj")))
         post_flops_step = 4.0 * B * 1089.2e6  # 4 * B * MAC_G per posterior step
