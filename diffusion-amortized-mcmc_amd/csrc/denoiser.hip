@@ -948,6 +948,8 @@ __device__ __forceinline__ void fs_block(FsCtx& c, const f32x4 (&bv)[EMB_G]) {
   constexpr int NTN = (DOUT + TC - 1) / TC, COL = fs_coloff(J, NZ, W), LDGH = 2 * fs_sumdout(NZ, W);
   constexpr bool FINAL = J == 6;
   static_assert(KPA <= 64 * CH_CHUNK && KPB <= 64 * CH_CHUNK, "one load chunk per half");
+  // the halves' k-groups per wave, compile-time: only live loads are issued (ts_mfma sums c < kps / 64 either way)
+  constexpr int NA = KPA / 64 > 0 ? KPA / 64 : 1, NB = KPB / 64 > 0 ? KPB / 64 : 1;
   const TsArgs& a = *c.a;
   const int B = c.B, tid = c.tid, wave = c.wave, m = c.m, q = c.q, er = c.er, ec = c.ec;
   const int nt = __builtin_amdgcn_readfirstlane(c.tinfo[J][0]);
@@ -977,7 +979,7 @@ __device__ __forceinline__ void fs_block(FsCtx& c, const f32x4 (&bv)[EMB_G]) {
       const int xrow = r0 + m;
       const bool xok = xrow < B;
       // ---- handed-off loads first
-      f32x4 xs[CH_CHUNK], xa[CH_CHUNK], zv4[EMB_G];
+      f32x4 xs[NB], xa[NA], zv4[EMB_G];
       auto load_z = [&]() {
 #pragma unroll
         for (int g = 0; g < EMB_G; ++g) {
@@ -988,8 +990,8 @@ __device__ __forceinline__ void fs_block(FsCtx& c, const f32x4 (&bv)[EMB_G]) {
       if constexpr (J == 0) {
         load_z();
       } else {
-        if constexpr (SB >= 0) ts_load<CH_CHUNK>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok);
-        ts_load<CH_CHUNK>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok);
+        if constexpr (SB >= 0) ts_load<NB>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok);
+        ts_load<NA>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok);
       }
       // ---- epilogue operands (xi first: the last load, bs, is consumed by every block, so nothing is in flight at
       // the next task; the Philox draw has its own register)
@@ -1040,27 +1042,26 @@ __device__ __forceinline__ void fs_block(FsCtx& c, const f32x4 (&bv)[EMB_G]) {
             }
           }
         }
-        if (wave == 0) {
+        // z into the image: wave w writes k-groups 2w, 2w + 1 (every wave holds all of zv4); the pad columns past
+        // 2 HALF + NZ were zeroed once in the prologue
 #pragma unroll
-          for (int g = 0; g < EMB_G; ++g)
+        for (int g = 0; g < EMB_G; ++g) {
+          if ((g >> 1) != wave) continue;  // wave-uniform; static register indices
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int kk = 16 * g + 4 * q + e;
-              if (kk < NZ) c.embs[m * ld0 + 2 * HALF + kk] = zv4[g][e];
-            }
+          for (int e = 0; e < 4; ++e) {
+            const int kk = 16 * g + 4 * q + e;
+            if (kk < NZ) c.embs[m * ld0 + 2 * HALF + kk] = zv4[g][e];
+          }
         }
-        for (int cc = 2 * HALF + NZ + tid; cc < KPA; cc += 256)
-#pragma unroll
-          for (int r = 0; r < TM; ++r) c.embs[r * ld0 + cc] = 0.f;
         __syncthreads();
         ts_half<true>(acc, wl, KPA, c.rr, 0, 0, xrow, xok, c.embs, ld0, 0);
       } else {
         if constexpr (SB >= 0) {
-          ts_ready<CH_CHUNK>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok, a.err, a.budget);
-          ts_mfma<CH_CHUNK>(acc, wl + 16 * KPA, KPB, xs, 0);
+          ts_ready<NB>(xs, KPB, c.rr, (long)B * fs_coloff(SB, NZ, W), WB, xrow, xok, a.err, a.budget);
+          ts_mfma<NB>(acc, wl + 16 * KPA, KPB, xs, 0);
         }
-        ts_ready<CH_CHUNK>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok, a.err, a.budget);
-        ts_mfma<CH_CHUNK>(acc, wl, KPA, xa, 0);
+        ts_ready<NA>(xa, KPA, c.rr, (long)B * fs_coloff(J - 1, NZ, W), WA, xrow, xok, a.err, a.budget);
+        ts_mfma<NA>(acc, wl, KPA, xa, 0);
       }
       float (*red)[TM][16] = c.red[c.par];
       c.par ^= 1;
@@ -1215,6 +1216,11 @@ __global__ __launch_bounds__(256) void sweep_fast_kernel(TsArgs a) {
       bv[g] = (own0 && col < NZ / 2 && kk < NZ) ? *reinterpret_cast<const f32x4*>(a.bmat + (long)col * NZ + kk)
                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  }
+  {  // the in0 image's pad columns (past 2 (NZ / 2) + NZ), zero for the whole sweep
+    const int ld0 = emb_ld(fs_pad64(2 * NZ));
+    for (int cc = 2 * (NZ / 2) + NZ + tid; cc < fs_pad64(2 * NZ); cc += 256)
+      for (int r = 0; r < TM; ++r) c.embs[r * ld0 + cc] = 0.f;
   }
   const long ring_bytes = a.ring_step * 4;
   for (int k = 0; k < a.n; ++k) {
