@@ -1537,6 +1537,39 @@ __global__ void ctx_kernel(const float* __restrict__ px, const float* __restrict
   c[i] = u / (1.f + expf(-u));
 }
 
+// the same, 4 columns per thread (S % 4 == 0), grid.y = step: no 64-bit division per element, and SiLU on the
+// transcendental unit (exp2 and reciprocal, ~1 ulp each) unless exact (DAMC_SWEEP_HYPER_SIGMOID=exact: ctx_kernel's
+// expf and IEEE division); 16 M SiLUs per CIFAR sweep
+__global__ __launch_bounds__(256) void ctx4_kernel(const float* __restrict__ px, const float* __restrict__ qt, int BS,
+                                                   int S, int exact, float* __restrict__ c) {
+  const int r4 = 4 * (blockIdx.x * 256 + threadIdx.x), k = blockIdx.y;
+  if (r4 >= BS) return;
+  const int s = r4 % S;
+  const f32x4 a = *reinterpret_cast<const f32x4*>(px + r4), b = *reinterpret_cast<const f32x4*>(qt + (long)k * S + s);
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float u = a[e] + b[e];
+    o[e] = exact ? u / (1.f + expf(-u)) : u * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-u * 1.4426950408889634f));
+  }
+  *reinterpret_cast<f32x4*>(c + (long)k * BS + r4) = o;
+}
+
+// the ctx launch of a sweep: ctx4_kernel where the rows allow float4 access
+int launch_ctx(const float* px, const float* qt, int n, int B, int S, float* cx, hipStream_t s) {
+  const char* hs = getenv("DAMC_SWEEP_HYPER_SIGMOID");  // (read per call)
+  const int exact = hs && strcmp(hs, "exact") == 0;
+  const long BS = (long)B * S;
+  if (S % 4 == 0 && BS < (1L << 31) && (uintptr_t)px % 16 == 0 && (uintptr_t)qt % 16 == 0 && (uintptr_t)cx % 16 == 0) {
+    hipLaunchKernelGGL(ctx4_kernel, dim3((unsigned)((BS / 4 + 255) / 256), (unsigned)n), dim3(256), 0, s, px, qt,
+                       (int)BS, S, exact, cx);
+  } else {
+    const long tot = (long)n * BS;
+    hipLaunchKernelGGL(ctx_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, px, qt, B, S, tot, cx);
+  }
+  return (int)hipGetLastError();
+}
+
 struct PackBlock {
   const float *wl, *bl, *ws, *bs, *wg, *bg, *wb, *wctx, *bctx;
   int din, dout, kp, coloff;
@@ -2470,9 +2503,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     g.silu_a = 1;
     g.Y = w.px;
     if ((rc = launch_skinny(g, "sweep_pre", s))) return rc;
-    const long tot = (long)n * B * S;
-    hipLaunchKernelGGL(ctx_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, w.px, w.qt, B, S, tot, w.cx);
-    DAMC_LAUNCH_CHECK();
+    if ((rc = launch_ctx(w.px, w.qt, n, B, S, w.cx, s))) return rc;
   } else {
     damc::GemmArgs g;
     g.M = n;
@@ -2523,9 +2554,7 @@ static int reverse_sweep_impl(const damc_denoiser_t* d, const float* xemb, float
     h.ldc = S;
     if ((rc = damc::launch_gemm(h, damc::A_DENSE, damc::EPI_STORE, damc::O_DENSE, 1, "sweep_pre", 2.0 * B * nx * S, s)))
       return rc;
-    const long tot = (long)n * B * S;
-    hipLaunchKernelGGL(ctx_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, w.px, w.qt, B, S, tot, w.cx);
-    DAMC_LAUNCH_CHECK();
+    if ((rc = launch_ctx(w.px, w.qt, n, B, S, w.cx, s))) return rc;
   }
 
   // ---- 3. every block's gate and hyper bias for every (step, row): [sigmoid(c Wg^T + bg) | c Wb^T]

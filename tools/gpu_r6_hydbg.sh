@@ -7,5 +7,5 @@ timeout -k 10 180 python tools/sweep_ab.py 128 DAMC_SWEEP_HYPER_SIGMOID=fast DAM
 grep sweep $O/sig_ab.txt
 for v in fast exact; do
   DAMC_SWEEP_HYPER_SIGMOID=$v timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/p_$v -o run --output-format csv -- python3 tools/sweep_profile.py 128 > $O/p_$v.log 2>&1 || exit 1
-  echo "$v: $(python3 tools/kstats.py $(find $O/p_$v -name '*kernel_stats.csv' | head -1) 3 | grep hyper)"
+  python3 tools/kstats.py $(find $O/p_$v -name '*kernel_stats.csv' | head -1) 12 | grep -E "hyper|ctx" | sed "s/^/$v: /"
 done
