@@ -305,9 +305,11 @@ class _netQ_U(nn.Module):
         return amortizer.q_forward(self, x=x, b=b, device=device, cond_w=cond_w)
 
     def calculate_loss(self, x=None, z=None, mask=None):
-        """Training loss of the denoiser (diffusion_net.py:624-645).  On ROCm tensors the denoiser's forward
-        and backward run on libdamc (Diffusion_UnetA.forward -> damc.training.denoiser_apply); the encoder,
-        prior_emb and the noising stay PyTorch."""
+        """Training loss of the denoiser (diffusion_net.py:624-645).  On ROCm tensors the denoiser's forward and
+        backward run on libdamc (Diffusion_UnetA.forward -> damc.training.denoiser_apply), as do the encoder's
+        (_EncoderBase.forward -> damc.training.encoder_apply) and the noising, time embedding and loss
+        (damc.training.q_noise_glue / q_loss); prior_emb (two Linears, used with x None or a mask) and the random
+        draws stay PyTorch."""
         assert z is not None
         if x is not None:
             xemb = self.encoder(x)
