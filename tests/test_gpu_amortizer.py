@@ -87,6 +87,31 @@ def test_prior_sweep_matches_reference(am, gpu_device, name):
     _check_sweep(name, eps, zt.cpu().numpy(), rec["q_prior_eps3"], rec["q_prior"], ref["prior_eps"], ref["prior"], 1)
 
 
+@pytest.mark.parametrize("name,B", [("q_cifar10_s", 4), ("q_svhn_s", 3), ("q_cifar10_s", 37), ("q_svhn_s", 150)])
+def test_shape_specialised_team_kernel_is_bitwise_the_generic(am, gpu_device, monkeypatch, name, B):
+    """sweep_fast_kernel<NZ, 128> (the default at the reference's nf = 4, nz 128 / 100) against the generic team
+    kernel (DAMC_SWEEP_FAST=0): the same fragments and MFMA order, so zt and the logged eps are bitwise equal, for a
+    ragged last row tile (B=37) and teams with more than one row tile (B=150 on 8 teams), Philox noise and in-kernel
+    eps logging."""
+    from damc import synth
+
+    c = build_q_case(name, gpu_device)
+    Q = c["Q"]
+    nz, nx = Q.nz, Q.nxemb
+    xemb = torch.from_numpy(synth.normal_f32(71, 0, (B, nx))).to(gpu_device)
+    zt0 = torch.from_numpy(synth.normal_f32(72, 0, (B, nz))).to(gpu_device)
+    out = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("DAMC_SWEEP_FAST", fast)
+        zt = zt0.clone()
+        eps = am.reverse_sweep(Q, xemb, zt, seed=17, eps_log_steps=2)
+        torch.cuda.synchronize()
+        out[fast] = (zt.cpu().numpy(), eps.cpu().numpy())
+    assert np.isfinite(out["1"][0]).all()
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+
+
 def test_denoise_step_vs_oracle_at_baseline_width(am, gpu_device):
     """Full-width CIFAR Q (nxemb=1024, ntemb=128) at B=128: first reverse step eps vs the fp32 oracle."""
     from damc import synth
