@@ -334,10 +334,11 @@ size_t damc_sweep_workspace_bytes(const damc_denoiser_t* d, int batch, int n_ste
  * Per call the library packs the weights, then evaluates everything that does not depend on zt for all
  * steps at once: the time MLP (batch-invariant), the ctx Linear's xemb part (step-invariant), and for every
  * (step, row) a block's ctx c = SiLU(Lc(SiLU(cat(temb, xemb)))), its gate sigmoid(c Wg^T + bg) and hyper
- * bias c Wb^T (fp32 MFMA GEMMs over n*B rows).  The dependent chain — per step the 7 blocks'
+ * bias c Wb^T (limb-product MFMA GEMMs over n*B rows).  The dependent chain — per step the 7 blocks'
  * x Wl^T / x Ws^T products plus the reverse-step update — then runs as ONE team launch (weights LDS-resident,
- * flag hand-offs between the workgroups of a team); DAMC_SWEEP_TEAM=0 runs it as 7 launches per step replayed
- * from a HIP graph cached per (workspace, shapes, schedule).
+ * data-driven hand-offs between the workgroups of a team; at the reference's widths, nf = 4 with nz 128 or 100, a
+ * kernel with those shapes compiled in, DAMC_SWEEP_FAST=0 the generic one, bitwise the same); DAMC_SWEEP_TEAM=0
+ * runs it as 7 launches per step replayed from a HIP graph cached per (workspace, shapes, schedule).
  *   eps = p(zt, l_t, xemb); pred = c0 * (zt - eps * c1); zt <- last ? pred : c2*zt + c3*pred (+ c4*xi)
  * temb_in (n_steps, ntemb): SinusoidalPosEmb of the step's logsnr input (host, fp32, as the reference);
  * coef (n_steps, 6), a HOST pointer: {sqrt(1+e^-lt), rsqrt(1+e^lt), r*alpha_st, (1-r)*alpha_s, std,
