@@ -248,11 +248,28 @@ __device__ __forceinline__ void conv3_octet(const float* __restrict__ win, int l
 // the strip's input window: rows r0-1 .. r0+R of sample b, columns -1 .. W, zero outside, [row][col][ci] in LDS
 template <int CIN>
 __device__ __forceinline__ void conv3_stage(const float* __restrict__ x, int b, int H, int W, int r0, int R, float* win) {
+  // element i = (rr CIN + ci) ld + cc: lanes run along one channel row of x (coalesced), 8 unconditional loads (clamped
+  // addresses, zeroed by select) in flight per thread before the LDS writes.  Round 5's loop took one element at a
+  // time and its load -> ds_write chain paid a full HBM latency per element: with 2 workgroups per CU it was the
+  // first layer's cost (40 us of CelebA-HQ B=8's stats pass)
   const int ld = W + 2, n = (R + 2) * ld * CIN;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int ci = i % CIN, rc = i / CIN, rr = rc / ld, cc = rc - rr * ld;
-    const int iy = r0 - 1 + rr, ix = cc - 1;
-    win[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? x[(((long)b * CIN + ci) * H + iy) * W + ix] : 0.f;
+  const float* xb = x + (long)b * CIN * H * W;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 8 * blockDim.x) {
+    float v[8];
+    int dst[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = min(i0 + j * (int)blockDim.x, n - 1);
+      const int q = i / ld, cc = i - q * ld, rr = q / CIN, ci = q - rr * CIN;
+      const int iy = r0 - 1 + rr, ix = cc - 1;
+      const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const float t = xb[((long)ci * H + min(max(iy, 0), H - 1)) * W + min(max(ix, 0), W - 1)];
+      v[j] = ok ? t : 0.f;
+      dst[j] = (rr * ld + cc) * CIN + ci;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j * (int)blockDim.x < n) win[dst[j]] = v[j];
   }
 }
 
@@ -388,6 +405,45 @@ __device__ __forceinline__ void c3_split8(const float (&v)[8], c3b8& h, c3b8& m,
     l[e] = (__bf16)sub_rn(r1, (float)b1);
   }
 }
+// the window as its three RNE bf16 limb planes (c3_split8's split, done once per window value instead of once per
+// im2col use: each value feeds 9 CIN taps)
+template <int CIN>
+__device__ __forceinline__ void conv3_stage_limbs(const float* __restrict__ x, int b, int H, int W, int r0, int R,
+                                                  __bf16* wh, __bf16* wm, __bf16* wl) {
+  // element (q = rr CIN + ci, cc) of the flattened (R + 2) CIN x (W + 2) window; a thread's elements step by blockDim
+  // (q and cc advanced incrementally: no division per element), 8 loads in flight; slots past the end repeat the last
+  // element (the same value to the same address), so the loads and LDS stores run unconditionally
+  const int ld = W + 2, nq = (R + 2) * CIN, n = nq * ld, dq = blockDim.x / ld, dc = blockDim.x - dq * ld;
+  const float* xb = x + (long)b * CIN * H * W;
+  int q = threadIdx.x / ld, cc = threadIdx.x - q * ld;
+  for (int i0 = 0; i0 < n; i0 += 8 * blockDim.x) {
+    float v[8];
+    int dst[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int past = q >= nq;
+      const int qc = past ? nq - 1 : q, ccc = past ? ld - 1 : cc;
+      const int rr = qc / CIN, ci = qc - rr * CIN, iy = r0 - 1 + rr, ix = ccc - 1;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const float t = xb[(unsigned)((ci * H + min(max(iy, 0), H - 1)) * W + min(max(ix, 0), W - 1))];
+      v[j] = ok ? t : 0.f;
+      dst[j] = (rr * ld + ccc) * CIN + ci;
+      cc += dc;
+      const int wr = cc >= ld;
+      cc -= ld & -wr;
+      q += dq + wr;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 b0 = (__bf16)v[j];
+      const float r1 = sub_rn(v[j], (float)b0);
+      const __bf16 b1 = (__bf16)r1;
+      wh[dst[j]] = b0;
+      wm[dst[j]] = b1;
+      wl[dst[j]] = (__bf16)sub_rn(r1, (float)b1);
+    }
+  }
+}
 template <int CIN, int NT, bool STATS>
 __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict__ x, int H, int W, int C, int R,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
@@ -395,13 +451,14 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
                                                          float slope, float* __restrict__ y32,
                                                          unsigned short* __restrict__ y3) {
   static_assert(9 * CIN <= 32 && NT * 16 <= 128, "one K tile, at most 128 channels");
-  extern __shared__ __attribute__((aligned(16))) float c3win[];  // the (R+2) x (W+2) x CIN window
+  extern __shared__ __attribute__((aligned(16))) __bf16 c3win[];  // the (R+2) x (W+2) x CIN window's 3 limb planes
   __shared__ Wf c3red[4][NT * 16];
   constexpr int OLD = NT * 16 + 4;  // the output staging tile's row stride (floats)
   __shared__ __attribute__((aligned(16))) float c3out[STATS ? 1 : 4][16][OLD];
   const int b = blockIdx.x, s = blockIdx.y, S = gridDim.y, r0 = s * R, rows = min(R, H - r0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
-  conv3_stage<CIN>(x, b, H, W, r0, R, c3win);
+  const int pst = (R + 2) * (W + 2) * CIN;  // the limb planes' stride (elements)
+  conv3_stage_limbs<CIN>(x, b, H, W, r0, R, c3win, c3win + pst, c3win + 2 * pst);
   // the weights' limbs: tile t, lane (channel 16 t + n, k-octet kq)
   c3b8 wb[NT][3];
   float bl[NT];
@@ -416,12 +473,13 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
     c3_split8(v, wb[t][0], wb[t][1], wb[t][2]);
     bl[t] = bias ? bias[16 * t + n] : 0.f;
   }
-  // the lane's im2col offsets within the window for its k-octet: tap (ky, kx) and ci of k = 8 kq + e
+  // the lane's im2col offsets within the window for its pixel n and k-octet: tap (ky, kx) and ci of k = 8 kq + e; a
+  // k >= 9 CIN reads the pixel's own first value (any finite value: its weight limbs are zero, so the products are)
   int koff[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = 8 * kq + e, tap = k / CIN, ci = k - tap * CIN;
-    koff[e] = k < 9 * CIN ? ((tap / 3) * (W + 2) + tap % 3) * CIN + ci : -1;
+    koff[e] = n * CIN + (k < 9 * CIN ? ((tap / 3) * (W + 2) + tap % 3) * CIN + ci : 0);
   }
   __syncthreads();
   const int ngrp = rows * W / 16;
@@ -429,23 +487,27 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t < NT; ++t) a[t] = Wf{0.f, 0.f, 0.f};
   float nn = 0.f;
-  float scl[NT], shf[NT];
+  float scl[NT], shf[NT];  // lrelu(acc scl + shf): the bias folded into the shift
   if constexpr (!STATS) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       scl[t] = ss[(long)b * 2 * C + 16 * t + n];
-      shf[t] = ss[(long)b * 2 * C + C + 16 * t + n];
+      shf[t] = fmaf(bl[t], scl[t], ss[(long)b * 2 * C + C + 16 * t + n]);
     }
   }
   for (int g = wave; g < ngrp; g += 4) {
-    // A: pixel m = 16 g + (lane & 15) of the strip (one row: W % 16 == 0), k-octet kq
-    const int p = 16 * g + n, r = p / W, xx = p - r * W;
-    const int base = (r * (W + 2) + xx) * CIN;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = koff[e] >= 0 ? c3win[base + koff[e]] : 0.f;
+    // A: pixel m = 16 g + (lane & 15) of the strip (one row: W % 16 == 0, so the group's row and first column are
+    // wave-uniform), k-octet kq
+    const int p0 = __builtin_amdgcn_readfirstlane(16 * g), r = p0 / W;
+    const int base = (r * (W + 2) + p0 - r * W) * CIN;
     c3b8 ah, am, al;
-    c3_split8(v, ah, am, al);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = base + koff[e];
+      ah[e] = c3win[idx];
+      am[e] = c3win[pst + idx];
+      al[e] = c3win[2 * pst + idx];
+    }
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -459,19 +521,20 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
     }
     // lane (n, kq) holds y[pixel 16 g + 4 kq + i][channel 16 t + n], i = 0..3
     if constexpr (STATS) {
+      // the lane's 4 values of channel 16 t + n as one chunk (its mean and m2 about it) merged into the lane's chain
+      // (Chan's update, one division per group; round 5 ran a Welford step per value).  The chain runs on acc, the
+      // bias joins the mean after the loop (y = acc + bias has acc's m2)
+      const float nb = nn + 4.f, f = 4.f / nb, cw = nn * f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        nn += 1.f;
-        const float inv = 1.f / nn;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float y = acc[t][i] + bl[t];
-          const float d = y - a[t].mean;
-          a[t].mean += d * inv;
-          a[t].m2 += d * (y - a[t].mean);
-          a[t].n = nn;
-        }
+      for (int t = 0; t < NT; ++t) {
+        const float mb = ((acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3])) * 0.25f;
+        const float d0 = acc[t][0] - mb, d1 = acc[t][1] - mb, d2 = acc[t][2] - mb, d3 = acc[t][3] - mb;
+        const float q = fmaf(d3, d3, fmaf(d2, d2, fmaf(d1, d1, d0 * d0)));
+        const float dl = mb - a[t].mean;
+        a[t].mean = fmaf(dl, f, a[t].mean);
+        a[t].m2 = fmaf(dl * dl, cw, a[t].m2 + q);
       }
+      nn = nb;
     } else {
       // through the wave's LDS tile to whole channel octets per lane: 16-B fp32 stores, or the limbs
       // (damc::store_x3_octet, the F32A conv's in-register split), so both output forms carry the same values
@@ -479,21 +542,20 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const float tt = fmaf(acc[t][i] + bl[t], scl[t], shf[t]);
-          c3out[wave][4 * kq + i][16 * t + n] = tt > 0.f ? tt : tt * slope;
+          const float tt = fmaf(acc[t][i], scl[t], shf[t]);
+          c3out[wave][4 * kq + i][16 * t + n] = fmaxf(tt, tt * slope);  // lrelu for 0 <= slope <= 1 (host-checked)
         }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int p0 = 16 * g, rr = p0 / W, x0 = p0 - rr * W;
-      const long obase = (((long)b * H + r0 + rr) * W + x0) * C;
+      const long obase = (((long)b * H + r0 + r) * W + p0 - r * W) * C;  // wave-uniform
 #pragma unroll
       for (int it = 0; it < 2 * NT * 16 / 64; ++it) {  // 16 pixels x NT * 2 octets
         const int id = lane + 64 * it, pp = id / (2 * NT), oc = id - pp * (2 * NT);
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = c3out[wave][pp][8 * oc + e];
-        const long off = obase + (long)pp * C + 8 * oc;
+        const long off = obase + (pp * (16 * NT) + 8 * oc);  // C == 16 NT
         if (y32) {
           *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
           *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
@@ -507,6 +569,11 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
     }
   }
   if constexpr (STATS) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a[t].n = nn;
+      a[t].mean += bl[t];
+    }
     // the four lanes of a channel (kq = 0..3), then the waves in order
 #pragma unroll
     for (int off = 16; off <= 32; off <<= 1)
@@ -1605,9 +1672,9 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     // K = 9 CIN fits one K tile, C is 64 or 128, rows are whole 16-pixel groups and the next conv stages fp32;
     // DAMC_ENC_FIRST_MFMA=0 (read per call) keeps the fmaf-chain passes below
     const char* fmf = getenv("DAMC_ENC_FIRST_MFMA");
+    const size_t smw = 3 * (size_t)(R + 2) * (W + 2) * L.cin * sizeof(__bf16);  // + ~11 KB static
     const bool mf = !one && !(fmf && fmf[0] == '0') && (L.cin == 1 || L.cin == 3) && (C == 64 || C == 128) &&
-                    W % 16 == 0;
-    const size_t smw = (size_t)(R + 2) * (W + 2) * L.cin * sizeof(float);
+                    W % 16 == 0 && smw <= 49152 && L.slope >= 0.f && L.slope <= 1.f;
 #define DAMC_C3M(CIN_, NT_)                                                                                          \
   if (mf && L.cin == CIN_ && C == 16 * NT_) {                                                                        \
     hipLaunchKernelGGL((conv3_mfma_kernel<CIN_, NT_, true>), dim3(B, S), dim3(256), smw, s, x, H, W, C, R, L.w_packed,\
