@@ -2576,6 +2576,8 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
 // the epilogue of one output octet (8 consecutive channels n .. n + 7 of GEMM row m) from its fp32 sums
 template <int EPI, int OM>
 __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int n, int py, int px, float (&v)[8]);
+template <int EPI>
+__device__ __forceinline__ void x3_octet_epilogue_at(const GemmArgs& p, long idx, int n, float (&v)[8]);
 
 // register slab layout, one wave per 16x16 MFMA tile: lane l sums its f32x4 (rows 4 (l >> 4) .. + 3, column l & 15)
 // over the blocks in order (1 KB per wave-load; a thread per 4 rows x 8 channels measured 5-10 % slower per step at B=8-32), then the tile goes through
@@ -2636,6 +2638,7 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
   constexpr int TS = X3_BN + 4, RW = 64;
   __shared__ __attribute__((aligned(16))) float tile[RW * TS];
   __shared__ long rowtab[RW];
+  __shared__ int rowpix[RW];  // rowtab / ldc: the projection's output row
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ntm = (p.M + X3_BM - 1) / X3_BM, ntn = (p.N + X3_BN - 1) / X3_BN;
   const long ntile = (long)ntm * ntn;
@@ -2694,7 +2697,9 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
     for (int r = 0; r < 4; ++r) tile[(16 * w + 4 * (lane >> 4) + r) * TS + 16 * u + (lane & 15)] = v[u][r];
   if (tid < RW) {
     const int m = tm * X3_BM + qtr * RW + tid;
-    rowtab[tid] = m < p.M ? gemm_row_offset<O_PHASE>(p, m, py, px) : -1;
+    const long ro = m < p.M ? gemm_row_offset<O_PHASE>(p, m, py, px) : -1;
+    rowtab[tid] = ro;
+    rowpix[tid] = ro >= 0 ? (int)(ro / p.ldc) : -1;
   }
   __syncthreads();
   GemmArgs q = p;
@@ -2706,7 +2711,7 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
     float e8[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) e8[c] = tile[row * TS + oc + c];
-    x3_octet_epilogue<EPI_BIAS_ACT, O_PHASE>(q, m, n, py, px, e8);
+    x3_octet_epilogue_at<EPI_BIAS_ACT>(q, rowtab[row] + n, n, e8);
     *reinterpret_cast<f32x4*>(tile + row * TS + oc) = f32x4{e8[0], e8[1], e8[2], e8[3]};
     *reinterpret_cast<f32x4*>(tile + row * TS + oc + 4) = f32x4{e8[4], e8[5], e8[6], e8[7]};
   }
@@ -2729,8 +2734,8 @@ __global__ __launch_bounds__(256) void x3_ksplit_reduce_proj_kernel(GemmArgs p, 
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const long ro = rowtab[16 * w + 4 * qq + r];
-      if (ro >= 0) Pc[(ro / p.ldc) * (16 * NT) + 16 * t + mm] = acc[t][r];
+      const int pix = rowpix[16 * w + 4 * qq + r];
+      if (pix >= 0) Pc[(long)pix * (16 * NT) + 16 * t + mm] = acc[t][r];
     }
 }
 
@@ -2756,9 +2761,9 @@ __global__ void x3_ksplit_reduce_kernel(GemmArgs p, int zdim) {
   x3_octet_epilogue<EPI, OM>(p, m, n, py, px, v);
 }
 
-template <int EPI, int OM>
-__device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int n, int py, int px, float (&v)[8]) {
-  const long idx = gemm_row_offset<OM>(p, m, py, px) + n;
+// the octet epilogue at output offset idx (row offset + n)
+template <int EPI>
+__device__ __forceinline__ void x3_octet_epilogue_at(const GemmArgs& p, long idx, int n, float (&v)[8]) {
   if (EPI == EPI_BIAS_ACT) {
     if (p.bias) {
       const int nb = p.bias_mod < p.N ? n % p.bias_mod : n;
@@ -2795,6 +2800,10 @@ __device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int 
     o[1] = mm;
     o[2] = l;
   }
+}
+template <int EPI, int OM>
+__device__ __forceinline__ void x3_octet_epilogue(const GemmArgs& p, int m, int n, int py, int px, float (&v)[8]) {
+  x3_octet_epilogue_at<EPI>(p, gemm_row_offset<OM>(p, m, py, px) + n, n, v);
 }
 
 // Skinny limb GEMM for the first layer at per-rank batches (z . W, M = B <= 32 rows, K <= negk: one sign block,
