@@ -900,7 +900,7 @@ __global__ __launch_bounds__(256, 2) void gemm_km_kernel(GemmArgs p) {
 // walks a slice's 8 K tiles through a 2-3 deep LDS pipeline, latency-bound at this size).  The same 32x32x2 MFMA
 // sequence per output (k-quad q, then step s; lane half lk takes k = 8 q + 4 lk + s of each 32-deep tile) from zero
 // per slice, so every slab value is bitwise gemm_km_kernel's.
-// MT = 2 (round 5): M <= 64 as two 32-row tiles per wave (SVHN's per-config batch of 64 at nz = 100 left the tiled
+// MT = 2 (round 5, DAMC_KM_SKINNY_MT=2 since round 6): M <= 64 as two 32-row tiles per wave (SVHN's per-config batch of 64 at nz = 100 left the tiled
 // kernel 22 us for a 52 MFLOP product), two K tiles' loads in flight so the fragments stay within the VGPRs
 template <int MT>
 __global__ __launch_bounds__(256) void km_skinny_kernel(GemmArgs p) {
@@ -1008,8 +1008,13 @@ static int launch_gemm_km(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     const int km_rows = ekr ? atoi(ekr) : 64;
     if (epi == EPI_STORE && om == O_DENSE && c.M <= km_rows && c.Hin == 1 && c.Win == 1 && c.Hq == 1 && c.Wq == 1 &&
         c.kw == 1 && c.Cg == c.K && !(esk && esk[0] == '0')) {
-      const dim3 g((unsigned)zdim, (unsigned)((c.N + 127) / 128), c.M <= 32 ? 1u : (unsigned)((c.M + 63) / 64));
-      if (c.M <= 32)
+      // rows in 32-row workgroups of km_skinny_kernel<1> (round 6: SVHN B=64's two workgroups per slice took 11.4 us
+      // against 17.2 for one 64-row workgroup of <2>, half the MFMA chain per wave, profiles/r06/km_skinny_mt.txt);
+      // DAMC_KM_SKINNY_MT=2 (read per call) keeps <2> for 33-64 rows
+      const char* emt = getenv("DAMC_KM_SKINNY_MT");
+      const bool mt1 = c.M <= 32 || !(emt && emt[0] == '2');
+      const dim3 g((unsigned)zdim, (unsigned)((c.N + 127) / 128), (unsigned)((c.M + (mt1 ? 31 : 63)) / (mt1 ? 32 : 64)));
+      if (mt1)
         hipLaunchKernelGGL(km_skinny_kernel<1>, g, dim3(256), 0, s, c);
       else
         hipLaunchKernelGGL(km_skinny_kernel<2>, g, dim3(256), 0, s, c);

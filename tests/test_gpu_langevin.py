@@ -470,23 +470,25 @@ def test_fused_output_projection_is_bitwise(lv, gpu_device, monkeypatch, B, f32a
 @pytest.mark.parametrize("B", [8, 16, 32, 48, 64, 128])
 def test_skinny_first_layer_is_bitwise(lv, gpu_device, monkeypatch, B):
     """The first layer at per-rank batches (B <= 32): z . W on gemm.hip's x3_skinny_kernel and its input gradient's
-    split-K slabs on km_skinny_kernel (fragments straight into registers; up to B = 64 as two 32-row tiles per wave,
-    round 5): 2 noisy posterior steps bitwise equal to
+    split-K slabs on km_skinny_kernel (fragments straight into registers; up to B = 64 as 32-row workgroups, round
+    6, or as two 32-row tiles per wave, DAMC_KM_SKINNY_MT=2, round 5): 2 noisy posterior steps bitwise equal to
     the tiled kernels (DAMC_X3_SKINNY=0, DAMC_KM_SKINNY=0), with the skinny kernel reading the weights as fp32 rows
     split in registers (round 5, default) and as the packed limbs (DAMC_X3_SKINNY_F32B=0)."""
     G, E, x, z0 = _cifar_full(gpu_device, B)
     out = {}
-    for mode, f32b in (("0", "1"), ("1", "1"), ("1", "0")):
+    for mode, f32b, mt in (("0", "1", "1"), ("1", "1", "1"), ("1", "0", "1"), ("1", "1", "2")):
         monkeypatch.setenv("DAMC_X3_SKINNY", mode)
         monkeypatch.setenv("DAMC_KM_SKINNY", mode)
         monkeypatch.setenv("DAMC_X3_SKINNY_F32B", f32b)
+        monkeypatch.setenv("DAMC_KM_SKINNY_MT", mt)
         z = z0.clone()
         lv.posterior_langevin(z, x, G, E, 2, 0.1, 0.1, True, seed=13)
         torch.cuda.synchronize()
-        out[mode + f32b] = z.cpu()
-    assert torch.isfinite(out["11"]).all()
-    assert torch.equal(out["01"], out["11"])
-    assert torch.equal(out["01"], out["10"])
+        out[mode + f32b + mt] = z.cpu()
+    assert torch.isfinite(out["111"]).all()
+    assert torch.equal(out["011"], out["111"])
+    assert torch.equal(out["011"], out["101"])
+    assert torch.equal(out["011"], out["112"])
 
 
 @pytest.mark.parametrize("net,B", [("cifar10", 100), ("cifar10", 128), ("celeba64", 32)])
