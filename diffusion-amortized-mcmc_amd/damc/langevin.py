@@ -6,6 +6,11 @@ diagnostics tensor is read by the caller), and update ``z`` in place.
 Noise: ``noise=None`` with ``with_noise`` draws xi in-kernel (Philox4x32-10) keyed by ``seed``
 and the chain's GLOBAL index ``chain_base + row`` and step ``step_offset + i``; passing
 ``noise`` (n_steps, B, nz) injects values instead (parity tests).
+
+Spectral-norm nets in train mode (nn.utils.spectral_norm, diffusion_net.py:8-16): every forward of the reference
+advances each layer's u, v by one power iteration, so the weights change from step to step.  The chains then run one
+step per library call, each after that step's power iterations (plans.spectral_norm_step) and a re-pack; the noise is
+the same Philox stream (keyed by step_offset + i), so a chain keeps its values whichever way it is cut.
 """
 import ctypes
 
@@ -13,7 +18,7 @@ import torch
 
 from . import _lib
 from ._lib import check, ptr
-from .plans import ebm_plan, generator_plan
+from .plans import ebm_plan, generator_plan, spectral_norm_step
 
 
 def _f32c(t, name):
@@ -43,9 +48,7 @@ def posterior_langevin(z, x, netG, netE, n_steps, sigma, step, with_noise, noise
     if z.shape[1] != gp.nz or x.shape[0] != B or x.numel() != B * gp.nc * gp.h * gp.w:
         raise _lib.DamcError("shape mismatch: z %s x %s for generator nz=%d out=(%d,%d,%d)"
                              % (tuple(z.shape), tuple(x.shape), gp.nz, gp.nc, gp.h, gp.w))
-    gdesc = gp.refresh(dev)
-    edesc = ebm_plan(netE).refresh(dev) if netE is not None else None
-    ws, nbytes = gp.workspace(B)
+    ep = ebm_plan(netE) if netE is not None else None
     if noise is not None:
         noise = _f32c(noise.to(dev), "noise")
         if noise.numel() < n_steps * B * gp.nz:
@@ -53,10 +56,25 @@ def posterior_langevin(z, x, netG, netE, n_steps, sigma, step, with_noise, noise
     if seed is None:
         seed = new_seed() if (with_noise and noise is None) else 0
     dg = torch.zeros(max(n_steps, 1), 4, dtype=torch.float32, device=dev) if diag else None
-    check(_lib.lib().damc_posterior_langevin(
-        ctypes.byref(gdesc), ctypes.byref(edesc) if edesc is not None else None, ptr(z), ptr(x), B, int(n_steps),
-        float(sigma), float(step), int(bool(with_noise)), ptr(noise), seed, step_offset, chain_base,
-        ptr(dg), ptr(ws), nbytes, _lib.stream_ptr(dev)), "damc_posterior_langevin")
+
+    def run(n, off, nz_, dg_):
+        gdesc = gp.refresh(dev)
+        edesc = ep.refresh(dev) if ep is not None else None
+        ws, nbytes = gp.workspace(B)
+        check(_lib.lib().damc_posterior_langevin(
+            ctypes.byref(gdesc), ctypes.byref(edesc) if edesc is not None else None, ptr(z), ptr(x), B, int(n),
+            float(sigma), float(step), int(bool(with_noise)), ptr(nz_), seed, off, chain_base,
+            ptr(dg_), ptr(ws), nbytes, _lib.stream_ptr(dev)), "damc_posterior_langevin")
+
+    sn = gp.sn_train() + (ep.sn_train() if ep is not None else [])
+    if not sn:
+        run(n_steps, step_offset, noise, dg)
+        return dg
+    # train-mode spectral norm: netG(z) and netE(z) once per reference step (MCMC.py:54-58), one power iteration each
+    nzs = noise.view(-1, B * gp.nz) if noise is not None else None
+    for i in range(int(n_steps)):
+        with spectral_norm_step(sn):
+            run(1, step_offset + i, nzs[i] if nzs is not None else None, dg[i] if dg is not None else None)
     return dg
 
 
@@ -66,7 +84,8 @@ def likelihood_grad(z, x, netG, sigma):
     dev = z.device
     x = x.to(device=dev, dtype=torch.float32).contiguous()
     gp = generator_plan(netG)
-    gdesc = gp.refresh(dev)
+    with spectral_norm_step(gp.sn_train()):  # one G forward (train-mode spectral norm: one power iteration)
+        gdesc = gp.refresh(dev)
     ws, nbytes = gp.workspace(z.shape[0])
     g = torch.empty_like(z)
     check(_lib.lib().damc_likelihood_grad(ctypes.byref(gdesc), ptr(z), ptr(x), z.shape[0], float(sigma), ptr(g),
@@ -79,7 +98,8 @@ def generator_forward(z, netG):
     z = _f32c(z.detach().contiguous() if not z.is_contiguous() else z.detach(), "z")
     dev = z.device
     gp = generator_plan(netG)
-    gdesc = gp.refresh(dev)
+    with spectral_norm_step(gp.sn_train()):  # one G forward (train-mode spectral norm: one power iteration)
+        gdesc = gp.refresh(dev)
     ws, nbytes = gp.workspace(z.shape[0])
     shape = (z.shape[0], gp.nc, gp.h, gp.w) if gp.is_conv else (z.shape[0], gp.nc)
     out = torch.empty(shape, dtype=torch.float32, device=dev)
@@ -112,7 +132,6 @@ def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, st
     ep = ebm_plan(netE)
     if z.shape[1] != ep.nz:
         raise _lib.DamcError("z has %d dims, EBM expects %d" % (z.shape[1], ep.nz))
-    edesc = ep.refresh(dev)
     B = z.shape[0]
     if noise is not None:
         noise = _f32c(noise.to(dev), "noise")
@@ -127,22 +146,37 @@ def prior_langevin(z, netE, n_steps, step, with_noise, noise=None, seed=None, st
     if engine == "auto":  # resolved here from the global chain count, never from the shard's
         code = 2 if int(global_batch if global_batch is not None else B) >= mfma_min_chains() else 1
 
-    def run(c):
-        return _lib.lib().damc_prior_langevin_engine(ctypes.byref(edesc), ptr(z), B, int(n_steps), float(step),
-                                                     int(bool(with_noise)), ptr(noise), seed, step_offset,
-                                                     chain_base, ptr(dg), c, _lib.stream_ptr(dev))
+    def run(n, off, nz_, dg_):
+        edesc = ep.refresh(dev)
 
-    rc = run(code)
-    if rc == _lib.DAMC_ERR_UNSUPPORTED and engine == "auto":  # the shape has no kernel of that engine: the other
-        rc = run(1 if code == 2 else 2)
-    check(rc, "damc_prior_langevin")
+        def call(c):
+            return _lib.lib().damc_prior_langevin_engine(ctypes.byref(edesc), ptr(z), B, int(n), float(step),
+                                                         int(bool(with_noise)), ptr(nz_), seed, off,
+                                                         chain_base, ptr(dg_), c, _lib.stream_ptr(dev))
+
+        rc = call(code)
+        if rc == _lib.DAMC_ERR_UNSUPPORTED and engine == "auto":  # the shape has no kernel of that engine: the other
+            rc = call(1 if code == 2 else 2)
+        check(rc, "damc_prior_langevin")
+
+    sn = ep.sn_train()
+    if not sn:
+        run(n_steps, step_offset, noise, dg)
+        return dg
+    # train-mode spectral norm: netE(z) once per reference step (MCMC.py:32), one power iteration each
+    nzs = noise.view(-1, B * ep.nz) if noise is not None else None
+    for i in range(int(n_steps)):
+        with spectral_norm_step(sn):
+            run(1, step_offset + i, nzs[i] if nzs is not None else None, dg[i] if dg is not None else None)
     return dg
 
 
 def ebm_energy_grad(z, netE):
     _f32c(z, "z")
     dev = z.device
-    edesc = ebm_plan(netE).refresh(dev)
+    ep = ebm_plan(netE)
+    with spectral_norm_step(ep.sn_train()):  # one E forward (train-mode spectral norm: one power iteration)
+        edesc = ep.refresh(dev)
     e = torch.empty(z.shape[0], dtype=torch.float32, device=dev)
     g = torch.empty_like(z)
     check(_lib.lib().damc_ebm_energy_grad(ctypes.byref(edesc), ptr(z), z.shape[0], ptr(e), ptr(g),

@@ -11,7 +11,9 @@ Generator structure: ``_netG_*.gen`` = [ConvTranspose2d, LeakyReLU(.2)]* ConvTra
 EBM structure: ``_netE.ebm`` = Linear, LeakyReLU(.2), Linear, LeakyReLU(.2), Linear
 (workspace/src/diffusion_net.py:207-223).
 """
+import contextlib
 import ctypes
+import threading
 import weakref
 
 import torch
@@ -46,23 +48,58 @@ def _require_plain_param(m):
         raise NotImplementedError("a reparametrised weight other than nn.utils.spectral_norm's")
 
 
+_SN = threading.local()  # set while spectral_norm_step's power iteration is the one the current forward runs
+
+
 def _live_weight(m):
     """The weight m's forward would use.  A spectral-norm layer (use_spc_norm=True generators, e_sn=True EBMs:
-    diffusion_net.py:8-16, 21-44, 208-210) recomputes it in its forward pre-hook from weight_orig and the u, v vectors;
-    in eval mode -- the mode the reference runs G and E in for the Langevin chains and the sweeps
+    diffusion_net.py:8-16, 21-44, 208-210) recomputes it in its forward pre-hook from weight_orig and the u, v vectors.
+    In eval mode -- the mode the reference runs G and E in for the Langevin chains and the sweeps
     (train_gen_recon.py:191-193) -- without a power iteration, so the value is fixed and is what every forward of the
     chain would use: it is computed here the way the hook does and set as the hook sets it.  In train mode every
-    forward advances u and v once, which one packing per call cannot follow through the chain's per-step forwards."""
+    forward advances u and v once: the caller runs that forward's power iteration first (spectral_norm_step), and the
+    weight it set is the one read here."""
     h = _sn_hook(m)
     if h is None:
         return m.weight
     if m.training:
-        raise NotImplementedError("spectral-norm layers in train mode: every forward runs a power iteration (call "
-                                  ".eval() before the Langevin chains, as the reference's drivers do)")
+        if not getattr(_SN, "on", False):
+            raise NotImplementedError("spectral-norm layer in train mode outside spectral_norm_step: its forward "
+                                      "would run a power iteration")
+        return getattr(m, h.name)
     with torch.no_grad():
         w = h.compute_weight(m, do_power_iteration=False)
     setattr(m, h.name, w)
     return w
+
+
+def sn_train_layers(modules):
+    """(module, SpectralNorm hook) of every layer in train mode with nn.utils.spectral_norm among modules."""
+    out = []
+    for m in modules:
+        h = _sn_hook(m)
+        if h is not None and m.training:
+            out.append((m, h))
+    return out
+
+
+@contextlib.contextmanager
+def spectral_norm_step(layers):
+    """One reference forward's worth of nn.utils.spectral_norm in train mode (torch/nn/utils/spectral_norm.py,
+    SpectralNorm.__call__ -> compute_weight(do_power_iteration=True)): each layer's u and v advance by the hook's own
+    power iteration, in place, and the normalised weight is set on the module as the hook sets it; inside the block
+    the plans pack that weight.  The reference's Langevin step calls netG(z) and netE(z) once each (MCMC.py:32,54-58),
+    so a chain in train mode runs one of these per step, and u, v, the weights and z follow the reference's."""
+    if layers:
+        with torch.no_grad():
+            for m, h in layers:
+                setattr(m, h.name, h.compute_weight(m, do_power_iteration=True))
+    prev = getattr(_SN, "on", False)
+    _SN.on = True
+    try:
+        yield
+    finally:
+        _SN.on = prev
 
 
 class GeneratorPlan:
@@ -180,6 +217,9 @@ class GeneratorPlan:
             out.layers[i].engine = engine
         return out
 
+    def sn_train(self):
+        return sn_train_layers(self.modules)
+
     def workspace(self, batch):
         L = _lib.lib()
         nbytes = int(L.damc_posterior_workspace_bytes(ctypes.byref(self.desc), int(batch)))
@@ -207,6 +247,9 @@ class EbmPlan:
         self.lin = lin
         self.nz, self.nh = lin[0].in_features, lin[0].out_features
         self.device = None
+
+    def sn_train(self):
+        return sn_train_layers(self.lin)
 
     def refresh(self, device):
         device = torch.device(device)

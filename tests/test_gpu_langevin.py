@@ -520,7 +520,7 @@ def test_spectral_norm_nets_in_eval_mode(lv, gpu_device):
     """use_spc_norm=True generators and e_sn=True EBMs (nn.utils.spectral_norm, diffusion_net.py:8-16, 21-44, 208-210)
     on the HIP path in eval mode, the mode of the reference's Langevin chains (train_gen_recon.py:191-193): after a few
     train-mode forwards have moved u and v, the posterior chain (10 no-noise steps) and the prior chain match the
-    oracle on the weights the layers' own forward pre-hooks compute; train mode is refused."""
+    oracle on the weights the layers' own forward pre-hooks compute (train mode: the next test)."""
     from damc import synth
     from damc import training
     from oracle import damc_oracle as orc
@@ -548,6 +548,89 @@ def test_spectral_norm_nets_in_eval_mode(lv, gpu_device):
     lv.prior_langevin(zp, E, 5, 0.4, False)
     refp = orc.prior_langevin(P, torch.cat([z0, z0]).cpu(), 5, 0.4)
     assert rel_l2(zp.cpu().numpy(), refp.numpy()) < 1e-5
-    G.train()
-    with pytest.raises(NotImplementedError):
-        lv.posterior_langevin(z0.clone(), x, G, E, 1, 0.3, 0.1, False)
+
+
+def _sn_buffers(net):
+    return [t for n, t in net.named_buffers() if n.endswith("weight_u") or n.endswith("weight_v")]
+
+
+def test_spectral_norm_nets_in_train_mode(lv, gpu_device):
+    """Spectral-norm G and E in train mode (nn.utils.spectral_norm, diffusion_net.py:8-16, 21-44, 208-210): every
+    forward of the reference advances u and v by one power iteration, so the weights move from step to step (fresh u:
+    sigma still converging).  The HIP chains run one step per call after that step's power iterations: against the
+    reference's own loops (MCMC.py:27-46, 48-74) on deep copies of the stock modules with the same injected noise, z
+    matches (fp32: rel-L2 <= 2e-4 over 6 posterior steps, <= 1e-5 over 5 prior steps) and every u, v buffer is bitwise
+    the reference's afterwards; likelihood_grad / generator_forward / ebm_energy_grad each advance once, as one forward."""
+    import copy
+
+    from damc import synth
+    from damc import training
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=16, nc=3, use_spc_norm=True), 4).to(gpu_device).train()
+    E = synth.load_into(dn._netE(nz=128, e_sn=True), 5).to(gpu_device).train()
+    G2, E2 = copy.deepcopy(G), copy.deepcopy(E)
+    z0 = torch.from_numpy(synth.normal_f32(93, 0, (8, 128))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(93, 1, (8, 3, 32, 32))).to(gpu_device)
+    noise = torch.from_numpy(synth.normal_f32(93, 2, (6, 8, 128))).to(gpu_device)
+    sigma, step = 0.3, 0.1
+    z = z0.clone()
+    lv.posterior_langevin(z, x, G, E, 6, sigma, step, True, noise=noise)
+    zr = z0.clone().requires_grad_(True)
+    with training.stock_pytorch():
+        for i in range(6):
+            lk = 1.0 / (2.0 * sigma * sigma) * torch.sum((G2(zr) - x) ** 2)
+            total = lk + E2(zr).sum() + 0.5 * torch.sum(zr ** 2)
+            g = torch.autograd.grad(total, zr)[0]
+            zr.data = zr.data - 0.5 * step * step * g + step * noise[i]
+    assert rel_l2(z.cpu().numpy(), zr.detach().cpu().numpy()) < 2e-4
+    for a, b in zip(_sn_buffers(G) + _sn_buffers(E), _sn_buffers(G2) + _sn_buffers(E2)):
+        assert torch.equal(a, b)
+    # a chain whose weights did not move would be far off: the stepping is what the match rests on
+    zf = z0.clone()
+    G3, E3 = copy.deepcopy(G).eval(), copy.deepcopy(E).eval()
+    lv.posterior_langevin(zf, x, G3, E3, 6, sigma, step, True, noise=noise)
+    assert rel_l2(zf.cpu().numpy(), zr.detach().cpu().numpy()) > 10 * rel_l2(z.cpu().numpy(), zr.detach().cpu().numpy())
+
+    zp = torch.cat([z0, z0]).contiguous()
+    pn = torch.from_numpy(synth.normal_f32(93, 3, (5, 16, 128))).to(gpu_device)
+    lv.prior_langevin(zp, E, 5, 0.4, True, noise=pn)
+    zq = torch.cat([z0, z0]).requires_grad_(True)
+    with training.stock_pytorch():
+        for i in range(5):
+            g = torch.autograd.grad(E2(zq).sum() + 0.5 * torch.sum(zq ** 2), zq)[0]
+            zq.data = zq.data - 0.5 * 0.4 * 0.4 * g + 0.4 * pn[i]
+    assert rel_l2(zp.cpu().numpy(), zq.detach().cpu().numpy()) < 1e-5
+    for a, b in zip(_sn_buffers(E), _sn_buffers(E2)):
+        assert torch.equal(a, b)
+
+    xh = lv.generator_forward(z0, G)
+    lv.ebm_energy_grad(z0, E)
+    with training.stock_pytorch(), torch.no_grad():
+        xr = G2(z0)
+        E2(z0)
+    assert rel_l2(xh.cpu().numpy(), xr.cpu().numpy()) < 1e-5
+    for a, b in zip(_sn_buffers(G) + _sn_buffers(E), _sn_buffers(G2) + _sn_buffers(E2)):
+        assert torch.equal(a, b)
+
+
+def test_chain_cut_into_single_steps_is_bitwise(lv, gpu_device):
+    """The stepping that train-mode spectral norm uses: a chain run as one call equals the same chain run one step per
+    call (step_offset = i keys the in-kernel Philox), bitwise, for the posterior and the prior."""
+    from damc import synth
+    from src import diffusion_net as dn
+
+    G = synth.load_into(dn._netG_cifar10(nz=128, ngf=32, nc=3), 4).to(gpu_device).eval()
+    E = synth.load_into(dn._netE(nz=128), 5).to(gpu_device).eval()
+    z0 = torch.from_numpy(synth.normal_f32(94, 0, (16, 128))).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(94, 1, (16, 3, 32, 32))).to(gpu_device)
+    z1, z2 = z0.clone(), z0.clone()
+    lv.posterior_langevin(z1, x, G, E, 5, 0.3, 0.1, True, seed=77)
+    for i in range(5):
+        lv.posterior_langevin(z2, x, G, E, 1, 0.3, 0.1, True, seed=77, step_offset=i)
+    assert torch.equal(z1, z2)
+    p1, p2 = torch.cat([z0, z0]).contiguous(), torch.cat([z0, z0]).contiguous()
+    lv.prior_langevin(p1, E, 5, 0.4, True, seed=78)
+    for i in range(5):
+        lv.prior_langevin(p2, E, 1, 0.4, True, seed=78, step_offset=i)
+    assert torch.equal(p1, p2)
