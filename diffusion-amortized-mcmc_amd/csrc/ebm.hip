@@ -1123,3 +1123,83 @@ extern "C" int damc_ebm_train_backward(const damc_ebm_t* e, const float* z, cons
   if (grad_z) g2[k++] = sg(w.dh1, nh, e->w1, nz, 0, nullptr, grad_z, nz, B, nz, nh, DAMC_ACT_NONE, 0.f);
   return k ? damc::launch_small_gemm_group(g2, k, s) : (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------ Q update: prior embedding
+// Q.prior_emb = Linear(nz, nh) -> LeakyReLU(slope) -> Linear(nh, nout) (workspace/src/diffusion_net.py:577-581) as the
+// Q update trains it through Q.calculate_loss (diffusion_net.py:624-641: the mask's prior rows, or every row with x
+// None) on the grouped small-GEMM kernel, the E update's building blocks (exact fp32 products, fp32 sums): two launches
+// forward keeping the hidden activation, backward a transpose, one grouped launch (W2, b2 and the hidden gradient), the
+// LReLU' mask and one grouped launch (W1, b1).  The input is a fresh draw: no input gradient.
+namespace {
+struct PeWs {
+  float *gT, *dhp, *dh, *dhT;
+};
+size_t pe_carve(const damc_prior_emb_t* e, int B, char* base, PeWs* w) {
+  size_t off = 0;
+  auto take = [&](long n) {
+    float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((size_t)n * sizeof(float) + 255) / 256 * 256;
+    return p;
+  };
+  PeWs t;
+  t.gT = take((long)B * e->nout);
+  t.dhp = take((long)B * e->nh);
+  t.dh = take((long)B * e->nh);
+  t.dhT = take((long)B * e->nh);
+  if (w) *w = t;
+  return off;
+}
+// the backward's LReLU' comes from the post-activation's sign: the pre-activation's only for slope >= 0
+bool pe_ok(const damc_prior_emb_t* e, int B) {
+  return e && e->nz > 0 && e->nh > 0 && e->nout > 0 && B > 0 && B % 4 == 0 && e->nz % 4 == 0 && e->nh % 4 == 0 &&
+         e->nout % 4 == 0 && e->slope >= 0.f && e->w1 && e->b1 && e->w2 && e->b2;
+}
+}  // namespace
+
+extern "C" size_t damc_prior_emb_train_workspace_bytes(const damc_prior_emb_t* e, int B) {
+  if (!pe_ok(e, B)) return 0;
+  return pe_carve(e, B, nullptr, nullptr);
+}
+
+extern "C" int damc_prior_emb_train_forward(const damc_prior_emb_t* e, const float* noise, int B, float* h, float* out,
+                                            void* stream) {
+  if (!e || !noise || !h || !out) return DAMC_ERR_ARG;
+  if (!pe_ok(e, B)) return DAMC_ERR_UNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  const damc::SmallGemm l1 = sg(noise, e->nz, e->w1, e->nz, 1, e->b1, h, e->nh, B, e->nh, e->nz, DAMC_ACT_LRELU, e->slope);
+  const damc::SmallGemm l2 = sg(h, e->nh, e->w2, e->nh, 1, e->b2, out, e->nout, B, e->nout, e->nh, DAMC_ACT_NONE, 0.f);
+  int rc = damc::launch_small_gemm_group(&l1, 1, s);
+  if (!rc) rc = damc::launch_small_gemm_group(&l2, 1, s);
+  return rc;
+}
+
+extern "C" int damc_prior_emb_train_backward(const damc_prior_emb_t* e, const float* noise, const float* h,
+                                             const float* grad_out, int B, const damc_prior_emb_grads_t* gr,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
+  if (!e || !noise || !h || !grad_out || !gr) return DAMC_ERR_ARG;
+  if (!pe_ok(e, B)) return DAMC_ERR_UNSUPPORTED;
+  if (!workspace || workspace_bytes < pe_carve(e, B, nullptr, nullptr)) return DAMC_ERR_WORKSPACE;
+  PeWs w;
+  pe_carve(e, B, static_cast<char*>(workspace), &w);
+  hipStream_t s = as_stream(stream);
+  const int nz = e->nz, nh = e->nh, no = e->nout;
+  const long ng = (long)B * no, nhb = (long)B * nh;
+  const bool down = gr->w1 || gr->b1;
+  damc::SmallGemm g1[3];
+  int k = 0;
+  if (gr->w2) {
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, grad_out, B, no, w.gT);
+    g1[k++] = sg(w.gT, B, h, nh, 0, nullptr, gr->w2, nh, no, nh, B, DAMC_ACT_NONE, 0.f);
+  }
+  if (gr->b2) g1[k++] = sg_colsum(grad_out, B, no, no, gr->b2);
+  if (down) g1[k++] = sg(grad_out, no, e->w2, nh, 0, nullptr, w.dhp, nh, B, nh, no, DAMC_ACT_NONE, 0.f);
+  int rc = k ? damc::launch_small_gemm_group(g1, k, s) : 0;
+  if (rc || !down) return rc ? rc : (int)hipGetLastError();
+  hipLaunchKernelGGL(et_mask_kernel, dim3((unsigned)((nhb + 255) / 256)), dim3(256), 0, s, (const float*)w.dhp, h, B, nh,
+                     e->slope, w.dh, w.dhT);
+  damc::SmallGemm g2[2];
+  k = 0;
+  if (gr->w1) g2[k++] = sg(w.dhT, B, noise, nz, 0, nullptr, gr->w1, nz, nh, nz, B, DAMC_ACT_NONE, 0.f);
+  if (gr->b1) g2[k++] = sg_colsum(w.dh, B, nh, nh, gr->b1);
+  return damc::launch_small_gemm_group(g2, k, s);
+}

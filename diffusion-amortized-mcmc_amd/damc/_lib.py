@@ -106,6 +106,15 @@ class EbmGrads(ctypes.Structure):  # damc_ebm_grads_t
     _fields_ = [(k, ctypes.c_void_p) for k in ("w1", "b1", "w2", "b2", "w3", "b3")]
 
 
+class PriorEmb(ctypes.Structure):  # damc_prior_emb_t
+    _fields_ = [("nz", ctypes.c_int), ("nh", ctypes.c_int), ("nout", ctypes.c_int), ("slope", ctypes.c_float)] + [
+        (k, ctypes.c_void_p) for k in ("w1", "b1", "w2", "b2")]
+
+
+class PriorEmbGrads(ctypes.Structure):  # damc_prior_emb_grads_t
+    _fields_ = [(k, ctypes.c_void_p) for k in ("w1", "b1", "w2", "b2")]
+
+
 class AdamHparams(ctypes.Structure):
     _fields_ = [("neg_step_size", ctypes.c_float), ("one_minus_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("one_minus_beta2", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("eps", ctypes.c_float),
@@ -154,6 +163,10 @@ _SIGS = {
     "damc_ebm_train_forward": (_I, [ctypes.POINTER(Ebm), _P, _I, _P, _P, _P, _P]),
     "damc_ebm_train_backward": (_I, [ctypes.POINTER(Ebm), _P, _P, _P, _P, ctypes.c_long, _I, ctypes.POINTER(EbmGrads),
                                      _P, _P, _SZ, _P]),
+    "damc_prior_emb_train_workspace_bytes": (_SZ, [ctypes.POINTER(PriorEmb), _I]),
+    "damc_prior_emb_train_forward": (_I, [ctypes.POINTER(PriorEmb), _P, _I, _P, _P, _P]),
+    "damc_prior_emb_train_backward": (_I, [ctypes.POINTER(PriorEmb), _P, _P, _P, _I, ctypes.POINTER(PriorEmbGrads), _P,
+                                           _SZ, _P]),
     "damc_q_noise_glue": (_I, [_P, _P, _P, _I, _I, _F, _F, _P, _I, _P, _P, _P, _P]),
     "damc_q_loss_forward": (_I, [_P, _P, _I, _I, _P, _P]),
     "damc_q_loss_backward": (_I, [_P, _P, _P, ctypes.c_long, _I, _I, _P, _P]),

@@ -425,6 +425,80 @@ def ebm_apply(E, z):
     return _EbmTrainFn.apply(z, d, slope, *params)
 
 
+# ------------------------------------------------------------------------ Q update: prior embedding
+# Q.prior_emb(torch.randn(B, nz)) inside Q.calculate_loss (diffusion_net.py:628-634: the mask's prior rows, or every row
+# with x None) on libdamc (damc_prior_emb_train_*): two small-GEMM launches forward, a transpose, two grouped launches
+# and the LReLU' mask backward.  Shapes the C side does not take keep the stock modules.
+
+def _prior_emb_layers(seq):
+    mods = list(seq)
+    if len(mods) != 3 or not isinstance(mods[0], torch.nn.Linear) or not isinstance(mods[2], torch.nn.Linear):
+        return None
+    if not isinstance(mods[1], torch.nn.LeakyReLU) or not mods[1].negative_slope >= 0:  # LReLU' from h's sign
+        return None
+    if any(hasattr(m, "weight_orig") or m.bias is None for m in (mods[0], mods[2])):
+        return None
+    return (mods[0], mods[2]), float(mods[1].negative_slope)
+
+
+class _PriorEmbTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, noise, desc, *params):
+        L = _lib.lib()
+        B = noise.shape[0]
+        dev = noise.device
+        h = torch.empty(B, desc.nh, dtype=torch.float32, device=dev)
+        out = torch.empty(B, desc.nout, dtype=torch.float32, device=dev)
+        check(L.damc_prior_emb_train_forward(ctypes.byref(desc), ptr(noise), B, ptr(h), ptr(out), _lib.stream_ptr(dev)),
+              "damc_prior_emb_train_forward")
+        ctx.desc = desc
+        ctx.save_for_backward(noise, h, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        noise, h = ctx.saved_tensors[:2]
+        params = ctx.saved_tensors[2:]
+        L = _lib.lib()
+        dev = g.device
+        B = noise.shape[0]
+        g = g.to(torch.float32).contiguous()
+        outs = _grad_buffers(params, ctx.needs_input_grad[2:])
+        grads = _lib.PriorEmbGrads()
+        for k, t in zip(("w1", "b1", "w2", "b2"), outs):
+            if t is not None:
+                setattr(grads, k, t.data_ptr())
+        nb = int(L.damc_prior_emb_train_workspace_bytes(ctypes.byref(ctx.desc), B))
+        ws = _scratch("prior_emb_bwd", dev, nb)
+        check(L.damc_prior_emb_train_backward(ctypes.byref(ctx.desc), ptr(noise), ptr(h), ptr(g), B,
+                                              ctypes.byref(grads), ptr(ws), nb, _lib.stream_ptr(dev)),
+              "damc_prior_emb_train_backward")
+        ctx.desc = None
+        return (None, None, *outs)
+
+
+def prior_emb_apply(seq, noise):
+    """Q.prior_emb(noise) on libdamc with grad (the Q update), or None where the C side does not take the module /
+    input (the caller then runs the stock modules).  noise is a fresh draw: no gradient flows into it."""
+    lay = _prior_emb_layers(seq)
+    if lay is None or noise.dim() != 2 or noise.dtype != torch.float32 or noise.shape[0] % 4 or noise.requires_grad:
+        return None
+    (l1, l2), slope = lay
+    params = [l1.weight, l1.bias, l2.weight, l2.bias]
+    if any(p.dtype != torch.float32 or not p.is_contiguous() or p.device != noise.device or p.data_ptr() % 16
+           for p in params):
+        return None
+    noise = noise.contiguous()
+    if noise.data_ptr() % 16:
+        return None
+    d = _lib.PriorEmb()
+    d.nz, d.nh, d.nout, d.slope = l1.in_features, l1.out_features, l2.out_features, slope
+    d.w1, d.b1, d.w2, d.b2 = [p.data_ptr() for p in params]
+    if l2.in_features != d.nh or int(_lib.lib().damc_prior_emb_train_workspace_bytes(ctypes.byref(d), noise.shape[0])) == 0:
+        return None
+    return _PriorEmbTrainFn.apply(noise, d, *params)
+
+
 # ------------------------------------------------------------------------------- Q update: encoder
 # Encoder_* (workspace/src/diffusion_net.py:227-413) as trained by Q.calculate_loss: forward on libdamc
 # keeping every conv output, InstanceNorm statistic and layer input; backward through
@@ -480,7 +554,7 @@ def encoder_train_supported(enc, x):
 # per-call scratch of the encoder's training forward / backward (packed weights, conv and InstanceNorm workspaces):
 # kernels are stream-ordered, so one buffer per purpose serves every stage and every call on a stream (round 5: ~20
 # torch.empty calls per Q update, ~0.1 ms of host time)
-_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd", "ebm_bwd", "enc_train")}
+_ENC_SCRATCH = {k: _lib.WorkspaceCache() for k in ("w3", "conv", "in", "in_bwd", "conv_bwd", "ebm_bwd", "enc_train", "prior_emb_bwd")}
 
 
 def _scratch(key, device, nbytes):

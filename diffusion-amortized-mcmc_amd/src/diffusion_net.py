@@ -304,20 +304,32 @@ class _netQ_U(nn.Module):
 
         return amortizer.q_forward(self, x=x, b=b, device=device, cond_w=cond_w)
 
+    def _prior_emb(self, noise):
+        """self.prior_emb(noise): on ROCm with autograd on, libdamc's forward / backward (damc.training.prior_emb_apply),
+        else (or where the C side does not take the shapes) the stock modules."""
+        if noise.is_cuda and torch.is_grad_enabled():
+            from damc import training
+
+            if training.ENABLED:
+                out = training.prior_emb_apply(self.prior_emb, noise)
+                if out is not None:
+                    return out
+        return self.prior_emb(noise)
+
     def calculate_loss(self, x=None, z=None, mask=None):
         """Training loss of the denoiser (diffusion_net.py:624-645).  On ROCm tensors the denoiser's forward and
         backward run on libdamc (Diffusion_UnetA.forward -> damc.training.denoiser_apply), as do the encoder's
         (_EncoderBase.forward -> damc.training.encoder_apply) and the noising, time embedding and loss
-        (damc.training.q_noise_glue / q_loss); prior_emb (two Linears, used with x None or a mask) and the random
-        draws stay PyTorch."""
+        (damc.training.q_noise_glue / q_loss) and prior_emb (two Linears, used with x None or a mask:
+        damc.training.prior_emb_apply); the random draws stay torch's, in the reference's order."""
         assert z is not None
         if x is not None:
             xemb = self.encoder(x)
             if mask is not None:
-                xemb = xemb * mask + self.prior_emb(torch.randn(len(x), self.nz, device=x.device)) * (1 - mask)
+                xemb = xemb * mask + self._prior_emb(torch.randn(len(x), self.nz, device=x.device)) * (1 - mask)
         else:
             assert mask is None
-            xemb = self.prior_emb(torch.randn(len(z), self.nz, device=z.device))
+            xemb = self._prior_emb(torch.randn(len(z), self.nz, device=z.device))
         if z.is_cuda and xemb is not None and not z.requires_grad and z.dtype == torch.float32:
             from damc import training
 

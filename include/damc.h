@@ -427,6 +427,27 @@ int damc_ebm_train_backward(const damc_ebm_t* e, const float* z, const float* h1
                             const float* grad_energy, long grad_stride, int batch, const damc_ebm_grads_t* grads,
                             float* grad_z, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------- Q update: prior embedding (round 6; SURVEY §8f, diffusion_net.py:624-641)
+ * Q.prior_emb = Linear(nz, nh) -> LeakyReLU(slope >= 0) -> Linear(nh, nout) (diffusion_net.py:577-581), PyTorch-layout
+ * weights; the forward keeps the hidden activation h (B, nh) for the backward.  Replaces the stock modules inside
+ * Q.calculate_loss (the mask's prior rows / x None).  Batch and widths multiples of 4, weights 16-B aligned
+ * (DAMC_ERR_UNSUPPORTED otherwise: the caller keeps PyTorch). */
+typedef struct {
+  int nz, nh, nout;
+  float slope;
+  const float *w1, *b1, *w2, *b2;
+} damc_prior_emb_t;
+typedef struct { /* gradients, PyTorch layouts (written, not accumulated; NULL entries are skipped) */
+  float *w1, *b1, *w2, *b2;
+} damc_prior_emb_grads_t;
+size_t damc_prior_emb_train_workspace_bytes(const damc_prior_emb_t* e, int batch);
+int damc_prior_emb_train_forward(const damc_prior_emb_t* e, const float* noise, int batch, float* h, float* out,
+                                 void* stream);
+/* grad_out (B, nout) contiguous -> the four parameter gradients (the input is a fresh draw: no input gradient) */
+int damc_prior_emb_train_backward(const damc_prior_emb_t* e, const float* noise, const float* h, const float* grad_out,
+                                  int batch, const damc_prior_emb_grads_t* grads, void* workspace,
+                                  size_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------------------- optimiser steps
  * Replaces the G/E/Q updates' torch.nn.utils.clip_grad_norm_ + optim.Adam / optim.AdamW.step()
  * (train_gen_recon.py:155-157, 219-231, 240-241) by multi-tensor kernels.  A launch covers up to

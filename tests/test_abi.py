@@ -207,6 +207,15 @@ def test_round5_host_only_entry_points():
     assert L.damc_q_noise_glue(8, 8, 8, 128, 128, -5.1, 9.8, 8, 127, None, 8, 8, None) == 1001
     assert L.damc_q_loss_forward(None, None, 128, 128, None, None) == 1001
     assert L.damc_q_loss_backward(8, 8, 8, -1, 128, 128, 8, None) == 1001
+    pe = _lib.PriorEmb()
+    pe.nz, pe.nh, pe.nout, pe.slope = 128, 128, 1024, 0.01
+    assert L.damc_prior_emb_train_workspace_bytes(ctypes.byref(pe), 128) == 0  # no weight pointers
+    pe.w1 = pe.b1 = pe.w2 = pe.b2 = 256
+    assert L.damc_prior_emb_train_workspace_bytes(ctypes.byref(pe), 128) > 0
+    assert L.damc_prior_emb_train_workspace_bytes(ctypes.byref(pe), 130) == 0
+    pe.slope = -0.1  # LReLU' is read from the activation's sign: negative slopes stay on the stock modules
+    assert L.damc_prior_emb_train_workspace_bytes(ctypes.byref(pe), 128) == 0
+    assert L.damc_prior_emb_train_forward(None, None, 128, None, None, None) == 1001
 
 
 def test_optim_step_counters_with_a_fixed_subset_host_only():

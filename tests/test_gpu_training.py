@@ -508,3 +508,54 @@ def test_encoder_train_one_call_is_bitwise_the_stage_calls(gpu_device, monkeypat
     assert 0 < e < 1e-5 if nif == 64 else e < 1e-5
     for a, b in zip(out["head"][1], out[True][1]):
         assert torch.equal(a, b)
+
+
+def test_prior_emb_train_vs_fp64(gpu_device):
+    """Q.prior_emb = Linear(nz, 128) -> LeakyReLU -> Linear(128, nxemb) (diffusion_net.py:577-581) as the Q update
+    trains it inside Q.calculate_loss (diffusion_net.py:628-634) on libdamc (damc_prior_emb_train_*): the output and
+    the four parameter gradients vs fp64 autograd of the same modules, each within 3x the stock fp32 ops' own distance
+    from fp64 (+1e-6); then a masked calculate_loss on the drop-in Q runs its prior rows through it."""
+    import copy
+
+    from damc import synth, training
+    from src import diffusion_net as dn
+
+    for nz, nout, B in ((128, 1024, 128), (100, 128, 64)):
+        seq = synth.load_into(torch.nn.Sequential(torch.nn.Linear(nz, 128), torch.nn.LeakyReLU(),
+                                                  torch.nn.Linear(128, nout)), 7).to(gpu_device)
+        noise = torch.from_numpy(synth.normal_f32(8, 0, (B, nz))).to(gpu_device)
+        w = torch.from_numpy(synth.normal_f32(8, 1, (B, nout))).to(gpu_device)
+
+        def run(mod, nse, hip):
+            mod.zero_grad()
+            out = training.prior_emb_apply(mod, nse) if hip else mod(nse)
+            assert out is not None
+            (out * w.to(out.dtype)).sum().backward()
+            return [out.detach().double().cpu()] + [p.grad.double().cpu() for p in mod.parameters()]
+
+        hip = run(seq, noise, True)
+        f32 = run(seq, noise, False)
+        s64 = copy.deepcopy(seq).double()
+        f64 = run(s64, noise.double(), False)
+        for k, (a, b, r) in enumerate(zip(hip, f32, f64)):
+            e_hip, e32 = rel_l2(a.numpy(), r.numpy()), rel_l2(b.numpy(), r.numpy())
+            print("nz %d nout %d B %d tensor %d: |hip - fp64| %.2e, |fp32 - fp64| %.2e" % (nz, nout, B, k, e_hip, e32))
+            assert e_hip <= 3 * e32 + 1e-6, (k, e_hip, e32)
+
+    Q = synth.load_into(dn._netQ_U(nc=3, nz=128, nxemb=128, ntemb=128, nif=8, diffusion_residual=True, n_interval=10,
+                                   logsnr_min=-5.1, logsnr_max=9.8, var_type="large", with_noise=True, cond_w=0.0,
+                                   net_arch="A", dataset="cifar10"), 9).to(gpu_device)
+    x = torch.from_numpy(synth.uniform_f32(9, 0, (8, 3, 32, 32))).to(gpu_device)
+    z = torch.from_numpy(synth.normal_f32(9, 1, (8, 128))).to(gpu_device)
+    mask = torch.ones(8, 1, device=gpu_device)
+    mask[1::3] = 0.0
+    calls = []
+    orig = training.prior_emb_apply
+    training.prior_emb_apply = lambda seq, nse: calls.append(1) or orig(seq, nse)
+    try:
+        Q.calculate_loss(x=x, z=z, mask=mask).mean().backward()
+    finally:
+        training.prior_emb_apply = orig
+    assert calls
+    for p in Q.prior_emb.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0
