@@ -164,6 +164,23 @@ __global__ __launch_bounds__(256) void in_merge_kernel(const float* __restrict__
   ss[(long)b * 2 * C + C + c] = beta[c] - a.mean * scale;
 }
 
+// the norm statistics of the 256-pixel strips (GemmArgs::in_part's partition and arithmetic: damc::strip256_stats)
+// from the stored conv output, for a conv whose launch could not take them in its epilogue (split-K at a small batch):
+// grid (HW / 256 strips, B, ceil(C / 128)), 512 threads; part as in_stats_kernel's with S = HW / 256
+__global__ __launch_bounds__(512) void in_strip_stats_kernel(const float* __restrict__ y, int HW, int C, float* part) {
+  __shared__ float red[1024];
+  const int sp = blockIdx.x, b = blockIdx.y, c0 = blockIdx.z * 128, tid = threadIdx.x;
+  const int S = HW >> 8;
+  float st[3];
+  damc::strip256_stats(y + ((long)b * HW + 256L * sp) * C + c0, C, tid, c0 + (tid & 127) < C, red, st);
+  if (tid < 128 && c0 + tid < C) {
+    float* o = part + (((long)b * C + c0 + tid) * S + sp) * 3;
+    o[0] = st[0];
+    o[1] = st[1];
+    o[2] = st[2];
+  }
+}
+
 // the normalise + affine + LeakyReLU of in_apply_kernel (same fmaf), written as the next convolution's limbs (x3
 // octets) instead of fp32 in place: the limb engine reads nothing else.  One thread per (pixel, channel octet).
 // y32 != NULL: fp32 in place instead (y32 == y; every thread rewrites only the octet it read), for a next conv that
@@ -1460,7 +1477,8 @@ bool enc_shapes(const damc_encoder_t* e, int B, EncShapes* sh) {
 // af32 != NULL: the input as fp32 NHWC, staged as fp32 and split into limbs in registers (X3_F32A; bitwise the limb
 // input a3 = the RNE limbs of af32)
 int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int win, const damc_enc_layer_t& L,
-                const void* w3, float* y, float* kslab, size_t kslab_floats, int* defer, hipStream_t s) {
+                const void* w3, float* y, float* kslab, size_t kslab_floats, int* defer, hipStream_t s,
+                float* in_part = nullptr, int* in_done = nullptr) {
   const int hout = (hin + 2 * L.pad - L.k) / L.stride + 1, wout = (win + 2 * L.pad - L.k) / L.stride + 1;
   damc::GemmArgs a;
   if (af32) {
@@ -1493,6 +1511,12 @@ int enc_conv_x3(const unsigned short* a3, const float* af32, int B, int hin, int
   a.kslab_floats = (long)kslab_floats;
   a.ksplit_deferred = defer;
   a.kwalk = damc::x3_conv_walk(L.k, L.cin);  // the weight operand's K order (every packer of it reads the same rule)
+  if (in_part) {  // the norm's statistics in the epilogue where the launch allows (GemmArgs::in_part)
+    a.in_part = in_part;
+    a.in_hw = hout * wout;
+    a.in_S = hout * wout / 256;
+    a.in_done = in_done;
+  }
   return damc::launch_gemm(a, damc::A_CONV, damc::EPI_BIAS_ACT, damc::O_DENSE, 1, "enc_conv",
                            2.0 * a.M * (double)L.cout * a.K, s);
 }
@@ -1713,6 +1737,13 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
     }
     // the norm after this conv is the one-pass kernel; it then also sums the conv's split-K slabs itself
     const bool in1 = L.in_gamma && i + 1 < n && sh.limb[i + 1] && L.cout % 32 == 0 && hw <= 256 && !(io && io[0] == '0');
+    // the three-kernel norm on 256-pixel strips, its statistics taken in the conv's epilogue (round 6; GemmArgs::in_part;
+    // in_strip_stats_kernel where the conv ran split): the stats pass's read of the conv output is gone (CelebA-HQ
+    // B=64: 537 + 268 + 67 MB).  DAMC_ENC_IN_STRIP=0 (read per call) keeps in_stats_kernel's partition
+    const char* istr = getenv("DAMC_ENC_IN_STRIP");
+    const bool strip = L.in_gamma && !in1 && i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0 && sh.limb[i] &&
+                       hw % 256 == 0 && hw / 256 <= 64 && !(istr && istr[0] == '0');
+    int strip_done = 1;
     int ks_def = 0;
     if (sh.limb[i]) {
       if (!a3_ready && !in32) {
@@ -1729,7 +1760,8 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
         wl = w3;
       }
       if ((rc = enc_conv_x3(a3, in32 ? buf[i & 1] : nullptr, B, sh.h[i], sh.w[i], L, wl, out, kslab, sh.ks_max,
-                            (in1 && !(isl && isl[0] == '0')) ? &ks_def : nullptr, s)))
+                            (in1 && !(isl && isl[0] == '0')) ? &ks_def : nullptr, s, strip ? inws : nullptr,
+                            strip ? &strip_done : nullptr)))
         return rc;
     } else {
       const size_t nsl = damc_conv2d_workspace_floats(B, sh.h[i], sh.w[i], L.cin, L.cout, L.k, L.stride, L.pad);
@@ -1762,10 +1794,14 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
       in32 = y32 != nullptr;
       a3_ready = !in32;
     } else if (i + 1 < n && sh.limb[i + 1] && L.cout % 8 == 0) {  // the norm writes the next convolution's limbs
-      const int S = in_splits(hw), cg = (L.cout + 63) / 64;
+      const int S = strip ? hw / 256 : in_splits(hw), cg = (L.cout + 63) / 64;
       float* ssb = inws + (size_t)B * L.cout * S * 3;
       ProfScope ps("instnorm", 0.0, s);
-      hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, out, B, hw, L.cout, S, inws);
+      if (!strip)
+        hipLaunchKernelGGL(in_stats_kernel, dim3(B * cg, S), dim3(256), 0, s, out, B, hw, L.cout, S, inws);
+      else if (!strip_done)
+        hipLaunchKernelGGL(in_strip_stats_kernel, dim3(S, B, (L.cout + 127) / 128), dim3(512), 0, s, out, hw, L.cout,
+                           inws);
       hipLaunchKernelGGL(in_merge_kernel, dim3((B * L.cout + 3) / 4), dim3(256), 0, s, inws, B, L.cout, S,
                          L.in_gamma, L.in_beta, L.in_eps, ssb);
       const long n8 = (long)B * hw * (L.cout / 8);

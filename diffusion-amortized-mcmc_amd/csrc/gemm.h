@@ -128,7 +128,59 @@ struct GemmArgs {
   // (x3_walk_tap): K tile kt = 32 channels 32 (kt / 16) .. of tap x3_walk_tap(kt % 16), and the weight operand is
   // packed in that order (x3_conv_walk); 0 = tap-major
   int kwalk = 0;
+  // InstanceNorm statistics of the epilogue result (round 6; limb engine, O_DENSE, EPI_BIAS_ACT, unsplit 256 x 128
+  // tiles: the encoder's norms): per (sample, 256-row strip, channel) {n, mean, m2} at
+  // in_part[((b * N + n) * in_S + strip) * 3] (in_stats_kernel's layout, in_merge_kernel reads it), computed by
+  // strip256_stats from the stored values; in_hw = output rows per sample (a multiple of 256), in_S = in_hw / 256.
+  // in_done (host): the caller sets it to 1; a launcher that cannot write the statistics (a split-K or narrow launch)
+  // clears it, and the caller then runs encoder.hip's in_strip_stats_kernel (the same arithmetic) over C
+  float* in_part = nullptr;
+  int in_hw = 0, in_S = 0;
+  int* in_done = nullptr;
 };
+
+// InstanceNorm statistics of one 256-row strip (256 consecutive output pixels of one sample) for 128 channels, by 512
+// threads: thread t takes channel t & 127 over rows 64 (t >> 7) .. + 63 in two passes (the sum, mean = sum / 64, then
+// the centred squares), and threads t < 128 merge the four quarters in order (Chan's pairwise update, in_stats_kernel's
+// wmerge at equal counts).  Fixed partition and order, every operation non-contractable, so the same values give the
+// same statistics in the conv's epilogue (gemm_x3_kernel, LDS tile) and in the stand-alone kernel (encoder.hip
+// in_strip_stats_kernel, global rows): the statistics, and so the normalised activation, do not depend on whether the
+// conv ran split, nor on the batch.  y: row r, channel c at y[r * ld + c] (LDS or global); live: c < the channel count;
+// red: 1024 floats of LDS; {n, mean, m2} returned in threads t < 128 (after the one barrier inside)
+__device__ __forceinline__ void strip256_stats(const float* y, long ld, int tid, bool live, float* red, float (&st)[3]) {
+  const int c = tid & 127, q = tid >> 7;
+  const float* col = y + (long)q * 64 * ld + c;
+  float s = 0.f, m2 = 0.f;
+  if (live) {
+#pragma unroll 16
+    for (int r = 0; r < 64; ++r) s = add_rn(s, col[r * ld]);
+    const float mean = mul_rn(s, 0.015625f);
+#pragma unroll 16
+    for (int r = 0; r < 64; ++r) {
+      const float d = sub_rn(col[r * ld], mean);
+      m2 = __builtin_fmaf(d, d, m2);
+    }
+    s = mean;
+  }
+  red[q * 256 + c] = s;
+  red[q * 256 + 128 + c] = m2;
+  __syncthreads();
+  if (tid < 128) {
+    float n = 64.f, mu = red[c], M2 = red[128 + c];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float mb = red[k * 256 + c], m2b = red[k * 256 + 128 + c];
+      const float fb = k == 1 ? 0.5f : k == 2 ? (1.f / 3.f) : 0.25f;  // 64 / (n + 64)
+      const float d = sub_rn(mb, mu);
+      mu = add_rn(mu, mul_rn(d, fb));
+      M2 = add_rn(add_rn(M2, m2b), mul_rn(mul_rn(mul_rn(d, d), n), fb));
+      n = add_rn(n, 64.f);
+    }
+    st[0] = n;
+    st[1] = mu;
+    st[2] = M2;
+  }
+}
 // opt-in (round 6): the encoder's 4 x 4 convs walk K slice-major with their taps grouped by (ky, kx) parity: a stride-2
 // tap reads one parity class of the input pixels, the four taps of a class read the same pixels shifted, and a
 // 32-channel slice keeps a workgroup's reuse distance within the XCD's L2.  At CelebA-HQ B=64 it cuts FETCH per conv

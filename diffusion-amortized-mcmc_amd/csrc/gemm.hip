@@ -2306,7 +2306,8 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
       o[1] = m;
       o[2] = l;
     }
-    if (OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A) && p.proj_out) {  // the activated row back into the tile
+    if ((OM == O_PHASE && EPI == EPI_BIAS_ACT && (WIDE || F32A) && p.proj_out) ||
+        (OM == O_DENSE && EPI == EPI_BIAS_ACT && !WIDE && !NARROW && p.in_part)) {  // the stored row back into the tile
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(tile + row * TS + oct * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
@@ -2574,6 +2575,23 @@ __global__ __launch_bounds__(512, (V & X3_NARROW) ? 2 : 1) void gemm_x3_kernel(G
     return;
   }
   epilogue(0, BM);
+  if constexpr (OM == O_DENSE && EPI == EPI_BIAS_ACT && !WIDE && !NARROW && !FIXUP && BM == 256 && BN == 128) {
+    // the encoder norm's statistics of this tile (GemmArgs::in_part): its 256 rows are one strip of one sample
+    static_assert(BM * TS * 4 + BM * 8 + 1024 * 4 <= 2 * (BM + BN) * X3_ROWB, "statistics scratch exceeds the LDS");
+    if (p.in_part && !KSPLIT) {  // workgroup-uniform
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem + BM * TS * 4 + BM * 8);
+      float st[3];
+      strip256_stats(tile, TS, tid, n0 + (tid & 127) < p.N, red, st);
+      if (tid < 128 && n0 + tid < p.N) {
+        const int b = m0 / p.in_hw, sp = (m0 - b * p.in_hw) >> 8;
+        float* o = p.in_part + (((long)b * p.N + n0 + tid) * p.in_S + sp) * 3;
+        o[0] = st[0];
+        o[1] = st[1];
+        o[2] = st[2];
+      }
+    }
+  }
 }
 
 // the split-K reduce: one thread per (phase, row, channel octet); the slices in fixed order, then the limb GEMM's
@@ -2958,6 +2976,15 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   GemmArgs a = a0;
   constexpr int BM = (V & 524288) ? 128 : X3_BM, BN = (V & 524288) ? 256 : X3_BN;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  // the norm statistics in the epilogue (GemmArgs::in_part): the unsplit 256 x 128 dense tile only; every other launch
+  // clears in_done and leaves them to the caller's kernel
+  auto no_stats = [&]() {
+    if (a.in_part && a.in_done) *a.in_done = 0;
+    a.in_part = nullptr;
+  };
+  if (a.in_part && !(OM == O_DENSE && EPI == EPI_BIAS_ACT && BM == 256 && BN == 128 && zdim == 1 && a.in_hw > 0 &&
+                     a.in_hw % 256 == 0 && a.M % a.in_hw == 0 && a.in_S == a.in_hw / 256))
+    no_stats();
   if constexpr (V == DAMC_X3_VARIANT && OM != O_WGRAD) {
     // opt-in (DAMC_X3_NARROW=1, read per call): an under-filled grid that the 64 x 128 tile fills (>= 256 workgroups)
     // runs unsplit on it instead of split-K.  Measured slower at the CIFAR B=16 per-rank step: 158.7 / 152.2 us for the
@@ -2967,6 +2994,7 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
     const long nnm = (a.M + 63) / 64;
     if (a.kslab && !a.proj_out && !a.kwalk && en && en[0] == '1' && (long)ntm * ntn * zdim < 256 &&
         nnm * ntn * zdim >= 256) {
+      no_stats();
       a.ksplit = 1;
       a.kbpw = 1;
       a.kslab_reg = 0;
@@ -2978,6 +3006,7 @@ static int launch_x3_t(const GemmArgs& a0, int zdim, hipStream_t s) {
   if (OM != O_WGRAD && a.kslab && !(V & 16)) {
     const int ks = x3_ksplit(a.M, a.N, a.K, zdim, BM, BN, a.negk);
     if (ks > 1 && (long)zdim * ks * a.M * a.N <= a.kslab_floats && a.N % 8 == 0) {
+      no_stats();
       a.ksplit = ks;
       const int nostore0 = a.proj_nostore;  // the caller's: honoured where the reduce runs the projection itself
       a.proj_nostore = 0;  // the reduce writes C; the projection then runs as proj_rows_kernel over it
@@ -3520,6 +3549,7 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     }
     if (a.A3) c.A3 = a.A3 + b0 * img * 3;
     if (a.a_f32) c.A = a.A + b0 * img;
+    if (a.in_part) c.in_part = a.in_part + b0 * hwq / (a.in_hw > 0 ? a.in_hw : 1) * (long)a.N * a.in_S * 3;
     if (a.C) c.C = a.C + b0 * cimg;
     if (a.C3) c.C3 = a.C3 + b0 * cimg * 3;
     if (a.sgn) c.sgn = a.sgn + b0 * cimg / 8;
@@ -3552,6 +3582,7 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
       // fp32 weights split in registers where the caller passes them (2/3 of the limb bytes; bitwise the same
       // operands); DAMC_X3_SKINNY_F32B=0 (read per call) reads the limbs
       const char* efb = getenv("DAMC_X3_SKINNY_F32B");
+      if (c.in_part && c.in_done) *c.in_done = 0;  // no norm statistics from this kernel
       const dim3 gsk((unsigned)((c.N + 63) / 64), (unsigned)((c.M + 15) / 16));
       // 32 columns per wave by default (NTW = 2: CIFAR B=16 step -5 to -17 us, B=32 -4 us against 16 columns, same-box
       // pairs in profiles/r05/skinny_ntw_ab.txt); DAMC_X3_SKINNY_NTW=1 (read per call) keeps 16
@@ -3568,6 +3599,7 @@ static int launch_gemm_x3(const GemmArgs& a, Epi epi, OMode om, int zdim, hipStr
     if (epi == EPI_BIAS_ACT && om == O_DENSE && c.M <= 128 && !c.a_f32 && !c.proj_out && c.kslab && !c.kwalk &&
         c.K % c.negk == 0 && c.K / c.negk >= 8 && c.N % 8 == 0 && (long)(c.K / c.negk) * c.M * c.N <= c.kslab_floats &&
         !(ens && ens[0] == '0')) {
+      if (c.in_part && c.in_done) *c.in_done = 0;  // no norm statistics from this kernel
       launch_x3_narrow_split<EPI_BIAS_ACT>(c, s);
       continue;
     }
