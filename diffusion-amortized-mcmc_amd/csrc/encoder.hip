@@ -181,6 +181,28 @@ __global__ __launch_bounds__(512) void in_strip_stats_kernel(const float* __rest
   }
 }
 
+// in_apply_x3_kernel's fp32 in-place form one channel quad per thread (round 6, late): the same fmaf and LReLU per
+// element, and every load / store instruction covers 1 KB without gaps (the octet form's pair of 16-B accesses per
+// lane half-covers two 2 KB spans)
+__global__ __launch_bounds__(256) void in_apply_f32_kernel(float* y, long n4, int HW, int C,
+                                                           const float* __restrict__ ss, float slope) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int C4 = C / 4;
+  const long pix = i / C4;
+  const int c0 = (int)(i - pix * C4) * 4;
+  const int b = (int)(pix / HW);
+  const float* sc = ss + (long)b * 2 * C + c0;
+  f32x4 v = *reinterpret_cast<const f32x4*>(y + 4 * i);
+  const f32x4 a = *reinterpret_cast<const f32x4*>(sc), h = *reinterpret_cast<const f32x4*>(sc + C);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float t = fmaf(v[e], a[e], h[e]);
+    v[e] = t > 0.f ? t : t * slope;
+  }
+  *reinterpret_cast<f32x4*>(y + 4 * i) = v;
+}
+
 // the normalise + affine + LeakyReLU of in_apply_kernel (same fmaf), written as the next convolution's limbs (x3
 // octets) instead of fp32 in place: the limb engine reads nothing else.  One thread per (pixel, channel octet).
 // y32 != NULL: fp32 in place instead (y32 == y; every thread rewrites only the octet it read), for a next conv that
@@ -566,18 +588,23 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const float* __restrict
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const long obase = (((long)b * H + r0 + r) * W + p0 - r * W) * C;  // wave-uniform
+      if (y32) {
+        // the group's 16 pixels x C channels are one contiguous run of the NHWC output: lane l of store j writes its
+        // 16 B at float 4 (l + 64 j), so every store instruction covers 1 KB without gaps (round 6, late: the octet
+        // form wrote two half-covered 2 KB spans per pair of stores)
 #pragma unroll
-      for (int it = 0; it < 2 * NT * 16 / 64; ++it) {  // 16 pixels x NT * 2 octets
-        const int id = lane + 64 * it, pp = id / (2 * NT), oc = id - pp * (2 * NT);
-        float v[8];
+        for (int it = 0; it < 16 * NT * 16 / 256; ++it) {
+          const int j = lane + 64 * it, pp = j / (4 * NT), c4 = j - pp * (4 * NT);
+          *reinterpret_cast<f32x4*>(y32 + obase + 4 * j) = *reinterpret_cast<const f32x4*>(&c3out[wave][pp][4 * c4]);
+        }
+      } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = c3out[wave][pp][8 * oc + e];
-        const long off = obase + (pp * (16 * NT) + 8 * oc);  // C == 16 NT
-        if (y32) {
-          *reinterpret_cast<f32x4*>(y32 + off) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(y32 + off + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-          damc::store_x3_octet(v, y3 + 3 * off);
+        for (int it = 0; it < 2 * NT * 16 / 64; ++it) {  // 16 pixels x NT * 2 octets
+          const int id = lane + 64 * it, pp = id / (2 * NT), oc = id - pp * (2 * NT);
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = c3out[wave][pp][8 * oc + e];
+          damc::store_x3_octet(v, y3 + 3 * (obase + (pp * (16 * NT) + 8 * oc)));  // C == 16 NT
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1806,8 +1833,14 @@ extern "C" int damc_q_encoder_fwd(const damc_encoder_t* e, const float* x, int B
                          L.in_gamma, L.in_beta, L.in_eps, ssb);
       const long n8 = (long)B * hw * (L.cout / 8);
       float* y32 = f32a_layer(i + 1) ? out : nullptr;  // in place: the next conv's fp32 input
-      hipLaunchKernelGGL(in_apply_x3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, out, n8, hw, L.cout,
-                         ssb, L.slope, a3, y32);
+      if (y32) {
+        const long n4 = 2 * n8;
+        hipLaunchKernelGGL(in_apply_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, out, n4, hw,
+                           L.cout, ssb, L.slope);
+      } else {
+        hipLaunchKernelGGL(in_apply_x3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, out, n8, hw,
+                           L.cout, ssb, L.slope, a3, y32);
+      }
       DAMC_LAUNCH_CHECK();
       in32 = y32 != nullptr;
       a3_ready = !in32;
